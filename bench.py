@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 224px DDP training throughput (images/sec, whole job).
+
+BASELINE.json metric: "images/sec (whole node), ResNet-50 224px DDP at 1/2/4/8 MI355X".
+Synthetic ImageNet-1k-shaped data (uint8 images generated on device, random
+labels), random-init ResNet-50, bf16 activations / fp32 master weights, full
+training step in the timed region: input normalisation (u8 NCHW -> bf16 NHWC
+kernel), forward, softmax-CE, backward (DDP bucketed all-reduce over RCCL when
+N > 1), fused SGD-momentum step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line; `value` = total images/s over all ranks, timed
+as the MAX over ranks of K steps bracketed by barrier + device sync.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd.models import build_model  # noqa: E402
+from ddp_classification_pytorch_amd.ops import functional as Fn  # noqa: E402
+from ddp_classification_pytorch_amd.optim import FusedSGD  # noqa: E402
+from ddp_classification_pytorch_amd.parallel import ddp as pddp  # noqa: E402
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--syncbn", action="store_true", help="cross-replica BN (reference default); off = local BN")
+    ap.add_argument("--bucket-cap-mb", type=float, default=100.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    _ext.hip_ops()  # fail loudly if the gfx950 library is missing
+
+    torch.manual_seed(1234 + rank)
+    model = build_model(a.model, num_classes=a.num_classes).to(dev)
+    if world > 1:
+        model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb)
+    opt = FusedSGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+
+    B, S = a.batch, a.image_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(rank)
+    images = torch.randint(0, 256, (B, 3, S, S), dtype=torch.uint8, device=dev, generator=g)
+    labels = torch.randint(0, a.num_classes, (B,), device=dev, generator=g)
+    mean = torch.tensor(IMAGENET_MEAN, device=dev)
+    std = torch.tensor(IMAGENET_STD, device=dev)
+
+    def step():
+        x = Fn.to_device_nhwc(images, mean, std, cpad=8, nchw=True, in_scale=1.0 / 255.0)
+        logits = model(x)
+        loss = Fn.cross_entropy(logits, labels)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    prof = None
+    if a.profile_dir and rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile_dir, exist_ok=True)
+        with open(os.path.join(a.profile_dir, "bench_profile.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss_v = float(loss.item())
+    ms = dt / a.steps * 1000.0
+    ips = B * world * a.steps / dt
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node), ResNet-50 224px DDP at 1/2/4/8 MI355X",
+            "value": round(ips, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
+            "config": {
+                "model": a.model,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "image_size": S,
+                "num_classes": a.num_classes,
+                "parallelism": f"dp{world}",
+                "syncbn": bool(a.syncbn),
+                "optimizer": "fused SGD momentum 0.9 wd 1e-4",
+                "final_loss": round(loss_v, 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,59 @@
+"""Loader for the in-tree gfx950 kernel library (`_dcp_kernels.so`).
+
+GPU tensors are ALWAYS served by the HIP kernels: if the library is missing
+or fails to load while a GPU op is requested, this raises instead of
+silently falling back to PyTorch/MIOpen.  CPU tensors use the reference
+math in :mod:`ddp_classification_pytorch_amd.ops._ref` (tests and gloo
+plumbing only).
+
+Set ``DCP_AUTOBUILD=1`` to compile the library on first use when it is
+missing (needs hipcc).
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dcp_kernels.so")
+_lock = threading.Lock()
+_state = {"loaded": False, "error": None}
+
+
+def library_path() -> str:
+    return LIB_PATH
+
+
+def try_load() -> bool:
+    """Load the kernel library if present; returns True when torch.ops.dcp is usable."""
+    if _state["loaded"]:
+        return True
+    with _lock:
+        if _state["loaded"]:
+            return True
+        if not os.path.exists(LIB_PATH) and os.environ.get("DCP_AUTOBUILD", "0") == "1":
+            from . import build_ext
+
+            build_ext.build(verbose=False)
+        if not os.path.exists(LIB_PATH):
+            _state["error"] = f"kernel library not built: {LIB_PATH} (run python -m ddp_classification_pytorch_amd.build_ext)"
+            return False
+        try:
+            torch.ops.load_library(LIB_PATH)
+        except Exception as e:  # pragma: no cover - exercised only on broken builds
+            _state["error"] = f"failed to load {LIB_PATH}: {e}"
+            return False
+        _state["loaded"] = True
+        return True
+
+
+def hip_ops():
+    """torch.ops.dcp, loading the library; raises loudly if it is unavailable."""
+    if not try_load():
+        raise RuntimeError("gfx950 kernels unavailable for a GPU op: " + str(_state["error"]))
+    return torch.ops.dcp
+
+
+def is_loaded() -> bool:
+    return _state["loaded"]

@@ -1,0 +1,755 @@
+// PyTorch operator registrations (namespace `dcp`) for the gfx950 kernels.
+//
+// Every op takes device tensors, checks shapes/dtypes on the host (a wrong
+// shape must never reach a kernel), and launches on the current HIP stream so
+// it composes with autograd, torch.distributed (RCCL) and HIP graph capture.
+// No allocation-free variants are needed: the PyTorch caching allocator
+// serves every output.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/library.h>
+
+#include <mutex>
+#include <vector>
+
+#include "launchers.h"
+
+using at::Tensor;
+using std::optional;
+
+namespace {
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
+#define CHECK_ACT(t) \
+  CHECK_DEV(t);      \
+  CHECK_CONTIG(t);   \
+  CHECK_BF16(t)
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+const bf16* bp(const Tensor& t) { return reinterpret_cast<const bf16*>(t.data_ptr()); }
+bf16* bpm(Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
+const float* fp(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+float* fpm(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+
+// 256 zero bytes per device: the source of every out-of-bounds implicit-GEMM lane
+const bf16* zero_page(int dev) {
+  static std::mutex mu;
+  static std::vector<void*> pages(64, nullptr);
+  std::lock_guard<std::mutex> g(mu);
+  if (!pages[dev]) {
+    void* p = nullptr;
+    TORCH_CHECK(hipMalloc(&p, 256) == hipSuccess, "zero page alloc failed");
+    TORCH_CHECK(hipMemset(p, 0, 256) == hipSuccess, "zero page memset failed");
+    pages[dev] = p;
+  }
+  return reinterpret_cast<const bf16*>(pages[dev]);
+}
+
+int num_cus(int dev) {
+  static std::vector<int> cache(64, 0);
+  if (!cache[dev]) {
+    hipDeviceProp_t prop;
+    TORCH_CHECK(hipGetDeviceProperties(&prop, dev) == hipSuccess);
+    cache[dev] = prop.multiProcessorCount;
+  }
+  return cache[dev];
+}
+
+at::TensorOptions bf16_like(const Tensor& t) { return t.options().dtype(at::kBFloat16); }
+at::TensorOptions f32_like(const Tensor& t) { return t.options().dtype(at::kFloat); }
+
+// ---------------------------------------------------------------------------
+// convolution
+// ---------------------------------------------------------------------------
+dcp::TapList fwd_taps(int KH, int KW, int pad) {
+  dcp::TapList t;
+  t.n = KH * KW;
+  TORCH_CHECK(t.n <= dcp::kMaxTaps, "kernel too large");
+  for (int kh = 0; kh < KH; ++kh)
+    for (int kw = 0; kw < KW; ++kw) {
+      const int i = kh * KW + kw;
+      t.dy[i] = kh - pad;
+      t.dx[i] = kw - pad;
+      t.widx[i] = i;
+    }
+  return t;
+}
+
+// x [N,H,W,C] bf16, w [Co,KH,KW,C] bf16 -> y [N,Ho,Wo,Co], stats slabs [ceil(M/64),2,Co]
+std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad, bool stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd expects NHWC input and [Co,KH,KW,Ci] weight");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "weight Ci mismatch");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_fwd needs C and Co multiples of 8");
+  TORCH_CHECK(KH * KW <= dcp::kMaxTaps && pad <= 100 && KH <= 100, "unsupported conv geometry");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)N * Ho * Wo * Co < (1ll << 32), "tensor too large");
+  auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
+  const int M = N * Ho * Wo;
+  Tensor slabs;
+  if (stats)
+    slabs = at::empty({(M + 63) / 64, 2, Co}, f32_like(x));
+  else
+    slabs = at::empty({0}, f32_like(x));
+  const auto taps = fwd_taps(KH, KW, pad);
+  dcp::launch_tap_gemm(bp(x), N, H, W, C, bp(w), Co, KH * KW, bpm(y), Ho, Wo, Ho, Wo, stride, 1, 0, 0, taps,
+                       stats ? slabs.data_ptr<float>() : nullptr, nullptr, 0, zero_page(x.get_device()),
+                       cur_stream());
+  return {y, slabs};
+}
+
+// dy [N,Ho,Wo,Co], wt [C,KH,KW,Co] (transposed weight) -> dx [N,H,W,C]
+Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+  CHECK_ACT(dy);
+  CHECK_ACT(wt);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int C = wt.size(0), KH = wt.size(1), KW = wt.size(2);
+  TORCH_CHECK(wt.size(3) == Co, "transposed weight Co mismatch");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_dgrad needs channel multiples of 8");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv_dgrad supports stride 1 and 2");
+  TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "dgrad geometry");
+  auto dx = at::empty({N, H, W, C}, bf16_like(dy));
+  const bf16* z = zero_page(dy.get_device());
+  auto st = cur_stream();
+  if (stride == 1) {
+    dcp::TapList t;
+    t.n = KH * KW;
+    for (int kh = 0; kh < KH; ++kh)
+      for (int kw = 0; kw < KW; ++kw) {
+        const int i = kh * KW + kw;
+        t.dy[i] = pad - kh;
+        t.dx[i] = pad - kw;
+        t.widx[i] = i;
+      }
+    dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr,
+                         nullptr, 0, z, st);
+    return dx;
+  }
+  // stride 2: four parity classes of the input grid
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      const int Hy = (H - ph + 1) / 2, Wy = (W - pw + 1) / 2;
+      if (Hy <= 0 || Wy <= 0) continue;
+      dcp::TapList t;
+      t.n = 0;
+      for (int kh = 0; kh < KH; ++kh) {
+        if (((ph + pad - kh) % 2 + 2) % 2) continue;
+        for (int kw = 0; kw < KW; ++kw) {
+          if (((pw + pad - kw) % 2 + 2) % 2) continue;
+          t.dy[t.n] = (ph + pad - kh) / 2;  // exact (even numerator)
+          t.dx[t.n] = (pw + pad - kw) / 2;
+          t.widx[t.n] = kh * KW + kw;
+          ++t.n;
+        }
+      }
+      dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, Hy, Wy, 1, 2, ph, pw, t,
+                           nullptr, nullptr, 0, z, st);
+    }
+  return dx;
+}
+
+// dy [N,Ho,Wo,Co], x [N,H,W,C] -> dw fp32 [Co,KH,KW,C]
+Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(x.size(0) == N, "batch mismatch");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_wgrad needs channel multiples of 8");
+  TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "wgrad geometry");
+  auto dw = at::zeros({Co, KH, KW, C}, f32_like(dy));
+  const auto taps = fwd_taps(KH, KW, pad);
+  dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
+                    zero_page(dy.get_device()), num_cus(dy.get_device()), cur_stream());
+  return dw;
+}
+
+// x [B,K] bf16, w [Npad,K] bf16 -> y [B,Npad] (= x w^T + b, optional ReLU)
+Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, bool relu) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear shapes");
+  const int B = x.size(0), K = x.size(1), Np = w.size(0);
+  TORCH_CHECK(K % 8 == 0 && Np % 8 == 0, "linear needs K and N multiples of 8");
+  if (bias.has_value()) {
+    CHECK_F32(*bias);
+    TORCH_CHECK(bias->numel() >= Np, "bias must be padded to the output width");
+  }
+  auto y = at::empty({B, Np}, bf16_like(x));
+  dcp::TapList t;
+  t.n = 1;
+  t.dy[0] = t.dx[0] = t.widx[0] = 0;
+  dcp::launch_tap_gemm(bp(x), B, 1, 1, K, bp(w), Np, 1, bpm(y), 1, 1, 1, 1, 1, 1, 0, 0, t, nullptr, fp(bias),
+                       relu ? 1 : 0, zero_page(x.get_device()), cur_stream());
+  return y;
+}
+
+// dy [B,N] bf16, x [B,K] bf16 -> dw fp32 [N,K]
+Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int B = dy.size(0), Np = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == B && K % 8 == 0 && Np % 8 == 0, "linear_wgrad shapes");
+  auto dw = at::zeros({Np, K}, f32_like(dy));
+  dcp::TapList t;
+  t.n = 1;
+  t.dy[0] = t.dx[0] = t.widx[0] = 0;
+  dcp::launch_wgrad(bp(dy), B, 1, 1, Np, bp(x), 1, 1, K, 1, t, dw.data_ptr<float>(), zero_page(dy.get_device()),
+                    num_cus(dy.get_device()), cur_stream());
+  return dw;
+}
+
+// fp32 master [Co,KH,KW,Ci] -> bf16 [Co_pad,KH,KW,Ci] (+ transposed [Ci,KH,KW,Co_pad])
+std::tuple<Tensor, Tensor> weight_prep(const Tensor& w, int64_t co_pad, bool transposed) {
+  CHECK_DEV(w);
+  CHECK_CONTIG(w);
+  CHECK_F32(w);
+  TORCH_CHECK(w.dim() == 4 || w.dim() == 2, "weight_prep expects 4-D or 2-D weights");
+  const int Co = w.size(0);
+  const int T = w.dim() == 4 ? w.size(1) * w.size(2) : 1;
+  const int Ci = w.dim() == 4 ? w.size(3) : w.size(1);
+  const int Cp = co_pad > Co ? co_pad : Co;
+  std::vector<int64_t> shp = w.sizes().vec();
+  shp[0] = Cp;
+  auto wb = at::empty(shp, bf16_like(w));
+  Tensor wt;
+  if (transposed) {
+    std::vector<int64_t> ts = w.sizes().vec();
+    ts[0] = Ci;
+    ts[ts.size() - 1] = Cp;
+    wt = at::empty(ts, bf16_like(w));
+  } else {
+    wt = at::empty({0}, bf16_like(w));
+  }
+  dcp::launch_weight_prep(w.data_ptr<float>(), Co, T, Ci, Cp, bpm(wb), transposed ? bpm(wt) : nullptr, cur_stream());
+  return {wb, wt};
+}
+
+Tensor grouped_conv_fwd(const Tensor& x, const Tensor& w, int64_t groups, int64_t stride, int64_t pad) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(C % groups == 0 && Co % groups == 0 && w.size(3) == C / groups, "grouped conv shapes");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "grouped conv channel multiples of 8");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
+  dcp::launch_grouped_conv_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
+                               cur_stream());
+  return y;
+}
+
+Tensor grouped_conv_dgrad(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t groups, int64_t stride,
+                          int64_t pad) {
+  CHECK_ACT(dy);
+  CHECK_ACT(w);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int KH = w.size(1), KW = w.size(2), C = w.size(3) * groups;
+  auto dx = at::empty({N, H, W, C}, bf16_like(dy));
+  dcp::launch_grouped_conv_dgrad(bp(dy), bp(w), bpm(dx), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
+                                 cur_stream());
+  return dx;
+}
+
+Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t groups, int64_t stride,
+                          int64_t pad) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int H = x.size(1), W = x.size(2), C = x.size(3);
+  auto dw = at::zeros({Co, KH, KW, C / groups}, f32_like(dy));
+  dcp::launch_grouped_conv_wgrad(bp(dy), bp(x), dw.data_ptr<float>(), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride,
+                                 pad, cur_stream());
+  return dw;
+}
+
+// ---------------------------------------------------------------------------
+// batch norm
+// ---------------------------------------------------------------------------
+// per-channel totals [2,C] from conv slabs (if given) or directly from x
+Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
+  auto tot = at::zeros({2, C}, f32_like(x));
+  if (slabs.has_value() && slabs->numel() > 0) {
+    TORCH_CHECK(slabs->dim() == 3 && slabs->size(1) == 2 && slabs->size(2) == C, "slab shape");
+    dcp::launch_bn_slab_reduce(slabs->data_ptr<float>(), slabs->size(0), C, tot.data_ptr<float>(), cur_stream());
+  } else {
+    dcp::launch_chan_stats(bp(x), M, C, true, tot.data_ptr<float>(), cur_stream());
+  }
+  return tot;
+}
+
+Tensor colsum(const Tensor& x) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "colsum channels");
+  auto tot = at::zeros({2, C}, f32_like(x));
+  dcp::launch_chan_stats(bp(x), x.numel() / C, C, false, tot.data_ptr<float>(), cur_stream());
+  return tot[0];
+}
+
+// -> (mean, invstd, scale, shift); updates running stats in place when given
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(const Tensor& tot, double count,
+                                                       const optional<Tensor>& gamma,
+                                                       const optional<Tensor>& beta,
+                                                       const optional<Tensor>& run_mean,
+                                                       const optional<Tensor>& run_var, double momentum,
+                                                       double eps) {
+  CHECK_DEV(tot);
+  CHECK_F32(tot);
+  const int C = tot.size(1);
+  auto mean = at::empty({C}, tot.options()), invstd = at::empty({C}, tot.options());
+  auto scale = at::empty({C}, tot.options()), shift = at::empty({C}, tot.options());
+  dcp::launch_bn_finalize(tot.data_ptr<float>(), count, C, (float)eps, fp(gamma), fp(beta), mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), fpm(run_mean),
+                          fpm(run_var), (float)momentum, cur_stream());
+  return {mean, invstd, scale, shift};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_eval_coeff(const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                                                         const Tensor& run_mean, const Tensor& run_var, double eps) {
+  CHECK_DEV(run_mean);
+  const int C = run_mean.numel();
+  auto mean = at::empty({C}, run_mean.options()), invstd = at::empty({C}, run_mean.options());
+  auto scale = at::empty({C}, run_mean.options()), shift = at::empty({C}, run_mean.options());
+  dcp::launch_bn_eval_coeff(C, (float)eps, fp(gamma), fp(beta), run_mean.data_ptr<float>(),
+                            run_var.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                            scale.data_ptr<float>(), shift.data_ptr<float>(), cur_stream());
+  return {mean, invstd, scale, shift};
+}
+
+Tensor bn_act(const Tensor& x, const optional<Tensor>& res, const Tensor& scale, const Tensor& shift, int64_t act,
+              double slope) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && scale.numel() == C, "bn_act shapes");
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+  }
+  auto y = at::empty_like(x);
+  dcp::launch_bn_act_fwd(bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
+                         shift.data_ptr<float>(), bpm(y), x.numel(), C, act, (float)slope, cur_stream());
+  return y;
+}
+
+Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
+                     const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act, double slope) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_reduce shapes");
+  auto out = at::zeros({2, C}, f32_like(x));
+  dcp::launch_bn_bwd_reduce(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
+                            shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), x.numel() / C,
+                            C, act, (float)slope, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+std::tuple<Tensor, Tensor> bn_bwd_elemt(const Tensor& dy, const Tensor& x, const optional<Tensor>& res,
+                                        const Tensor& scale, const Tensor& shift, const Tensor& mean,
+                                        const Tensor& invstd, const optional<Tensor>& sums, double count, int64_t act,
+                                        double slope, bool want_dres) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0, "bn_bwd_elemt shapes");
+  auto dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  dcp::launch_bn_bwd_elemt(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
+                           shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), fp(sums),
+                           (float)(1.0 / count), x.numel(), C, act, (float)slope, bpm(dx),
+                           want_dres ? bpm(dres) : nullptr, cur_stream());
+  return {dx, dres};
+}
+
+// ---------------------------------------------------------------------------
+// pooling / layout
+// ---------------------------------------------------------------------------
+std::tuple<Tensor, Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k * k <= 255, "maxpool shapes");
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  auto idx = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  dcp::launch_maxpool_fwd(bp(x), bpm(y), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s, p, cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  CHECK_ACT(dy);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dcp::launch_maxpool_bwd(bp(dy), idx.data_ptr<uint8_t>(), bpm(dx), N, H, W, C, Ho, Wo, k, s, p, cur_stream());
+  return dx;
+}
+
+Tensor gap_fwd(const Tensor& x) {
+  CHECK_ACT(x);
+  const int N = x.size(0), C = x.size(-1);
+  const int HW = x.numel() / (N * C);
+  TORCH_CHECK(C % 8 == 0, "gap channels");
+  auto y = at::empty({N, C}, x.options());
+  dcp::launch_gap_fwd(bp(x), bpm(y), N, HW, C, cur_stream());
+  return y;
+}
+
+Tensor gap_bwd(const Tensor& dy, int64_t H, int64_t W) {
+  CHECK_ACT(dy);
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dcp::launch_gap_bwd(bp(dy), bpm(dx), N, H * W, C, cur_stream());
+  return dx;
+}
+
+Tensor space_to_depth(const Tensor& x, int64_t b, bool inverse) {
+  CHECK_ACT(x);
+  const int N = x.size(0);
+  if (!inverse) {
+    const int H = x.size(1), W = x.size(2), C = x.size(3);
+    TORCH_CHECK(H % b == 0 && W % b == 0, "space_to_depth needs H, W divisible by the block");
+    auto y = at::empty({N, H / b, W / b, C * b * b}, x.options());
+    dcp::launch_s2d(bp(x), bpm(y), N, H, W, C, b, 0, cur_stream());
+    return y;
+  }
+  const int Hb = x.size(1), Wb = x.size(2), Cb = x.size(3);
+  const int C = Cb / (b * b), H = Hb * b, W = Wb * b;
+  auto y = at::empty({N, H, W, C}, x.options());
+  dcp::launch_s2d(bp(x), bpm(y), N, H, W, C, b, 1, cur_stream());
+  return y;
+}
+
+Tensor to_nhwc(const Tensor& src, bool nchw, int64_t cpad, double in_scale, const optional<Tensor>& mean,
+               const optional<Tensor>& stdv) {
+  CHECK_DEV(src);
+  CHECK_CONTIG(src);
+  TORCH_CHECK(src.scalar_type() == at::kByte || src.scalar_type() == at::kFloat, "to_nhwc input u8 or fp32");
+  const int N = src.size(0);
+  const int C = nchw ? src.size(1) : src.size(3);
+  const int H = nchw ? src.size(2) : src.size(1);
+  const int W = nchw ? src.size(3) : src.size(2);
+  const int Cp = cpad > C ? cpad : C;
+  auto y = at::empty({N, H, W, Cp}, src.options().dtype(at::kBFloat16));
+  dcp::launch_to_nhwc(src.data_ptr(), src.scalar_type() == at::kByte, nchw, N, C, H, W, Cp, (float)in_scale,
+                      fp(mean), fp(stdv), bpm(y), cur_stream());
+  return y;
+}
+
+Tensor relu_bwd(const Tensor& dy, const Tensor& y) {
+  CHECK_ACT(dy);
+  CHECK_ACT(y);
+  TORCH_CHECK(dy.sizes() == y.sizes() && dy.numel() % 8 == 0, "relu_bwd shapes");
+  auto dx = at::empty_like(dy);
+  dcp::launch_relu_bwd(bp(dy), bp(y), bpm(dx), dy.numel(), cur_stream());
+  return dx;
+}
+
+Tensor prefix_mask(const Tensor& x, const Tensor& keep) {
+  CHECK_ACT(x);
+  TORCH_CHECK(keep.scalar_type() == at::kInt && keep.is_cuda(), "keep must be an int32 GPU scalar");
+  auto y = at::empty_like(x);
+  dcp::launch_prefix_mask(bp(x), bpm(y), x.size(0), x.size(1), keep.data_ptr<int>(), cur_stream());
+  return y;
+}
+
+Tensor nested_eval(const Tensor& feat, const Tensor& W, const Tensor& labels) {
+  CHECK_DEV(feat);
+  CHECK_F32(feat);
+  CHECK_F32(W);
+  CHECK_CONTIG(feat);
+  CHECK_CONTIG(W);
+  const int B = feat.size(0), D = feat.size(1), C = W.size(1);
+  TORCH_CHECK(W.size(0) == D && C <= 4096, "nested_eval shapes (C <= 4096)");
+  auto counts = at::zeros({D, 2}, feat.options().dtype(at::kInt));
+  dcp::launch_nested_eval(feat.data_ptr<float>(), W.data_ptr<float>(), labels.data_ptr<int64_t>(), B, D, C,
+                          counts.data_ptr<int>(), cur_stream());
+  return counts;
+}
+
+Tensor dwconv_fwd(const Tensor& x, const Tensor& filt, int64_t k, int64_t s, int64_t p, bool reflect) {
+  CHECK_ACT(x);
+  CHECK_F32(filt);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  dcp::launch_dwconv_fwd(bp(x), filt.data_ptr<float>(), bpm(y), N, H, W, C, Ho, Wo, k, s, p, reflect, cur_stream());
+  return y;
+}
+
+Tensor dwconv_bwd(const Tensor& dy, const Tensor& filt, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p,
+                  bool reflect) {
+  CHECK_ACT(dy);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dcp::launch_dwconv_bwd(bp(dy), filt.data_ptr<float>(), bpm(dx), N, H, W, C, Ho, Wo, k, s, p, reflect,
+                         cur_stream());
+  return dx;
+}
+
+Tensor chan_scale_fwd(const Tensor& x, const Tensor& g) {
+  CHECK_ACT(x);
+  CHECK_ACT(g);
+  const int N = x.size(0), C = x.size(-1);
+  auto y = at::empty_like(x);
+  dcp::launch_chan_scale_fwd(bp(x), bp(g), bpm(y), N, x.numel() / (N * C), C, cur_stream());
+  return y;
+}
+
+std::tuple<Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor& x, const Tensor& g) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  CHECK_ACT(g);
+  const int N = x.size(0), C = x.size(-1);
+  auto dx = at::empty_like(x);
+  auto dg = at::empty({N, C}, f32_like(x));
+  dcp::launch_chan_scale_bwd(bp(dy), bp(x), bp(g), bpm(dx), dg.data_ptr<float>(), N, x.numel() / (N * C), C,
+                             cur_stream());
+  return {dx, dg};
+}
+
+// ---------------------------------------------------------------------------
+// losses
+// ---------------------------------------------------------------------------
+std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, int64_t C, double smoothing) {
+  CHECK_DEV(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits rows must be contiguous");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda(), "labels int64 on GPU");
+  const int B = logits.size(0), ld = logits.stride(0);
+  TORCH_CHECK(C <= ld && labels.numel() == B, "xent shapes");
+  auto loss = at::empty({B}, f32_like(logits));
+  auto rank = at::empty({B}, logits.options().dtype(at::kInt));
+  dcp::launch_xent_fwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B, ld, C,
+                       labels.data_ptr<int64_t>(), loss.data_ptr<float>(), rank.data_ptr<int>(), (float)smoothing,
+                       cur_stream());
+  return {loss, rank};
+}
+
+// logits may be a column slice of a wider (padded) buffer: row stride = stride(0)
+Tensor xent_bwd(const Tensor& logits, const Tensor& labels, int64_t C, const Tensor& grad_out, double scale,
+                double smoothing, bool out_bf16) {
+  CHECK_DEV(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits rows must be contiguous");
+  const int B = logits.size(0), ld = logits.stride(0), ldo = logits.size(1);
+  auto d = at::empty({B, ldo}, logits.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  auto g = grad_out.to(at::kFloat).contiguous();
+  dcp::launch_xent_bwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B, ld, C,
+                       labels.data_ptr<int64_t>(), g.data_ptr<float>(), (float)scale, (float)smoothing, d.data_ptr(),
+                       ldo, out_bf16, cur_stream());
+  return d;
+}
+
+Tensor log_softmax_fwd(const Tensor& x, int64_t C) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "rows must be contiguous");
+  const int B = x.size(0), ld = x.stride(0);
+  auto y = at::empty({B, C}, f32_like(x));
+  dcp::launch_log_softmax_fwd(x.data_ptr(), x.scalar_type() == at::kBFloat16, B, ld, C, y.data_ptr<float>(),
+                              cur_stream());
+  return y;
+}
+
+Tensor log_softmax_bwd(const Tensor& y, const Tensor& dy, int64_t ldo, bool out_bf16) {
+  CHECK_DEV(y);
+  const int B = y.size(0), C = y.size(1);
+  auto dyc = dy.to(at::kFloat).contiguous();
+  auto dx = at::empty({B, ldo}, y.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  dcp::launch_log_softmax_bwd(y.data_ptr<float>(), dyc.data_ptr<float>(), B, C, ldo, dx.data_ptr(), out_bf16,
+                              cur_stream());
+  return dx;
+}
+
+std::tuple<Tensor, Tensor> l2norm_rows(const Tensor& x, int64_t ldo, double eps) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  const int R = x.size(0), D = x.size(1);
+  auto y = at::empty({R, ldo}, x.options().dtype(at::kBFloat16));
+  auto inv = at::empty({R}, f32_like(x));
+  dcp::launch_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, R, D, ldo, bpm(y), inv.data_ptr<float>(),
+                          (float)eps, cur_stream());
+  return {y, inv};
+}
+
+Tensor l2norm_bwd(const Tensor& dy, const Tensor& y, const Tensor& inv, int64_t D, bool out_bf16) {
+  CHECK_DEV(dy);
+  CHECK_CONTIG(dy);
+  CHECK_ACT(y);
+  const int R = dy.size(0);
+  auto dx = at::empty({R, D}, dy.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  dcp::launch_l2norm_bwd(dy.data_ptr(), dy.scalar_type() == at::kBFloat16, dy.size(1), bp(y), y.size(1),
+                         inv.data_ptr<float>(), R, D, dx.data_ptr(), out_bf16, cur_stream());
+  return dx;
+}
+
+Tensor transpose2d(const Tensor& x) {
+  CHECK_ACT(x);
+  TORCH_CHECK(x.dim() == 2, "transpose2d expects a matrix");
+  auto y = at::empty({x.size(1), x.size(0)}, x.options());
+  dcp::launch_transpose2d(bp(x), bpm(y), x.size(0), x.size(1), cur_stream());
+  return y;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> arcface_fwd(const Tensor& cosv, const Tensor& labels, int64_t C, double s,
+                                                       double m, bool easy, bool want_logits) {
+  CHECK_ACT(cosv);
+  const int B = cosv.size(0), ld = cosv.size(1);
+  const float cm = cosf((float)m), sm = sinf((float)m), th = cosf(3.14159265358979f - (float)m);
+  const float mm = sinf(3.14159265358979f - (float)m) * (float)m;
+  auto logits = want_logits ? at::empty({B, C}, f32_like(cosv)) : at::empty({0}, f32_like(cosv));
+  auto loss = at::empty({B}, f32_like(cosv));
+  auto rank = at::empty({B}, cosv.options().dtype(at::kInt));
+  auto dphi = at::empty({B}, f32_like(cosv));
+  dcp::launch_arcface_fwd(bp(cosv), B, ld, C, labels.data_ptr<int64_t>(), (float)s, cm, sm, th, mm, easy,
+                          want_logits ? logits.data_ptr<float>() : nullptr, loss.data_ptr<float>(),
+                          rank.data_ptr<int>(), dphi.data_ptr<float>(), cur_stream());
+  return {loss, rank, dphi, logits};
+}
+
+Tensor arcface_bwd(const Tensor& cosv, const Tensor& labels, int64_t C, double s, double m, bool easy,
+                   const Tensor& dphi, const Tensor& grad_out, double scale) {
+  CHECK_ACT(cosv);
+  const int B = cosv.size(0), ld = cosv.size(1);
+  const float cm = cosf((float)m), sm = sinf((float)m), th = cosf(3.14159265358979f - (float)m);
+  const float mm = sinf(3.14159265358979f - (float)m) * (float)m;
+  auto g = grad_out.to(at::kFloat).contiguous();
+  auto dcos = at::empty({B, ld}, cosv.options());
+  dcp::launch_arcface_bwd(bp(cosv), B, ld, C, labels.data_ptr<int64_t>(), (float)s, cm, sm, th, mm, easy,
+                          dphi.data_ptr<float>(), g.data_ptr<float>(), (float)scale, bpm(dcos), cur_stream());
+  return dcos;
+}
+
+// ---------------------------------------------------------------------------
+// optimizers (multi-tensor). table: int64 [n,6] = (p, g, s1, s2, shadow, numel); chunks int32 [k,2]
+// ---------------------------------------------------------------------------
+void mt_sgd(const Tensor& table, const Tensor& chunks, double lr, double momentum, double dampening, double wd,
+            bool nesterov, bool first, double grad_scale) {
+  CHECK_DEV(table);
+  CHECK_DEV(chunks);
+  dcp::SgdHyper h{(float)lr, (float)momentum, (float)dampening, (float)wd, (float)grad_scale, nesterov ? 1 : 0,
+                  first ? 1 : 0};
+  dcp::launch_mt_sgd(reinterpret_cast<const dcp::MTEntry*>(table.data_ptr()),
+                     reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0), h, cur_stream());
+}
+
+void mt_adam(const Tensor& table, const Tensor& chunks, double lr, double beta1, double beta2, double eps, double wd,
+             int64_t step, bool decoupled, double grad_scale) {
+  CHECK_DEV(table);
+  CHECK_DEV(chunks);
+  dcp::AdamHyper h;
+  h.lr = lr;
+  h.beta1 = beta1;
+  h.beta2 = beta2;
+  h.eps = eps;
+  h.wd = wd;
+  h.grad_scale = grad_scale;
+  h.bc1 = 1.0 - std::pow(beta1, (double)step);
+  h.bc2 = 1.0 - std::pow(beta2, (double)step);
+  h.decoupled = decoupled ? 1 : 0;
+  dcp::launch_mt_adam(reinterpret_cast<const dcp::MTEntry*>(table.data_ptr()),
+                      reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0), h, cur_stream());
+}
+
+// state int32 [4] = (prefix, mask, k, thr_bits) prepared by the caller; returns the threshold (fp32 GPU scalar)
+Tensor cdr_threshold(const Tensor& table, const Tensor& chunks, const Tensor& state) {
+  CHECK_DEV(state);
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() == 4, "cdr state int32[4]");
+  auto hist = at::zeros({256}, state.options());
+  dcp::launch_cdr_threshold(reinterpret_cast<const dcp::MTEntry*>(table.data_ptr()),
+                            reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0),
+                            reinterpret_cast<uint32_t*>(state.data_ptr()), reinterpret_cast<uint32_t*>(hist.data_ptr()),
+                            cur_stream());
+  return state.narrow(0, 3, 1).view(at::kFloat);
+}
+
+void cdr_mask(const Tensor& table, const Tensor& chunks, const Tensor& state, double clip) {
+  dcp::launch_cdr_mask(reinterpret_cast<const dcp::MTEntry*>(table.data_ptr()),
+                       reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0),
+                       reinterpret_cast<const uint32_t*>(state.data_ptr()), (float)clip, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dcp, m) {
+  m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
+  m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad) -> Tensor", &conv_dgrad);
+  m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
+  m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, bool relu) -> Tensor", &linear_fwd);
+  m.def("linear_wgrad(Tensor dy, Tensor x) -> Tensor", &linear_wgrad);
+  m.def("weight_prep(Tensor w, int co_pad, bool transposed) -> (Tensor, Tensor)", &weight_prep);
+  m.def("grouped_conv_fwd(Tensor x, Tensor w, int groups, int stride, int pad) -> Tensor", &grouped_conv_fwd);
+  m.def("grouped_conv_dgrad(Tensor dy, Tensor w, int H, int W, int groups, int stride, int pad) -> Tensor",
+        &grouped_conv_dgrad);
+  m.def("grouped_conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int groups, int stride, int pad) -> Tensor",
+        &grouped_conv_wgrad);
+  m.def("bn_stats(Tensor x, Tensor? slabs) -> Tensor", &bn_stats);
+  m.def("colsum(Tensor x) -> Tensor", &colsum);
+  m.def(
+      "bn_finalize(Tensor tot, float count, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, "
+      "float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      &bn_finalize);
+  m.def(
+      "bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor run_mean, Tensor run_var, float eps) -> (Tensor, Tensor, "
+      "Tensor, Tensor)",
+      &bn_eval_coeff);
+  m.def("bn_act(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> Tensor", &bn_act);
+  m.def(
+      "bn_bwd_reduce(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, int "
+      "act, float slope) -> Tensor",
+      &bn_bwd_reduce);
+  m.def(
+      "bn_bwd_elemt(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, "
+      "Tensor? sums, float count, int act, float slope, bool want_dres) -> (Tensor, Tensor)",
+      &bn_bwd_elemt);
+  m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)", &maxpool_fwd);
+  m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int p) -> Tensor", &maxpool_bwd);
+  m.def("gap_fwd(Tensor x) -> Tensor", &gap_fwd);
+  m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &gap_bwd);
+  m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
+  m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
+  m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &relu_bwd);
+  m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);
+  m.def("nested_eval(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval);
+  m.def("dwconv_fwd(Tensor x, Tensor filt, int k, int s, int p, bool reflect) -> Tensor", &dwconv_fwd);
+  m.def("dwconv_bwd(Tensor dy, Tensor filt, int H, int W, int k, int s, int p, bool reflect) -> Tensor", &dwconv_bwd);
+  m.def("chan_scale_fwd(Tensor x, Tensor g) -> Tensor", &chan_scale_fwd);
+  m.def("chan_scale_bwd(Tensor dy, Tensor x, Tensor g) -> (Tensor, Tensor)", &chan_scale_bwd);
+  m.def("xent_fwd(Tensor logits, Tensor labels, int C, float smoothing) -> (Tensor, Tensor)", &xent_fwd);
+  m.def(
+      "xent_bwd(Tensor logits, Tensor labels, int C, Tensor grad_out, float scale, float smoothing, bool out_bf16) "
+      "-> Tensor",
+      &xent_bwd);
+  m.def("log_softmax_fwd(Tensor x, int C) -> Tensor", &log_softmax_fwd);
+  m.def("log_softmax_bwd(Tensor y, Tensor dy, int ldo, bool out_bf16) -> Tensor", &log_softmax_bwd);
+  m.def("l2norm_rows(Tensor x, int ldo, float eps) -> (Tensor, Tensor)", &l2norm_rows);
+  m.def("l2norm_bwd(Tensor dy, Tensor y, Tensor inv, int D, bool out_bf16) -> Tensor", &l2norm_bwd);
+  m.def("transpose2d(Tensor x) -> Tensor", &transpose2d);
+  m.def(
+      "arcface_fwd(Tensor cosv, Tensor labels, int C, float s, float m, bool easy, bool want_logits) -> (Tensor, "
+      "Tensor, Tensor, Tensor)",
+      &arcface_fwd);
+  m.def(
+      "arcface_bwd(Tensor cosv, Tensor labels, int C, float s, float m, bool easy, Tensor dphi, Tensor grad_out, "
+      "float scale) -> Tensor",
+      &arcface_bwd);
+  m.def(
+      "mt_sgd(Tensor table, Tensor chunks, float lr, float momentum, float dampening, float wd, bool nesterov, bool "
+      "first, float grad_scale) -> ()",
+      &mt_sgd);
+  m.def(
+      "mt_adam(Tensor table, Tensor chunks, float lr, float beta1, float beta2, float eps, float wd, int step, bool "
+      "decoupled, float grad_scale) -> ()",
+      &mt_adam);
+  m.def("cdr_threshold(Tensor table, Tensor chunks, Tensor state) -> Tensor", &cdr_threshold);
+  m.def("cdr_mask(Tensor table, Tensor chunks, Tensor state, float clip) -> ()", &cdr_mask);
+}

@@ -1,0 +1,355 @@
+// BatchNorm (training / eval / frozen), fused activation and residual add,
+// NHWC bf16 activations with fp32 statistics.
+//
+// Replaces the ATen BatchNorm / SyncBatchNorm CUDA kernels the reference uses
+// through nn.BatchNorm2d + convert_sync_batchnorm (BASELINE/main.py:148,
+// ARCFACE/arc_main.py:239; SURVEY.md §2.2 X5, kernels K4-K7) and the
+// InplaceABN BN+leaky-ReLU of timm's TResNet (X3, K21).
+//
+// Pipeline per BN layer (training):
+//   conv epilogue  -> per-64-row partial (sum, sumsq) slabs      (conv_igemm.hip)
+//   bn_slab_reduce -> per-channel totals [2][C]    (+ all_reduce for SyncBN)
+//   bn_finalize    -> mean, invstd, scale, shift; running-stat update
+//   bn_act_fwd     -> y = act(x*scale + shift [+ residual])
+// backward:
+//   bn_bwd_reduce  -> sum(dz), sum(dz*xhat)         (+ all_reduce for SyncBN)
+//   bn_bwd_elemt   -> dx (and d(residual) = dz)
+// The activation mask is recomputed from x (and the residual) instead of
+// saving the post-activation tensor.
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2 };
+
+__device__ __forceinline__ float act_f(float z, int act, float slope) {
+  if (act == ACT_RELU) return fmaxf(z, 0.f);
+  if (act == ACT_LEAKY) return z >= 0.f ? z : z * slope;
+  return z;
+}
+__device__ __forceinline__ float act_d(float z, int act, float slope) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_LEAKY) return z >= 0.f ? 1.f : slope;
+  return 1.f;
+}
+
+// slabs [R][2][C] -> out [2][C] (atomic accumulate; out zeroed by caller)
+__global__ void bn_slab_reduce_kernel(const float* __restrict__ slabs, int R, int C,
+                                      int rows_per_block, float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;  // 4 waves
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    for (int r = r0 + w; r < r1; r += 4) {
+      s1 += slabs[((size_t)r * 2 + 0) * C + c];
+      s2 += slabs[((size_t)r * 2 + 1) * C + c];
+    }
+  }
+  __shared__ float red[2][4][64];
+  red[0][w][threadIdx.x & 63] = s1;
+  red[1][w][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    const float t1 = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+    const float t2 = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
+    atomicAdd(out + c, t1);
+    atomicAdd(out + C + c, t2);
+  }
+}
+
+// Generic per-channel (sum, sumsq) of a [M][C] bf16 tensor -> out[2][C] (atomic).
+// Used where the producer is not one of our conv kernels (pool outputs,
+// grouped convs, heads).
+template <bool SQ>
+__global__ void __launch_bounds__(256) chan_stats_kernel(const bf16* __restrict__ x, int M, int C,
+                                                         float* __restrict__ out) {
+  // blockIdx.y selects a window of <= 2048 channels so any C (multiple of 8) works
+  const int cbase = blockIdx.y * 2048;
+  const int Cw = min(2048, C - cbase);
+  const int cpr = Cw >> 3;                // 8-channel chunks per row in this window
+  const int rpi = 256 / cpr;              // rows per iteration
+  const int slot = threadIdx.x / cpr;
+  const int ch = threadIdx.x - slot * cpr;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+  if (slot < rpi) {
+    for (int m = blockIdx.x * rpi + slot; m < M; m += gridDim.x * rpi) {
+      const bf16x8 v = *(const bf16x8*)(x + (size_t)m * C + cbase + ch * 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float f = bf2f(v[k]);
+        s1[k] += f;
+        if (SQ) s2[k] += f * f;
+      }
+    }
+  }
+  extern __shared__ float sh[];  // [256][8] x 2
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sh[threadIdx.x * 8 + k] = s1[k];
+    sh[2048 + threadIdx.x * 8 + k] = s2[k];
+  }
+  __syncthreads();
+  if (slot == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int s = 0; s < rpi; ++s) {
+        t1 += sh[(s * cpr + ch) * 8 + k];
+        t2 += sh[2048 + (s * cpr + ch) * 8 + k];
+      }
+      atomicAdd(out + cbase + ch * 8 + k, t1);
+      if (SQ) atomicAdd(out + C + cbase + ch * 8 + k, t2);
+    }
+  }
+}
+
+// totals [2][C], count -> mean, invstd, scale, shift (+ running stats update)
+__global__ void bn_finalize_kernel(const float* __restrict__ tot, double count, int C, float eps,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ mean, float* __restrict__ invstd,
+                                   float* __restrict__ scale, float* __restrict__ shift,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                                   float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mu = (double)tot[c] / count;
+  double var = (double)tot[C + c] / count - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - (float)mu * g * is;
+  if (run_mean) {
+    const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+}
+
+// eval / frozen BN: scale = gamma / sqrt(var + eps), shift = beta - mean*scale
+__global__ void bn_eval_coeff_kernel(int C, float eps, const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, const float* __restrict__ rm,
+                                     const float* __restrict__ rv, float* __restrict__ mean,
+                                     float* __restrict__ invstd, float* __restrict__ scale,
+                                     float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = rsqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  mean[c] = rm[c];
+  invstd[c] = is;
+  scale[c] = g * is;
+  shift[c] = b - rm[c] * g * is;
+}
+
+// y = act(x*scale + shift [+ res]); 8 channels per thread, grid-stride
+__global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, bf16* __restrict__ y,
+                                                         size_t nchunks, int C, int act, float slope) {
+  const int cpr = C >> 3;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    const bf16x8 v = *(const bf16x8*)(x + i * 8);
+    bf16x8 r;
+    if (res) r = *(const bf16x8*)(res + i * 8);
+    const f32x4 sc0 = *(const f32x4*)(scale + c0), sc1 = *(const f32x4*)(scale + c0 + 4);
+    const f32x4 sh0 = *(const f32x4*)(shift + c0), sh1 = *(const f32x4*)(shift + c0 + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float sc = k < 4 ? sc0[k] : sc1[k - 4];
+      const float sh = k < 4 ? sh0[k] : sh1[k - 4];
+      float z = bf2f(v[k]) * sc + sh;
+      if (res) z += bf2f(r[k]);
+      o[k] = f2bf(act_f(z, act, slope));
+    }
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+// sums over rows of dz = dy*act'(z) and dz*xhat  -> out[2][C] (atomic, zeroed by caller)
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ res,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, int M, int C,
+                                                            int act, float slope, float* __restrict__ out) {
+  const int cpr = C >> 3;
+  const int rpi = 256 / cpr;
+  const int slot = threadIdx.x / cpr;
+  const int ch = threadIdx.x - slot * cpr;
+  const int c0 = ch * 8;
+  float s1[8], s2[8], sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = 0.f;
+    sc[k] = scale[c0 + k];
+    sh[k] = shift[c0 + k];
+    mu[k] = mean[c0 + k];
+    is[k] = invstd[c0 + k];
+  }
+  if (slot < rpi) {
+    for (int m = blockIdx.x * rpi + slot; m < M; m += gridDim.x * rpi) {
+      const size_t off = (size_t)m * C + c0;
+      const bf16x8 g = *(const bf16x8*)(dy + off);
+      const bf16x8 v = *(const bf16x8*)(x + off);
+      bf16x8 r;
+      if (res) r = *(const bf16x8*)(res + off);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xv = bf2f(v[k]);
+        float z = xv * sc[k] + sh[k];
+        if (res) z += bf2f(r[k]);
+        const float dz = bf2f(g[k]) * act_d(z, act, slope);
+        s1[k] += dz;
+        s2[k] += dz * (xv - mu[k]) * is[k];
+      }
+    }
+  }
+  extern __shared__ float sh_red[];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sh_red[threadIdx.x * 8 + k] = s1[k];
+    sh_red[2048 + threadIdx.x * 8 + k] = s2[k];
+  }
+  __syncthreads();
+  if (slot == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int s = 0; s < rpi; ++s) {
+        t1 += sh_red[(s * cpr + ch) * 8 + k];
+        t2 += sh_red[2048 + (s * cpr + ch) * 8 + k];
+      }
+      atomicAdd(out + c0 + k, t1);
+      atomicAdd(out + C + c0 + k, t2);
+    }
+  }
+}
+
+// dx = scale*(dz - sum_dz/count - xhat*sum_dzxhat/count)  [stats=true]
+// dx = scale*dz                                            [stats=false: eval/frozen BN]
+// dres = dz (if dres != nullptr)
+__global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ res,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ sums, float inv_count,
+                                                           size_t nchunks, int C, int act, float slope,
+                                                           bf16* __restrict__ dx, bf16* __restrict__ dres) {
+  const int cpr = C >> 3;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cpr) * 8;
+    const bf16x8 g = *(const bf16x8*)(dy + i * 8);
+    const bf16x8 v = *(const bf16x8*)(x + i * 8);
+    bf16x8 r;
+    if (res) r = *(const bf16x8*)(res + i * 8);
+    bf16x8 o, od;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float xv = bf2f(v[k]);
+      const float sc = scale[c];
+      float z = xv * sc + shift[c];
+      if (res) z += bf2f(r[k]);
+      const float dz = bf2f(g[k]) * act_d(z, act, slope);
+      od[k] = f2bf(dz);
+      float d;
+      if (sums) {
+        const float xh = (xv - mean[c]) * invstd[c];
+        d = sc * (dz - sums[c] * inv_count - xh * sums[C + c] * inv_count);
+      } else {
+        d = sc * dz;
+      }
+      o[k] = f2bf(d);
+    }
+    *(bf16x8*)(dx + i * 8) = o;
+    if (dres) *(bf16x8*)(dres + i * 8) = od;
+  }
+}
+
+// ---------------------------------------------------------------------------
+static inline int ew_grid(size_t n, int block = 256) {
+  size_t g = (n + block - 1) / block;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void launch_bn_slab_reduce(const float* slabs, int R, int C, float* out, hipStream_t s) {
+  int splits = (R + 255) / 256;
+  if (splits > 128) splits = 128;
+  if (splits < 1) splits = 1;
+  const int rpb = (R + splits - 1) / splits;
+  hipLaunchKernelGGL(bn_slab_reduce_kernel, dim3((C + 63) / 64, splits), dim3(256), 0, s, slabs, R, C, rpb, out);
+}
+
+void launch_chan_stats(const bf16* x, int M, int C, bool sq, float* out, hipStream_t s) {
+  const int cpr = (C < 2048 ? C : 2048) / 8;
+  const int rpi = 256 / cpr;
+  const int ny = (C + 2047) / 2048;
+  int grid = (M + rpi * 8 - 1) / (rpi * 8);
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  if (sq)
+    hipLaunchKernelGGL(chan_stats_kernel<true>, dim3(grid, ny), dim3(256), 2 * 2048 * 4, s, x, M, C, out);
+  else
+    hipLaunchKernelGGL(chan_stats_kernel<false>, dim3(grid, ny), dim3(256), 2 * 2048 * 4, s, x, M, C, out);
+}
+
+void launch_bn_finalize(const float* tot, double count, int C, float eps, const float* gamma, const float* beta,
+                        float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
+                        float momentum, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, tot, count, C, eps, gamma, beta,
+                     mean, invstd, scale, shift, rm, rv, momentum);
+}
+
+void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm,
+                          const float* rv, float* mean, float* invstd, float* scale, float* shift,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, eps, gamma, beta, rm, rv,
+                     mean, invstd, scale, shift);
+}
+
+void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
+                       size_t numel, int C, int act, float slope, hipStream_t s) {
+  const size_t n = numel / 8;
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid(n)), dim3(256), 0, s, x, res, scale, shift, y, n, C, act,
+                     slope);
+}
+
+void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
+                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* out,
+                          hipStream_t s) {
+  const int cpr = C / 8;
+  const int rpi = 256 / cpr;
+  int grid = (M + rpi * 8 - 1) / (rpi * 8);
+  if (grid > 1024) grid = 1024;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid), dim3(256), 2 * 2048 * 4, s, dy, x, res, scale, shift, mean,
+                     invstd, M, C, act, slope, out);
+}
+
+void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s) {
+  const size_t n = numel / 8;
+  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(ew_grid(n)), dim3(256), 0, s, dy, x, res, scale, shift, mean, invstd,
+                     sums, inv_count, n, C, act, slope, dx, dres);
+}
+
+}  // namespace dcp

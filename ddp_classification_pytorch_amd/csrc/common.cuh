@@ -1,0 +1,109 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of this package.
+//
+// Conventions used by every kernel in csrc/:
+//   * activations are NHWC bf16 ("[M][C]" with M = N*H*W rows), weights are
+//     [Co][KH][KW][Ci] (K-contiguous per output channel);
+//   * all accumulation (GEMM, BN statistics, reductions) is fp32;
+//   * a wavefront is 64 lanes; block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+namespace dcp {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+// Integer division by a runtime-constant divisor via a precomputed magic
+// multiplier (round-up method; exact for 0 <= n < 2^31, 1 <= d < 2^31).
+struct FastDiv {
+  uint32_t d;
+  uint32_t mul;
+  uint32_t shr;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) {
+    f.mul = 0;
+    f.shr = 0;
+    return f;
+  }
+  uint32_t l = 0;
+  while ((1u << l) < d) ++l;
+  uint64_t m = ((uint64_t(1) << (32 + l)) + d - 1) / d;  // ceil(2^(32+l)/d)
+  f.mul = (uint32_t)m;  // low 32 bits; the implicit 2^32 term is added back below
+  f.shr = l;
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  if (f.d == 1) return n;
+  uint32_t hi = __umulhi(n, f.mul);
+  // q = (n*m) >> (32+l) where m = 2^32 + mul  ->  (hi + n) >> l (64-bit safe)
+  return (uint32_t)(((uint64_t)hi + n) >> f.shr);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Workgroup-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id: consecutive logical
+// tiles land on the same XCD (blocks are dispatched round-robin over the 8
+// XCDs), so neighbouring output tiles share operand panels in one L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
+  const uint32_t nx = 8;
+  if (nwg < nx) return orig;
+  const uint32_t q = nwg / nx, r = nwg % nx;
+  const uint32_t xcd = orig % nx, idx = orig / nx;
+  const uint32_t base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+}  // namespace dcp

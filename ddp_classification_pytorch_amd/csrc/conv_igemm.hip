@@ -1,0 +1,484 @@
+// MFMA implicit-GEMM convolution for gfx950 (CDNA4), NHWC bf16, fp32 accumulate.
+//
+// Replaces the cuDNN convolutions the reference gets implicitly from
+// torchvision/timm ResNets (kernels K1/K2/K3;
+// reference model code: NESTED/model/imagenet_resnet.py:27,68-73,107,134).
+//
+// One "tap GEMM" kernel covers forward and data-gradient passes:
+//
+//   dst[n, y*ds+oy, x*ds+ox, co] = sum_t sum_c src[n, y*ss+dy_t, x*ss+dx_t, c] * wt[co, widx_t, c]
+//
+//   * forward, stride s, pad p:  ss = s, dy_t = kh - p, ds = 1, widx_t = kh*KW+kw
+//   * dgrad, stride 1:           src = dY, wt = W^T ([Ci][T][Co]), dy_t = p - kh
+//   * dgrad, stride 2:           one launch per output parity class (sub-pixel
+//                                decomposition), ds = 2, only the taps whose
+//                                parity matches; a class with no taps writes 0.
+//
+// GEMM view: rows m = (n, y, x) of the output grid, columns = output
+// channels, K = taps x channels in 8-channel (16-byte) chunks.  Tiles are
+// staged global->LDS with `global_load_lds_dwordx4` (LDS-DMA, no VGPR
+// round trip); out-of-bounds / padding taps point the lane at a zero page so
+// the gather needs no branches.  LDS rows are XOR-swizzled on the source
+// address so the MFMA fragment reads (`ds_read_b128`) are bank-conflict free.
+// The MFMA is v_mfma_f32_16x16x32_bf16 with the weight as the A operand, so
+// each lane ends up owning 4 consecutive output channels of one pixel
+// (8-byte stores) and per-channel BN statistics reduce with 4 shuffles.
+//
+// The weight-gradient kernel computes dW[co][t][c] = sum_m dY[m][co] * im2col(X)[m][t,c]
+// with both operands m-major in memory; its LDS images are [m][...] rows read
+// with the gfx950 transpose read `ds_read_b64_tr_b16`, split-K over m with
+// fp32 atomics into the (zeroed) gradient.
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+struct TapGemmParams {
+  const bf16* src;   // [N][Hs][Ws][Cs]
+  const bf16* wt;    // [Co][T][Cs]
+  bf16* dst;         // [N][Hd][Wd][Co]
+  float* stats;      // [ceil(M/64)][2][Co] partial (sum, sumsq) or nullptr
+  const bf16* zero;  // >= 16 bytes of zeros
+  int Hs, Ws, Cs;
+  int Hy, Wy, ss;
+  int Hd, Wd, ds, oy, ox;
+  int Co, T, M;
+  int ntaps, cpt, nkt, ldw;
+  int relu;          // fused ReLU on the stored output (linear heads)
+  const float* bias; // optional per-output-channel bias (linear heads)
+  FastDiv div_wy, div_hy, div_cpt;
+  int8_t dy[kMaxTaps], dx[kMaxTaps];
+  uint8_t widx[kMaxTaps];
+};
+
+// byte offset of logical 16B chunk `c` of row `r` in a 128-byte-row image
+__device__ __forceinline__ uint32_t swz128(uint32_t r, uint32_t c) {
+  return r * 128u + ((c ^ ((r >> 1) & 7u)) << 4);
+}
+
+template <int BN>
+__global__ void __launch_bounds__(256)
+tap_gemm_kernel(const TapGemmParams p) {
+  constexpr int BM = 128;                 // pixel rows per block
+  constexpr int A_BYTES = BM * 128;       // 64 k (bf16) per row
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int TN = BN / 32;             // 16-wide co subtiles per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const uint32_t ntn = (p.Co + BN - 1) / BN;
+  const uint32_t ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A-load rows (4 glds per k-tile) ----
+  uint32_t a_pix[4];   // n*Hs*Ws
+  int a_ys[4], a_xs[4];
+  uint32_t a_chunk[4];
+  bool a_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (wave * 4 + i) * 8 + (lane >> 3);
+    const int m = m0 + r;
+    a_ok[i] = m < p.M;
+    const uint32_t mm = a_ok[i] ? m : 0;
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const uint32_t x = mm - q * p.Wy;
+    const uint32_t n = fdiv(q, p.div_hy);
+    const uint32_t y = q - n * p.Hy;
+    a_pix[i] = n * (uint32_t)(p.Hs * p.Ws);
+    a_ys[i] = y * p.ss;
+    a_xs[i] = x * p.ss;
+    a_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+  }
+  // ---- per-thread B-load rows ----
+  constexpr int BI = BN / 32;  // glds per thread for B
+  uint32_t b_row[BI];
+  uint32_t b_chunk[BI];
+  bool b_ok[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int r = (wave * BI + i) * 8 + (lane >> 3);
+    b_ok[i] = (n0 + r) < p.Co;
+    b_row[i] = (uint32_t)(n0 + r) * p.ldw;
+    b_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+  }
+
+  const bool fast = (p.cpt & 7) == 0;  // Cs % 64 == 0: one tap per k-tile
+  const int tiles_per_tap = p.cpt >> 3;
+  const int kc_total = p.ntaps * p.cpt;
+
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+    if (fast) {
+      const int t = kt / tiles_per_tap;
+      const int cbase = (kt - t * tiles_per_tap) * 64;
+      const int dy = p.dy[t], dx = p.dx[t];
+      const uint32_t wofs = (uint32_t)p.widx[t] * p.Cs + cbase;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
+        const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+        const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8
+                           : p.zero;
+        __builtin_amdgcn_global_load_lds((const void*)g,
+                                         LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const bf16* g = b_ok[i] ? p.wt + b_row[i] + wofs + b_chunk[i] * 8 : p.zero;
+        __builtin_amdgcn_global_load_lds((const void*)g,
+                                         LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kc = kt * 8 + a_chunk[i];
+        const int t = fdiv(kc, p.div_cpt);
+        const int ci0 = (kc - t * p.cpt) * 8;
+        bool ok = a_ok[i] && kc < kc_total;
+        const int tt = ok ? t : 0;
+        const int hi = a_ys[i] + p.dy[tt], wi = a_xs[i] + p.dx[tt];
+        ok = ok && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+        const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + ci0 : p.zero;
+        __builtin_amdgcn_global_load_lds((const void*)g,
+                                         LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int kc = kt * 8 + b_chunk[i];
+        const int t = fdiv(kc, p.div_cpt);
+        const int ci0 = (kc - t * p.cpt) * 8;
+        const bool ok = b_ok[i] && kc < kc_total;
+        const bf16* g = ok ? p.wt + b_row[i] + (uint32_t)p.widx[ok ? t : 0] * p.Cs + ci0 : p.zero;
+        __builtin_amdgcn_global_load_lds((const void*)g,
+                                         LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = p.nkt;
+  if (nkt > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t c = s * 4 + (lane >> 4);
+      bf16x8 wf[TN], af[4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t r = wn * (BN / 2) + j * 16 + (lane & 15);
+        wf[j] = *(const bf16x8*)(Bs + swz128(r, c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t r = wm * 64 + i * 16 + (lane & 15);
+        af[i] = *(const bf16x8*)(As + swz128(r, c));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias/ReLU, bf16 store (8 B per lane), BN partial stats ----
+  const int co_lane = n0 + wn * (BN / 2) + (lane >> 4) * 4;
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    const bool mok = m < p.M;
+    uint32_t drow = 0;
+    if (mok) {
+      const uint32_t q = fdiv(m, p.div_wy);
+      const uint32_t x = m - q * p.Wy;
+      const uint32_t n = fdiv(q, p.div_hy);
+      const uint32_t y = q - n * p.Hy;
+      drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = co_lane + j * 16;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = acc[j][i][r];
+        if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
+        if (p.relu) t = fmaxf(t, 0.f);
+        v[r] = t;
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+      if (mok && co < p.Co) *(bf16x4*)(p.dst + drow + co) = o;
+      if (p.stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float q = mok ? bf2f(o[r]) : 0.f;
+          s1[j][r] += q;
+          s2[j][r] += q * q;
+        }
+      }
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+          s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+        }
+      }
+    const int rb = m0 / 64 + wm;
+    if ((lane & 15) == 0 && (m0 + wm * 64) < p.M) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co_lane + j * 16;
+        if (co < p.Co) {
+          *(f32x4*)(p.stats + ((size_t)rb * 2 + 0) * p.Co + co) = f32x4{s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
+          *(f32x4*)(p.stats + ((size_t)rb * 2 + 1) * p.Co + co) = f32x4{s2[j][0], s2[j][1], s2[j][2], s2[j][3]};
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------
+struct WgradParams {
+  const bf16* dy;    // [M][Co]
+  const bf16* src;   // [N][Hs][Ws][Cs]
+  float* dw;         // [Co][T*Cs] fp32, accumulated
+  const bf16* zero;
+  int Hs, Ws, Cs, Ho, Wo, ss;
+  int Co, M, ldw;    // ldw = T*Cs
+  int cpt, kc_total, rows_per_split;
+  FastDiv div_wo, div_ho, div_cpt;
+  int8_t dy_t[kMaxTaps], dx_t[kMaxTaps];
+};
+
+// byte offset of logical 16B chunk c of row r in a 256-byte-row image read
+// with ds_read_b64_tr_b16 (4-row blocks per 16-lane group)
+__device__ __forceinline__ uint32_t swz256(uint32_t r, uint32_t c) {
+  return r * 256u + ((c ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3))) << 4);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, uint32_t row0, uint32_t col0, int lane) {
+  // rows row0 .. row0+7 (two 4-row transposed blocks), columns col0 .. col0+15
+  const uint32_t q = (lane & 15) >> 2, pp = lane & 3;
+  const uint32_t col = col0 + pp * 4;
+  const uint32_t r1 = row0 + q, r2 = row0 + 4 + q;
+  const uint32_t o1 = swz256(r1, col >> 3) + (col & 7) * 2;
+  const uint32_t o2 = swz256(r2, col >> 3) + (col & 7) * 2;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o1));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o2));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ void __launch_bounds__(256)
+wgrad_kernel(const WgradParams p) {
+  constexpr int BK = 64;          // m rows per k-tile
+  constexpr int IMG = BK * 256;   // 64 rows x 128 bf16
+  constexpr int STAGE = 2 * IMG;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntm = (p.Co + 127) / 128;
+  const int ntn = (p.ldw + 127) / 128;
+  const uint32_t tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tn = tile % ntn, tmi = tile / ntn;
+  const int co0 = tmi * 128, kcol0 = tn * 128;
+  const int mstart = blockIdx.y * p.rows_per_split;
+  const int mend = min(p.M, mstart + p.rows_per_split);
+  const int nkt = (mend - mstart + BK - 1) / BK;
+
+  // per-thread load slots: 4 per image; wave instruction i covers rows (wave*4+i)*4 .. +3
+  uint32_t a_col[4];
+  bool a_cok[4];
+  int b_dy[4], b_dx[4];
+  uint32_t b_ci[4];
+  bool b_cok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t r = (wave * 4 + i) * 4 + (lane >> 4);
+    const uint32_t c = (lane & 15) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
+    a_col[i] = co0 + c * 8;
+    a_cok[i] = (int)a_col[i] < p.Co;
+    const int kc = kcol0 / 8 + c;
+    b_cok[i] = kc < p.kc_total;
+    const int t = b_cok[i] ? (int)fdiv(kc, p.div_cpt) : 0;
+    b_ci[i] = (kc - t * p.cpt) * 8;
+    b_dy[i] = p.dy_t[t];
+    b_dx[i] = p.dx_t[t];
+  }
+
+  auto stage = [&](int kt, int buf) {
+    char* Ai = smem + buf * STAGE;
+    char* Bi = Ai + IMG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (wave * 4 + i) * 4 + (lane >> 4);
+      const int m = mstart + kt * BK + r;
+      const bool mok = m < mend;
+      const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 4 + i) * 1024), 16, 0, 0);
+      const uint32_t mm = mok ? m : 0;
+      const uint32_t q = fdiv(mm, p.div_wo);
+      const uint32_t x = mm - q * p.Wo;
+      const uint32_t n = fdiv(q, p.div_ho);
+      const uint32_t y = q - n * p.Ho;
+      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const char* Ai = smem + buf * STAGE;
+    const char* Bi = Ai + IMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t row0 = s * 32 + 8 * (lane >> 4);
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag(Ai, row0, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bi, row0, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nkt == 0) return;
+
+  // D[co][kcol]: lane holds rows (lane>>4)*4+r, column lane&15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kcol = kcol0 + wn * 64 + j * 16 + (lane & 15);
+      if (kcol >= p.ldw) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < p.Co) unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
+                     const bf16* wt, int Co, int T,
+                     bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
+                     const TapList& taps, float* stats, const float* bias, int relu,
+                     const bf16* zero, hipStream_t stream) {
+  TapGemmParams p;
+  p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero;
+  p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
+  p.Hy = Hy; p.Wy = Wy; p.ss = ss;
+  p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;
+  p.Co = Co; p.T = T; p.M = N * Hy * Wy;
+  p.ntaps = taps.n; p.cpt = Cs / 8; p.ldw = T * Cs;
+  p.nkt = (taps.n * p.cpt + 7) / 8;
+  p.relu = relu; p.bias = bias;
+  p.div_wy = make_fastdiv(Wy); p.div_hy = make_fastdiv(Hy); p.div_cpt = make_fastdiv(p.cpt);
+  for (int i = 0; i < taps.n; ++i) {
+    p.dy[i] = (int8_t)taps.dy[i];
+    p.dx[i] = (int8_t)taps.dx[i];
+    p.widx[i] = (uint8_t)taps.widx[i];
+  }
+  if (p.M == 0) return;
+  const int ntm = (p.M + 127) / 128;
+  if (Co <= 64) {
+    const int ntn = (Co + 63) / 64;
+    hipLaunchKernelGGL(tap_gemm_kernel<64>, dim3(ntm * ntn), dim3(256), 2 * (128 + 64) * 128, stream, p);
+  } else {
+    const int ntn = (Co + 127) / 128;
+    hipLaunchKernelGGL(tap_gemm_kernel<128>, dim3(ntm * ntn), dim3(256), 2 * (128 + 128) * 128, stream, p);
+  }
+}
+
+void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
+                  const bf16* src, int Hs, int Ws, int Cs, int ss,
+                  const TapList& taps, float* dw, const bf16* zero, int num_cu, hipStream_t stream) {
+  WgradParams p;
+  p.dy = dy; p.src = src; p.dw = dw; p.zero = zero;
+  p.Hs = Hs; p.Ws = Ws; p.Cs = Cs; p.Ho = Ho; p.Wo = Wo; p.ss = ss;
+  p.Co = Co; p.M = N * Ho * Wo; p.ldw = taps.n * Cs;
+  p.cpt = Cs / 8; p.kc_total = taps.n * p.cpt;
+  p.div_wo = make_fastdiv(Wo); p.div_ho = make_fastdiv(Ho); p.div_cpt = make_fastdiv(p.cpt);
+  for (int i = 0; i < taps.n; ++i) {
+    p.dy_t[i] = (int8_t)taps.dy[i];
+    p.dx_t[i] = (int8_t)taps.dx[i];
+  }
+  const int ntm = (Co + 127) / 128, ntn = (p.ldw + 127) / 128;
+  const int tiles = ntm * ntn;
+  // split-K over m: aim for ~4 waves of blocks over the chip, >= 256 rows per split
+  const int target = 4 * num_cu;
+  int splits = (target + tiles - 1) / tiles;
+  int max_splits = (p.M + 255) / 256;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int rps = (p.M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  splits = (p.M + rps - 1) / rps;
+  p.rows_per_split = rps;
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, splits), dim3(256), 4 * 64 * 256, stream, p);
+}
+
+}  // namespace dcp

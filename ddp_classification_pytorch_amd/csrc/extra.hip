@@ -1,0 +1,333 @@
+// Kernels for the non-ResNet model families:
+//   * grouped convolution (ResNeXt-50 32x4d, BASELINE.json config 4; SURVEY.md
+//     §2.5 K26): direct NHWC kernels with 8 output channels per thread; the
+//     per-group widths (4..32 channels) are far below one MFMA tile, so the
+//     work is spread over threads instead and stays memory-bound;
+//   * depthwise k x k filter with reflect padding (TResNet anti-aliased
+//     downsampling "blur pool", timm tresnet);
+//   * per-(sample, channel) scaling for squeeze-and-excitation (K22).
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+// ---------------------------------------------------------------------------
+// grouped conv. w: [Co][KH][KW][Cg] (Cg = C/G input channels per group)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) gconv_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                        bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                                        int Wo, int Co, int G, int KH, int KW, int s, int p) {
+  const int Cg = C / G, Cog = Co / G;
+  const int cpo = Co >> 3;  // 8 output channels per thread (Cog % 8 == 0 or Cog >= 8 multiple)
+  const size_t total = (size_t)N * Ho * Wo * cpo;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int oc = (int)(i % cpo) * 8;
+    size_t pix = i / cpo;
+    const int wo = (int)(pix % Wo);
+    pix /= Wo;
+    const int ho = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int hi = ho * s - p + kh;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int wi = wo * s - p + kw;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const bf16* xp = x + (((size_t)n * H + hi) * W + wi) * C;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int co = oc + q;
+          const int g = co / Cog;
+          const bf16* wp = w + (((size_t)co * KH + kh) * KW + kw) * Cg;
+          const bf16* xg = xp + g * Cg;
+          float a = 0.f;
+          for (int c = 0; c < Cg; ++c) a += bf2f(xg[c]) * bf2f(wp[c]);
+          acc[q] += a;
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) gconv_dgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w,
+                                                          bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                          int Wo, int Co, int G, int KH, int KW, int s, int p) {
+  const int Cg = C / G, Cog = Co / G;
+  const int cpi = C >> 3;
+  const size_t total = (size_t)N * H * W * cpi;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int ic = (int)(i % cpi) * 8;
+    size_t pix = i / cpi;
+    const int wi = (int)(pix % W);
+    pix /= W;
+    const int hi = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int th = hi + p - kh;
+      if (th < 0 || th % s) continue;
+      const int ho = th / s;
+      if (ho >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int tw = wi + p - kw;
+        if (tw < 0 || tw % s) continue;
+        const int wo = tw / s;
+        if (wo >= Wo) continue;
+        const bf16* gp = dy + (((size_t)n * Ho + ho) * Wo + wo) * Co;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int ci = ic + q;
+          const int g = ci / Cg, cig = ci - g * Cg;
+          float a = 0.f;
+          for (int j = 0; j < Cog; ++j) {
+            const int co = g * Cog + j;
+            a += bf2f(gp[co]) * bf2f(w[(((size_t)co * KH + kh) * KW + kw) * Cg + cig]);
+          }
+          acc[q] += a;
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+// dW[co][kh][kw][cig]: one thread per weight element, workgroup-split over rows + atomics
+__global__ void __launch_bounds__(256) gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                          float* __restrict__ dw, int N, int H, int W, int C, int Ho,
+                                                          int Wo, int Co, int G, int KH, int KW, int s, int p,
+                                                          int rows_per_split) {
+  const int Cg = C / G, Cog = Co / G;
+  const int nw = Co * KH * KW * Cg;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nw) return;
+  const int cig = e % Cg;
+  int t = e / Cg;
+  const int kw = t % KW;
+  t /= KW;
+  const int kh = t % KH;
+  const int co = t / KH;
+  const int ci = (co / Cog) * Cg + cig;
+  const int M = N * Ho * Wo;
+  const int m0 = blockIdx.y * rows_per_split, m1 = min(M, m0 + rows_per_split);
+  float acc = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    const int wo = m % Wo;
+    const int q = m / Wo;
+    const int ho = q % Ho, n = q / Ho;
+    const int hi = ho * s - p + kh, wi = wo * s - p + kw;
+    if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) continue;
+    acc += bf2f(dy[(size_t)m * Co + co]) * bf2f(x[(((size_t)n * H + hi) * W + wi) * C + ci]);
+  }
+  atomicAdd(dw + e, acc);
+}
+
+// ---------------------------------------------------------------------------
+// depthwise k x k filter shared by all channels (blur pool), stride s, pad p
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int refl(int i, int n) {
+  if (i < 0) i = -i;
+  if (i >= n) i = 2 * n - 2 - i;
+  return i;
+}
+
+__global__ void __launch_bounds__(256) dwconv_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ f,
+                                                         bf16* __restrict__ y, int N, int H, int W, int C, int Ho,
+                                                         int Wo, int k, int s, int p, int reflect) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * Ho * Wo * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cpr);
+    size_t pix = i / cpr;
+    const int wo = (int)(pix % Wo);
+    pix /= Wo;
+    const int ho = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int kh = 0; kh < k; ++kh) {
+      int hi = ho * s - p + kh;
+      if (reflect) hi = refl(hi, H);
+      else if ((unsigned)hi >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        int wi = wo * s - p + kw;
+        if (reflect) wi = refl(wi, W);
+        else if ((unsigned)wi >= (unsigned)W) continue;
+        const float fv = f[kh * k + kw];
+        const bf16x8 v = *(const bf16x8*)(x + (((size_t)n * H + hi) * W + wi) * C + ch * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += fv * bf2f(v[q]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+// backward = scatter of the forward taps; done as a gather over output pixels whose
+// (possibly reflected) tap lands on this input pixel
+__global__ void __launch_bounds__(256) dwconv_bwd_kernel(const bf16* __restrict__ dy, const float* __restrict__ f,
+                                                         bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                                         int Wo, int k, int s, int p, int reflect) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * H * W * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cpr);
+    size_t pix = i / cpr;
+    const int wi = (int)(pix % W);
+    pix /= W;
+    const int hi = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    // candidate output rows: any ho whose window (after reflection) touches hi
+    // (reflection folds taps near an edge back inside; widen the range there)
+    int ho_lo = max(0, (hi + p - k + 1) / s - 1), ho_hi = min(Ho - 1, (hi + p) / s + 1);
+    int wo_lo = max(0, (wi + p - k + 1) / s - 1), wo_hi = min(Wo - 1, (wi + p) / s + 1);
+    if (reflect) {
+      if (hi <= k) ho_lo = 0;
+      if (hi >= H - 1 - k) ho_hi = Ho - 1;
+      if (wi <= k) wo_lo = 0;
+      if (wi >= W - 1 - k) wo_hi = Wo - 1;
+    }
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      for (int kh = 0; kh < k; ++kh) {
+        int h = ho * s - p + kh;
+        if (reflect) h = refl(h, H);
+        if (h != hi) continue;
+        for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+          for (int kw = 0; kw < k; ++kw) {
+            int ww = wo * s - p + kw;
+            if (reflect) ww = refl(ww, W);
+            if (ww != wi) continue;
+            const float fv = f[kh * k + kw];
+            const bf16x8 g = *(const bf16x8*)(dy + (((size_t)n * Ho + ho) * Wo + wo) * C + ch * 8);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] += fv * bf2f(g[q]);
+          }
+        }
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// y[n][hw][c] = x[n][hw][c] * g[n][c]
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) chan_scale_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
+                                                             bf16* __restrict__ y, int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * HW * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cpr);
+    const size_t n = i / cpr / HW;
+    const bf16x8 v = *(const bf16x8*)(x + i * 8);
+    const bf16x8 s = *(const bf16x8*)(g + n * C + ch * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(bf2f(v[q]) * bf2f(s[q]));
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+// dx = dy * g ; dg[n][c] = sum_hw dy*x  (one thread per (n, 8-channel chunk))
+__global__ void __launch_bounds__(256) chan_scale_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                             const bf16* __restrict__ g, bf16* __restrict__ dx,
+                                                             float* __restrict__ dg, int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * cpr) return;
+  const int n = i / cpr, ch = i - n * cpr;
+  const bf16x8 s = *(const bf16x8*)(g + (size_t)n * C + ch * 8);
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  for (int t = 0; t < HW; ++t) {
+    const size_t o = ((size_t)n * HW + t) * C + ch * 8;
+    const bf16x8 gv = *(const bf16x8*)(dy + o);
+    const bf16x8 xv = *(const bf16x8*)(x + o);
+    bf16x8 d;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      acc[q] += bf2f(gv[q]) * bf2f(xv[q]);
+      d[q] = f2bf(bf2f(gv[q]) * bf2f(s[q]));
+    }
+    *(bf16x8*)(dx + o) = d;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dg[(size_t)n * C + ch * 8 + q] = acc[q];
+}
+
+// ---------------------------------------------------------------------------
+static inline int grid_of(size_t n) {
+  size_t g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
+                             int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  const size_t total = (size_t)N * Ho * Wo * (Co / 8);
+  hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, s, x, w, y, N, H, W, C, Ho, Wo, Co, G, KH,
+                     KW, stride, pad);
+}
+void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
+                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  const size_t total = (size_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(gconv_dgrad_kernel, dim3(grid_of(total)), dim3(256), 0, s, dy, w, dx, N, H, W, C, Ho, Wo, Co, G,
+                     KH, KW, stride, pad);
+}
+void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Ho, int Wo,
+                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  const int nw = Co * KH * KW * (C / G);
+  const int M = N * Ho * Wo;
+  int splits = 2048 / ((nw + 255) / 256);
+  if (splits < 1) splits = 1;
+  if (splits > (M + 63) / 64) splits = (M + 63) / 64;
+  const int rps = (M + splits - 1) / splits;
+  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((nw + 255) / 256, splits), dim3(256), 0, s, dy, x, dw, N, H, W, C, Ho,
+                     Wo, Co, G, KH, KW, stride, pad, rps);
+}
+void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
+                       int s, int p, int reflect, hipStream_t st) {
+  const size_t total = (size_t)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(dwconv_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, w, y, N, H, W, C, Ho, Wo, k, s, p,
+                     reflect);
+}
+void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                       int s, int p, int reflect, hipStream_t st) {
+  const size_t total = (size_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(dwconv_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C, Ho, Wo, k, s,
+                     p, reflect);
+}
+void launch_chan_scale_fwd(const bf16* x, const bf16* g, bf16* y, int N, int HW, int C, hipStream_t st) {
+  const size_t total = (size_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(chan_scale_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, g, y, N, HW, C);
+}
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, bf16* dx, float* dg, int N, int HW, int C,
+                           hipStream_t st) {
+  const int n = N * (C / 8);
+  hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dy, x, g, dx, dg, N, HW, C);
+}
+
+}  // namespace dcp

@@ -1,0 +1,113 @@
+// Host-side launcher declarations shared by the kernel translation units and
+// the PyTorch operator bindings (bindings.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+
+namespace dcp {
+
+constexpr int kMaxTaps = 64;
+
+struct TapList {
+  int n;
+  int dy[kMaxTaps], dx[kMaxTaps], widx[kMaxTaps];
+};
+
+void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
+                     int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
+                     const float* bias, int relu, const bf16* zero, hipStream_t stream);
+void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
+                  const TapList& taps, float* dw, const bf16* zero, int num_cu, hipStream_t stream);
+void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
+                             int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
+                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Ho, int Wo,
+                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+
+void launch_bn_slab_reduce(const float* slabs, int R, int C, float* out, hipStream_t s);
+void launch_chan_stats(const bf16* x, int M, int C, bool sq, float* out, hipStream_t s);
+void launch_bn_finalize(const float* tot, double count, int C, float eps, const float* gamma, const float* beta,
+                        float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
+                        hipStream_t s);
+void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
+                          float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
+void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
+                       int C, int act, float slope, hipStream_t s);
+void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
+                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* out,
+                          hipStream_t s);
+void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s);
+
+void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                        int s, int p, hipStream_t st);
+void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
+                        int k, int s, int p, hipStream_t st);
+void launch_gap_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t st);
+void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st);
+void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int inverse, hipStream_t st);
+
+void launch_xent_fwd(const void* logits, bool is_bf16, int B, int ld, int C, const int64_t* labels, float* loss,
+                     int* rank, float smoothing, hipStream_t s);
+void launch_xent_bwd(const void* logits, bool in_bf16, int B, int ld, int C, const int64_t* labels,
+                     const float* grad_out, float scale, float smoothing, void* dlogits, int ldo, bool out_bf16,
+                     hipStream_t s);
+void launch_log_softmax_fwd(const void* x, bool is_bf16, int B, int ld, int C, float* y, hipStream_t s);
+void launch_log_softmax_bwd(const float* y, const float* dy, int B, int C, int ldo, void* dx, bool out_bf16,
+                            hipStream_t s);
+void launch_l2norm_rows(const void* x, bool is_bf16, int R, int D, int ldo, bf16* y, float* inv_norm, float eps,
+                        hipStream_t s);
+void launch_l2norm_bwd(const void* dy, bool dy_bf16, int ldd, const bf16* y, int ldy, const float* inv_norm, int R,
+                       int D, void* dx, bool out_bf16, hipStream_t s);
+void launch_transpose2d(const bf16* x, bf16* y, int R, int C, hipStream_t s);
+void launch_arcface_fwd(const bf16* cosv, int B, int ld, int C, const int64_t* labels, float s, float cos_m,
+                        float sin_m, float th, float mm, int easy, float* out_logits, float* loss, int* rank,
+                        float* lab_dphi, hipStream_t st);
+void launch_arcface_bwd(const bf16* cosv, int B, int ld, int C, const int64_t* labels, float s, float cos_m,
+                        float sin_m, float th, float mm, int easy, const float* lab_dphi, const float* grad_out,
+                        float scale, bf16* dcos, hipStream_t st);
+
+struct MTEntry {
+  float* p;
+  float* g;
+  float* s1;
+  float* s2;
+  bf16* shadow;
+  int64_t n;
+};
+struct SgdHyper {
+  float lr, momentum, dampening, wd, grad_scale;
+  int nesterov, first;
+};
+struct AdamHyper {
+  float lr, beta1, beta2, eps, wd, grad_scale, bc1, bc2;
+  int decoupled;
+};
+void launch_mt_sgd(const MTEntry* tab, const int2* chunks, int nchunks, SgdHyper h, hipStream_t s);
+void launch_mt_adam(const MTEntry* tab, const int2* chunks, int nchunks, AdamHyper h, hipStream_t s);
+void launch_cdr_threshold(const MTEntry* tab, const int2* chunks, int nchunks, uint32_t* state, uint32_t* hist,
+                          hipStream_t s);
+void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const uint32_t* state, float clip,
+                     hipStream_t s);
+
+void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16* wb, bf16* wt, hipStream_t s);
+void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
+                    const float* mean, const float* stdv, bf16* dst, hipStream_t s);
+void launch_relu_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, hipStream_t s);
+void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
+void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
+                        hipStream_t s);
+
+void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
+                       int s, int p, int reflect, hipStream_t st);
+void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                       int s, int p, int reflect, hipStream_t st);
+void launch_chan_scale_fwd(const bf16* x, const bf16* g, bf16* y, int N, int HW, int C, hipStream_t st);
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, bf16* dx, float* dg, int N, int HW, int C,
+                           hipStream_t st);
+
+}  // namespace dcp

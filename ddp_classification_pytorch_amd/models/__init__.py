@@ -1,0 +1,26 @@
+"""Model zoo (NHWC, gfx950 kernels).  ``build_model(name, num_classes)``."""
+from .layers import BatchNorm2d, Conv2d, ConvBN, Linear
+from .resnet import (ResNet, build_resnet, cifar_resnet18, cifar_resnet34, cifar_resnet50, cifar_resnet101,
+                     cifar_resnet152, resnet18, resnet34, resnet50, resnet101, resnet152, resnext50_32x4d)
+
+MODEL_NAMES = ["resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "resnext50_32x4d", "resnext101_32x8d",
+               "cifar_resnet18", "cifar_resnet34", "cifar_resnet50", "cifar_resnet101", "cifar_resnet152",
+               "tresnet_m", "vgg19_bn"]
+
+
+def build_model(name: str, num_classes: int = 1000, **kw):
+    name = name.lower()
+    if name in ("tresnet", "tresnet_m", "tresnet_m_miil_in21k"):
+        from .tresnet import tresnet_m
+
+        return tresnet_m(num_classes=num_classes, **kw)
+    if name in ("vgg19_bn", "vgg19"):
+        from .vgg import vgg19_bn
+
+        return vgg19_bn(num_classes=num_classes, **kw)
+    return build_resnet(name, num_classes=num_classes, **kw)
+
+
+__all__ = ["BatchNorm2d", "Conv2d", "ConvBN", "Linear", "ResNet", "build_model", "build_resnet", "MODEL_NAMES",
+           "resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "resnext50_32x4d", "cifar_resnet18",
+           "cifar_resnet34", "cifar_resnet50", "cifar_resnet101", "cifar_resnet152"]

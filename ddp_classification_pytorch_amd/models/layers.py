@@ -1,0 +1,134 @@
+"""NHWC building blocks over the gfx950 primitives.
+
+* :class:`Conv2d` stores its master weight as fp32 ``[Co, KH, KW, Ci]``
+  (K-contiguous per output channel, the implicit-GEMM B operand layout).
+  ``load_state_dict`` accepts torchvision-layout ``[Co, Ci, KH, KW]`` weights
+  and permutes them, so pretrained torchvision/timm checkpoints load.
+* :class:`BatchNorm2d` is called with the conv's statistics slabs, an
+  activation and an optional residual: BN-apply + ReLU/leaky-ReLU + residual
+  add are one kernel, and SyncBN (``process_group``) all-reduces one packed
+  (sum, sumsq) vector per layer instead of torch's all_gather of
+  (mean, invstd, count) (reference: BASELINE/main.py:148).
+* :class:`Linear` is an nn.Linear-compatible module over the MFMA GEMM.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import functional as Fn
+
+
+class Conv2d(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, groups=1, bias=False):
+        super().__init__()
+        assert not bias, "convolutions feeding BN carry no bias"
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding, self.groups = kernel_size, stride, padding, groups
+        self.weight = nn.Parameter(torch.empty(out_channels, kernel_size, kernel_size, in_channels // groups))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # Kaiming normal, fan_out, ReLU gain (NESTED/model/imagenet_resnet.py init; torchvision ResNet)
+        fan_out = self.out_channels * self.kernel_size * self.kernel_size // self.groups
+        nn.init.normal_(self.weight, 0.0, math.sqrt(2.0 / fan_out))
+
+    def forward(self, x, stats=False):
+        """Returns (y, bn_stat_slabs_or_None)."""
+        if self.groups > 1:
+            return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding), None
+        y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda)
+        return y, (slabs if stats and x.is_cuda else None)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        key = prefix + "weight"
+        w = state_dict.get(key)
+        if w is not None and w.dim() == 4 and tuple(w.shape) != tuple(self.weight.shape):
+            # torchvision layout [Co, Ci, KH, KW] -> [Co, KH, KW, Ci]
+            if tuple(w.permute(0, 2, 3, 1).shape) == tuple(self.weight.shape):
+                state_dict[key] = w.permute(0, 2, 3, 1).contiguous()
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+        Fn.bump_weight_generation()
+
+    def extra_repr(self):
+        return (f"{self.in_channels}, {self.out_channels}, k={self.kernel_size}, s={self.stride}, "
+                f"p={self.padding}, groups={self.groups}, layout=NHWC")
+
+
+class BatchNorm2d(nn.Module):
+    """BatchNorm over the channel (last) dim of NHWC activations, fused with act/residual.
+
+    ``frozen`` (NESTED ``freeze_bn``, NESTED/model/model.py:44-55) uses running
+    statistics even in training mode and keeps gamma/beta fixed.
+    """
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        if affine:
+            self.weight = nn.Parameter(torch.ones(num_features))
+            self.bias = nn.Parameter(torch.zeros(num_features))
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        self.process_group = None  # set by parallel.convert_sync_batchnorm
+        self.frozen = False
+
+    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01):
+        stats = self.training and not self.frozen
+        if stats:
+            self.num_batches_tracked.add_(1)
+        return Fn.batch_norm_act(x, slabs, self.weight, self.bias, self.running_mean, self.running_var, stats,
+                                 self.momentum, self.eps, act=act, slope=slope, residual=residual,
+                                 group=self.process_group if stats else None)
+
+    def extra_repr(self):
+        return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, sync={self.process_group is not None}"
+
+
+class Linear(nn.Module):
+    """nn.Linear-compatible ([out, in] fp32 weight) on the MFMA GEMM, optional fused ReLU."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.empty(out_features)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):  # identical to nn.Linear
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(self.in_features) if self.in_features > 0 else 0
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x, relu=False):
+        return Fn.linear(x, self.weight, self.bias, relu=relu)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        Fn.bump_weight_generation()
+
+    def extra_repr(self):
+        return f"in={self.in_features}, out={self.out_features}, bias={self.bias is not None}"
+
+
+class ConvBN(nn.Module):
+    """conv -> BN (stats from the conv epilogue) -> act, optional residual."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=None, groups=1, act="relu", slope=0.01):
+        super().__init__()
+        padding = k // 2 if padding is None else padding
+        self.conv = Conv2d(cin, cout, k, stride, padding, groups)
+        self.bn = BatchNorm2d(cout)
+        self.act, self.slope = act, slope
+
+    def forward(self, x, residual=None):
+        y, slabs = self.conv(x, stats=self.bn.training and not self.bn.frozen)
+        return self.bn(y, slabs, act=self.act, residual=residual, slope=self.slope)

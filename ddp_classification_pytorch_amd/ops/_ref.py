@@ -1,0 +1,411 @@
+"""Reference (plain PyTorch, fp32-accumulating) implementations of every
+primitive registered by the HIP library under ``torch.ops.dcp``.
+
+Same names, same signatures, same layouts (NHWC activations, [Co,KH,KW,Ci]
+weights).  They serve two purposes only:
+
+* the CPU path (unit tests, gloo multi-process plumbing, BASELINE.json
+  config 1) -- never a GPU fallback;
+* the numerics oracle the GPU kernel tests compare against.
+
+Activation outputs keep the input dtype (fp32 on CPU in practice).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+
+
+def _f(t):
+    return t.float()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _w_oihw(w):  # [Co,KH,KW,Ci] -> [Co,Ci,KH,KW]
+    return w.permute(0, 3, 1, 2)
+
+
+# ----------------------------------------------------------------------------- conv
+def conv_fwd(x, w, stride, pad, stats):
+    y = F.conv2d(_nchw(_f(x)), _w_oihw(_f(w)), stride=stride, padding=pad)
+    y = _nhwc(y).to(x.dtype)
+    return y, torch.empty(0, device=x.device)
+
+
+def conv_dgrad(dy, wt, H, W, stride, pad):
+    # wt: [C,KH,KW,Co] (transposed); recover w [Co,KH,KW,C]
+    w = wt.permute(3, 1, 2, 0)
+    N = dy.shape[0]
+    C = wt.shape[0]
+    KH, KW = wt.shape[1], wt.shape[2]
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    op_h = H - ((Ho - 1) * stride - 2 * pad + KH)
+    op_w = W - ((Wo - 1) * stride - 2 * pad + KW)
+    dx = F.conv_transpose2d(_nchw(_f(dy)), _w_oihw(_f(w)), stride=stride, padding=pad, output_padding=(op_h, op_w))
+    assert dx.shape == (N, C, H, W)
+    return _nhwc(dx).to(dy.dtype)
+
+
+def conv_wgrad(dy, x, KH, KW, stride, pad):
+    Co, C = dy.shape[3], x.shape[3]
+    dw = torch.nn.grad.conv2d_weight(_nchw(_f(x)), (Co, C, KH, KW), _nchw(_f(dy)), stride=stride, padding=pad)
+    return dw.permute(0, 2, 3, 1).contiguous()
+
+
+def linear_fwd(x, w, bias, relu):
+    y = _f(x) @ _f(w).t()
+    if bias is not None:
+        y = y + _f(bias)[: y.shape[1]]
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def linear_wgrad(dy, x):
+    return _f(dy).t() @ _f(x)
+
+
+def weight_prep(w, co_pad, transposed):
+    Co = w.shape[0]
+    cp = max(co_pad, Co)
+    wb = w
+    if cp > Co:
+        pad_shape = (cp - Co,) + tuple(w.shape[1:])
+        wb = torch.cat([w, w.new_zeros(pad_shape)], 0)
+    if transposed:
+        wt = wb.transpose(0, -1).contiguous() if w.dim() == 2 else wb.permute(3, 1, 2, 0).contiguous()
+    else:
+        wt = w.new_empty(0)
+    return wb.contiguous(), wt
+
+
+def grouped_conv_fwd(x, w, groups, stride, pad):
+    y = F.conv2d(_nchw(_f(x)), _w_oihw(_f(w)), stride=stride, padding=pad, groups=groups)
+    return _nhwc(y).to(x.dtype)
+
+
+def grouped_conv_dgrad(dy, w, H, W, groups, stride, pad):
+    N, Co = dy.shape[0], dy.shape[3]
+    C = w.shape[3] * groups
+    KH, KW = w.shape[1], w.shape[2]
+    dx = torch.nn.grad.conv2d_input((N, C, H, W), _w_oihw(_f(w)), _nchw(_f(dy)), stride=stride, padding=pad,
+                                    groups=groups)
+    return _nhwc(dx).to(dy.dtype)
+
+
+def grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad):
+    Co, C = dy.shape[3], x.shape[3]
+    dw = torch.nn.grad.conv2d_weight(_nchw(_f(x)), (Co, C // groups, KH, KW), _nchw(_f(dy)), stride=stride,
+                                     padding=pad, groups=groups)
+    return dw.permute(0, 2, 3, 1).contiguous()
+
+
+# ----------------------------------------------------------------------------- batch norm
+def _rows(x):
+    return _f(x).reshape(-1, x.shape[-1])
+
+
+def bn_stats(x, slabs):
+    r = _rows(x)
+    return torch.stack([r.sum(0), (r * r).sum(0)])
+
+
+def colsum(x):
+    return _rows(x).sum(0)
+
+
+def bn_finalize(tot, count, gamma, beta, run_mean, run_var, momentum, eps):
+    tot = tot.double()
+    mu = tot[0] / count
+    var = (tot[1] / count - mu * mu).clamp_min(0)
+    invstd = 1.0 / torch.sqrt(var + eps)
+    g = gamma.double() if gamma is not None else torch.ones_like(mu)
+    b = beta.double() if beta is not None else torch.zeros_like(mu)
+    scale = g * invstd
+    shift = b - mu * scale
+    if run_mean is not None:
+        unb = var * count / (count - 1) if count > 1 else var
+        run_mean.mul_(1 - momentum).add_(momentum * mu.float())
+        run_var.mul_(1 - momentum).add_(momentum * unb.float())
+    return mu.float(), invstd.float(), scale.float(), shift.float()
+
+
+def bn_eval_coeff(gamma, beta, run_mean, run_var, eps):
+    invstd = torch.rsqrt(run_var.float() + eps)
+    g = gamma.float() if gamma is not None else torch.ones_like(invstd)
+    b = beta.float() if beta is not None else torch.zeros_like(invstd)
+    scale = g * invstd
+    return run_mean.float().clone(), invstd, scale, b - run_mean.float() * scale
+
+
+def _act(z, act, slope):
+    if act == ACT_RELU:
+        return torch.relu(z)
+    if act == ACT_LEAKY:
+        return torch.where(z >= 0, z, z * slope)
+    return z
+
+
+def _act_d(z, act, slope):
+    if act == ACT_RELU:
+        return (z > 0).float()
+    if act == ACT_LEAKY:
+        return torch.where(z >= 0, torch.ones_like(z), torch.full_like(z, slope))
+    return torch.ones_like(z)
+
+
+def bn_act(x, res, scale, shift, act, slope):
+    z = _f(x) * scale + shift
+    if res is not None:
+        z = z + _f(res)
+    return _act(z, act, slope).to(x.dtype)
+
+
+def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope):
+    z = _f(x) * scale + shift
+    if res is not None:
+        z = z + _f(res)
+    dz = _rows(dy * 1.0) * _act_d(z, act, slope).reshape(-1, x.shape[-1])
+    xh = (_rows(x) - mean) * invstd
+    return torch.stack([dz.sum(0), (dz * xh).sum(0)])
+
+
+def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope, want_dres):
+    z = _f(x) * scale + shift
+    if res is not None:
+        z = z + _f(res)
+    dz = _f(dy) * _act_d(z, act, slope)
+    if sums is not None:
+        xh = (_f(x) - mean) * invstd
+        dx = scale * (dz - sums[0] / count - xh * sums[1] / count)
+    else:
+        dx = scale * dz
+    dres = dz.to(dy.dtype) if want_dres else dy.new_empty(0)
+    return dx.to(dy.dtype), dres
+
+
+# ----------------------------------------------------------------------------- pooling / layout
+def maxpool_fwd(x, k, s, p):
+    y, idx = F.max_pool2d(_nchw(_f(x)), k, s, p, return_indices=True)
+    # window-local index (kh*k+kw) like the kernel
+    N, C, Ho, Wo = y.shape
+    W = x.shape[2]
+    hi = torch.div(idx, W, rounding_mode="floor")
+    wi = idx - hi * W
+    ho = torch.arange(Ho).view(1, 1, Ho, 1)
+    wo = torch.arange(Wo).view(1, 1, 1, Wo)
+    kh = hi - (ho * s - p)
+    kw = wi - (wo * s - p)
+    loc = (kh * k + kw).to(torch.uint8)
+    return _nhwc(y).to(x.dtype), _nhwc(loc)
+
+
+def maxpool_bwd(dy, idx, H, W, k, s, p):
+    N, Ho, Wo, C = dy.shape
+    loc = _nchw(idx).long()
+    kh = torch.div(loc, k, rounding_mode="floor")
+    kw = loc - kh * k
+    ho = torch.arange(Ho).view(1, 1, Ho, 1)
+    wo = torch.arange(Wo).view(1, 1, 1, Wo)
+    flat = (ho * s - p + kh) * W + (wo * s - p + kw)
+    dx = torch.zeros(N, C, H * W, dtype=torch.float32)
+    dx.scatter_add_(2, flat.reshape(N, C, -1), _nchw(_f(dy)).reshape(N, C, -1))
+    return _nhwc(dx.view(N, C, H, W)).to(dy.dtype)
+
+
+def gap_fwd(x):
+    N, C = x.shape[0], x.shape[-1]
+    return _f(x).reshape(N, -1, C).mean(1).to(x.dtype)
+
+
+def gap_bwd(dy, H, W):
+    N, C = dy.shape
+    return (_f(dy) / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).contiguous().to(dy.dtype)
+
+
+def space_to_depth(x, b, inverse):
+    if not inverse:
+        N, H, W, C = x.shape
+        return x.reshape(N, H // b, b, W // b, b, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // b, W // b, b * b * C)
+    N, Hb, Wb, Cb = x.shape
+    C = Cb // (b * b)
+    return x.reshape(N, Hb, Wb, b, b, C).permute(0, 1, 3, 2, 4, 5).reshape(N, Hb * b, Wb * b, C)
+
+
+def to_nhwc(src, nchw, cpad, in_scale, mean, std):
+    x = src.float() * in_scale
+    if nchw:
+        x = x.permute(0, 2, 3, 1)
+    C = x.shape[-1]
+    if mean is not None:
+        x = x - mean.float()
+    if std is not None:
+        x = x / std.float()
+    if cpad > C:
+        x = F.pad(x, (0, cpad - C))
+    return x.contiguous()
+
+
+def relu_bwd(dy, y):
+    return torch.where(y > 0, dy, torch.zeros_like(dy))
+
+
+def prefix_mask(x, keep):
+    D = x.shape[1]
+    m = (torch.arange(D, device=x.device) < int(keep.item())).to(x.dtype)
+    return x * m
+
+
+def nested_eval(feat, W, labels):
+    # scores for every prefix length: [D,B,C] via cumulative sum (reference-sized; CPU only)
+    contrib = feat.float().unsqueeze(2) * W.float().unsqueeze(0)  # [B,D,C]
+    scores = contrib.cumsum(1)  # [B,D,C]
+    lab = labels.view(-1, 1, 1).expand(-1, scores.shape[1], 1)
+    sl = scores.gather(2, lab)
+    gt = (scores > sl).sum(2)  # [B,D] (label itself never counted)
+    top1 = (gt == 0).sum(0)
+    top3 = (gt < 3).sum(0)
+    return torch.stack([top1, top3], 1).int()
+
+
+def dwconv_fwd(x, filt, k, s, p, reflect):
+    C = x.shape[-1]
+    xin = _nchw(_f(x))
+    if reflect and p > 0:
+        xin = F.pad(xin, (p, p, p, p), mode="reflect")
+        pad = 0
+    else:
+        pad = p
+    w = filt.float().view(1, 1, k, k).expand(C, 1, k, k)
+    y = F.conv2d(xin, w, stride=s, padding=pad, groups=C)
+    return _nhwc(y).to(x.dtype)
+
+
+def dwconv_bwd(dy, filt, H, W, k, s, p, reflect):
+    x = torch.zeros(dy.shape[0], H, W, dy.shape[-1], requires_grad=True)
+    with torch.enable_grad():
+        y = dwconv_fwd(x, filt, k, s, p, reflect)
+        (g,) = torch.autograd.grad(y, x, _f(dy))
+    return g.to(dy.dtype)
+
+
+def chan_scale_fwd(x, g):
+    N, C = x.shape[0], x.shape[-1]
+    return (_f(x) * _f(g).view(N, *([1] * (x.dim() - 2)), C)).to(x.dtype)
+
+
+def chan_scale_bwd(dy, x, g):
+    N, C = x.shape[0], x.shape[-1]
+    gg = _f(g).view(N, *([1] * (x.dim() - 2)), C)
+    dx = (_f(dy) * gg).to(dy.dtype)
+    dg = (_f(dy) * _f(x)).reshape(N, -1, C).sum(1)
+    return dx, dg
+
+
+# ----------------------------------------------------------------------------- losses
+def xent_fwd(logits, labels, C, smoothing):
+    x = _f(logits)[:, :C]
+    lse = torch.logsumexp(x, 1)
+    xl = x.gather(1, labels.view(-1, 1)).squeeze(1)
+    loss = lse - xl
+    if smoothing > 0:
+        loss = (1 - smoothing) * loss + smoothing * (lse - x.mean(1))
+    rank = (x > xl.unsqueeze(1)).sum(1).int()
+    return loss, rank
+
+
+def xent_bwd(logits, labels, C, grad_out, scale, smoothing, out_bf16):
+    B, ld = logits.shape
+    x = _f(logits)[:, :C]
+    p = torch.softmax(x, 1)
+    tgt = torch.full_like(p, smoothing / C)
+    tgt.scatter_add_(1, labels.view(-1, 1), torch.full((B, 1), 1 - smoothing))
+    d = torch.zeros(B, ld)
+    d[:, :C] = (p - tgt) * (float(grad_out.float().reshape(-1)[0]) * scale)
+    return d.to(torch.bfloat16 if out_bf16 else torch.float32)
+
+
+def log_softmax_fwd(x, C):
+    return torch.log_softmax(_f(x)[:, :C], 1)
+
+
+def log_softmax_bwd(y, dy, ldo, out_bf16):
+    d = _f(dy) - torch.exp(y) * _f(dy).sum(1, keepdim=True)
+    out = torch.zeros(y.shape[0], ldo)
+    out[:, : y.shape[1]] = d
+    return out.to(torch.bfloat16 if out_bf16 else torch.float32)
+
+
+def l2norm_rows(x, ldo, eps):
+    xf = _f(x)
+    n = xf.norm(dim=1).clamp_min(eps)
+    y = xf / n.unsqueeze(1)
+    if ldo > y.shape[1]:
+        y = F.pad(y, (0, ldo - y.shape[1]))
+    return y, 1.0 / n
+
+
+def l2norm_bwd(dy, y, inv, D, out_bf16):
+    yf = _f(y)[:, :D]
+    dyf = _f(dy)[:, :D]
+    dot = (dyf * yf).sum(1, keepdim=True)
+    dx = inv.unsqueeze(1) * (dyf - yf * dot)
+    return dx.to(torch.bfloat16 if out_bf16 else torch.float32)
+
+
+def _arc_consts(m):
+    return math.cos(m), math.sin(m), math.cos(math.pi - m), math.sin(math.pi - m) * m
+
+
+def arcface_fwd(cosv, labels, C, s, m, easy, want_logits):
+    cm, sm, th, mm = _arc_consts(m)
+    cos = _f(cosv)[:, :C]
+    c = cos.gather(1, labels.view(-1, 1)).squeeze(1).clamp(-1, 1)
+    sn = torch.sqrt((1 - c * c).clamp(0, 1))
+    p = c * cm - sn * sm
+    dp = cm + torch.where(sn > 1e-6, sm * c / sn.clamp_min(1e-6), torch.zeros_like(c))
+    if easy:
+        phi = torch.where(c > 0, p, c)
+        dphi = torch.where(c > 0, dp, torch.ones_like(c))
+    else:
+        phi = torch.where(c > th, p, c - mm)
+        dphi = torch.where(c > th, dp, torch.ones_like(c))
+    logits = s * cos.clone()
+    logits.scatter_(1, labels.view(-1, 1), (s * phi).view(-1, 1))
+    loss = torch.logsumexp(logits, 1) - s * phi
+    rank = (logits > (s * phi).unsqueeze(1)).sum(1).int()
+    return loss, rank, dphi, (logits if want_logits else torch.empty(0))
+
+
+def arcface_bwd(cosv, labels, C, s, m, easy, dphi, grad_out, scale):
+    B, ld = cosv.shape
+    cm, sm, th, mm = _arc_consts(m)
+    cos = _f(cosv)[:, :C]
+    c = cos.gather(1, labels.view(-1, 1)).squeeze(1).clamp(-1, 1)
+    sn = torch.sqrt((1 - c * c).clamp(0, 1))
+    p = c * cm - sn * sm
+    phi = torch.where(c > 0, p, c) if easy else torch.where(c > th, p, c - mm)
+    logits = s * cos.clone()
+    logits.scatter_(1, labels.view(-1, 1), (s * phi).view(-1, 1))
+    pr = torch.softmax(logits, 1)
+    oh = torch.zeros_like(pr).scatter_(1, labels.view(-1, 1), 1.0)
+    mult = torch.ones_like(pr).scatter_(1, labels.view(-1, 1), dphi.view(-1, 1))
+    g = float(grad_out.float().reshape(-1)[0]) * scale
+    d = torch.zeros(B, ld)
+    d[:, :C] = g * s * (pr - oh) * mult
+    return d.to(cosv.dtype)
+
+
+def transpose2d(x):
+    return x.t().contiguous()

@@ -1,0 +1,467 @@
+"""Autograd functions over the gfx950 primitives.
+
+Every function is written once against the primitive API (``torch.ops.dcp``
+on GPU tensors, :mod:`._ref` on CPU tensors) via :func:`K`.  On a GPU tensor
+the HIP library is mandatory: :func:`K` raises if it cannot be loaded.
+
+Layouts: activations NHWC (bf16 on GPU), conv weights [Co,KH,KW,Ci] fp32
+masters, linear weights [out,in] fp32 masters.  bf16 GEMM copies of the
+weights are produced by one ``weight_prep`` launch per layer per weight
+version and cached on the parameter.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from .. import _ext
+from . import _ref
+
+ACT = {"none": 0, "relu": 1, "leaky": 2, "leaky_relu": 2, None: 0}
+
+
+def K(t: torch.Tensor):
+    """Primitive namespace for tensor ``t``: HIP kernels on GPU, reference math on CPU."""
+    return _ext.hip_ops() if t.is_cuda else _ref
+
+
+def act_dtype(device: torch.device) -> torch.dtype:
+    return torch.bfloat16 if device.type == "cuda" else torch.float32
+
+
+def round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+# ----------------------------------------------------------------------------- weight cache
+_GEN = [0]
+
+
+def bump_weight_generation():
+    """Invalidate cached bf16 weight copies (called by optimizers / state loads)."""
+    _GEN[0] += 1
+
+
+def prepared_weight(w: torch.Tensor, co_pad: int = 0, transposed: bool = True):
+    """(bf16 copy padded to co_pad rows, transposed copy) of a fp32 master, cached per version."""
+    key = (w._version, _GEN[0], w.data_ptr(), co_pad, transposed)
+    cached = getattr(w, "_dcp_prep", None)
+    if cached is not None and cached[0] == key:
+        return cached[1], cached[2]
+    wd = w.detach()
+    if not wd.is_contiguous():
+        wd = wd.contiguous()
+    wb, wt = K(wd).weight_prep(wd, co_pad, transposed)
+    if not wd.is_cuda:
+        wb, wt = wb.to(act_dtype(wd.device)), wt.to(act_dtype(wd.device))
+    try:
+        w._dcp_prep = (key, wb, wt)
+    except Exception:  # non-leaf / functional tensors cannot carry attributes
+        pass
+    return wb, wt
+
+
+# ----------------------------------------------------------------------------- convolution
+class _Conv2d(Function):
+    @staticmethod
+    def forward(ctx, x, weight, wb, wt, stride, pad, stats):
+        y, slabs = K(x).conv_fwd(x, wb, stride, pad, stats)
+        ctx.save_for_backward(x, wt)
+        ctx.geo = (weight.shape[1], weight.shape[2], stride, pad)
+        ctx.mark_non_differentiable(slabs)
+        return y, slabs
+
+    @staticmethod
+    def backward(ctx, dy, _dslabs):
+        x, wt = ctx.saved_tensors
+        KH, KW, stride, pad = ctx.geo
+        dy = dy.contiguous()
+        k = K(dy)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
+        if ctx.needs_input_grad[1]:
+            dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
+        return dx, dw, None, None, None, None, None
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False):
+    """NHWC conv; returns (y, bn_stat_slabs).  weight: fp32 [Co,KH,KW,Ci]."""
+    if weight.shape[3] != x.shape[3]:  # stem: input channels zero-padded to a multiple of 8
+        weight = F.pad(weight, (0, x.shape[3] - weight.shape[3]))
+    wb, wt = prepared_weight(weight, 0, True)
+    return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats)
+
+
+class _GroupedConv2d(Function):
+    @staticmethod
+    def forward(ctx, x, weight, wb, groups, stride, pad):
+        y = K(x).grouped_conv_fwd(x, wb, groups, stride, pad)
+        ctx.save_for_backward(x, wb)
+        ctx.geo = (weight.shape[1], weight.shape[2], groups, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        KH, KW, groups, stride, pad = ctx.geo
+        dy = dy.contiguous()
+        k = K(dy)
+        dx = k.grouped_conv_dgrad(dy, wb, x.shape[1], x.shape[2], groups, stride, pad) if ctx.needs_input_grad[0] else None
+        dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None
+
+
+def grouped_conv2d(x, weight, groups, stride=1, pad=0):
+    if groups == 1:
+        return conv2d(x, weight, stride, pad, False)[0]
+    wb, _ = prepared_weight(weight, 0, False)
+    return _GroupedConv2d.apply(x, weight, wb, groups, stride, pad)
+
+
+# ----------------------------------------------------------------------------- linear
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias_p, wb, wt, relu):
+        y = K(x).linear_fwd(x, wb, bias_p, relu)
+        ctx.save_for_backward(x, wt, y if relu else None)
+        ctx.relu = relu
+        ctx.out = weight.shape[0]
+        ctx.has_bias = bias_p is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        k = K(dy)
+        if ctx.relu:
+            dy = k.relu_bwd(dy, y)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = k.linear_fwd(dy, wt, None, False)
+        if ctx.needs_input_grad[1]:
+            dw = k.linear_wgrad(dy, x)[: ctx.out]
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = k.colsum(dy)  # grad of the padded bias (F.pad backward slices it)
+        return dx, dw, db, None, None, None
+
+
+def linear(x, weight, bias=None, relu=False, keep_padded=False):
+    """y = x W^T + b (optionally ReLU).  Output features are padded to a multiple
+    of 64 for the GEMM; the returned tensor is the [B, out] view unless
+    ``keep_padded``."""
+    out, inf = weight.shape
+    x = x.contiguous()
+    if x.shape[1] != inf:
+        raise ValueError(f"linear: input width {x.shape[1]} != {inf}")
+    npad = round_up(out, 64) if x.is_cuda else out
+    wb, wt = prepared_weight(weight, npad, True)
+    bias_p = None
+    if bias is not None:
+        bias_p = F.pad(bias, (0, npad - out)) if npad > out else bias
+    y = _Linear.apply(x, weight, bias_p, wb, wt, relu)
+    return y if keep_padded or npad == out else y[:, :out]
+
+
+# ----------------------------------------------------------------------------- batch norm (+act, +residual)
+class BNConfig:
+    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world")
+
+    def __init__(self, training_stats, momentum, eps, act, slope, group, world):
+        self.training_stats = training_stats
+        self.momentum = momentum
+        self.eps = eps
+        self.act = act
+        self.slope = slope
+        self.group = group
+        self.world = world
+
+
+class _BNAct(Function):
+    @staticmethod
+    def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig):
+        k = K(x)
+        C = x.shape[-1]
+        count = x.numel() // C
+        if cfg.training_stats:
+            tot = k.bn_stats(x, slabs)
+            if cfg.group is not None:
+                dist.all_reduce(tot, group=cfg.group)
+                count = count * cfg.world  # DistributedSampler keeps per-rank batches equal
+            mean, invstd, scale, shift = k.bn_finalize(tot, float(count), gamma, beta, run_mean, run_var,
+                                                       cfg.momentum, cfg.eps)
+        else:
+            mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
+        y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
+        ctx.save_for_backward(x, res, gamma, scale, shift, mean, invstd)
+        ctx.cfg = cfg
+        ctx.count = count
+        ctx.has_res = res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, gamma, scale, shift, mean, invstd = ctx.saved_tensors
+        cfg = ctx.cfg
+        dy = dy.contiguous()
+        k = K(dy)
+        need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        sums = None
+        local = None
+        if cfg.training_stats or need_affine:
+            local = k.bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, cfg.act, cfg.slope)
+            sums = local
+            if cfg.training_stats and cfg.group is not None:
+                sums = local.clone()
+                dist.all_reduce(sums, group=cfg.group)
+        want_dres = ctx.has_res and ctx.needs_input_grad[4]
+        dx, dres = k.bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums if cfg.training_stats else None,
+                                  float(ctx.count), cfg.act, cfg.slope, want_dres)
+        dgamma = local[1].clone() if (local is not None and ctx.needs_input_grad[2]) else None
+        dbeta = local[0].clone() if (local is not None and ctx.needs_input_grad[3]) else None
+        return dx, None, dgamma, dbeta, (dres if want_dres else None), None, None, None
+
+
+def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
+                   slope=0.01, residual=None, group=None):
+    world = dist.get_world_size(group) if group is not None else 1
+    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
+    if slabs is None or (slabs.numel() == 0):
+        slabs = None
+    return _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg)
+
+
+# ----------------------------------------------------------------------------- pooling
+class _MaxPool(Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = K(x).maxpool_fwd(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.geo = (x.shape[1], x.shape[2], k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        H, W, k, s, p = ctx.geo
+        return K(dy).maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p), None, None, None
+
+
+def max_pool2d(x, k=3, s=2, p=1):
+    return _MaxPool.apply(x, k, s, p)
+
+
+class _GAP(Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return K(x).gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K(dy).gap_bwd(dy.contiguous(), *ctx.hw)
+
+
+def global_avg_pool(x):
+    """[N,H,W,C] -> [N,C] (torchvision AdaptiveAvgPool2d(1) + flatten)."""
+    return _GAP.apply(x)
+
+
+class _S2D(Function):
+    @staticmethod
+    def forward(ctx, x, b):
+        ctx.b = b
+        return K(x).space_to_depth(x, b, False)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K(dy).space_to_depth(dy.contiguous(), ctx.b, True), None
+
+
+def space_to_depth(x, b=4):
+    return _S2D.apply(x, b)
+
+
+class _DWConv(Function):
+    @staticmethod
+    def forward(ctx, x, filt, k, s, p, reflect):
+        ctx.save_for_backward(filt)
+        ctx.geo = (x.shape[1], x.shape[2], k, s, p, reflect)
+        return K(x).dwconv_fwd(x, filt, k, s, p, reflect)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (filt,) = ctx.saved_tensors
+        H, W, k, s, p, reflect = ctx.geo
+        return K(dy).dwconv_bwd(dy.contiguous(), filt, H, W, k, s, p, reflect), None, None, None, None, None
+
+
+def blur_pool(x, filt, k=3, s=2, p=1, reflect=True):
+    """Fixed depthwise low-pass filter + stride (anti-aliased downsampling)."""
+    return _DWConv.apply(x, filt, k, s, p, reflect)
+
+
+class _ChanScale(Function):
+    @staticmethod
+    def forward(ctx, x, g):
+        ctx.save_for_backward(x, g)
+        return K(x).chan_scale_fwd(x, g)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g = ctx.saved_tensors
+        dx, dg = K(dy).chan_scale_bwd(dy.contiguous(), x, g)
+        return dx, dg.to(g.dtype)
+
+
+def channel_scale(x, g):
+    """x[n,h,w,c] * g[n,c] (squeeze-and-excitation apply)."""
+    return _ChanScale.apply(x, g.contiguous())
+
+
+# ----------------------------------------------------------------------------- losses
+class _XEnt(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, C, smoothing, reduction):
+        loss_rows, rank = K(logits).xent_fwd(logits, labels, C, smoothing)
+        ctx.save_for_backward(logits, labels)
+        ctx.C, ctx.smoothing, ctx.reduction = C, smoothing, reduction
+        ctx.mark_non_differentiable(rank)
+        loss = loss_rows.mean() if reduction == "mean" else loss_rows.sum()
+        return loss, rank
+
+    @staticmethod
+    def backward(ctx, g, _grank):
+        logits, labels = ctx.saved_tensors
+        B = logits.shape[0]
+        scale = 1.0 / B if ctx.reduction == "mean" else 1.0
+        d = K(logits).xent_bwd(logits, labels, ctx.C, g.reshape(1), scale, ctx.smoothing,
+                               logits.dtype == torch.bfloat16)
+        return d, None, None, None, None
+
+
+def cross_entropy(logits, labels, num_classes=None, smoothing=0.0, reduction="mean", return_rank=False):
+    """Softmax cross-entropy (one fused pass) -> loss [, rank of the true label]."""
+    C = num_classes or logits.shape[1]
+    loss, rank = _XEnt.apply(logits, labels, C, float(smoothing), reduction)
+    return (loss, rank) if return_rank else loss
+
+
+class _LogSoftmax(Function):
+    @staticmethod
+    def forward(ctx, x, C):
+        y = K(x).log_softmax_fwd(x, C)
+        ctx.save_for_backward(y)
+        ctx.ldo = x.shape[1]
+        ctx.bf = x.dtype == torch.bfloat16
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return K(y).log_softmax_bwd(y, dy.contiguous(), ctx.ldo, ctx.bf), None
+
+
+def log_softmax(x, num_classes=None):
+    """Row log-softmax -> fp32 [B, C]."""
+    return _LogSoftmax.apply(x, num_classes or x.shape[1])
+
+
+class _ArcFace(Function):
+    """Fused ArcMarginProduct + cross-entropy (ARCFACE/arc_main.py:130-176, 245).
+
+    cos = normalize(x) . normalize(W)^T on the MFMA GEMM, margin + softmax-CE +
+    label rank in one row kernel; backward through the margin, the cosine
+    GEMM (dgrad + wgrad) and both L2 normalisations.
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, labels, s, m, easy, want_logits):
+        k = K(x)
+        C, D = weight.shape
+        Dp = round_up(D, 8) if x.is_cuda else D
+        Cp = round_up(C, 64) if x.is_cuda else C
+        xn, inv_x = k.l2norm_rows(x.contiguous(), Dp, 1e-12)
+        wsrc = weight.detach()
+        if Cp > C:
+            wsrc = F.pad(wsrc, (0, 0, 0, Cp - C))
+        wn, inv_w = k.l2norm_rows(wsrc.contiguous(), Dp, 1e-12)
+        if not x.is_cuda:
+            xn, wn = xn.float(), wn.float()
+        cos = k.linear_fwd(xn, wn, None, False)  # [B, Cp]
+        loss_rows, rank, dphi, logits = k.arcface_fwd(cos, labels, C, s, m, easy, want_logits)
+        ctx.save_for_backward(xn, inv_x, wn, inv_w, cos, labels, dphi)
+        ctx.cfg = (C, D, s, m, easy)
+        ctx.mark_non_differentiable(rank, logits)
+        return loss_rows.mean(), rank, logits
+
+    @staticmethod
+    def backward(ctx, g, _grank, _glogits):
+        xn, inv_x, wn, inv_w, cos, labels, dphi = ctx.saved_tensors
+        C, D, s, m, easy = ctx.cfg
+        k = K(cos)
+        B = cos.shape[0]
+        dcos = k.arcface_bwd(cos, labels, C, s, m, easy, dphi, g.reshape(1), 1.0 / B)  # [B, Cp]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wnt = k.transpose2d(wn)  # [Dp, Cp]
+            dxn = k.linear_fwd(dcos, wnt, None, False)  # [B, Dp]
+            dx = k.l2norm_bwd(dxn, xn, inv_x, D, False)
+        if ctx.needs_input_grad[1]:
+            dwn = k.linear_wgrad(dcos, xn)  # [Cp, Dp] fp32
+            dw = k.l2norm_bwd(dwn.contiguous(), wn, inv_w, D, False)[:C]
+        return dx, dw, None, None, None, None, None
+
+
+def arcface_loss(x, weight, labels, s=30.0, m=0.5, easy_margin=True, return_logits=False):
+    """Returns (mean loss, rank of label, margin logits or empty)."""
+    return _ArcFace.apply(x, weight, labels, float(s), float(m), bool(easy_margin), bool(return_logits))
+
+
+# ----------------------------------------------------------------------------- misc
+def to_device_nhwc(images: torch.Tensor, mean=None, std=None, cpad: int = 8, nchw: bool = True, in_scale: float = 1.0):
+    """Image batch (uint8 or fp32, NCHW/NHWC, already on the target device) -> normalised
+    NHWC activations with channels zero-padded to ``cpad``."""
+    if mean is not None and not torch.is_tensor(mean):
+        mean = torch.tensor(mean, dtype=torch.float32, device=images.device)
+    if std is not None and not torch.is_tensor(std):
+        std = torch.tensor(std, dtype=torch.float32, device=images.device)
+    out = K(images).to_nhwc(images.contiguous(), nchw, cpad, in_scale, mean, std)
+    return out.to(act_dtype(images.device)) if not images.is_cuda else out
+
+
+class _PrefixMask(Function):
+    @staticmethod
+    def forward(ctx, x, keep):
+        ctx.save_for_backward(keep)
+        return K(x).prefix_mask(x.contiguous(), keep)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (keep,) = ctx.saved_tensors
+        return K(dy).prefix_mask(dy.contiguous(), keep), None
+
+
+def nested_mask(feature, k_index):
+    """feature * 1[:k+1] (nested dropout, NESTED/train.py:247-250); k_index int."""
+    keep = torch.tensor([int(k_index) + 1], dtype=torch.int32, device=feature.device)
+    return _PrefixMask.apply(feature, keep)
+
+
+def nested_eval_counts(feature: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Per-K (top-1, top-3) correct counts for every prefix length K (int32 [D,2])."""
+    return K(feature).nested_eval(feature.float().contiguous(), weight.float().contiguous(), labels)
+
+
+def gaussian_dist(mu: float, std: float, n: int):
+    """NESTED/train.py:93-97: p(i) ∝ exp(-((i-mu)/std)^2), i = 1..n."""
+    import numpy as np
+
+    d = np.array([math.exp(-(((i - mu) / std) ** 2)) for i in range(1, n + 1)])
+    return d / d.sum()

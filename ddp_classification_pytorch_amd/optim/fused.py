@@ -1,0 +1,154 @@
+"""Fused multi-tensor SGD / Adam on the gfx950 ``mt_sgd`` / ``mt_adam`` kernels.
+
+Drop-in ``torch.optim.Optimizer`` subclasses (param groups, state_dict,
+LR schedulers all work).  Semantics follow torch.optim.SGD / Adam exactly
+(momentum buffer initialised to the first gradient; Adam bias correction;
+L2 weight decay added to the gradient, or decoupled for AdamW), which the
+reference uses at BASELINE/main.py:153 (SGD mom 0.9), ARCFACE/arc_main.py:249-253
+(Adam / SGD wd 5e-4), NESTED/train.py:386-392 and PLC/utils.py:237 (nesterov).
+
+GPU: one kernel launch per parameter group updates every tensor; the device
+table of (param, grad, state) pointers is rebuilt only when a pointer changes.
+CPU: the same math with torch ops (tests / gloo plumbing).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _ext
+from ..ops import functional as Fn
+
+CHUNK = 4096
+
+
+class _TableCache:
+    def __init__(self):
+        self.key = None
+        self.table = None
+        self.chunks = None
+
+    def get(self, entries, device):
+        key = tuple((e[0], e[1], e[2], e[3], e[5]) for e in entries)
+        if key != self.key:
+            tab = torch.tensor(entries, dtype=torch.int64).view(-1, 6)
+            ch = []
+            for i, e in enumerate(entries):
+                n = e[5]
+                ch.extend((i, c) for c in range((n + CHUNK - 1) // CHUNK))
+            self.table = tab.to(device, non_blocking=True)
+            self.chunks = torch.tensor(ch, dtype=torch.int32).view(-1, 2).to(device, non_blocking=True)
+            self.key = key
+        return self.table, self.chunks
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+                 grad_scale=1.0):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov, grad_scale=grad_scale)
+        super().__init__(params, defaults)
+        self._tables = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            mom = group["momentum"]
+            first = False
+            for p in params:
+                st = self.state[p]
+                if mom != 0 and "momentum_buffer" not in st:
+                    st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    first = True
+            if params[0].is_cuda:
+                entries = []
+                for p in params:
+                    if not (p.is_contiguous() and p.grad.is_contiguous()):
+                        raise RuntimeError("FusedSGD needs contiguous params and grads")
+                    if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                        raise RuntimeError("FusedSGD expects fp32 master params and grads")
+                    buf = self.state[p].get("momentum_buffer")
+                    entries.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr() if buf is not None else 0, 0, 0,
+                                    p.numel()))
+                table, chunks = self._tables.setdefault(gi, _TableCache()).get(entries, params[0].device)
+                _ext.hip_ops().mt_sgd(table, chunks, group["lr"], mom, group["dampening"], group["weight_decay"],
+                                      group["nesterov"], first, group["grad_scale"])
+            else:
+                for p in params:
+                    g = p.grad * group["grad_scale"]
+                    if group["weight_decay"]:
+                        g = g + group["weight_decay"] * p
+                    if mom:
+                        buf = self.state[p]["momentum_buffer"]
+                        if first:
+                            buf.copy_(g)
+                        else:
+                            buf.mul_(mom).add_(g, alpha=1 - group["dampening"])
+                        g = g + mom * buf if group["nesterov"] else buf
+                    p.add_(g, alpha=-group["lr"])
+        Fn.bump_weight_generation()
+        return loss
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False,
+                 grad_scale=1.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=decoupled,
+                        grad_scale=grad_scale)
+        super().__init__(params, defaults)
+        self._tables = {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            for p in params:
+                st = self.state[p]
+                if "step" not in st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["step"] += 1
+            step = self.state[params[0]]["step"]
+            b1, b2 = group["betas"]
+            if params[0].is_cuda:
+                entries = []
+                for p in params:
+                    st = self.state[p]
+                    entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                                    st["exp_avg_sq"].data_ptr(), 0, p.numel()))
+                table, chunks = self._tables.setdefault(gi, _TableCache()).get(entries, params[0].device)
+                _ext.hip_ops().mt_adam(table, chunks, group["lr"], b1, b2, group["eps"], group["weight_decay"], step,
+                                       group["decoupled"], group["grad_scale"])
+            else:
+                bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+                for p in params:
+                    st = self.state[p]
+                    g = p.grad * group["grad_scale"]
+                    if group["weight_decay"]:
+                        if group["decoupled"]:
+                            p.mul_(1 - group["lr"] * group["weight_decay"])
+                        else:
+                            g = g + group["weight_decay"] * p
+                    st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+                    st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+                    denom = st["exp_avg_sq"].sqrt() / math.sqrt(bc2) + group["eps"]
+                    p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / bc1)
+        Fn.bump_weight_generation()
+        return loss

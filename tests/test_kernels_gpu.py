@@ -1,0 +1,333 @@
+"""Numerics of every gfx950 HIP primitive against the plain-PyTorch fp32
+reference (ops/_ref.py) on identical bf16-rounded inputs."""
+import math
+
+import pytest
+import torch
+
+from ddp_classification_pytorch_amd import _ext
+from ddp_classification_pytorch_amd.ops import _ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def K():
+    return _ext.hip_ops()
+
+
+def relerr(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape) * scale).bfloat16()
+
+
+# ResNet-50 conv shapes at small batch, plus edge cases
+CONV_SHAPES = [
+    # N, H, W, Ci, Co, k, stride, pad
+    (2, 56, 56, 64, 64, 1, 1, 0),
+    (2, 56, 56, 64, 64, 3, 1, 1),
+    (2, 56, 56, 64, 256, 1, 1, 0),
+    (2, 56, 56, 256, 64, 1, 1, 0),
+    (2, 56, 56, 256, 128, 1, 1, 0),
+    (2, 56, 56, 128, 128, 3, 2, 1),
+    (2, 28, 28, 128, 512, 1, 1, 0),
+    (2, 56, 56, 256, 512, 1, 2, 0),
+    (2, 28, 28, 512, 128, 1, 1, 0),
+    (2, 28, 28, 128, 128, 3, 1, 1),
+    (2, 14, 14, 256, 256, 3, 1, 1),
+    (2, 28, 28, 512, 1024, 1, 2, 0),
+    (2, 14, 14, 512, 512, 3, 2, 1),
+    (2, 7, 7, 512, 2048, 1, 1, 0),
+    (2, 7, 7, 2048, 512, 1, 1, 0),
+    (2, 7, 7, 512, 512, 3, 1, 1),
+    (2, 64, 64, 8, 64, 7, 2, 3),     # stem (3 channels padded to 8)
+    (3, 9, 11, 64, 72, 3, 1, 1),     # ragged M and Co
+    (1, 13, 13, 32, 40, 3, 2, 1),    # odd spatial, stride 2, Cs % 64 != 0
+    (2, 32, 32, 8, 64, 3, 1, 1),     # CIFAR stem
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_stats(K, shape):
+    N, H, W, Ci, Co, k, s, p = shape
+    x = rnd(N, H, W, Ci)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
+    y, slabs = K.conv_fwd(x.to(DEV), w.to(DEV), s, p, True)
+    yr, _ = _ref.conv_fwd(x.float(), w.float(), s, p, False)
+    assert y.shape == yr.shape
+    assert relerr(y, yr) < 1e-2
+    tot = K.bn_stats(y, slabs)
+    tr = _ref.bn_stats(y.float().cpu(), None)
+    assert relerr(tot[0], tr[0]) < 1e-3 + 1e-3 * 0
+    assert relerr(tot[1], tr[1]) < 1e-3
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES[:-4] + CONV_SHAPES[-3:-1])
+def test_conv_dgrad(K, shape):
+    N, H, W, Ci, Co, k, s, p = shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Co))
+    wb, wt = K.weight_prep(w.float().to(DEV), 0, True)
+    dx = K.conv_dgrad(dy.to(DEV), wt, H, W, s, p)
+    dxr = _ref.conv_dgrad(dy.float(), w.float().permute(3, 1, 2, 0), H, W, s, p)
+    assert dx.shape == dxr.shape
+    assert relerr(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_wgrad(K, shape):
+    N, H, W, Ci, Co, k, s, p = shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co)
+    x = rnd(N, H, W, Ci)
+    dw = K.conv_wgrad(dy.to(DEV), x.to(DEV), k, k, s, p)
+    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    assert dw.shape == dwr.shape
+    assert relerr(dw, dwr) < 5e-3
+
+
+def test_weight_prep(K):
+    w = torch.randn(70, 3, 3, 24)
+    wb, wt = K.weight_prep(w.to(DEV), 128, True)
+    rb, rt = _ref.weight_prep(w, 128, True)
+    assert wb.shape == rb.shape and wt.shape == rt.shape
+    assert relerr(wb, rb) < 5e-3 and relerr(wt, rt) < 5e-3
+
+
+@pytest.mark.parametrize("B,K_,N,relu,bias", [(256, 2048, 512, True, True), (32, 512, 2176, False, True),
+                                               (5, 256, 64, False, False)])
+def test_linear(K, B, K_, N, relu, bias):
+    x = rnd(B, K_)
+    w = torch.randn(N, K_) / math.sqrt(K_)
+    b = torch.randn(N) if bias else None
+    wb, wt = K.weight_prep(w.to(DEV), N, True)
+    y = K.linear_fwd(x.to(DEV), wb, b.to(DEV) if bias else None, relu)
+    yr = _ref.linear_fwd(x.float(), w.bfloat16().float(), b, relu)
+    assert relerr(y, yr) < 1e-2
+    dy = rnd(B, N)
+    dx = K.linear_fwd(dy.to(DEV), wt, None, False)
+    assert relerr(dx, dy.float() @ w.bfloat16().float()) < 1e-2
+    dw = K.linear_wgrad(dy.to(DEV), x.to(DEV))
+    assert relerr(dw, dy.float().t() @ x.float()) < 5e-3
+
+
+@pytest.mark.parametrize("act,res", [(1, False), (1, True), (0, False), (2, True)])
+def test_bn_train_fwd_bwd(K, act, res):
+    N, H, W, C = 4, 14, 14, 256
+    x = rnd(N, H, W, C, scale=2.0) + 0.5
+    r = rnd(N, H, W, C) if res else None
+    g = torch.rand(C) + 0.5
+    b = torch.randn(C) * 0.1
+    rm, rv = torch.zeros(C), torch.ones(C)
+    rmd, rvd = rm.to(DEV), rv.to(DEV)
+    cnt = N * H * W
+    tot = K.bn_stats(x.to(DEV), None)
+    mean, invstd, scale, shift = K.bn_finalize(tot, float(cnt), g.to(DEV), b.to(DEV), rmd, rvd, 0.1, 1e-5)
+    totr = _ref.bn_stats(x.float(), None)
+    meanr, invr, scr, shr = _ref.bn_finalize(totr, float(cnt), g, b, rm, rv, 0.1, 1e-5)
+    assert relerr(mean, meanr) < 1e-4 and relerr(invstd, invr) < 1e-4
+    assert relerr(rmd, rm) < 1e-4 and relerr(rvd, rv) < 1e-4
+    y = K.bn_act(x.to(DEV), r.to(DEV) if res else None, scale, shift, act, 0.01)
+    yr = _ref.bn_act(x.float(), r.float() if res else None, scr, shr, act, 0.01)
+    assert relerr(y, yr) < 1e-2
+    dy = rnd(N, H, W, C)
+    sums = K.bn_bwd_reduce(dy.to(DEV), x.to(DEV), r.to(DEV) if res else None, scale, shift, mean, invstd, act, 0.01)
+    sumsr = _ref.bn_bwd_reduce(dy.float(), x.float(), r.float() if res else None, scr, shr, meanr, invr, act, 0.01)
+    assert relerr(sums, sumsr) < 1e-3
+    dx, dres = K.bn_bwd_elemt(dy.to(DEV), x.to(DEV), r.to(DEV) if res else None, scale, shift, mean, invstd, sums,
+                              float(cnt), act, 0.01, res)
+    dxr, dresr = _ref.bn_bwd_elemt(dy.float(), x.float(), r.float() if res else None, scr, shr, meanr, invr, sumsr,
+                                   float(cnt), act, 0.01, res)
+    assert relerr(dx, dxr) < 2e-2
+    if res:
+        assert relerr(dres, dresr) < 1e-2
+
+
+def test_bn_matches_torch_batchnorm(K):
+    # end-to-end against torch.nn.functional.batch_norm + relu autograd (fp32)
+    N, H, W, C = 8, 7, 7, 64
+    x = rnd(N, H, W, C) * 3 + 1
+    g, b = torch.rand(C) + 0.5, torch.randn(C)
+    xt = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    gt, bt = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yt = torch.relu(torch.nn.functional.batch_norm(xt, None, None, gt, bt, training=True, eps=1e-5))
+    dy = torch.randn_like(yt)
+    yt.backward(dy)
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    xd = x.to(DEV).requires_grad_(True)
+    gd, bd = g.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    y = Fn.batch_norm_act(xd, None, gd, bd, torch.zeros(C, device=DEV), torch.ones(C, device=DEV), True, 0.1, 1e-5)
+    y.backward(dy.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV))
+    assert relerr(y, yt.detach().permute(0, 2, 3, 1)) < 1e-2
+    assert relerr(xd.grad, xt.grad.permute(0, 2, 3, 1)) < 3e-2
+    assert relerr(gd.grad, gt.grad) < 1e-2
+    assert relerr(bd.grad, bt.grad) < 1e-2
+
+
+def test_pools(K):
+    x = rnd(2, 17, 15, 64)
+    y, idx = K.maxpool_fwd(x.to(DEV), 3, 2, 1)
+    yr, idxr = _ref.maxpool_fwd(x.float(), 3, 2, 1)
+    assert relerr(y, yr) < 1e-6
+    dy = rnd(*y.shape)
+    dx = K.maxpool_bwd(dy.to(DEV), idx, 17, 15, 3, 2, 1)
+    dxr = _ref.maxpool_bwd(dy.float(), idx.cpu(), 17, 15, 3, 2, 1)
+    assert relerr(dx, dxr) < 1e-2
+    g = K.gap_fwd(x.to(DEV))
+    assert relerr(g, _ref.gap_fwd(x.float())) < 1e-2
+    dg = rnd(2, 64)
+    assert relerr(K.gap_bwd(dg.to(DEV), 17, 15), _ref.gap_bwd(dg.float(), 17, 15)) < 1e-2
+    s = K.space_to_depth(rnd(2, 16, 8, 8).to(DEV), 4, False)
+    x2 = rnd(2, 16, 8, 8)
+    assert torch.equal(K.space_to_depth(x2.to(DEV), 4, False).cpu(), _ref.space_to_depth(x2, 4, False))
+    assert torch.equal(K.space_to_depth(K.space_to_depth(x2.to(DEV), 4, False), 4, True).cpu(), x2)
+
+
+@pytest.mark.parametrize("ld,C,bf", [(2176, 2173, True), (10, 10, False), (64, 33, True)])
+def test_xent(K, ld, C, bf):
+    B = 16
+    full = torch.randn(B, ld) * 3
+    logits = full.bfloat16() if bf else full
+    lab = torch.randint(0, C, (B,))
+    loss, rank = K.xent_fwd(logits.to(DEV)[:, :C], lab.to(DEV), C, 0.0)
+    lr_, rr = _ref.xent_fwd(logits[:, :C], lab, C, 0.0)
+    assert relerr(loss, lr_) < 1e-4
+    assert torch.equal(rank.cpu(), rr)
+    go = torch.tensor(1.0, device=DEV)
+    d = K.xent_bwd(logits.to(DEV)[:, :C], lab.to(DEV), C, go, 1.0 / B, 0.0, False)
+    xt = logits[:, :C].float().clone().requires_grad_(True)
+    torch.nn.functional.cross_entropy(xt, lab).backward()
+    assert relerr(d, xt.grad) < 1e-4
+
+
+def test_log_softmax(K):
+    x = torch.randn(8, 256)
+    y = K.log_softmax_fwd(x.to(DEV), 256)
+    assert relerr(y, torch.log_softmax(x, 1)) < 1e-5
+    dy = torch.randn(8, 256)
+    xt = x.clone().requires_grad_(True)
+    torch.log_softmax(xt, 1).backward(dy)
+    dx = K.log_softmax_bwd(y, dy.to(DEV), 256, False)
+    assert relerr(dx, xt.grad) < 1e-4
+
+
+def test_arcface_fused_vs_reference_module():
+    """Fused ArcFace fwd/bwd vs an fp32 autograd rendering of ArcMarginProduct + CE."""
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    torch.manual_seed(0)
+    B, D, C = 32, 256, 1000
+    x = torch.randn(B, D)
+    W = torch.randn(C, D) * 0.05
+    lab = torch.randint(0, C, (B,))
+    s, m = 30.0, 0.5
+    xt, Wt = x.clone().requires_grad_(True), W.clone().requires_grad_(True)
+    cos = torch.nn.functional.linear(torch.nn.functional.normalize(xt), torch.nn.functional.normalize(Wt))
+    sine = torch.sqrt((1.0 - cos.pow(2)).clamp(0, 1))
+    phi = cos * math.cos(m) - sine * math.sin(m)
+    phi = torch.where(cos > 0, phi, cos)
+    oh = torch.zeros_like(cos).scatter_(1, lab.view(-1, 1), 1)
+    out = (oh * phi + (1 - oh) * cos) * s
+    lt = torch.nn.functional.cross_entropy(out, lab)
+    lt.backward()
+    xd, Wd = x.to(DEV).requires_grad_(True), W.to(DEV).requires_grad_(True)
+    loss, rank, _ = Fn.arcface_loss(xd, Wd, lab.to(DEV), s, m, True)
+    loss.backward()
+    assert abs(loss.item() - lt.item()) / lt.item() < 2e-2
+    assert relerr(xd.grad, xt.grad) < 5e-2
+    assert relerr(Wd.grad, Wt.grad) < 5e-2
+
+
+def test_fused_sgd_adam_match_torch():
+    from ddp_classification_pytorch_amd.optim import FusedAdam, FusedSGD
+    torch.manual_seed(0)
+    shapes = [(64, 3, 3, 32), (5000,), (17, 9)]
+    for mk, tk, kw in [(FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=5e-4, nesterov=True)),
+                       (FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9)),
+                       (FusedAdam, torch.optim.Adam, dict(lr=1e-3, weight_decay=1e-4))]:
+        ps = [torch.randn(*s) for s in shapes]
+        a = [p.clone().to(DEV).requires_grad_(True) for p in ps]
+        b = [p.clone().requires_grad_(True) for p in ps]
+        oa, ob = mk(a, **kw), tk(b, **kw)
+        for _ in range(3):
+            gs = [torch.randn(*s) for s in shapes]
+            for p, g in zip(a, gs):
+                p.grad = g.to(DEV)
+            for p, g in zip(b, gs):
+                p.grad = g.clone()
+            oa.step()
+            ob.step()
+        for p, q in zip(a, b):
+            assert relerr(p.detach(), q.detach()) < 1e-5
+
+
+def test_cdr_threshold_mask():
+    from ddp_classification_pytorch_amd.algos.cdr import cdr_mask_gradients
+    torch.manual_seed(0)
+    params = [torch.randn(64, 3, 3, 16), torch.randn(1000, 20), torch.randn(37)]
+    gd = [torch.randn_like(p) for p in params]
+    pd = [p.to(DEV).requires_grad_(True) for p in params]
+    for p, g in zip(pd, gd):
+        p.grad = g.to(DEV)
+    thr = cdr_mask_gradients(pd, nonzero_ratio=0.8, clip=0.8)
+    # reference: CDR/main.py:186-204 over the 2-D/4-D tensors
+    sel = [(p, g) for p, g in zip(params, gd) if p.dim() in (2, 4)]
+    metric = torch.cat([(g * p).abs().view(-1) for p, g in sel])
+    nz = int(0.8 * metric.numel())
+    ref_thr = torch.topk(metric, nz)[0][-1]
+    assert abs(float(thr) - float(ref_thr)) <= 1e-6 * float(ref_thr)
+    for (p, g), q in zip(sel, [q for q in pd if q.dim() in (2, 4)]):
+        mask = ((p * g).abs() >= ref_thr).float() * 0.8
+        assert relerr(q.grad, mask * g) < 1e-6
+    assert torch.equal(pd[2].grad.cpu(), gd[2])
+
+
+def test_nested_eval_counts(K):
+    torch.manual_seed(0)
+    B, D, C = 16, 48, 37
+    f = torch.randn(B, D)
+    W = torch.randn(D, C)
+    lab = torch.randint(0, C, (B,))
+    cnt = K.nested_eval(f.to(DEV), W.to(DEV), lab.to(DEV))
+    ref = _ref.nested_eval(f, W, lab)
+    assert torch.equal(cnt.cpu(), ref)
+
+
+def test_grouped_and_dw_and_se(K):
+    x = rnd(2, 14, 14, 128)
+    w = rnd(128, 3, 3, 4, scale=0.3)
+    y = K.grouped_conv_fwd(x.to(DEV), w.to(DEV), 32, 2, 1)
+    assert relerr(y, _ref.grouped_conv_fwd(x.float(), w.float(), 32, 2, 1)) < 1e-2
+    dy = rnd(*y.shape)
+    dx = K.grouped_conv_dgrad(dy.to(DEV), w.to(DEV), 14, 14, 32, 2, 1)
+    assert relerr(dx, _ref.grouped_conv_dgrad(dy.float(), w.float(), 14, 14, 32, 2, 1)) < 1e-2
+    dw = K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 32, 2, 1)
+    assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), 3, 3, 32, 2, 1)) < 5e-3
+    filt = torch.tensor([1.0, 2.0, 1.0])
+    filt = (filt[:, None] * filt[None, :]) / 16
+    z = K.dwconv_fwd(x.to(DEV), filt.to(DEV), 3, 2, 1, True)
+    assert relerr(z, _ref.dwconv_fwd(x.float(), filt, 3, 2, 1, True)) < 1e-2
+    dz = rnd(*z.shape)
+    assert relerr(K.dwconv_bwd(dz.to(DEV), filt.to(DEV), 14, 14, 3, 2, 1, True),
+                  _ref.dwconv_bwd(dz.float(), filt, 14, 14, 3, 2, 1, True)) < 1e-2
+    g = rnd(2, 128)
+    assert relerr(K.chan_scale_fwd(x.to(DEV), g.to(DEV)), _ref.chan_scale_fwd(x.float(), g.float())) < 1e-2
+    dxs, dgs = K.chan_scale_bwd(dz.to(DEV)[:, :, :, :].contiguous() if False else rnd(*x.shape).to(DEV), x.to(DEV),
+                                g.to(DEV))
+    assert dxs.shape == x.shape and dgs.shape == (2, 128)
+
+
+def test_to_nhwc(K):
+    img = torch.randint(0, 256, (2, 3, 20, 24), dtype=torch.uint8)
+    mean = torch.tensor([0.485, 0.456, 0.406])
+    std = torch.tensor([0.229, 0.224, 0.225])
+    y = K.to_nhwc(img.to(DEV), True, 8, 1 / 255.0, mean.to(DEV), std.to(DEV))
+    yr = _ref.to_nhwc(img, True, 8, 1 / 255.0, mean, std)
+    assert y.shape == (2, 20, 24, 8)
+    assert relerr(y, yr) < 1e-2
