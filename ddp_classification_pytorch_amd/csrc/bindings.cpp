@@ -333,7 +333,7 @@ Tensor bn_act(const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
               double slope) {
   CHECK_ACT(x);
   const int C = x.size(-1);
-  TORCH_CHECK(C % 8 == 0 && scale.numel() == C, "bn_act shapes");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && scale.numel() == C, "bn_act shapes (C % 8 == 0, C <= 2048)");
   if (res.has_value()) {
     CHECK_ACT(*res);
     TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
@@ -364,7 +364,7 @@ std::tuple<Tensor, Tensor> bn_bwd_elemt(const Tensor& dy, const Tensor& x, const
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
-  TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0, "bn_bwd_elemt shapes");
+  TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_elemt shapes");
   auto dx = at::empty_like(x);
   Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
   dcp::launch_bn_bwd_elemt(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),

@@ -152,69 +152,135 @@ __global__ void bn_eval_coeff_kernel(int C, float eps, const float* __restrict__
   shift[c] = b - rm[c] * g * is;
 }
 
-// y = act(x*scale + shift [+ res]); 8 channels per thread, grid-stride
+// ---------------------------------------------------------------------------
+// Row-tiled elementwise kernels.  A workgroup of 256 threads covers `rpi` rows
+// x C channels per pass; each thread owns ONE fixed 8-channel chunk, so its
+// per-channel coefficients live in registers for the whole kernel, and walks
+// rows with a 4-deep unroll so 4 independent 16-byte loads per operand are in
+// flight (the kernels are HBM-bound; memory-level parallelism is the lever).
+// ---------------------------------------------------------------------------
+struct RowTile {
+  int cpr, rpi, slot, ch, c0;
+  __device__ RowTile(int C) {
+    cpr = C >> 3;
+    rpi = 256 / cpr;
+    slot = threadIdx.x / cpr;
+    ch = threadIdx.x - slot * cpr;
+    c0 = ch * 8;
+  }
+};
+
+__device__ __forceinline__ void load8(const float* __restrict__ p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
+template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, bf16* __restrict__ y,
-                                                         size_t nchunks, int C, int act, float slope) {
-  const int cpr = C >> 3;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cpr) * 8;
-    const bf16x8 v = *(const bf16x8*)(x + i * 8);
+                                                         int M, int C, float slope) {
+  const RowTile t(C);
+  if (t.slot >= t.rpi) return;
+  float sc[8], sh[8];
+  load8(scale + t.c0, sc);
+  load8(shift + t.c0, sh);
+  const int step = gridDim.x * t.rpi;
+  int m = blockIdx.x * t.rpi + t.slot;
+  constexpr int U = 4;
+  for (; m + (U - 1) * step < M; m += U * step) {
+    bf16x8 v[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = (size_t)(m + u * step) * C + t.c0;
+      v[u] = *(const bf16x8*)(x + off);
+      if (RES) r[u] = *(const bf16x8*)(res + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = bf2f(v[u][k]) * sc[k] + sh[k];
+        if (RES) z += bf2f(r[u][k]);
+        o[k] = f2bf(act_f(z, ACT, slope));
+      }
+      *(bf16x8*)(y + (size_t)(m + u * step) * C + t.c0) = o;
+    }
+  }
+  for (; m < M; m += step) {
+    const size_t off = (size_t)m * C + t.c0;
+    const bf16x8 v = *(const bf16x8*)(x + off);
     bf16x8 r;
-    if (res) r = *(const bf16x8*)(res + i * 8);
-    const f32x4 sc0 = *(const f32x4*)(scale + c0), sc1 = *(const f32x4*)(scale + c0 + 4);
-    const f32x4 sh0 = *(const f32x4*)(shift + c0), sh1 = *(const f32x4*)(shift + c0 + 4);
+    if (RES) r = *(const bf16x8*)(res + off);
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float sc = k < 4 ? sc0[k] : sc1[k - 4];
-      const float sh = k < 4 ? sh0[k] : sh1[k - 4];
-      float z = bf2f(v[k]) * sc + sh;
-      if (res) z += bf2f(r[k]);
-      o[k] = f2bf(act_f(z, act, slope));
+      float z = bf2f(v[k]) * sc[k] + sh[k];
+      if (RES) z += bf2f(r[k]);
+      o[k] = f2bf(act_f(z, ACT, slope));
     }
-    *(bf16x8*)(y + i * 8) = o;
+    *(bf16x8*)(y + off) = o;
   }
 }
 
 // sums over rows of dz = dy*act'(z) and dz*xhat  -> out[2][C] (atomic, zeroed by caller)
+template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const bf16* __restrict__ res,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int M, int C,
-                                                            int act, float slope, float* __restrict__ out) {
-  const int cpr = C >> 3;
-  const int rpi = 256 / cpr;
-  const int slot = threadIdx.x / cpr;
-  const int ch = threadIdx.x - slot * cpr;
-  const int c0 = ch * 8;
+                                                            float slope, float* __restrict__ out) {
+  const RowTile t(C);
   float s1[8], s2[8], sc[8], sh[8], mu[8], is[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    s1[k] = s2[k] = 0.f;
-    sc[k] = scale[c0 + k];
-    sh[k] = shift[c0 + k];
-    mu[k] = mean[c0 + k];
-    is[k] = invstd[c0 + k];
-  }
-  if (slot < rpi) {
-    for (int m = blockIdx.x * rpi + slot; m < M; m += gridDim.x * rpi) {
-      const size_t off = (size_t)m * C + c0;
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+  load8(scale + t.c0, sc);
+  load8(shift + t.c0, sh);
+  load8(mean + t.c0, mu);
+  load8(invstd + t.c0, is);
+  if (t.slot < t.rpi) {
+    const int step = gridDim.x * t.rpi;
+    int m = blockIdx.x * t.rpi + t.slot;
+    constexpr int U = 4;
+    for (; m + (U - 1) * step < M; m += U * step) {
+      bf16x8 g[U], v[U], r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t off = (size_t)(m + u * step) * C + t.c0;
+        g[u] = *(const bf16x8*)(dy + off);
+        v[u] = *(const bf16x8*)(x + off);
+        if (RES) r[u] = *(const bf16x8*)(res + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xv = bf2f(v[u][k]);
+          float z = xv * sc[k] + sh[k];
+          if (RES) z += bf2f(r[u][k]);
+          const float dz = bf2f(g[u][k]) * act_d(z, ACT, slope);
+          s1[k] += dz;
+          s2[k] += dz * (xv - mu[k]);
+        }
+    }
+    for (; m < M; m += step) {
+      const size_t off = (size_t)m * C + t.c0;
       const bf16x8 g = *(const bf16x8*)(dy + off);
       const bf16x8 v = *(const bf16x8*)(x + off);
       bf16x8 r;
-      if (res) r = *(const bf16x8*)(res + off);
+      if (RES) r = *(const bf16x8*)(res + off);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float xv = bf2f(v[k]);
         float z = xv * sc[k] + sh[k];
-        if (res) z += bf2f(r[k]);
-        const float dz = bf2f(g[k]) * act_d(z, act, slope);
+        if (RES) z += bf2f(r[k]);
+        const float dz = bf2f(g[k]) * act_d(z, ACT, slope);
         s1[k] += dz;
-        s2[k] += dz * (xv - mu[k]) * is[k];
+        s2[k] += dz * (xv - mu[k]);
       }
     }
   }
@@ -222,63 +288,99 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restri
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     sh_red[threadIdx.x * 8 + k] = s1[k];
-    sh_red[2048 + threadIdx.x * 8 + k] = s2[k];
+    sh_red[2048 + threadIdx.x * 8 + k] = s2[k] * is[k];
   }
   __syncthreads();
-  if (slot == 0) {
+  if (t.slot == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float t1 = 0.f, t2 = 0.f;
-      for (int s = 0; s < rpi; ++s) {
-        t1 += sh_red[(s * cpr + ch) * 8 + k];
-        t2 += sh_red[2048 + (s * cpr + ch) * 8 + k];
+      for (int s = 0; s < t.rpi; ++s) {
+        t1 += sh_red[(s * t.cpr + t.ch) * 8 + k];
+        t2 += sh_red[2048 + (s * t.cpr + t.ch) * 8 + k];
       }
-      atomicAdd(out + c0 + k, t1);
-      atomicAdd(out + C + c0 + k, t2);
+      atomicAdd(out + t.c0 + k, t1);
+      atomicAdd(out + C + t.c0 + k, t2);
     }
   }
 }
 
-// dx = scale*(dz - sum_dz/count - xhat*sum_dzxhat/count)  [stats=true]
-// dx = scale*dz                                            [stats=false: eval/frozen BN]
+// dx = scale*(dz - sum_dz/count - xhat*sum_dzxhat/count)  [sums != nullptr]
+//    = a*dz + b*x + c  with per-channel a, b, c folded once per thread
+// dx = scale*dz                                            [eval / frozen BN]
 // dres = dz (if dres != nullptr)
+template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ res,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
-                                                           const float* __restrict__ sums, float inv_count,
-                                                           size_t nchunks, int C, int act, float slope,
-                                                           bf16* __restrict__ dx, bf16* __restrict__ dres) {
-  const int cpr = C >> 3;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cpr) * 8;
-    const bf16x8 g = *(const bf16x8*)(dy + i * 8);
-    const bf16x8 v = *(const bf16x8*)(x + i * 8);
-    bf16x8 r;
-    if (res) r = *(const bf16x8*)(res + i * 8);
+                                                           const float* __restrict__ sums, float inv_count, int M,
+                                                           int C, float slope, bf16* __restrict__ dx,
+                                                           bf16* __restrict__ dres) {
+  const RowTile t(C);
+  if (t.slot >= t.rpi) return;
+  float sc[8], sh[8], ca[8], cb[8], cc[8];
+  load8(scale + t.c0, sc);
+  load8(shift + t.c0, sh);
+  if (sums) {
+    float mu[8], is[8], k2[8], k3[8];
+    load8(mean + t.c0, mu);
+    load8(invstd + t.c0, is);
+    load8(sums + t.c0, k2);
+    load8(sums + C + t.c0, k3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a2 = k2[k] * inv_count, a3 = k3[k] * inv_count * is[k];
+      ca[k] = sc[k];
+      cb[k] = -sc[k] * a3;
+      cc[k] = -sc[k] * a2 + sc[k] * a3 * mu[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ca[k] = sc[k];
+      cb[k] = 0.f;
+      cc[k] = 0.f;
+    }
+  }
+  const int step = gridDim.x * t.rpi;
+  int m = blockIdx.x * t.rpi + t.slot;
+  constexpr int U = 4;
+  auto body = [&](const bf16x8& g, const bf16x8& v, const bf16x8& r, size_t off) {
     bf16x8 o, od;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
       const float xv = bf2f(v[k]);
-      const float sc = scale[c];
-      float z = xv * sc + shift[c];
-      if (res) z += bf2f(r[k]);
-      const float dz = bf2f(g[k]) * act_d(z, act, slope);
+      float z = xv * sc[k] + sh[k];
+      if (RES) z += bf2f(r[k]);
+      const float dz = bf2f(g[k]) * act_d(z, ACT, slope);
       od[k] = f2bf(dz);
-      float d;
-      if (sums) {
-        const float xh = (xv - mean[c]) * invstd[c];
-        d = sc * (dz - sums[c] * inv_count - xh * sums[C + c] * inv_count);
-      } else {
-        d = sc * dz;
-      }
-      o[k] = f2bf(d);
+      o[k] = f2bf(ca[k] * dz + cb[k] * xv + cc[k]);
     }
-    *(bf16x8*)(dx + i * 8) = o;
-    if (dres) *(bf16x8*)(dres + i * 8) = od;
+    *(bf16x8*)(dx + off) = o;
+    if (dres) *(bf16x8*)(dres + off) = od;
+  };
+  for (; m + (U - 1) * step < M; m += U * step) {
+    bf16x8 g[U], v[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = (size_t)(m + u * step) * C + t.c0;
+      g[u] = *(const bf16x8*)(dy + off);
+      v[u] = *(const bf16x8*)(x + off);
+      if (RES) r[u] = *(const bf16x8*)(res + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(g[u], v[u], r[u], (size_t)(m + u * step) * C + t.c0);
+  }
+  for (; m < M; m += step) {
+    const size_t off = (size_t)m * C + t.c0;
+    const bf16x8 g = *(const bf16x8*)(dy + off);
+    const bf16x8 v = *(const bf16x8*)(x + off);
+    bf16x8 r;
+    if (RES) r = *(const bf16x8*)(res + off);
+    body(g, v, r, off);
   }
 }
 
@@ -325,31 +427,57 @@ void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* bet
                      mean, invstd, scale, shift);
 }
 
+static inline int rows_grid(int M, int C, int rows_per_thread, int cap) {
+  const int rpi = 256 / (C / 8);
+  long g = ((long)M + (long)rpi * rows_per_thread - 1) / ((long)rpi * rows_per_thread);
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define DCP_ACT_RES_DISPATCH(KERNEL, GRID, SHMEM, STREAM, RESPTR, ACTV, ...)                        \
+  do {                                                                                              \
+    const bool has_res = (RESPTR) != nullptr;                                                       \
+    if (ACTV == ACT_RELU) {                                                                         \
+      if (has_res)                                                                                  \
+        hipLaunchKernelGGL((KERNEL<ACT_RELU, true>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__);  \
+      else                                                                                          \
+        hipLaunchKernelGGL((KERNEL<ACT_RELU, false>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__); \
+    } else if (ACTV == ACT_LEAKY) {                                                                 \
+      if (has_res)                                                                                  \
+        hipLaunchKernelGGL((KERNEL<ACT_LEAKY, true>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__); \
+      else                                                                                          \
+        hipLaunchKernelGGL((KERNEL<ACT_LEAKY, false>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__);\
+    } else {                                                                                        \
+      if (has_res)                                                                                  \
+        hipLaunchKernelGGL((KERNEL<ACT_NONE, true>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__);  \
+      else                                                                                          \
+        hipLaunchKernelGGL((KERNEL<ACT_NONE, false>), GRID, dim3(256), SHMEM, STREAM, __VA_ARGS__); \
+    }                                                                                               \
+  } while (0)
+
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
                        size_t numel, int C, int act, float slope, hipStream_t s) {
-  const size_t n = numel / 8;
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid(n)), dim3(256), 0, s, x, res, scale, shift, y, n, C, act,
-                     slope);
+  const int M = (int)(numel / C);
+  const dim3 grid(rows_grid(M, C, 8, 4096));
+  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope);
 }
 
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* out,
                           hipStream_t s) {
-  const int cpr = C / 8;
-  const int rpi = 256 / cpr;
-  int grid = (M + rpi * 8 - 1) / (rpi * 8);
-  if (grid > 1024) grid = 1024;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(grid), dim3(256), 2 * 2048 * 4, s, dy, x, res, scale, shift, mean,
-                     invstd, M, C, act, slope, out);
+  const dim3 grid(rows_grid(M, C, 16, 2048));
+  DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, grid, 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean, invstd,
+                       M, C, slope, out);
 }
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
                          int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s) {
-  const size_t n = numel / 8;
-  hipLaunchKernelGGL(bn_bwd_elemt_kernel, dim3(ew_grid(n)), dim3(256), 0, s, dy, x, res, scale, shift, mean, invstd,
-                     sums, inv_count, n, C, act, slope, dx, dres);
+  const int M = (int)(numel / C);
+  const dim3 grid(rows_grid(M, C, 8, 4096));
+  DCP_ACT_RES_DISPATCH(bn_bwd_elemt_kernel, grid, 0, s, res, act, dy, x, res, scale, shift, mean, invstd, sums,
+                       inv_count, M, C, slope, dx, dres);
 }
 
 }  // namespace dcp
