@@ -274,44 +274,48 @@ Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t
 // ---------------------------------------------------------------------------
 // batch norm
 // ---------------------------------------------------------------------------
-// per-channel totals [2,C] from conv slabs (if given) or directly from x
+// per-channel (n, mean, M2) [1,3,C] from conv slabs (if given) or directly from x
 Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
-  auto tot = at::zeros({2, C}, f32_like(x));
-  if (slabs.has_value() && slabs->numel() > 0) {
-    TORCH_CHECK(slabs->dim() == 3 && slabs->size(1) == 2 && slabs->size(2) == C, "slab shape");
-    dcp::launch_bn_slab_reduce(slabs->data_ptr<float>(), slabs->size(0), C, tot.data_ptr<float>(), cur_stream());
-  } else {
-    dcp::launch_chan_stats(bp(x), M, C, true, tot.data_ptr<float>(), cur_stream());
-  }
-  return tot;
+  const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
+  if (from_slabs)
+    TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 63) / 64 && slabs->size(1) == 2 && slabs->size(2) == C,
+                "slab shape");
+  auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
+  auto out = at::empty({1, 3, C}, f32_like(x));
+  dcp::launch_bn_stats(bp(x), from_slabs ? slabs->data_ptr<float>() : nullptr, M, C, part.data_ptr<float>(),
+                       out.data_ptr<float>(), cur_stream());
+  return out;
 }
 
 Tensor colsum(const Tensor& x) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   TORCH_CHECK(C % 8 == 0, "colsum channels");
-  auto tot = at::zeros({2, C}, f32_like(x));
-  dcp::launch_chan_stats(bp(x), x.numel() / C, C, false, tot.data_ptr<float>(), cur_stream());
-  return tot[0];
+  const int M = x.numel() / C;
+  auto part = at::empty({dcp::colsum_partials(M), C}, f32_like(x));
+  auto out = at::empty({C}, f32_like(x));
+  dcp::launch_colsum(bp(x), M, C, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  return out;
 }
 
-// -> (mean, invstd, scale, shift); updates running stats in place when given
-std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(const Tensor& tot, double count,
-                                                       const optional<Tensor>& gamma,
+// stats [W,3,C] (n, mean, M2 per rank) -> (mean, invstd, scale, shift); updates running stats in place
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(const Tensor& st, const optional<Tensor>& gamma,
                                                        const optional<Tensor>& beta,
                                                        const optional<Tensor>& run_mean,
                                                        const optional<Tensor>& run_var, double momentum,
                                                        double eps) {
-  CHECK_DEV(tot);
-  CHECK_F32(tot);
-  const int C = tot.size(1);
-  auto mean = at::empty({C}, tot.options()), invstd = at::empty({C}, tot.options());
-  auto scale = at::empty({C}, tot.options()), shift = at::empty({C}, tot.options());
-  dcp::launch_bn_finalize(tot.data_ptr<float>(), count, C, (float)eps, fp(gamma), fp(beta), mean.data_ptr<float>(),
+  CHECK_DEV(st);
+  CHECK_F32(st);
+  CHECK_CONTIG(st);
+  TORCH_CHECK(st.dim() == 3 && st.size(1) == 3, "stats must be [W,3,C]");
+  const int W = st.size(0), C = st.size(2);
+  auto mean = at::empty({C}, st.options()), invstd = at::empty({C}, st.options());
+  auto scale = at::empty({C}, st.options()), shift = at::empty({C}, st.options());
+  dcp::launch_bn_finalize(st.data_ptr<float>(), W, C, (float)eps, fp(gamma), fp(beta), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), fpm(run_mean),
                           fpm(run_var), (float)momentum, cur_stream());
   return {mean, invstd, scale, shift};
@@ -350,10 +354,13 @@ Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& 
   CHECK_ACT(x);
   const int C = x.size(-1);
   TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_reduce shapes");
-  auto out = at::zeros({2, C}, f32_like(x));
+  if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "residual shape");
+  const int M = x.numel() / C;
+  auto part = at::empty({dcp::bn_bwd_reduce_blocks(M, C), 2, C}, f32_like(x));
+  auto out = at::empty({2, C}, f32_like(x));
   dcp::launch_bn_bwd_reduce(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
-                            shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), x.numel() / C,
-                            C, act, (float)slope, out.data_ptr<float>(), cur_stream());
+                            shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, C, act,
+                            (float)slope, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
   return out;
 }
 
@@ -695,8 +702,8 @@ TORCH_LIBRARY(dcp, m) {
   m.def("bn_stats(Tensor x, Tensor? slabs) -> Tensor", &bn_stats);
   m.def("colsum(Tensor x) -> Tensor", &colsum);
   m.def(
-      "bn_finalize(Tensor tot, float count, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, "
-      "float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      "bn_finalize(Tensor stats, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, float momentum, "
+      "float eps) -> (Tensor, Tensor, Tensor, Tensor)",
       &bn_finalize);
   m.def(
       "bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor run_mean, Tensor run_var, float eps) -> (Tensor, Tensor, "

@@ -6,14 +6,20 @@
 // ARCFACE/arc_main.py:239; SURVEY.md §2.2 X5, kernels K4-K7) and the
 // InplaceABN BN+leaky-ReLU of timm's TResNet (X3, K21).
 //
+// Statistics are carried as (count, mean, M2) and combined with Chan's
+// parallel-variance formula at every level, never as (sum, sumsq): deep
+// ResNets feed BN inputs whose mean is large against their spread (post-ReLU
+// inputs to 1x1 convs) and E[x^2]-E[x]^2 in fp32 loses the variance.
 // Pipeline per BN layer (training):
-//   conv epilogue  -> per-64-row partial (sum, sumsq) slabs      (conv_igemm.hip)
-//   bn_slab_reduce -> per-channel totals [2][C]    (+ all_reduce for SyncBN)
-//   bn_finalize    -> mean, invstd, scale, shift; running-stat update
-//   bn_act_fwd     -> y = act(x*scale + shift [+ residual])
+//   conv epilogue    -> per-64-row tile (mean, M2) slabs            (conv_igemm.hip)
+//   bn_slab_partial  -> per-split (n, mean, M2) partials  } bn_stats -> [1][3][C]
+//   bn_merge         -> one (n, mean, M2) per channel     }   (SyncBN: all_gather -> [W][3][C])
+//   bn_finalize      -> merge W entries; mean, invstd, scale, shift; running-stat update
+//   bn_act_fwd       -> y = act(x*scale + shift [+ residual])
 // backward:
-//   bn_bwd_reduce  -> sum(dz), sum(dz*xhat)         (+ all_reduce for SyncBN)
-//   bn_bwd_elemt   -> dx (and d(residual) = dz)
+//   bn_bwd_reduce    -> per-workgroup partial (sum dz, sum dz*xhat) -> partial_sum -> [2][C]
+//                       (+ all_reduce for SyncBN)
+//   bn_bwd_elemt     -> dx (and d(residual) = dz)
 // The activation mask is recomputed from x (and the residual) instead of
 // saving the post-activation tensor.
 #include "common.cuh"
@@ -34,83 +40,123 @@ __device__ __forceinline__ float act_d(float z, int act, float slope) {
   return 1.f;
 }
 
-// slabs [R][2][C] -> out [2][C] (atomic accumulate; out zeroed by caller)
-__global__ void bn_slab_reduce_kernel(const float* __restrict__ slabs, int R, int C,
-                                      int rows_per_block, float* __restrict__ out) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;  // 4 waves
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(R, r0 + rows_per_block);
-  float s1 = 0.f, s2 = 0.f;
+// Chan et al. pairwise merge of (n, mean, M2) accumulators
+struct Welford {
+  float n, mean, m2;
+  __device__ __forceinline__ void merge(float nb, float meanb, float m2b) {
+    if (nb <= 0.f) return;
+    const float nt = n + nb;
+    const float d = meanb - mean;
+    const float f = nb / nt;
+    mean += d * f;
+    m2 += m2b + d * d * n * f;
+    n = nt;
+  }
+};
+
+// conv slabs [R][2][C] = per-64-row tile (mean, M2); tile r holds min(64, M-64r) rows.
+// out[blockIdx.y][3][C] = (n, mean, M2) over this split's tiles.
+__global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __restrict__ slabs, int R, int M, int C,
+                                                              int tiles_per_split, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * tiles_per_split;
+  const int r1 = min(R, r0 + tiles_per_split);
+  Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     for (int r = r0 + w; r < r1; r += 4) {
-      s1 += slabs[((size_t)r * 2 + 0) * C + c];
-      s2 += slabs[((size_t)r * 2 + 1) * C + c];
+      const float nb = (float)min(64, M - 64 * r);
+      a.merge(nb, slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
     }
   }
-  __shared__ float red[2][4][64];
-  red[0][w][threadIdx.x & 63] = s1;
-  red[1][w][threadIdx.x & 63] = s2;
+  __shared__ float red[3][4][64];
+  red[0][w][lane] = a.n;
+  red[1][w][lane] = a.mean;
+  red[2][w][lane] = a.m2;
   __syncthreads();
   if (w == 0 && c < C) {
-    const int l = threadIdx.x & 63;
-    const float t1 = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
-    const float t2 = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
-    atomicAdd(out + c, t1);
-    atomicAdd(out + C + c, t2);
+    for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+    out[((size_t)blockIdx.y * 3 + 0) * C + c] = a.n;
+    out[((size_t)blockIdx.y * 3 + 1) * C + c] = a.mean;
+    out[((size_t)blockIdx.y * 3 + 2) * C + c] = a.m2;
   }
 }
 
-// Generic per-channel (sum, sumsq) of a [M][C] bf16 tensor -> out[2][C] (atomic).
-// Used where the producer is not one of our conv kernels (pool outputs,
-// grouped convs, heads).
-template <bool SQ>
-__global__ void __launch_bounds__(256) chan_stats_kernel(const bf16* __restrict__ x, int M, int C,
-                                                         float* __restrict__ out) {
-  // blockIdx.y selects a window of <= 2048 channels so any C (multiple of 8) works
-  const int cbase = blockIdx.y * 2048;
-  const int Cw = min(2048, C - cbase);
-  const int cpr = Cw >> 3;                // 8-channel chunks per row in this window
-  const int rpi = 256 / cpr;              // rows per iteration
-  const int slot = threadIdx.x / cpr;
-  const int ch = threadIdx.x - slot * cpr;
-  float s1[8], s2[8];
+// raw activations [M][C] -> out[blockIdx][3][C] (n, mean, M2).  Each thread
+// accumulates sums shifted by its first observed value (a per-channel
+// estimate of the mean), converts to (n, mean, M2), then the workgroup's row
+// slots are merged with Chan's formula.
+__global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* __restrict__ x, int M, int C,
+                                                                   float* __restrict__ out) {
+  const int cpr = C >> 3, rpi = 256 / cpr;
+  const int slot = threadIdx.x / cpr, ch = threadIdx.x - slot * cpr, c0 = ch * 8;
+  float n = 0.f, sh[8], s1[8], s2[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-  if (slot < rpi) {
-    for (int m = blockIdx.x * rpi + slot; m < M; m += gridDim.x * rpi) {
-      const bf16x8 v = *(const bf16x8*)(x + (size_t)m * C + cbase + ch * 8);
+  for (int k = 0; k < 8; ++k) sh[k] = s1[k] = s2[k] = 0.f;
+  const int first = blockIdx.x * rpi + slot;
+  if (slot < rpi && first < M) {
+    const bf16x8 v0 = *(const bf16x8*)(x + (size_t)first * C + c0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[k] = bf2f(v0[k]);
+    for (int m = first; m < M; m += gridDim.x * rpi) {
+      const bf16x8 v = *(const bf16x8*)(x + (size_t)m * C + c0);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float f = bf2f(v[k]);
-        s1[k] += f;
-        if (SQ) s2[k] += f * f;
+        const float d = bf2f(v[k]) - sh[k];
+        s1[k] += d;
+        s2[k] += d * d;
       }
+      n += 1.f;
     }
   }
-  extern __shared__ float sh[];  // [256][8] x 2
+  extern __shared__ float shm[];  // [3][256][8]
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    sh[threadIdx.x * 8 + k] = s1[k];
-    sh[2048 + threadIdx.x * 8 + k] = s2[k];
+    const float mean = n > 0.f ? sh[k] + s1[k] / n : 0.f;
+    const float m2 = n > 0.f ? fmaxf(s2[k] - s1[k] * s1[k] / n, 0.f) : 0.f;
+    shm[threadIdx.x * 8 + k] = n;
+    shm[2048 + threadIdx.x * 8 + k] = mean;
+    shm[4096 + threadIdx.x * 8 + k] = m2;
   }
   __syncthreads();
   if (slot == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float t1 = 0.f, t2 = 0.f;
-      for (int s = 0; s < rpi; ++s) {
-        t1 += sh[(s * cpr + ch) * 8 + k];
-        t2 += sh[2048 + (s * cpr + ch) * 8 + k];
+      Welford a{0.f, 0.f, 0.f};
+      for (int sl = 0; sl < rpi; ++sl) {
+        const int t = (sl * cpr + ch) * 8 + k;
+        a.merge(shm[t], shm[2048 + t], shm[4096 + t]);
       }
-      atomicAdd(out + cbase + ch * 8 + k, t1);
-      if (SQ) atomicAdd(out + C + cbase + ch * 8 + k, t2);
+      out[((size_t)blockIdx.x * 3 + 0) * C + c0 + k] = a.n;
+      out[((size_t)blockIdx.x * 3 + 1) * C + c0 + k] = a.mean;
+      out[((size_t)blockIdx.x * 3 + 2) * C + c0 + k] = a.m2;
     }
   }
 }
 
-// totals [2][C], count -> mean, invstd, scale, shift (+ running stats update)
-__global__ void bn_finalize_kernel(const float* __restrict__ tot, double count, int C, float eps,
+// partials [P][3][C] -> out [3][C]
+__global__ void bn_merge_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  Welford a{0.f, 0.f, 0.f};
+  for (int p = 0; p < P; ++p)
+    a.merge(part[((size_t)p * 3 + 0) * C + c], part[((size_t)p * 3 + 1) * C + c], part[((size_t)p * 3 + 2) * C + c]);
+  out[c] = a.n;
+  out[C + c] = a.mean;
+  out[2 * C + c] = a.m2;
+}
+
+// [P][K] -> [K] column sums (deterministic second stage of the backward reduction / colsum)
+__global__ void partial_sum_kernel(const float* __restrict__ part, int P, int K, float* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * K + k];
+  out[k] = s;
+}
+
+// stats [W][3][C] (one (n, mean, M2) per rank) -> mean, invstd, scale, shift (+ running stats)
+__global__ void bn_finalize_kernel(const float* __restrict__ st, int W, int C, float eps,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ mean, float* __restrict__ invstd,
                                    float* __restrict__ scale, float* __restrict__ shift,
@@ -118,20 +164,21 @@ __global__ void bn_finalize_kernel(const float* __restrict__ tot, double count, 
                                    float momentum) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double mu = (double)tot[c] / count;
-  double var = (double)tot[C + c] / count - mu * mu;
-  if (var < 0.0) var = 0.0;
-  const float is = (float)(1.0 / sqrt(var + (double)eps));
-  mean[c] = (float)mu;
+  Welford a{0.f, 0.f, 0.f};
+  for (int w = 0; w < W; ++w)
+    a.merge(st[((size_t)w * 3 + 0) * C + c], st[((size_t)w * 3 + 1) * C + c], st[((size_t)w * 3 + 2) * C + c]);
+  const float var = a.n > 0.f ? a.m2 / a.n : 0.f;
+  const float is = rsqrtf(var + eps);
+  mean[c] = a.mean;
   invstd[c] = is;
   const float g = gamma ? gamma[c] : 1.f;
   const float b = beta ? beta[c] : 0.f;
   scale[c] = g * is;
-  shift[c] = b - (float)mu * g * is;
+  shift[c] = b - a.mean * g * is;
   if (run_mean) {
-    const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mu;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    const float unb = a.n > 1.f ? a.m2 / (a.n - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * a.mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
   }
 }
 
@@ -150,6 +197,35 @@ __global__ void bn_eval_coeff_kernel(int C, float eps, const float* __restrict__
   invstd[c] = is;
   scale[c] = g * is;
   shift[c] = b - rm[c] * g * is;
+}
+
+// plain column sums of [M][C] -> per-workgroup partials out[blockIdx][C]
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16* __restrict__ x, int M, int C,
+                                                             float* __restrict__ out) {
+  const int cbase = blockIdx.y * 2048;
+  const int Cw = min(2048, C - cbase);
+  const int cpr = Cw >> 3, rpi = 256 / cpr;
+  const int slot = threadIdx.x / cpr, ch = threadIdx.x - slot * cpr;
+  float s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = 0.f;
+  if (slot < rpi)
+    for (int m = blockIdx.x * rpi + slot; m < M; m += gridDim.x * rpi) {
+      const bf16x8 v = *(const bf16x8*)(x + (size_t)m * C + cbase + ch * 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s1[k] += bf2f(v[k]);
+    }
+  __shared__ float sh[2048];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = s1[k];
+  __syncthreads();
+  if (slot == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = 0.f;
+      for (int sl = 0; sl < rpi; ++sl) t += sh[(sl * cpr + ch) * 8 + k];
+      out[(size_t)blockIdx.x * C + cbase + ch * 8 + k] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -225,7 +301,8 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
   }
 }
 
-// sums over rows of dz = dy*act'(z) and dz*xhat  -> out[2][C] (atomic, zeroed by caller)
+// sums over rows of dz = dy*act'(z) and dz*xhat -> per-workgroup partials out[blockIdx][2][C]
+// (deterministic; summed by partial_sum_kernel -- no contended atomics)
 template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const bf16* __restrict__ res,
@@ -299,8 +376,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restri
         t1 += sh_red[(s * t.cpr + t.ch) * 8 + k];
         t2 += sh_red[2048 + (s * t.cpr + t.ch) * 8 + k];
       }
-      atomicAdd(out + t.c0 + k, t1);
-      atomicAdd(out + C + t.c0 + k, t2);
+      out[((size_t)blockIdx.x * 2 + 0) * C + t.c0 + k] = t1;
+      out[((size_t)blockIdx.x * 2 + 1) * C + t.c0 + k] = t2;
     }
   }
 }
@@ -384,40 +461,50 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
   }
 }
 
+
 // ---------------------------------------------------------------------------
-static inline int ew_grid(size_t n, int block = 256) {
-  size_t g = (n + block - 1) / block;
-  if (g > 4096) g = 4096;
-  if (g < 1) g = 1;
-  return (int)g;
+int bn_stats_partials(int M, int C, bool from_slabs) {
+  if (from_slabs) {
+    const int R = (M + 63) / 64;
+    int splits = (R + 31) / 32;
+    return splits > 64 ? 64 : (splits < 1 ? 1 : splits);
+  }
+  const int rpi = 256 / (C / 8);
+  int g = (M + rpi * 32 - 1) / (rpi * 32);
+  return g > 256 ? 256 : (g < 1 ? 1 : g);
 }
 
-void launch_bn_slab_reduce(const float* slabs, int R, int C, float* out, hipStream_t s) {
-  int splits = (R + 255) / 256;
-  if (splits > 128) splits = 128;
-  if (splits < 1) splits = 1;
-  const int rpb = (R + splits - 1) / splits;
-  hipLaunchKernelGGL(bn_slab_reduce_kernel, dim3((C + 63) / 64, splits), dim3(256), 0, s, slabs, R, C, rpb, out);
+// part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
+void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
+  if (slabs) {
+    const int R = (M + 63) / 64;
+    const int P = bn_stats_partials(M, C, true);
+    const int tps = (R + P - 1) / P;
+    hipLaunchKernelGGL(bn_slab_partial_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps, part);
+    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+  } else {
+    const int P = bn_stats_partials(M, C, false);
+    hipLaunchKernelGGL(chan_welford_partial_kernel, dim3(P), dim3(256), 3 * 2048 * 4, s, x, M, C, part);
+    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+  }
 }
 
-void launch_chan_stats(const bf16* x, int M, int C, bool sq, float* out, hipStream_t s) {
-  const int cpr = (C < 2048 ? C : 2048) / 8;
-  const int rpi = 256 / cpr;
-  const int ny = (C + 2047) / 2048;
-  int grid = (M + rpi * 8 - 1) / (rpi * 8);
-  if (grid > 1024) grid = 1024;
-  if (grid < 1) grid = 1;
-  if (sq)
-    hipLaunchKernelGGL(chan_stats_kernel<true>, dim3(grid, ny), dim3(256), 2 * 2048 * 4, s, x, M, C, out);
-  else
-    hipLaunchKernelGGL(chan_stats_kernel<false>, dim3(grid, ny), dim3(256), 2 * 2048 * 4, s, x, M, C, out);
+int colsum_partials(int M) {
+  int g = (M + 255) / 256;
+  return g > 128 ? 128 : (g < 1 ? 1 : g);
 }
 
-void launch_bn_finalize(const float* tot, double count, int C, float eps, const float* gamma, const float* beta,
-                        float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
-                        float momentum, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, tot, count, C, eps, gamma, beta,
-                     mean, invstd, scale, shift, rm, rv, momentum);
+void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s) {
+  const int P = colsum_partials(M);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(P, (C + 2047) / 2048), dim3(256), 0, s, x, M, C, part);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+}
+
+void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
+                        float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, st, W, C, eps, gamma, beta, mean,
+                     invstd, scale, shift, rm, rv, momentum);
 }
 
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm,
@@ -463,12 +550,16 @@ void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const
   DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope);
 }
 
+int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }
+
+// partials must hold bn_bwd_reduce_blocks(M, C) x 2 x C floats; out [2][C]
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
-                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* out,
-                          hipStream_t s) {
-  const dim3 grid(rows_grid(M, C, 16, 2048));
-  DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, grid, 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean, invstd,
-                       M, C, slope, out);
+                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,
+                          float* out, hipStream_t s) {
+  const int g = bn_bwd_reduce_blocks(M, C);
+  DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, dim3(g), 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean,
+                       invstd, M, C, slope, partials);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, partials, g, 2 * C, out);
 }
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,

@@ -37,7 +37,7 @@ struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
   const bf16* wt;    // [Co][T][Cs]
   bf16* dst;         // [N][Hd][Wd][Co]
-  float* stats;      // [ceil(M/64)][2][Co] partial (sum, sumsq) or nullptr
+  float* stats;      // [ceil(M/64)][2][Co] per-64-row tile (mean, M2) or nullptr
   const bf16* zero;  // >= 16 bytes of zeros
   int Hs, Ws, Cs;
   int Hy, Wy, ss;
@@ -242,27 +242,50 @@ tap_gemm_kernel(const TapGemmParams p) {
       if (mok && co < p.Co) *(bf16x4*)(p.dst + drow + co) = o;
       if (p.stats) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float q = mok ? bf2f(o[r]) : 0.f;
-          s1[j][r] += q;
-          s2[j][r] += q * q;
-        }
+        for (int r = 0; r < 4; ++r) s1[j][r] += mok ? bf2f(o[r]) : 0.f;
       }
     }
   }
   if (p.stats) {
+    // Per 64-row wave tile and channel: (mean, M2) with M2 around the tile mean
+    // (two passes over the register-resident tile), merged later with Chan's
+    // formula -- no E[x^2]-E[x]^2 cancellation.
+    const int nvalid = min(64, p.M - (m0 + wm * 64));
+    const float inv_n = nvalid > 0 ? 1.f / nvalid : 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-          s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+        for (int o = 1; o < 16; o <<= 1) s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+        s1[j][r] *= inv_n;  // tile mean
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      const bool mok = m < p.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = co_lane + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[j][i][r];
+          if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
+          if (p.relu) t = fmaxf(t, 0.f);
+          const float d = bf2f(f2bf(t)) - s1[j][r];
+          s2[j][r] += mok ? d * d : 0.f;
         }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      }
     const int rb = m0 / 64 + wm;
-    if ((lane & 15) == 0 && (m0 + wm * 64) < p.M) {
+    if ((lane & 15) == 0 && nvalid > 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int co = co_lane + j * 16;

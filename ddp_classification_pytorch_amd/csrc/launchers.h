@@ -27,18 +27,21 @@ void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, i
 void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Ho, int Wo,
                                int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
 
-void launch_bn_slab_reduce(const float* slabs, int R, int C, float* out, hipStream_t s);
-void launch_chan_stats(const bf16* x, int M, int C, bool sq, float* out, hipStream_t s);
-void launch_bn_finalize(const float* tot, double count, int C, float eps, const float* gamma, const float* beta,
-                        float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
+int bn_stats_partials(int M, int C, bool from_slabs);
+void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s);
+int colsum_partials(int M);
+void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s);
+void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
+                        float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
                         hipStream_t s);
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                           float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
                        int C, int act, float slope, hipStream_t s);
+int bn_bwd_reduce_blocks(int M, int C);
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
-                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* out,
-                          hipStream_t s);
+                          const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,
+                          float* out, hipStream_t s);
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
                          int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s);

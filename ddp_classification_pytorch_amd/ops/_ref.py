@@ -117,25 +117,32 @@ def _rows(x):
 
 
 def bn_stats(x, slabs):
-    r = _rows(x)
-    return torch.stack([r.sum(0), (r * r).sum(0)])
+    """-> [1, 3, C] = (n, mean, M2) per channel."""
+    r = x.double().reshape(-1, x.shape[-1])
+    n = r.shape[0]
+    mean = r.mean(0)
+    m2 = ((r - mean) ** 2).sum(0)
+    return torch.stack([torch.full_like(mean, float(n)), mean, m2]).float().unsqueeze(0)
 
 
 def colsum(x):
     return _rows(x).sum(0)
 
 
-def bn_finalize(tot, count, gamma, beta, run_mean, run_var, momentum, eps):
-    tot = tot.double()
-    mu = tot[0] / count
-    var = (tot[1] / count - mu * mu).clamp_min(0)
+def bn_finalize(stats, gamma, beta, run_mean, run_var, momentum, eps):
+    """stats [W,3,C] (n, mean, M2 per rank) merged with Chan's formula."""
+    st = stats.double()
+    n_t = st[:, 0].sum(0)
+    mu = (st[:, 0] * st[:, 1]).sum(0) / n_t
+    m2 = st[:, 2].sum(0) + (st[:, 0] * (st[:, 1] - mu) ** 2).sum(0)
+    var = m2 / n_t
     invstd = 1.0 / torch.sqrt(var + eps)
     g = gamma.double() if gamma is not None else torch.ones_like(mu)
     b = beta.double() if beta is not None else torch.zeros_like(mu)
     scale = g * invstd
     shift = b - mu * scale
     if run_mean is not None:
-        unb = var * count / (count - 1) if count > 1 else var
+        unb = torch.where(n_t > 1, m2 / (n_t - 1).clamp_min(1), var)
         run_mean.mul_(1 - momentum).add_(momentum * mu.float())
         run_var.mul_(1 - momentum).add_(momentum * unb.float())
     return mu.float(), invstd.float(), scale.float(), shift.float()

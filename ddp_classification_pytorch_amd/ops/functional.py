@@ -190,12 +190,13 @@ class _BNAct(Function):
         C = x.shape[-1]
         count = x.numel() // C
         if cfg.training_stats:
-            tot = k.bn_stats(x, slabs)
+            st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
             if cfg.group is not None:
-                dist.all_reduce(tot, group=cfg.group)
+                gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
+                dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+                st = gathered
                 count = count * cfg.world  # DistributedSampler keeps per-rank batches equal
-            mean, invstd, scale, shift = k.bn_finalize(tot, float(count), gamma, beta, run_mean, run_var,
-                                                       cfg.momentum, cfg.eps)
+            mean, invstd, scale, shift = k.bn_finalize(st, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps)
         else:
             mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
         y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
