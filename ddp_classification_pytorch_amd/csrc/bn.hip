@@ -134,25 +134,49 @@ __global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* _
   }
 }
 
-// partials [P][3][C] -> out [3][C]
-__global__ void bn_merge_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// partials [P][3][C] -> out [3][C]; one workgroup per 64 channels, 4 waves split P
+__global__ void __launch_bounds__(256) bn_merge_kernel(const float* __restrict__ part, int P, int C,
+                                                       float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
-  for (int p = 0; p < P; ++p)
-    a.merge(part[((size_t)p * 3 + 0) * C + c], part[((size_t)p * 3 + 1) * C + c], part[((size_t)p * 3 + 2) * C + c]);
-  out[c] = a.n;
-  out[C + c] = a.mean;
-  out[2 * C + c] = a.m2;
+  if (c < C)
+    for (int p = w; p < P; p += 4)
+      a.merge(part[((size_t)p * 3 + 0) * C + c], part[((size_t)p * 3 + 1) * C + c],
+              part[((size_t)p * 3 + 2) * C + c]);
+  __shared__ float red[3][4][64];
+  red[0][w][lane] = a.n;
+  red[1][w][lane] = a.mean;
+  red[2][w][lane] = a.m2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+    out[c] = a.n;
+    out[C + c] = a.mean;
+    out[2 * C + c] = a.m2;
+  }
 }
 
-// [P][K] -> [K] column sums (deterministic second stage of the backward reduction / colsum)
-__global__ void partial_sum_kernel(const float* __restrict__ part, int P, int K, float* __restrict__ out) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * K + k];
-  out[k] = s;
+// [P][K] -> [K] column sums; one workgroup per 64 columns, 4 waves x 4-deep unroll over P
+__global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restrict__ part, int P, int K,
+                                                          float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (k < K) {
+    int p = w;
+    for (; p + 12 < P; p += 16) {
+      s0 += part[(size_t)p * K + k];
+      s1 += part[(size_t)(p + 4) * K + k];
+      s2 += part[(size_t)(p + 8) * K + k];
+      s3 += part[(size_t)(p + 12) * K + k];
+    }
+    for (; p < P; p += 4) s0 += part[(size_t)p * K + k];
+  }
+  __shared__ float red[4][64];
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && k < K) out[k] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // stats [W][3][C] (one (n, mean, M2) per rank) -> mean, invstd, scale, shift (+ running stats)
@@ -481,11 +505,11 @@ void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* par
     const int P = bn_stats_partials(M, C, true);
     const int tps = (R + P - 1) / P;
     hipLaunchKernelGGL(bn_slab_partial_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps, part);
-    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
   } else {
     const int P = bn_stats_partials(M, C, false);
     hipLaunchKernelGGL(chan_welford_partial_kernel, dim3(P), dim3(256), 3 * 2048 * 4, s, x, M, C, part);
-    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
   }
 }
 
@@ -497,7 +521,7 @@ int colsum_partials(int M) {
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s) {
   const int P = colsum_partials(M);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(P, (C + 2047) / 2048), dim3(256), 0, s, x, M, C, part);
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, P, C, out);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
 }
 
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
@@ -559,7 +583,7 @@ void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const 
   const int g = bn_bwd_reduce_blocks(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, dim3(g), 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean,
                        invstd, M, C, slope, partials);
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, partials, g, 2 * C, out);
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, partials, g, 2 * C, out);
 }
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,

@@ -224,8 +224,8 @@ class _BNAct(Function):
         want_dres = ctx.has_res and ctx.needs_input_grad[4]
         dx, dres = k.bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums if cfg.training_stats else None,
                                   float(ctx.count), cfg.act, cfg.slope, want_dres)
-        dgamma = local[1].clone() if (local is not None and ctx.needs_input_grad[2]) else None
-        dbeta = local[0].clone() if (local is not None and ctx.needs_input_grad[3]) else None
+        dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
+        dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
         return dx, None, dgamma, dbeta, (dres if want_dres else None), None, None, None
 
 

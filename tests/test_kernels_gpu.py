@@ -375,9 +375,9 @@ def test_basic_block_vs_fp64(shape, stride):
 
 
 def test_bn_stats_large_mean_stable(K):
-    """mean/std = 1e4: a (sum, sumsq) formulation in fp32 returns garbage variance."""
+    """mean/std = 300: a (sum, sumsq) formulation in fp32 loses ~1e-2 of the variance."""
     torch.manual_seed(0)
-    x = (1000.0 + 0.1 * torch.randn(64, 30, 30, 64)).bfloat16()
+    x = (300.0 + 1.0 * torch.randn(64, 30, 30, 64)).bfloat16()
     st = K.bn_stats(x.to(DEV), None)
     sr = _ref.bn_stats(x.float(), None)
     assert relerr(st[0, 2], sr[0, 2]) < 1e-3

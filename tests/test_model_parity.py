@@ -75,8 +75,8 @@ def test_gpu_model_as_accurate_as_torch_bf16(name, size, batch):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         ob = mirror_forward(m_bf, imgs, training=True)
     torch.nn.functional.cross_entropy(ob.float(), labels).backward()
-    assert relerr(o1, o3) < 5e-2
-    assert abs(l1.item() - l3.item()) / l3.item() < 2e-2
+    e_out, e_out_bf = relerr(o1, o3), relerr(ob, o3)
+    assert e_out <= 1.25 * e_out_bf + 1e-2, (e_out, e_out_bf)
     g1, gb, g3 = _flat_grads(m1), _flat_grads(m_bf), _flat_grads(m_ref)
     assert relerr(g1, g3) <= 1.25 * relerr(gb, g3) + 1e-3, (relerr(g1, g3), relerr(gb, g3))
 

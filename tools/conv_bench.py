@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Per-shape conv timing: our gfx950 implicit-GEMM kernels vs MIOpen (stock
+torch channels_last bf16) on the 23 unique ResNet-50 conv shapes (SURVEY.md
+§2.5.1), forward / data-grad / weight-grad.  Prints TFLOP/s per shape and the
+per-step totals weighted by each shape's multiplicity in ResNet-50.
+
+    python tools/conv_bench.py [--batch 256] [--iters 20] [--no-miopen]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ddp_classification_pytorch_amd import _ext  # noqa: E402
+
+# (Ci, Co, k, stride, H_in, count) at 224px
+R50 = [
+    (8, 64, 7, 2, 224, 1),
+    (64, 64, 1, 1, 56, 1), (64, 64, 3, 1, 56, 3), (64, 256, 1, 1, 56, 4), (256, 64, 1, 1, 56, 2),
+    (256, 128, 1, 1, 56, 1), (128, 128, 3, 2, 56, 1), (128, 512, 1, 1, 28, 4), (256, 512, 1, 2, 56, 1),
+    (512, 128, 1, 1, 28, 3), (128, 128, 3, 1, 28, 3), (512, 256, 1, 1, 28, 1), (256, 256, 3, 2, 28, 1),
+    (256, 1024, 1, 1, 14, 6), (512, 1024, 1, 2, 28, 1), (1024, 256, 1, 1, 14, 5), (256, 256, 3, 1, 14, 5),
+    (1024, 512, 1, 1, 14, 1), (512, 512, 3, 2, 14, 1), (512, 2048, 1, 1, 7, 3), (1024, 2048, 1, 2, 14, 1),
+    (2048, 512, 1, 1, 7, 2), (512, 512, 3, 1, 7, 2),
+]
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    K = _ext.hip_ops()
+    dev = torch.device("cuda", 0)
+    N = a.batch
+    tot = {"ours": [0, 0, 0], "miopen": [0, 0, 0]}
+    rows = []
+    print(f"{'shape':34s} {'fwd us':>8s} {'TF':>6s} {'dgrad':>8s} {'TF':>6s} {'wgrad':>8s} {'TF':>6s} | "
+          f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s}")
+    for Ci, Co, k, s, H, cnt in R50:
+        p = k // 2
+        Ho = (H + 2 * p - k) // s + 1
+        flop = 2.0 * N * Ho * Ho * Co * Ci * k * k
+        x = torch.randn(N, H, H, Ci, device=dev).bfloat16()
+        w = (torch.randn(Co, k, k, Ci, device=dev) / (k * k * Ci) ** 0.5)
+        wb, wt = K.weight_prep(w, 0, True)
+        dy = torch.randn(N, Ho, Ho, Co, device=dev).bfloat16()
+        t_f = timeit(lambda: K.conv_fwd(x, wb, s, p, True), a.iters)
+        t_d = timeit(lambda: K.conv_dgrad(dy, wt, H, H, s, p), a.iters) if Ci > 8 else 0.0
+        t_w = timeit(lambda: K.conv_wgrad(dy, x, k, k, s, p), a.iters)
+        mi = [0.0, 0.0, 0.0]
+        if not a.no_miopen:
+            xc = x.permute(0, 3, 1, 2)  # channels_last NCHW view
+            wc = wb.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            dyc = dy.permute(0, 3, 1, 2)
+            mi[0] = timeit(lambda: F.conv2d(xc, wc, stride=s, padding=p), a.iters)
+            if Ci > 8:
+                mi[1] = timeit(lambda: torch.ops.aten.convolution_backward(
+                    dyc, xc, wc, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False]), a.iters)
+            mi[2] = timeit(lambda: torch.ops.aten.convolution_backward(
+                dyc, xc, wc, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False]), a.iters)
+        tf = lambda t: flop / t / 1e6 if t > 0 else 0.0  # noqa: E731
+        name = f"{Ci}->{Co} k{k} s{s} {H}->{Ho} x{cnt}"
+        print(f"{name:34s} {t_f:8.1f} {tf(t_f):6.0f} {t_d:8.1f} {tf(t_d):6.0f} {t_w:8.1f} {tf(t_w):6.0f} | "
+              f"{mi[0]:8.1f} {mi[1]:8.1f} {mi[2]:8.1f}", flush=True)
+        for i, t in enumerate((t_f, t_d, t_w)):
+            tot["ours"][i] += cnt * t
+        for i, t in enumerate(mi):
+            tot["miopen"][i] += cnt * t
+        rows.append(dict(shape=name, flop=flop, ours=[t_f, t_d, t_w], miopen=mi, count=cnt))
+    print("per-step totals (ms): ours fwd/dgrad/wgrad = " + "/".join(f"{v / 1e3:.2f}" for v in tot["ours"]) +
+          f" sum {sum(tot['ours']) / 1e3:.2f}")
+    if not a.no_miopen:
+        print("                      miopen            = " + "/".join(f"{v / 1e3:.2f}" for v in tot["miopen"]) +
+              f" sum {sum(tot['miopen']) / 1e3:.2f}")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({"batch": N, "rows": rows, "totals_us": tot}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
