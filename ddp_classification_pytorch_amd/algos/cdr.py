@@ -74,3 +74,48 @@ def clip_schedule(noise_rate: float, num_gradual: int, epoch: int) -> float:
     sched = np.linspace(1 - noise_rate, 1, num=num_gradual)[::-1]
     _ = sched[epoch] if epoch < num_gradual else None
     return 1.0 - noise_rate
+
+
+def run(args):
+    """CDR/main.py:286-383: ResNet-50 + MLP head + LogSoftmax, SGD(momentum 0.9),
+    MultiStepLR([10, 20]) stepped BEFORE each epoch (reference order), CE on the
+    log-probabilities, critical-parameter masking after every backward."""
+    from ..algos.baseline import build_classifier
+    from ..engine.loop import ClassificationLoop
+    from ..engine.logger import rotate_results_file
+    from ..engine.runtime import build_data, setup
+    from ..ops import functional as Fn
+    from ..optim import MultiStepLR, build_optimizer
+    import os
+
+    rt = setup(args)
+    rotate_results_file(os.path.join(args.out_dir, "results_cdr.txt"))
+    train_data, val_data, _, _ = build_data(args, rt)
+    model = build_classifier(args, log_softmax=True).to(rt.device)
+    opt = build_optimizer("sgd", model.parameters(), args.lr, args.momentum, 0.0)
+    sched = MultiStepLR(opt, milestones=args.milestones, gamma=args.gamma)
+    C = args.num_classes
+    state = {"epoch": 0}
+
+    def fwd_train(batch):
+        return Fn.cross_entropy(model(batch[0]), batch[1], C, return_rank=True)
+
+    def fwd_eval(batch):
+        return Fn.cross_entropy_rows(model(batch[0]), batch[1], C)
+
+    def post_backward():
+        clip = clip_schedule(args.noise_rate, args.num_gradual, state["epoch"])
+        cdr_mask_gradients(model.parameters(), nonzero_ratio=clip, clip=clip)
+
+    class _Loop(ClassificationLoop):
+        def train_epoch(self, epoch):
+            state["epoch"] = epoch
+            return super().train_epoch(epoch)
+
+    loop = _Loop(args, rt, {"model": model}, opt, sched, train_data, val_data, fwd_train, fwd_eval,
+                 post_backward=post_backward, scheduler_before_epoch=True)
+    best = loop.run()
+    hist = loop.logger.history.get("val/top1", [])
+    if rt.is_main and hist:  # the reference crashes on an empty list here (CDR/main.py:381)
+        loop.logger.line(f"best val top1 {100 * max(hist):.3f} at epoch {int(np.argmax(hist)) + 1}")
+    return best

@@ -1,0 +1,183 @@
+"""Generic epoch loop for the single-loss classification workloads
+(BASELINE ``train_and_valid`` BASELINE/main.py:258-314, ARCFACE loop
+ARCFACE/arc_main.py:302-414, CDR ``train``/``evaluate`` CDR/main.py:218-283).
+
+Differences from the reference, all deliberate:
+* metrics (loss sum, top-1, top-3, count) accumulate on the device every
+  step and are reduced with ONE all_reduce per log interval / epoch, so they
+  are exact over the global batch (the reference multiplies rank-0 counts by
+  world_size, BASELINE/main.py:247-249) and cost no per-step host syncs;
+* validation excludes the DistributedSampler padding duplicates;
+* ``set_epoch`` is always called (ARCFACE forgets it);
+* checkpoints are state_dicts written once by rank 0 (``last.pth`` /
+  ``best.pth``) and ``--resume`` restores model/optimizer/scheduler/epoch/RNG;
+* ``--fail-at-step`` injects a failure for resume testing.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from .checkpoint import load_checkpoint, save_checkpoint
+from .logger import MetricsLogger
+
+
+class InjectedFailure(RuntimeError):
+    pass
+
+
+def _allreduce(t):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t)
+    return t
+
+
+def valid_count(sampler, n_total):
+    """Samples of this rank that are not DistributedSampler padding."""
+    if sampler is None or not hasattr(sampler, "world"):
+        return n_total
+    return max(0, math.ceil((sampler.n - sampler.rank) / sampler.world))
+
+
+class ClassificationLoop:
+    """``forward_train(batch) -> (loss, rank)``; ``forward_eval(batch) -> (loss_rows, rank)``;
+    optional ``post_backward()`` (e.g. CDR gradient masking) and ``epoch_hook(epoch)``."""
+
+    def __init__(self, args, rt, models: dict, optimizer, scheduler, train_data, val_data, forward_train,
+                 forward_eval, post_backward=None, logger: MetricsLogger = None, scheduler_before_epoch=False,
+                 train_modules=None):
+        self.args, self.rt = args, rt
+        self.models, self.optimizer, self.scheduler = models, optimizer, scheduler
+        self.train_data, self.val_data = train_data, val_data
+        self.forward_train, self.forward_eval = forward_train, forward_eval
+        self.post_backward = post_backward
+        self.logger = logger or MetricsLogger(args.out_dir if rt.is_main else None)
+        self.scheduler_before_epoch = scheduler_before_epoch  # CDR steps its scheduler before training (:365-366)
+        self.train_modules = train_modules or list(models.values())
+        self.start_epoch, self.global_step, self.best = 0, 0, -1.0
+
+    # ------------------------------------------------------------------ persistence
+    def _ckpt(self, name):
+        return os.path.join(self.args.out_dir, name)
+
+    def maybe_resume(self):
+        path = self.args.resume
+        if path is None and os.path.exists(self._ckpt("last.pth")) and getattr(self.args, "auto_resume", False):
+            path = self._ckpt("last.pth")
+        if not path:
+            return
+        extra = load_checkpoint(path, self.models, {"opt": self.optimizer},
+                                {"sched": self.scheduler} if self.scheduler is not None else None,
+                                map_location=self.rt.device)
+        self.start_epoch = int(extra.get("epoch", -1)) + 1
+        self.global_step = int(extra.get("global_step", 0))
+        self.best = float(extra.get("best", -1.0))
+        self.logger.line(f"resumed from {path}: epoch {self.start_epoch}, step {self.global_step}")
+
+    def save(self, epoch, val_top1):
+        kw = dict(epoch=epoch, global_step=self.global_step, best=max(self.best, val_top1),
+                  config={k: v for k, v in vars(self.args).items() if isinstance(v, (int, float, str, bool, list))})
+        sched = {"sched": self.scheduler} if self.scheduler is not None else None
+        save_checkpoint(self._ckpt("last.pth"), self.models, {"opt": self.optimizer}, sched, **kw)
+        if val_top1 > self.best:
+            self.best = val_top1
+            save_checkpoint(self._ckpt("best.pth"), self.models, {"opt": self.optimizer}, sched, **kw)
+
+    # ------------------------------------------------------------------ epochs
+    def train_epoch(self, epoch):
+        a, dev = self.args, self.rt.device
+        for m in self.train_modules:
+            m.train()
+        sampler = getattr(self.train_data, "sampler", None)
+        if sampler is not None and hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(epoch)
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)  # loss*B, top1, top3, count
+        win = torch.zeros(4, dtype=torch.float64, device=dev)
+        n_steps = len(self.train_data)
+        if a.max_steps_per_epoch:
+            n_steps = min(n_steps, a.max_steps_per_epoch)
+        t0 = time.time()
+        for i, batch in enumerate(self.train_data):
+            if i >= n_steps:
+                break
+            if a.fail_at_step is not None and self.global_step == a.fail_at_step:
+                raise InjectedFailure(f"injected failure at global step {self.global_step}")
+            loss, rank = self.forward_train(batch)
+            self.optimizer.zero_grad(set_to_none=True)
+            loss.backward()
+            if self.post_backward is not None:
+                self.post_backward()
+            self.optimizer.step()
+            B = rank.numel()
+            step_stats = torch.stack([loss.detach().double() * B, (rank < 1).sum().double(),
+                                      (rank < 3).sum().double(), torch.tensor(float(B), device=dev,
+                                                                                dtype=torch.float64)])
+            acc += step_stats
+            win += step_stats
+            self.global_step += 1
+            if (i + 1) % a.log_interval == 0 or i + 1 == n_steps:
+                w = _allreduce(win.clone()).tolist()
+                dt = time.time() - t0
+                eta = dt / (i + 1) * (n_steps - i - 1)
+                lr = self.optimizer.param_groups[0]["lr"]
+                self.logger.progress(
+                    f"Epoch [{epoch + 1}/{a.epochs}] Iter [{i + 1}/{n_steps}] loss {w[0] / max(w[3], 1):.4f} "
+                    f"top1 {100 * w[1] / max(w[3], 1):.2f} top3 {100 * w[2] / max(w[3], 1):.2f} lr {lr:.3g} "
+                    f"{(i + 1) * B * self.rt.world / max(dt, 1e-9):.0f} img/s "
+                    f"eta {eta:.0f}s")
+                self.logger.log("train_iter", epoch=epoch, step=self.global_step, loss=w[0] / max(w[3], 1),
+                                top1=w[1] / max(w[3], 1), top3=w[2] / max(w[3], 1), lr=lr)
+                win.zero_()
+        tot = _allreduce(acc).tolist()
+        self.logger.progress("", end="\n")
+        n = max(tot[3], 1)
+        return {"loss": tot[0] / n, "top1": tot[1] / n, "top3": tot[2] / n, "count": tot[3],
+                "time": time.time() - t0}
+
+    @torch.no_grad()
+    def evaluate(self):
+        for m in self.train_modules:
+            m.eval()
+        dev = self.rt.device
+        sampler = getattr(self.val_data, "sampler", None)
+        left = valid_count(sampler, float("inf"))
+        acc = torch.zeros(4, dtype=torch.float64, device=dev)
+        for batch in self.val_data:
+            loss_rows, rank = self.forward_eval(batch)
+            B = rank.numel()
+            k = int(min(B, left))
+            left -= k
+            if k <= 0:
+                continue
+            loss_rows, rank = loss_rows[:k], rank[:k]
+            acc += torch.stack([loss_rows.double().sum(), (rank < 1).sum().double(), (rank < 3).sum().double(),
+                                torch.tensor(float(k), device=dev, dtype=torch.float64)])
+        tot = _allreduce(acc).tolist()
+        n = max(tot[3], 1)
+        return {"loss": tot[0] / n, "top1": tot[1] / n, "top3": tot[2] / n, "count": tot[3]}
+
+    def run(self):
+        a = self.args
+        self.maybe_resume()
+        for epoch in range(self.start_epoch, a.epochs):
+            if self.scheduler is not None and self.scheduler_before_epoch:
+                self.scheduler.step()
+            tr = self.train_epoch(epoch)
+            self.logger.log("train_epoch", epoch=epoch, **tr)
+            va = {"top1": -1.0}
+            if self.val_data is not None and ((epoch + 1) % a.eval_every == 0 or epoch + 1 == a.epochs):
+                va = self.evaluate()
+                self.logger.log("val", epoch=epoch, **va)
+                self.logger.line(f"VAL Epoch {epoch + 1}: loss {va['loss']:.4f} top1 {100 * va['top1']:.3f} "
+                                 f"top3 {100 * va['top3']:.3f} (n={int(va['count'])}) | train loss {tr['loss']:.4f} "
+                                 f"top1 {100 * tr['top1']:.3f} ({tr['time']:.1f}s)")
+            if self.scheduler is not None and not self.scheduler_before_epoch:
+                self.scheduler.step()
+            if (epoch + 1) % a.save_every == 0 or epoch + 1 == a.epochs:
+                self.save(epoch, va["top1"])
+        self.logger.dump_history()
+        return self.best

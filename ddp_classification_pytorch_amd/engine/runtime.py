@@ -1,0 +1,105 @@
+"""Process / device / data setup shared by every workload.
+
+* :func:`setup` — torchrun-compatible process group (RCCL on GPU, gloo on CPU)
+  with an explicit timeout (the reference uses the default
+  and a hard-wired tcp://127.0.0.1:8989 with rank=local_rank,
+  BASELINE/main.py:35-38), device selection, seeding (BASELINE/main.py:43-50),
+  output directory.
+* :func:`build_data` — train/val loaders for ``--data folder | imagefolder |
+  list | synthetic`` with rank-sharded samplers and the on-device prefetcher.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _ext
+from ..data import (CappedImageFolder, DevicePrefetcher, ImageFolder, ListDataset, ShardSampler, SyntheticImages,
+                    build_loader, build_transform, norm_stats)
+from ..parallel.ddp import init_distributed
+from ..utils.misc import set_seed, worker_init_fn
+
+
+class Runtime:
+    def __init__(self, rank, local_rank, world, device):
+        self.rank, self.local_rank, self.world, self.device = rank, local_rank, world, device
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+
+def setup(args) -> Runtime:
+    want_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
+    backend = args.dist_backend or ("nccl" if want_cuda else "gloo")
+    rank, local, world = init_distributed(backend)
+    if want_cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        _ext.hip_ops()  # GPU path requires the gfx950 library: fail loudly here, not mid-epoch
+    else:
+        device = torch.device("cpu")
+    set_seed(args.seed + rank)
+    if rank == 0:
+        os.makedirs(args.out_dir, exist_ok=True)
+    return Runtime(rank, local, world, device)
+
+
+def _datasets(args):
+    tr_t = build_transform(args.transform, True, args.image_size)
+    va_t = build_transform(args.transform, False, args.image_size)
+    if args.data == "synthetic":
+        n_tr, n_va = args.synthetic_train_size, args.synthetic_val_size
+        size = args.image_size if args.transform != "baseline" or args.image_size != 224 else 224
+        tr = SyntheticImages(n_tr, size=size, num_classes=args.num_classes, seed=args.seed,
+                             return_index=args.workload == "plc")
+        va = SyntheticImages(n_va, size=size, num_classes=args.num_classes, seed=args.seed + 1,
+                             return_index=args.workload == "plc")
+        return tr, va
+    if args.data == "list":
+        tr = ListDataset(args.folder, "train", tr_t, seed=args.seed)
+        va = ListDataset(args.folder, "val", va_t)
+        return tr, va
+    train_dir = args.train_dir or os.path.join(args.folder, "train")
+    val_dir = args.val_dir or os.path.join(args.folder, "test")
+    if args.data == "imagefolder":
+        return ImageFolder(train_dir, tr_t), ImageFolder(val_dir, va_t)
+    tr = CappedImageFolder(train_dir, tr_t, args.imgs_limited, args.num_class_dirs, args.glob_order)
+    va = CappedImageFolder(val_dir, va_t, args.imgs_limited, args.num_class_dirs, args.glob_order)
+    return tr, va
+
+
+class WithIndex(torch.utils.data.Dataset):
+    """(img, label) -> (img, label, index) (PLC needs dataset indices)."""
+
+    def __init__(self, ds):
+        self.ds = ds
+
+    def __len__(self):
+        return len(self.ds)
+
+    def __getitem__(self, i):
+        item = self.ds[i]
+        return (item[0], item[1], i) if len(item) == 2 else item
+
+    def __getattr__(self, name):
+        if name == "ds":
+            raise AttributeError(name)
+        return getattr(self.ds, name)
+
+
+def build_data(args, rt: Runtime, drop_last_train=False):
+    tr, va = _datasets(args)
+    if args.workload == "plc" and args.data != "synthetic" and not isinstance(tr, ListDataset):
+        tr, va = WithIndex(tr), WithIndex(va)
+    mean, std = norm_stats(args.dataset if "CIFAR" in args.dataset.upper() else "imagenet")
+    cpad = 3 if str(args.model).startswith("tresnet") else 8
+    tr_s = ShardSampler(tr, rt.world, rt.rank, shuffle=True, seed=args.seed, drop_last=drop_last_train)
+    va_s = ShardSampler(va, rt.world, rt.rank, shuffle=False, seed=args.seed)
+    workers = args.workers if args.data != "synthetic" else min(args.workers, 2)
+    tr_l = build_loader(tr, args.batchsize, tr_s, workers=workers, drop_last=drop_last_train,
+                        worker_init_fn=worker_init_fn)
+    va_l = build_loader(va, args.batchsize, va_s, workers=workers, drop_last=False, worker_init_fn=worker_init_fn)
+    return (DevicePrefetcher(tr_l, rt.device, mean, std, cpad), DevicePrefetcher(va_l, rt.device, mean, std, cpad),
+            tr, va)

@@ -354,6 +354,34 @@ def cross_entropy(logits, labels, num_classes=None, smoothing=0.0, reduction="me
     return (loss, rank) if return_rank else loss
 
 
+@torch.no_grad()
+def cross_entropy_rows(logits, labels, num_classes=None):
+    """Per-sample CE loss and label rank (evaluation; no autograd)."""
+    return K(logits).xent_fwd(logits, labels, num_classes or logits.shape[1], 0.0)
+
+
+@torch.no_grad()
+def arcface_rows(x, weight, labels, s=30.0, m=0.5, easy_margin=True, with_margin=True):
+    """Per-sample (loss, rank) of the ArcFace head.  ``with_margin=False`` ranks the
+    plain scaled cosines (a label-free prediction)."""
+    k = K(x)
+    C, D = weight.shape
+    Dp = round_up(D, 8) if x.is_cuda else D
+    Cp = round_up(C, 64) if x.is_cuda else C
+    xn, _ = k.l2norm_rows(x.contiguous(), Dp, 1e-12)
+    w = weight.detach()
+    if Cp > C:
+        w = F.pad(w, (0, 0, 0, Cp - C))
+    wn, _ = k.l2norm_rows(w.contiguous(), Dp, 1e-12)
+    if not x.is_cuda:
+        xn, wn = xn.float(), wn.float()
+    cos = k.linear_fwd(xn, wn, None, False)
+    if with_margin:
+        loss, rank, _, _ = k.arcface_fwd(cos, labels, C, s, m, easy_margin, False)
+        return loss, rank
+    return k.xent_fwd(cos[:, :C] * s if not x.is_cuda else cos[:, :C], labels, C, 0.0)
+
+
 class _LogSoftmax(Function):
     @staticmethod
     def forward(ctx, x, C):
