@@ -172,8 +172,8 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   return dw;
 }
 
-// x [B,K] bf16, w [Npad,K] bf16 -> y [B,Npad] (= x w^T + b, optional ReLU)
-Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, bool relu) {
+// x [B,K] bf16, w [Npad,K] bf16 -> y [B,Npad] (= act(x w^T + b)); act 0 none, 1 ReLU, 2 sigmoid
+Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t act) {
   CHECK_ACT(x);
   CHECK_ACT(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear shapes");
@@ -187,8 +187,9 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias
   dcp::TapList t;
   t.n = 1;
   t.dy[0] = t.dx[0] = t.widx[0] = 0;
+  TORCH_CHECK(act >= 0 && act <= 2, "linear act must be 0 (none), 1 (relu) or 2 (sigmoid)");
   dcp::launch_tap_gemm(bp(x), B, 1, 1, K, bp(w), Np, 1, bpm(y), 1, 1, 1, 1, 1, 1, 0, 0, t, nullptr, fp(bias),
-                       relu ? 1 : 0, zero_page(x.get_device()), cur_stream());
+                       (int)act, zero_page(x.get_device()), cur_stream());
   return y;
 }
 
@@ -454,12 +455,12 @@ Tensor to_nhwc(const Tensor& src, bool nchw, int64_t cpad, double in_scale, cons
   return y;
 }
 
-Tensor relu_bwd(const Tensor& dy, const Tensor& y) {
+Tensor act_bwd(const Tensor& dy, const Tensor& y, int64_t act) {
   CHECK_ACT(dy);
   CHECK_ACT(y);
-  TORCH_CHECK(dy.sizes() == y.sizes() && dy.numel() % 8 == 0, "relu_bwd shapes");
+  TORCH_CHECK(dy.sizes() == y.sizes() && dy.numel() % 8 == 0, "act_bwd shapes");
   auto dx = at::empty_like(dy);
-  dcp::launch_relu_bwd(bp(dy), bp(y), bpm(dx), dy.numel(), cur_stream());
+  dcp::launch_act_bwd(bp(dy), bp(y), bpm(dx), dy.numel(), (int)act, cur_stream());
   return dx;
 }
 
@@ -505,25 +506,34 @@ Tensor dwconv_bwd(const Tensor& dy, const Tensor& filt, int64_t H, int64_t W, in
   return dx;
 }
 
-Tensor chan_scale_fwd(const Tensor& x, const Tensor& g) {
+Tensor chan_scale_fwd(const Tensor& x, const Tensor& g, const optional<Tensor>& res, bool relu) {
   CHECK_ACT(x);
   CHECK_ACT(g);
   const int N = x.size(0), C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && g.numel() == (int64_t)N * C, "chan_scale shapes");
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+  }
   auto y = at::empty_like(x);
-  dcp::launch_chan_scale_fwd(bp(x), bp(g), bpm(y), N, x.numel() / (N * C), C, cur_stream());
+  dcp::launch_chan_scale_fwd(bp(x), bp(g), res.has_value() ? bp(*res) : nullptr, bpm(y), N, x.numel() / (N * C), C,
+                             relu ? 1 : 0, cur_stream());
   return y;
 }
 
-std::tuple<Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor& x, const Tensor& g) {
+std::tuple<Tensor, Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor& x, const Tensor& g,
+                                                  const optional<Tensor>& res, bool relu, bool want_dres) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   CHECK_ACT(g);
   const int N = x.size(0), C = x.size(-1);
   auto dx = at::empty_like(x);
   auto dg = at::empty({N, C}, f32_like(x));
-  dcp::launch_chan_scale_bwd(bp(dy), bp(x), bp(g), bpm(dx), dg.data_ptr<float>(), N, x.numel() / (N * C), C,
-                             cur_stream());
-  return {dx, dg};
+  Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  dcp::launch_chan_scale_bwd(bp(dy), bp(x), bp(g), res.has_value() ? bp(*res) : nullptr, bpm(dx),
+                             dg.data_ptr<float>(), want_dres ? bpm(dres) : nullptr, N, x.numel() / (N * C), C,
+                             relu ? 1 : 0, cur_stream());
+  return {dx, dg, dres};
 }
 
 // ---------------------------------------------------------------------------
@@ -691,7 +701,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
-  m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, bool relu) -> Tensor", &linear_fwd);
+  m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, int act) -> Tensor", &linear_fwd);
   m.def("linear_wgrad(Tensor dy, Tensor x) -> Tensor", &linear_wgrad);
   m.def("weight_prep(Tensor w, int co_pad, bool transposed) -> (Tensor, Tensor)", &weight_prep);
   m.def("grouped_conv_fwd(Tensor x, Tensor w, int groups, int stride, int pad) -> Tensor", &grouped_conv_fwd);
@@ -724,13 +734,15 @@ TORCH_LIBRARY(dcp, m) {
   m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &gap_bwd);
   m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
   m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
-  m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &relu_bwd);
+  m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor", &act_bwd);
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);
   m.def("nested_eval(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval);
   m.def("dwconv_fwd(Tensor x, Tensor filt, int k, int s, int p, bool reflect) -> Tensor", &dwconv_fwd);
   m.def("dwconv_bwd(Tensor dy, Tensor filt, int H, int W, int k, int s, int p, bool reflect) -> Tensor", &dwconv_bwd);
-  m.def("chan_scale_fwd(Tensor x, Tensor g) -> Tensor", &chan_scale_fwd);
-  m.def("chan_scale_bwd(Tensor dy, Tensor x, Tensor g) -> (Tensor, Tensor)", &chan_scale_bwd);
+  m.def("chan_scale_fwd(Tensor x, Tensor g, Tensor? res, bool relu) -> Tensor", &chan_scale_fwd);
+  m.def("chan_scale_bwd(Tensor dy, Tensor x, Tensor g, Tensor? res, bool relu, bool want_dres) -> (Tensor, Tensor, "
+        "Tensor)",
+        &chan_scale_bwd);
   m.def("xent_fwd(Tensor logits, Tensor labels, int C, float smoothing) -> (Tensor, Tensor)", &xent_fwd);
   m.def(
       "xent_bwd(Tensor logits, Tensor labels, int C, Tensor grad_out, float scale, float smoothing, bool out_bf16) "

@@ -44,7 +44,7 @@ struct TapGemmParams {
   int Hd, Wd, ds, oy, ox;
   int Co, T, M;
   int ntaps, cpt, nkt, ldw;
-  int relu;          // fused ReLU on the stored output (linear heads)
+  int relu;          // fused activation on the stored output: 0 none, 1 ReLU, 2 sigmoid (linear heads)
   const float* bias; // optional per-output-channel bias (linear heads)
   FastDiv div_wy, div_hy, div_cpt;
   int8_t dy[kMaxTaps], dx[kMaxTaps];
@@ -233,7 +233,8 @@ tap_gemm_kernel(const TapGemmParams p) {
       for (int r = 0; r < 4; ++r) {
         float t = acc[j][i][r];
         if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
-        if (p.relu) t = fmaxf(t, 0.f);
+        if (p.relu == 1) t = fmaxf(t, 0.f);
+        else if (p.relu == 2) t = 1.f / (1.f + __expf(-t));
         v[r] = t;
       }
       bf16x4 o;
@@ -271,7 +272,8 @@ tap_gemm_kernel(const TapGemmParams p) {
         for (int r = 0; r < 4; ++r) {
           float t = acc[j][i][r];
           if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
-          if (p.relu) t = fmaxf(t, 0.f);
+          if (p.relu == 1) t = fmaxf(t, 0.f);
+          else if (p.relu == 2) t = 1.f / (1.f + __expf(-t));
           const float d = bf2f(f2bf(t)) - s1[j][r];
           s2[j][r] += mok ? d * d : 0.f;
         }

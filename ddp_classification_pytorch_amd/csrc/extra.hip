@@ -231,10 +231,12 @@ __global__ void __launch_bounds__(256) dwconv_bwd_kernel(const bf16* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// y[n][hw][c] = x[n][hw][c] * g[n][c]
+// squeeze-and-excitation apply, optionally fused with the block's residual add
+// and ReLU:  y[n][hw][c] = act(x[n][hw][c] * g[n][c] (+ res[n][hw][c]))
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) chan_scale_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ g,
-                                                             bf16* __restrict__ y, int N, int HW, int C) {
+                                                             const bf16* __restrict__ res, bf16* __restrict__ y,
+                                                             int N, int HW, int C, int relu) {
   const int cpr = C >> 3;
   const size_t total = (size_t)N * HW * cpr;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -242,17 +244,27 @@ __global__ void __launch_bounds__(256) chan_scale_fwd_kernel(const bf16* __restr
     const size_t n = i / cpr / HW;
     const bf16x8 v = *(const bf16x8*)(x + i * 8);
     const bf16x8 s = *(const bf16x8*)(g + n * C + ch * 8);
+    bf16x8 r;
+    if (res) r = *(const bf16x8*)(res + i * 8);
     bf16x8 o;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = f2bf(bf2f(v[q]) * bf2f(s[q]));
+    for (int q = 0; q < 8; ++q) {
+      float z = bf2f(v[q]) * bf2f(s[q]);
+      if (res) z += bf2f(r[q]);
+      if (relu) z = fmaxf(z, 0.f);
+      o[q] = f2bf(z);
+    }
     *(bf16x8*)(y + i * 8) = o;
   }
 }
 
-// dx = dy * g ; dg[n][c] = sum_hw dy*x  (one thread per (n, 8-channel chunk))
+// dz = dy * relu'(z);  dx = dz * g ; dg[n][c] = sum_hw dz*x ; dres = dz
+// one thread per (n, 8-channel chunk); recomputes z from x, g, res
 __global__ void __launch_bounds__(256) chan_scale_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                             const bf16* __restrict__ g, bf16* __restrict__ dx,
-                                                             float* __restrict__ dg, int N, int HW, int C) {
+                                                             const bf16* __restrict__ g, const bf16* __restrict__ res,
+                                                             bf16* __restrict__ dx, float* __restrict__ dg,
+                                                             bf16* __restrict__ dres, int N, int HW, int C,
+                                                             int relu) {
   const int cpr = C >> 3;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N * cpr) return;
@@ -265,13 +277,23 @@ __global__ void __launch_bounds__(256) chan_scale_bwd_kernel(const bf16* __restr
     const size_t o = ((size_t)n * HW + t) * C + ch * 8;
     const bf16x8 gv = *(const bf16x8*)(dy + o);
     const bf16x8 xv = *(const bf16x8*)(x + o);
-    bf16x8 d;
+    bf16x8 rv;
+    if (res) rv = *(const bf16x8*)(res + o);
+    bf16x8 d, dz8;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      acc[q] += bf2f(gv[q]) * bf2f(xv[q]);
-      d[q] = f2bf(bf2f(gv[q]) * bf2f(s[q]));
+      float dz = bf2f(gv[q]);
+      if (relu) {
+        float z = bf2f(xv[q]) * bf2f(s[q]);
+        if (res) z += bf2f(rv[q]);
+        dz = z > 0.f ? dz : 0.f;
+      }
+      acc[q] += dz * bf2f(xv[q]);
+      d[q] = f2bf(dz * bf2f(s[q]));
+      dz8[q] = f2bf(dz);
     }
     *(bf16x8*)(dx + o) = d;
+    if (dres) *(bf16x8*)(dres + o) = dz8;
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) dg[(size_t)n * C + ch * 8 + q] = acc[q];
@@ -320,14 +342,16 @@ void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, i
   hipLaunchKernelGGL(dwconv_bwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, dy, w, dx, N, H, W, C, Ho, Wo, k, s,
                      p, reflect);
 }
-void launch_chan_scale_fwd(const bf16* x, const bf16* g, bf16* y, int N, int HW, int C, hipStream_t st) {
-  const size_t total = (size_t)N * HW * (C / 8);
-  hipLaunchKernelGGL(chan_scale_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, g, y, N, HW, C);
-}
-void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, bf16* dx, float* dg, int N, int HW, int C,
+void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* y, int N, int HW, int C, int relu,
                            hipStream_t st) {
+  const size_t total = (size_t)N * HW * (C / 8);
+  hipLaunchKernelGGL(chan_scale_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, g, res, y, N, HW, C, relu);
+}
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg,
+                           bf16* dres, int N, int HW, int C, int relu, hipStream_t st) {
   const int n = N * (C / 8);
-  hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dy, x, g, dx, dg, N, HW, C);
+  hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3((n + 63) / 64), dim3(64), 0, st, dy, x, g, res, dx, dg, dres, N, HW,
+                     C, relu);
 }
 
 }  // namespace dcp

@@ -100,7 +100,7 @@ void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const 
 void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16* wb, bf16* wt, hipStream_t s);
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s);
-void launch_relu_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, hipStream_t s);
+void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
                         hipStream_t s);
@@ -109,8 +109,9 @@ void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int
                        int s, int p, int reflect, hipStream_t st);
 void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
                        int s, int p, int reflect, hipStream_t st);
-void launch_chan_scale_fwd(const bf16* x, const bf16* g, bf16* y, int N, int HW, int C, hipStream_t st);
-void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, bf16* dx, float* dg, int N, int HW, int C,
+void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* y, int N, int HW, int C, int relu,
                            hipStream_t st);
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg,
+                           bf16* dres, int N, int HW, int C, int relu, hipStream_t st);
 
 }  // namespace dcp

@@ -57,14 +57,19 @@ __global__ void __launch_bounds__(256) to_nhwc_kernel(const void* __restrict__ s
   }
 }
 
-__global__ void __launch_bounds__(256) relu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
-                                                       bf16* __restrict__ dx, size_t n8) {
+// backward of an activation from its OUTPUT y: 1 ReLU (y>0), 2 sigmoid (y(1-y))
+__global__ void __launch_bounds__(256) act_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                      bf16* __restrict__ dx, size_t n8, int act) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const bf16x8 g = *(const bf16x8*)(dy + i * 8);
     const bf16x8 v = *(const bf16x8*)(y + i * 8);
     bf16x8 o;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = bf2f(v[q]) > 0.f ? g[q] : f2bf(0.f);
+    for (int q = 0; q < 8; ++q) {
+      const float yv = bf2f(v[q]);
+      const float d = act == 2 ? yv * (1.f - yv) : (yv > 0.f ? 1.f : 0.f);
+      o[q] = f2bf(bf2f(g[q]) * d);
+    }
     *(bf16x8*)(dx + i * 8) = o;
   }
 }
@@ -153,12 +158,12 @@ void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, i
                      stdv, dst);
 }
 
-void launch_relu_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, hipStream_t s) {
+void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s) {
   const size_t n8 = numel / 8;
   size_t g = (n8 + 255) / 256;
   if (g > 4096) g = 4096;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3((int)g), dim3(256), 0, s, dy, y, dx, n8);
+  hipLaunchKernelGGL(act_bwd_kernel, dim3((int)g), dim3(256), 0, s, dy, y, dx, n8, act);
 }
 
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s) {

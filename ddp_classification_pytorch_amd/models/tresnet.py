@@ -1,0 +1,168 @@
+"""TResNet-M (the BASELINE default ``tresnet_m_miil_in21k``, BASELINE/main.py:29,143-144)
+on the gfx950 kernels.
+
+Architecture (timm TResNet; not vendored in the reference):
+* SpaceToDepth(4) stem: [N,224,224,3] -> [N,56,56,48] (``space_to_depth`` kernel)
+  then conv3x3(48->64) + InplaceABN(leaky 0.01);
+* layer1: 3 x BasicBlock(64), layer2: 4 x BasicBlock(128), layer3: 11 x
+  Bottleneck(256 -> 1024), layer4: 3 x Bottleneck(512 -> 2048);
+  SE in layers 1-3; stride-2 blocks downsample with a stride-1 conv followed
+  by an anti-aliased 3x3 blur (reflect pad; ``dwconv`` kernel); the residual
+  path downsamples with AvgPool2d(2) + 1x1 conv-BN;
+* InplaceABN = BN + leaky-ReLU (slope 1e-3 inside blocks) fused in one
+  kernel with its backward recomputing the activation from the BN input
+  (no extra activation tensor kept);
+* global average pool -> fc.
+Input: NHWC activations with 3 channels (``cpad=3``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as Fn
+from .layers import BatchNorm2d, Conv2d, ConvBN, Linear
+
+LEAKY_BLOCK = 1e-3
+LEAKY_STEM = 1e-2
+
+
+def _blur_filter():
+    f = torch.tensor([1.0, 2.0, 1.0])
+    return (f[:, None] * f[None, :]) / 16.0
+
+
+class AntiAliasDownsample(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("filt", _blur_filter(), persistent=False)
+
+    def forward(self, x):
+        return Fn.blur_pool(x, self.filt.to(x.device), k=3, s=2, p=1, reflect=True)
+
+
+class AvgPool2x2(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("filt", torch.full((2, 2), 0.25), persistent=False)
+
+    def forward(self, x):
+        return Fn.blur_pool(x, self.filt.to(x.device), k=2, s=2, p=0, reflect=False)
+
+
+class SEModule(nn.Module):
+    """avg-pool -> fc(C->R)+ReLU -> fc(R->C)+sigmoid -> channel scale (fused with residual+ReLU)."""
+
+    def __init__(self, channels, reduction_channels):
+        super().__init__()
+        self.fc1 = Linear(channels, reduction_channels)
+        self.fc2 = Linear(reduction_channels, channels)
+
+    def gate(self, x):
+        h = self.fc1(Fn.global_avg_pool(x), relu=True)
+        return Fn.linear(h, self.fc2.weight, self.fc2.bias, act="sigmoid")
+
+    def forward(self, x, residual=None, relu=False):
+        return Fn.channel_scale(x, self.gate(x), residual, relu)
+
+
+class Downsample(nn.Module):
+    def __init__(self, inplanes, planes, stride):
+        super().__init__()
+        self.pool = AvgPool2x2() if stride == 2 else None
+        self.conv = ConvBN(inplanes, planes, 1, 1, 0, act="none")
+
+    def forward(self, x):
+        if self.pool is not None:
+            x = self.pool(x)
+        return self.conv(x)
+
+
+class TBasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, use_se=True):
+        super().__init__()
+        self.conv1 = ConvBN(inplanes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK)
+        self.aa = AntiAliasDownsample() if stride == 2 else None
+        self.conv2 = ConvBN(planes, planes, 3, 1, act="none")
+        self.se = SEModule(planes, max(planes // 4, 64)) if use_se else None
+        self.downsample = Downsample(inplanes, planes, stride) if (stride != 1 or inplanes != planes) else None
+
+    def forward(self, x):
+        shortcut = self.downsample(x) if self.downsample is not None else x
+        out = self.conv1(x)
+        if self.aa is not None:
+            out = self.aa(out)
+        if self.se is None:
+            y, s = self.conv2.conv(out, stats=self.conv2.bn.training and not self.conv2.bn.frozen)
+            return self.conv2.bn(y, s, act="relu", residual=shortcut)
+        out = self.conv2(out)
+        return self.se(out, residual=shortcut, relu=True)
+
+
+class TBottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, use_se=True):
+        super().__init__()
+        self.conv1 = ConvBN(inplanes, planes, 1, 1, 0, act="leaky", slope=LEAKY_BLOCK)
+        self.conv2 = ConvBN(planes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK)
+        self.aa = AntiAliasDownsample() if stride == 2 else None
+        self.se = SEModule(planes, max(planes * 4 // 8, 64)) if use_se else None
+        self.conv3 = ConvBN(planes, planes * 4, 1, 1, 0, act="none")
+        self.downsample = (Downsample(inplanes, planes * 4, stride)
+                           if (stride != 1 or inplanes != planes * 4) else None)
+
+    def forward(self, x):
+        shortcut = self.downsample(x) if self.downsample is not None else x
+        out = self.conv1(x)
+        out = self.conv2(out)
+        if self.aa is not None:
+            out = self.aa(out)
+        if self.se is not None:
+            out = self.se(out)
+        y, s = self.conv3.conv(out, stats=self.conv3.bn.training and not self.conv3.bn.frozen)
+        return self.conv3.bn(y, s, act="relu", residual=shortcut)
+
+
+class TResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 11, 3), num_classes=1000, width_factor=1.0, in_chans=3):
+        super().__init__()
+        self.inplanes = self.planes = int(64 * width_factor)
+        self.stem = ConvBN(in_chans * 16, self.planes, 3, 1, act="leaky", slope=LEAKY_STEM)
+        self.layer1 = self._make(TBasicBlock, self.planes, layers[0], 1, True)
+        self.layer2 = self._make(TBasicBlock, self.planes * 2, layers[1], 2, True)
+        self.layer3 = self._make(TBottleneck, self.planes * 4, layers[2], 2, True)
+        self.layer4 = self._make(TBottleneck, self.planes * 8, layers[3], 2, False)
+        self.feat_dim = self.planes * 8 * TBottleneck.expansion
+        self.fc = Linear(self.feat_dim, num_classes) if num_classes > 0 else None
+        for m in self.modules():  # timm: zero-init the last BN of each residual branch
+            if isinstance(m, TBasicBlock):
+                nn.init.zeros_(m.conv2.bn.weight)
+            elif isinstance(m, TBottleneck):
+                nn.init.zeros_(m.conv3.bn.weight)
+
+    def _make(self, block, planes, n, stride, use_se):
+        layers = [block(self.inplanes, planes, stride, use_se)]
+        self.inplanes = planes * block.expansion
+        layers += [block(self.inplanes, planes, 1, use_se) for _ in range(1, n)]
+        return nn.Sequential(*layers)
+
+    def forward_features(self, x):
+        """x: NHWC [N,H,W,3] (H, W divisible by 32)."""
+        x = Fn.space_to_depth(x, 4)
+        x = self.stem(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        x = self.layer4(x)
+        return Fn.global_avg_pool(x)
+
+    def forward(self, x):
+        f = self.forward_features(x)
+        return self.fc(f) if self.fc is not None else f
+
+
+def tresnet_m(num_classes=1000, **kw):
+    return TResNet((3, 4, 11, 3), num_classes=num_classes, **kw)

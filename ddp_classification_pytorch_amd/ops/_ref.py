@@ -63,12 +63,14 @@ def conv_wgrad(dy, x, KH, KW, stride, pad):
     return dw.permute(0, 2, 3, 1).contiguous()
 
 
-def linear_fwd(x, w, bias, relu):
+def linear_fwd(x, w, bias, act):
     y = _f(x) @ _f(w).t()
     if bias is not None:
         y = y + _f(bias)[: y.shape[1]]
-    if relu:
+    if int(act) == 1:
         y = torch.relu(y)
+    elif int(act) == 2:
+        y = torch.sigmoid(y)
     return y.to(x.dtype)
 
 
@@ -264,7 +266,9 @@ def to_nhwc(src, nchw, cpad, in_scale, mean, std):
     return x.contiguous()
 
 
-def relu_bwd(dy, y):
+def act_bwd(dy, y, act):
+    if int(act) == 2:
+        return (_f(dy) * _f(y) * (1 - _f(y))).to(dy.dtype)
     return torch.where(y > 0, dy, torch.zeros_like(dy))
 
 
@@ -307,17 +311,26 @@ def dwconv_bwd(dy, filt, H, W, k, s, p, reflect):
     return g.to(dy.dtype)
 
 
-def chan_scale_fwd(x, g):
+def chan_scale_fwd(x, g, res, relu):
     N, C = x.shape[0], x.shape[-1]
-    return (_f(x) * _f(g).view(N, *([1] * (x.dim() - 2)), C)).to(x.dtype)
+    z = _f(x) * _f(g).view(N, *([1] * (x.dim() - 2)), C)
+    if res is not None:
+        z = z + _f(res)
+    if relu:
+        z = torch.relu(z)
+    return z.to(x.dtype)
 
 
-def chan_scale_bwd(dy, x, g):
+def chan_scale_bwd(dy, x, g, res, relu, want_dres):
     N, C = x.shape[0], x.shape[-1]
     gg = _f(g).view(N, *([1] * (x.dim() - 2)), C)
-    dx = (_f(dy) * gg).to(dy.dtype)
-    dg = (_f(dy) * _f(x)).reshape(N, -1, C).sum(1)
-    return dx, dg
+    dz = _f(dy)
+    if relu:
+        z = _f(x) * gg + (_f(res) if res is not None else 0)
+        dz = torch.where(z > 0, dz, torch.zeros_like(dz))
+    dx = (dz * gg).to(dy.dtype)
+    dg = (dz * _f(x)).reshape(N, -1, C).sum(1)
+    return dx, dg, (dz.to(dy.dtype) if want_dres else dy.new_empty(0))
 
 
 # ----------------------------------------------------------------------------- losses

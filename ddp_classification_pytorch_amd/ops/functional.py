@@ -127,10 +127,10 @@ def grouped_conv2d(x, weight, groups, stride=1, pad=0):
 # ----------------------------------------------------------------------------- linear
 class _Linear(Function):
     @staticmethod
-    def forward(ctx, x, weight, bias_p, wb, wt, relu):
-        y = K(x).linear_fwd(x, wb, bias_p, relu)
-        ctx.save_for_backward(x, wt, y if relu else None)
-        ctx.relu = relu
+    def forward(ctx, x, weight, bias_p, wb, wt, act):
+        y = K(x).linear_fwd(x, wb, bias_p, act)
+        ctx.save_for_backward(x, wt, y if act else None)
+        ctx.act = act
         ctx.out = weight.shape[0]
         ctx.has_bias = bias_p is not None
         return y
@@ -140,11 +140,11 @@ class _Linear(Function):
         x, wt, y = ctx.saved_tensors
         dy = dy.contiguous()
         k = K(dy)
-        if ctx.relu:
-            dy = k.relu_bwd(dy, y)
+        if ctx.act:
+            dy = k.act_bwd(dy, y, ctx.act)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = k.linear_fwd(dy, wt, None, False)
+            dx = k.linear_fwd(dy, wt, None, 0)
         if ctx.needs_input_grad[1]:
             dw = k.linear_wgrad(dy, x)[: ctx.out]
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -152,10 +152,11 @@ class _Linear(Function):
         return dx, dw, db, None, None, None
 
 
-def linear(x, weight, bias=None, relu=False, keep_padded=False):
-    """y = x W^T + b (optionally ReLU).  Output features are padded to a multiple
-    of 64 for the GEMM; the returned tensor is the [B, out] view unless
-    ``keep_padded``."""
+def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
+    """y = act(x W^T + b), act in {None/'none', 'relu', 'sigmoid'} (``relu=True`` = 'relu').
+    Output features are padded to a multiple of 64 for the GEMM; the returned
+    tensor is the [B, out] view unless ``keep_padded``."""
+    act_code = {None: 0, "none": 0, "relu": 1, "sigmoid": 2}[act] if act is not None else (1 if relu else 0)
     out, inf = weight.shape
     x = x.contiguous()
     if x.shape[1] != inf:
@@ -165,7 +166,7 @@ def linear(x, weight, bias=None, relu=False, keep_padded=False):
     bias_p = None
     if bias is not None:
         bias_p = F.pad(bias, (0, npad - out)) if npad > out else bias
-    y = _Linear.apply(x, weight, bias_p, wb, wt, relu)
+    y = _Linear.apply(x, weight, bias_p, wb, wt, act_code)
     return y if keep_padded or npad == out else y[:, :out]
 
 
@@ -310,20 +311,23 @@ def blur_pool(x, filt, k=3, s=2, p=1, reflect=True):
 
 class _ChanScale(Function):
     @staticmethod
-    def forward(ctx, x, g):
-        ctx.save_for_backward(x, g)
-        return K(x).chan_scale_fwd(x, g)
+    def forward(ctx, x, g, res, relu):
+        ctx.save_for_backward(x, g, res)
+        ctx.relu = relu
+        return K(x).chan_scale_fwd(x, g, res, relu)
 
     @staticmethod
     def backward(ctx, dy):
-        x, g = ctx.saved_tensors
-        dx, dg = K(dy).chan_scale_bwd(dy.contiguous(), x, g)
-        return dx, dg.to(g.dtype)
+        x, g, res = ctx.saved_tensors
+        want_dres = res is not None and ctx.needs_input_grad[2]
+        dx, dg, dres = K(dy).chan_scale_bwd(dy.contiguous(), x, g, res, ctx.relu, want_dres)
+        return dx, dg.to(g.dtype), (dres if want_dres else None), None
 
 
-def channel_scale(x, g):
-    """x[n,h,w,c] * g[n,c] (squeeze-and-excitation apply)."""
-    return _ChanScale.apply(x, g.contiguous())
+def channel_scale(x, g, residual=None, relu=False):
+    """act(x[n,h,w,c] * g[n,c] (+ residual)) — squeeze-and-excitation apply fused
+    with the block's residual add and ReLU."""
+    return _ChanScale.apply(x, g.contiguous(), residual, bool(relu))
 
 
 # ----------------------------------------------------------------------------- losses
@@ -375,7 +379,7 @@ def arcface_rows(x, weight, labels, s=30.0, m=0.5, easy_margin=True, with_margin
     wn, _ = k.l2norm_rows(w.contiguous(), Dp, 1e-12)
     if not x.is_cuda:
         xn, wn = xn.float(), wn.float()
-    cos = k.linear_fwd(xn, wn, None, False)
+    cos = k.linear_fwd(xn, wn, None, 0)
     if with_margin:
         loss, rank, _, _ = k.arcface_fwd(cos, labels, C, s, m, easy_margin, False)
         return loss, rank
@@ -423,7 +427,7 @@ class _ArcFace(Function):
         wn, inv_w = k.l2norm_rows(wsrc.contiguous(), Dp, 1e-12)
         if not x.is_cuda:
             xn, wn = xn.float(), wn.float()
-        cos = k.linear_fwd(xn, wn, None, False)  # [B, Cp]
+        cos = k.linear_fwd(xn, wn, None, 0)  # [B, Cp]
         loss_rows, rank, dphi, logits = k.arcface_fwd(cos, labels, C, s, m, easy, want_logits)
         ctx.save_for_backward(xn, inv_x, wn, inv_w, cos, labels, dphi)
         ctx.cfg = (C, D, s, m, easy)
@@ -440,7 +444,7 @@ class _ArcFace(Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             wnt = k.transpose2d(wn)  # [Dp, Cp]
-            dxn = k.linear_fwd(dcos, wnt, None, False)  # [B, Dp]
+            dxn = k.linear_fwd(dcos, wnt, None, 0)  # [B, Dp]
             dx = k.l2norm_bwd(dxn, xn, inv_x, D, False)
         if ctx.needs_input_grad[1]:
             dwn = k.linear_wgrad(dcos, xn)  # [Cp, Dp] fp32

@@ -1,0 +1,125 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2):
+* DDP + SyncBN over two half-batches == one process over the full batch
+  (loss, BN running stats, every gradient);
+* exact distributed metrics (one packed all_reduce);
+* the full training entry point under 2 ranks (checkpoint written once)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _ddp_syncbn_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.parallel.ddp import wrap_ddp
+
+    torch.manual_seed(0)
+    model = build_model("cifar_resnet18", num_classes=10)
+    imgs = torch.randn(8, 3, 32, 32, generator=torch.Generator().manual_seed(1))
+    labels = torch.randint(0, 10, (8,), generator=torch.Generator().manual_seed(2))
+    net = wrap_ddp(model, None, syncbn=True, bucket_cap_mb=1)
+    sl = slice(rank * 4, rank * 4 + 4)
+    x = Fn.to_device_nhwc(imgs[sl], cpad=8)
+    loss = Fn.cross_entropy(net(x), labels[sl])
+    loss.backward()
+    lt = loss.detach().clone()
+    dist.all_reduce(lt)
+    if rank == 0:
+        torch.save({"loss": lt / world, "grads": {n: p.grad.clone() for n, p in model.named_parameters()},
+                    "rm": model.bn1.running_mean.clone(), "rv": model.bn1.running_var.clone()},
+                   os.path.join(out_dir, "ddp.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_syncbn_equals_single_process_full_batch():
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ddp_syncbn_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        got = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
+    imgs = torch.randn(8, 3, 32, 32, generator=torch.Generator().manual_seed(1))
+    labels = torch.randint(0, 10, (8,), generator=torch.Generator().manual_seed(2))
+
+    def single(x):
+        torch.manual_seed(0)
+        model = build_model("cifar_resnet18", num_classes=10)
+        loss = Fn.cross_entropy(model(Fn.to_device_nhwc(x, cpad=8)), labels)
+        loss.backward()
+        return model, loss
+
+    model, loss = single(imgs)
+    # Numerical floor of this net: ReLU kinks make its gradient move ~2e-3 under a 1e-7
+    # relative input perturbation, which is the size of fp32 reordering differences
+    # between two-rank (Chan-merged) and one-rank BN statistics.
+    model_p, _ = single(imgs * (1 + 1e-7 * torch.randn(imgs.shape, generator=torch.Generator().manual_seed(5))))
+    flat = lambda m: torch.cat([p.grad.flatten() for p in m.parameters()])  # noqa: E731
+    g_ref, g_perm = flat(model), flat(model_p)
+    g_ddp = torch.cat([got["grads"][n].flatten() for n, _ in model.named_parameters()])
+    floor = ((g_perm - g_ref).norm() / g_ref.norm()).item()
+    err = ((g_ddp - g_ref).norm() / g_ref.norm()).item()
+    # the mean of two half-batch means == the full-batch mean for equal halves
+    assert abs(float(got["loss"]) - loss.item()) < 1e-5
+    assert torch.allclose(got["rm"], model.bn1.running_mean, atol=1e-6)
+    assert torch.allclose(got["rv"], model.bn1.running_var, atol=1e-5)
+    assert err <= 3 * floor + 1e-5, (err, floor)
+
+
+def _metrics_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from ddp_classification_pytorch_amd.parallel.ddp import all_reduce_metrics, reduce_loss
+
+    vec = torch.tensor([float(rank + 1), 2.0 * rank, 1.0, 10.0], dtype=torch.float64)
+    all_reduce_metrics(vec)
+    rl = reduce_loss(torch.tensor(float(rank + 1)), world)
+    if rank == 0:
+        torch.save({"vec": vec, "rl": rl}, os.path.join(out_dir, "m.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exact_metric_allreduce_and_reduce_loss():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_metrics_worker, args=(3, _free_port(), d), nprocs=3, join=True)
+        got = torch.load(os.path.join(d, "m.pt"), weights_only=True)
+    assert got["vec"].tolist() == [6.0, 6.0, 3.0, 30.0]
+    assert float(got["rl"]) == pytest.approx(2.0)  # (1+2+3)/3 on rank 0 (BASELINE/main.py:52-56)
+
+
+def _entry_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import main as entry
+
+    entry.main(["--workload", "baseline", "--model", "cifar_resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+                "--batchsize", "4", "--synthetic-train-size", "24", "--synthetic-val-size", "10", "--workers", "0",
+                "--epochs", "1", "--device", "cpu", "--syncbn", "--out-dir", out_dir, "--log-interval", "100"])
+
+
+def test_entry_point_two_ranks_gloo():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_entry_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        assert os.path.exists(os.path.join(d, "last.pth"))
+        txt = open(os.path.join(d, "output.txt")).read()
+        assert "(n=10)" in txt  # exact val count: sampler padding excluded

@@ -113,11 +113,11 @@ def test_linear(K, B, K_, N, relu, bias):
     w = torch.randn(N, K_) / math.sqrt(K_)
     b = torch.randn(N) if bias else None
     wb, wt = K.weight_prep(w.to(DEV), N, True)
-    y = K.linear_fwd(x.to(DEV), wb, b.to(DEV) if bias else None, relu)
-    yr = _ref.linear_fwd(x.float(), w.bfloat16().float(), b, relu)
+    y = K.linear_fwd(x.to(DEV), wb, b.to(DEV) if bias else None, int(relu))
+    yr = _ref.linear_fwd(x.float(), w.bfloat16().float(), b, int(relu))
     assert relerr(y, yr) < 1e-2
     dy = rnd(B, N)
-    dx = K.linear_fwd(dy.to(DEV), wt, None, False)
+    dx = K.linear_fwd(dy.to(DEV), wt, None, 0)
     assert relerr(dx, dy.float() @ w.bfloat16().float()) < 1e-2
     dw = K.linear_wgrad(dy.to(DEV), x.to(DEV))
     assert relerr(dw, dy.float().t() @ x.float()) < 5e-3
@@ -325,10 +325,25 @@ def test_grouped_and_dw_and_se(K):
     assert relerr(K.dwconv_bwd(dz.to(DEV), filt.to(DEV), 14, 14, 3, 2, 1, True),
                   _ref.dwconv_bwd(dz.float(), filt, 14, 14, 3, 2, 1, True)) < 1e-2
     g = rnd(2, 128)
-    assert relerr(K.chan_scale_fwd(x.to(DEV), g.to(DEV)), _ref.chan_scale_fwd(x.float(), g.float())) < 1e-2
-    dxs, dgs = K.chan_scale_bwd(dz.to(DEV)[:, :, :, :].contiguous() if False else rnd(*x.shape).to(DEV), x.to(DEV),
-                                g.to(DEV))
-    assert dxs.shape == x.shape and dgs.shape == (2, 128)
+    r = rnd(*x.shape)
+    for res, relu in [(None, False), (r, True)]:
+        rd = res.to(DEV) if res is not None else None
+        rf = res.float() if res is not None else None
+        assert relerr(K.chan_scale_fwd(x.to(DEV), g.to(DEV), rd, relu),
+                      _ref.chan_scale_fwd(x.float(), g.float(), rf, relu)) < 1e-2
+        dyy = rnd(*x.shape)
+        got = K.chan_scale_bwd(dyy.to(DEV), x.to(DEV), g.to(DEV), rd, relu, res is not None)
+        want = _ref.chan_scale_bwd(dyy.float(), x.float(), g.float(), rf, relu, res is not None)
+        assert relerr(got[0], want[0]) < 1e-2 and relerr(got[1], want[1]) < 1e-2
+        if res is not None:
+            assert relerr(got[2], want[2]) < 1e-2
+    # sigmoid linear + its backward
+    xs, ws = rnd(8, 64), torch.randn(64, 64) / 8
+    wb, _ = K.weight_prep(ws.to(DEV), 64, False)
+    ys = K.linear_fwd(xs.to(DEV), wb, None, 2)
+    assert relerr(ys, torch.sigmoid(xs.float() @ ws.bfloat16().float().t())) < 1e-2
+    dys = rnd(8, 64)
+    assert relerr(K.act_bwd(dys.to(DEV), ys, 2), _ref.act_bwd(dys.float(), ys.float().cpu(), 2)) < 2e-2
 
 
 def test_to_nhwc(K):

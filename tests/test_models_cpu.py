@@ -1,0 +1,90 @@
+"""Model zoo: parameter counts (SURVEY.md §2.5.1 / torchvision / timm), shapes,
+reference smoke test (NESTED/model/model.py:79-90), checkpoint formats."""
+import pytest
+import torch
+
+from ddp_classification_pytorch_amd.models import build_model
+from ddp_classification_pytorch_amd.models.heads import ArcMarginProduct, MLPHead, NetClassifier
+from ddp_classification_pytorch_amd.models.nested import NetFeat
+from ddp_classification_pytorch_amd.ops import functional as Fn
+
+
+def nparams(m):
+    return sum(p.numel() for p in m.parameters())
+
+
+@pytest.mark.parametrize("name,classes,expected", [
+    ("resnet18", 1000, 11_689_512),
+    ("resnet50", 1000, 25_557_032),
+    ("resnet101", 1000, 44_549_160),
+    ("resnet152", 1000, 60_192_808),
+    ("resnet34", 1000, 21_797_672),
+    ("cifar_resnet18", 100, 11_220_132),
+    ("resnext50_32x4d", 1000, 25_028_904),
+    ("tresnet_m", 1000, 31_389_032),  # timm tresnet_m
+    ("vgg19_bn", 1000, 143_678_248 - 5_504),  # torchvision minus the conv biases BN makes redundant
+])
+def test_param_counts(name, classes, expected):
+    assert nparams(build_model(name, num_classes=classes)) == expected
+
+
+def test_baseline_head_param_count():
+    # ResNet-50 + BASELINE MLP head (2048->512->2173) = 25,671,869 ... minus fc(2048->1000)
+    bb = build_model("resnet50", num_classes=0)
+    head = MLPHead(2048, 512, 2173)
+    assert nparams(bb) + nparams(head) == 23_508_032 + 2048 * 512 + 512 + 512 * 2173 + 2173
+
+
+@pytest.mark.parametrize("name,size,cpad", [("resnet18", 64, 8), ("resnext50_32x4d", 64, 8), ("tresnet_m", 64, 3),
+                                            ("cifar_resnet18", 32, 8)])
+def test_forward_backward_shapes(name, size, cpad):
+    torch.manual_seed(0)
+    m = build_model(name, num_classes=7)
+    x = Fn.to_device_nhwc(torch.randn(2, 3, size, size), cpad=cpad)
+    y = m(x)
+    assert y.shape == (2, 7)
+    Fn.cross_entropy(y, torch.tensor([0, 6])).backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters() if p.requires_grad)
+
+
+def test_reference_nested_smoke():
+    """NESTED/model/model.py:79-90: CIFAR NetFeat(resnet18) -> [3,512]; NetClassifier(512,10) -> [3,10]."""
+    feat = NetFeat("resnet18", "CIFAR100")
+    cls = NetClassifier(feat.feat_dim, 10)
+    x = Fn.to_device_nhwc(torch.randn(3, 3, 32, 32), cpad=8)
+    f = feat(x)
+    assert f.shape == (3, 512)
+    assert cls(f).shape == (3, 10)
+    assert cls.weight.shape == (512, 10)  # reference layout [feat_dim, nb_cls]
+
+
+def test_netfeat_freeze_bn():
+    feat = NetFeat("resnet18", "Clothing1M")
+    feat.train(True, freeze_bn=True)
+    bns = [m for m in feat.modules() if m.__class__.__name__ == "BatchNorm2d"]
+    assert bns and all(not b.training and not b.weight.requires_grad for b in bns)
+    rm = bns[0].running_mean.clone()
+    feat(Fn.to_device_nhwc(torch.randn(2, 3, 64, 64), cpad=8))
+    assert torch.equal(rm, bns[0].running_mean)  # frozen: running stats untouched
+
+
+def test_torchvision_layout_state_dict_loads():
+    m = build_model("resnet18", num_classes=10)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    # convert our NHWC conv weights to torchvision [Co,Ci,KH,KW] and back through load_state_dict
+    tv = {k: (v.permute(0, 3, 1, 2).contiguous() if v.dim() == 4 else v) for k, v in sd.items()}
+    m2 = build_model("resnet18", num_classes=10)
+    m2.load_state_dict(tv)
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+
+
+def test_arc_margin_reference_formula():
+    torch.manual_seed(0)
+    arc = ArcMarginProduct(16, 9, s=30, m=0.5, easy_margin=True)
+    x = torch.randn(5, 16)
+    y = torch.randint(0, 9, (5,))
+    logits = arc.margin_logits(x, y)
+    loss, rank, out = arc(x, y, return_logits=True)
+    assert torch.allclose(out, logits, atol=1e-4)
+    assert abs(loss.item() - torch.nn.functional.cross_entropy(logits, y).item()) < 1e-4
