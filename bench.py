@@ -41,12 +41,15 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="r50", choices=["r50", "arcface", "resnext", "r101", "tresnet"],
+                    help="BASELINE.json config: r50 (headline), arcface (R50+ArcFace 10k cls @112), "
+                         "resnext (ResNeXt-50 32x4d), r101 (ResNet-101 large batch), tresnet (BASELINE default)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--image-size", type=int, default=None)
+    ap.add_argument("--num-classes", type=int, default=None)
     ap.add_argument("--syncbn", action="store_true", help="cross-replica BN (reference default); off = local BN")
     ap.add_argument("--bucket-cap-mb", type=float, default=100.0)
     ap.add_argument("--lr", type=float, default=0.1)
@@ -54,8 +57,38 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+CONFIGS = {
+    "r50": dict(model="resnet50", batch=256, image_size=224, num_classes=1000),
+    "arcface": dict(model="resnet50", batch=256, image_size=112, num_classes=10000),
+    "resnext": dict(model="resnext50_32x4d", batch=128, image_size=224, num_classes=1000),
+    "r101": dict(model="resnet101", batch=512, image_size=224, num_classes=1000),
+    "tresnet": dict(model="tresnet_m", batch=256, image_size=224, num_classes=1000),
+}
+METRICS = {
+    "r50": "images/sec (whole node), ResNet-50 224px DDP at 1/2/4/8 MI355X",
+    "arcface": "images/sec (whole node), ResNet-50 + ArcFace head, 10k-class 112px, DDP",
+    "resnext": "images/sec (whole node), ResNeXt-50 32x4d 224px, DDP",
+    "r101": "images/sec (whole node), ResNet-101 224px large per-GPU batch, DDP",
+    "tresnet": "images/sec (whole node), TResNet-M 224px, DDP",
+}
+
+
+def build_bench_model(a):
+    if a.config == "arcface":
+        from ddp_classification_pytorch_amd.algos.arcface import ArcFaceModel
+        from ddp_classification_pytorch_amd.models.heads import ArcMarginProduct, MLPHead
+
+        bb = build_model(a.model, num_classes=0)
+        return ArcFaceModel(bb, MLPHead(bb.feat_dim, 512, 256, log_softmax=True),
+                            ArcMarginProduct(256, a.num_classes, s=30.0, m=0.5, easy_margin=True))
+    return build_model(a.model, num_classes=a.num_classes)
+
+
 def main(argv=None):
     a = parse(argv)
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -68,7 +101,7 @@ def main(argv=None):
     _ext.hip_ops()  # fail loudly if the gfx950 library is missing
 
     torch.manual_seed(1234 + rank)
-    model = build_model(a.model, num_classes=a.num_classes).to(dev)
+    model = build_bench_model(a).to(dev)
     if world > 1:
         model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb)
     opt = FusedSGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
@@ -81,10 +114,14 @@ def main(argv=None):
     mean = torch.tensor(IMAGENET_MEAN, device=dev)
     std = torch.tensor(IMAGENET_STD, device=dev)
 
+    cpad = 3 if a.model.startswith("tresnet") else 8
+
     def step():
-        x = Fn.to_device_nhwc(images, mean, std, cpad=8, nchw=True, in_scale=1.0 / 255.0)
-        logits = model(x)
-        loss = Fn.cross_entropy(logits, labels)
+        x = Fn.to_device_nhwc(images, mean, std, cpad=cpad, nchw=True, in_scale=1.0 / 255.0)
+        if a.config == "arcface":
+            loss, _ = model(x, labels)
+        else:
+            loss = Fn.cross_entropy(model(x), labels)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
@@ -121,7 +158,7 @@ def main(argv=None):
     ips = B * world * a.steps / dt
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node), ResNet-50 224px DDP at 1/2/4/8 MI355X",
+            "metric": METRICS[a.config],
             "value": round(ips, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -130,7 +167,7 @@ def main(argv=None):
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": None,  # the reference publishes no throughput
             "dtype": "bf16",
             "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
             "config": {
