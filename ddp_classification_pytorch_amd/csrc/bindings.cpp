@@ -243,7 +243,8 @@ Tensor grouped_conv_fwd(const Tensor& x, const Tensor& w, int64_t groups, int64_
   TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "grouped conv channel multiples of 8");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
-  dcp::launch_grouped_conv_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
+  auto frag = at::empty({std::max(dcp::gconv_frag_elems(C, groups, KH, KW), 8)}, bf16_like(x));
+  dcp::launch_grouped_conv_fwd(bp(x), bp(w), bpm(y), bpm(frag), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
                                cur_stream());
   return y;
 }
@@ -255,7 +256,8 @@ Tensor grouped_conv_dgrad(const Tensor& dy, const Tensor& w, int64_t H, int64_t 
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
   const int KH = w.size(1), KW = w.size(2), C = w.size(3) * groups;
   auto dx = at::empty({N, H, W, C}, bf16_like(dy));
-  dcp::launch_grouped_conv_dgrad(bp(dy), bp(w), bpm(dx), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
+  auto frag = at::empty({std::max(dcp::gconv_frag_elems(C, groups, KH, KW), 8)}, bf16_like(dy));
+  dcp::launch_grouped_conv_dgrad(bp(dy), bp(w), bpm(dx), bpm(frag), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride, pad,
                                  cur_stream());
   return dx;
 }
@@ -266,9 +268,12 @@ Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t
   CHECK_ACT(x);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
   const int H = x.size(1), W = x.size(2), C = x.size(3);
-  auto dw = at::zeros({Co, KH, KW, C / groups}, f32_like(dy));
-  dcp::launch_grouped_conv_wgrad(bp(dy), bp(x), dw.data_ptr<float>(), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride,
-                                 pad, cur_stream());
+  auto dw = at::empty({Co, KH, KW, C / groups}, f32_like(dy));
+  const int splits = Co == C ? dcp::gconv_mfma_wgrad_splits(N, Ho, Wo, C, groups) : 0;
+  auto part = at::empty({std::max(splits, 1) * (int64_t)dw.numel()}, f32_like(dy));
+  dcp::launch_grouped_conv_wgrad(bp(dy), bp(x), dw.data_ptr<float>(), part.data_ptr<float>(), splits,
+                                 zero_page(dy.get_device()), N, H, W, C, Ho,
+                                 Wo, Co, groups, KH, KW, stride, pad, cur_stream());
   return dw;
 }
 

@@ -1,8 +1,6 @@
 // Kernels for the non-ResNet model families:
-//   * grouped convolution (ResNeXt-50 32x4d, BASELINE.json config 4; SURVEY.md
-//     §2.5 K26): direct NHWC kernels with 8 output channels per thread; the
-//     per-group widths (4..32 channels) are far below one MFMA tile, so the
-//     work is spread over threads instead and stays memory-bound;
+//   * grouped convolution fallback (shapes the MFMA super-group kernels of
+//     gconv.hip do not cover): direct NHWC kernels, 8 channels per thread;
 //   * depthwise k x k filter with reflect padding (TResNet anti-aliased
 //     downsampling "blur pool", timm tresnet);
 //   * per-(sample, channel) scaling for squeeze-and-excitation (K22).
@@ -131,175 +129,6 @@ __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const bf16* __restrict
     acc += bf2f(dy[(size_t)m * Co + co]) * bf2f(x[(((size_t)n * H + hi) * W + wi) * C + ci]);
   }
   atomicAdd(dw + e, acc);
-}
-
-// ---------------------------------------------------------------------------
-// Specialised grouped conv (CG input / COG output channels per group, both in
-// {4, 8, 16, 32}: ResNeXt 32xNd).  One thread = one output (fwd) or input
-// (dgrad) pixel of ONE group; the group's weights sit in LDS as fp32 laid out
-// so every lane reads the same address (broadcast); channel vectors load as
-// 8..64-byte chunks.  The wgrad assigns weight elements to lanes and splits
-// the pixel reduction over lanes + workgroups.
-// ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void load_bf16(const bf16* __restrict__ p, float* out) {
-  if constexpr (N % 8 == 0) {
-#pragma unroll
-    for (int i = 0; i < N / 8; ++i) {
-      const bf16x8 v = *(const bf16x8*)(p + i * 8);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) out[i * 8 + k] = bf2f(v[k]);
-    }
-  } else {
-    const bf16x4 v = *(const bf16x4*)p;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = bf2f(v[k]);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void store_bf16(bf16* __restrict__ p, const float* in) {
-  if constexpr (N % 8 == 0) {
-#pragma unroll
-    for (int i = 0; i < N / 8; ++i) {
-      bf16x8 v;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = f2bf(in[i * 8 + k]);
-      *(bf16x8*)(p + i * 8) = v;
-    }
-  } else {
-    bf16x4 v;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = f2bf(in[k]);
-    *(bf16x4*)p = v;
-  }
-}
-
-// fwd: y[pix][g*COG + j] = sum_{t,c} x[src(pix,t)][g*CG + c] * w[g*COG + j][t][c]
-template <int CG, int COG>
-__global__ void __launch_bounds__(256) gconv_fwd_t(const bf16* __restrict__ x, const bf16* __restrict__ w,
-                                                   bf16* __restrict__ y, int N, int H, int W, int C, int Ho, int Wo,
-                                                   int Co, int KH, int KW, int s, int p) {
-  extern __shared__ float wl[];  // [t][c][j]
-  const int g = blockIdx.y;
-  const int T = KH * KW;
-  for (int e = threadIdx.x; e < COG * T * CG; e += 256) {
-    const int c = e % CG, t = (e / CG) % T, j = e / (CG * T);
-    wl[(t * CG + c) * COG + j] = bf2f(w[((size_t)(g * COG + j) * T + t) * CG + c]);
-  }
-  __syncthreads();
-  const int pix = blockIdx.x * 256 + threadIdx.x;
-  if (pix >= N * Ho * Wo) return;
-  const int wo = pix % Wo, ho = (pix / Wo) % Ho, n = pix / (Wo * Ho);
-  float acc[COG];
-#pragma unroll
-  for (int j = 0; j < COG; ++j) acc[j] = 0.f;
-  for (int kh = 0; kh < KH; ++kh) {
-    const int hi = ho * s - p + kh;
-    if ((unsigned)hi >= (unsigned)H) continue;
-    for (int kw = 0; kw < KW; ++kw) {
-      const int wi = wo * s - p + kw;
-      if ((unsigned)wi >= (unsigned)W) continue;
-      float xv[CG];
-      load_bf16<CG>(x + (((size_t)n * H + hi) * W + wi) * C + g * CG, xv);
-      const float* wt = wl + (kh * KW + kw) * CG * COG;
-#pragma unroll
-      for (int c = 0; c < CG; ++c)
-#pragma unroll
-        for (int j = 0; j < COG; ++j) acc[j] += xv[c] * wt[c * COG + j];
-    }
-  }
-  store_bf16<COG>(y + (size_t)pix * Co + g * COG, acc);
-}
-
-// dgrad: dx[pix_in][g*CG + c] = sum_{t,j} dy[dst(pix_in,t)][g*COG + j] * w[g*COG + j][t][c]
-template <int CG, int COG>
-__global__ void __launch_bounds__(256) gconv_dgrad_t(const bf16* __restrict__ dy, const bf16* __restrict__ w,
-                                                     bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
-                                                     int Wo, int Co, int KH, int KW, int s, int p) {
-  extern __shared__ float wl[];  // [t][j][c]
-  const int g = blockIdx.y;
-  const int T = KH * KW;
-  for (int e = threadIdx.x; e < COG * T * CG; e += 256) {
-    const int c = e % CG, t = (e / CG) % T, j = e / (CG * T);
-    wl[(t * COG + j) * CG + c] = bf2f(w[((size_t)(g * COG + j) * T + t) * CG + c]);
-  }
-  __syncthreads();
-  const int pix = blockIdx.x * 256 + threadIdx.x;
-  if (pix >= N * H * W) return;
-  const int wi = pix % W, hi = (pix / W) % H, n = pix / (W * H);
-  float acc[CG];
-#pragma unroll
-  for (int c = 0; c < CG; ++c) acc[c] = 0.f;
-  for (int kh = 0; kh < KH; ++kh) {
-    const int th = hi + p - kh;
-    if (th < 0 || th % s) continue;
-    const int ho = th / s;
-    if (ho >= Ho) continue;
-    for (int kw = 0; kw < KW; ++kw) {
-      const int tw = wi + p - kw;
-      if (tw < 0 || tw % s) continue;
-      const int wo = tw / s;
-      if (wo >= Wo) continue;
-      float gv[COG];
-      load_bf16<COG>(dy + (((size_t)n * Ho + ho) * Wo + wo) * Co + g * COG, gv);
-      const float* wt = wl + (kh * KW + kw) * COG * CG;
-#pragma unroll
-      for (int j = 0; j < COG; ++j)
-#pragma unroll
-        for (int c = 0; c < CG; ++c) acc[c] += gv[j] * wt[j * CG + c];
-    }
-  }
-  store_bf16<CG>(dx + (size_t)pix * C + g * CG, acc);
-}
-
-// wgrad: lane owns (j, c) of group g for all taps; pixels split over PS lanes and gridDim.x
-template <int CG, int COG>
-__global__ void __launch_bounds__(256) gconv_wgrad_t(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                     float* __restrict__ dw, int N, int H, int W, int C, int Ho,
-                                                     int Wo, int Co, int KH, int KW, int s, int p,
-                                                     int rows_per_split) {
-  constexpr int PAIRS = CG * COG;
-  constexpr int PS = PAIRS >= 256 ? 1 : 256 / PAIRS;  // pixel lanes per pair
-  constexpr int TMAX = 9;
-  const int g = blockIdx.y;
-  const int T = KH * KW;
-  const int M = N * Ho * Wo;
-  const int m0 = blockIdx.x * rows_per_split, m1 = min(M, m0 + rows_per_split);
-  for (int pb = 0; pb < PAIRS; pb += 256 / PS) {
-    const int pair = pb + threadIdx.x % (256 / PS);
-    const int lane_p = threadIdx.x / (256 / PS);
-    const bool active = pair < PAIRS;
-    const int j = pair / CG, c = pair % CG;
-    float acc[TMAX];
-#pragma unroll
-    for (int t = 0; t < TMAX; ++t) acc[t] = 0.f;
-    if (active && T <= TMAX) {
-      for (int m = m0 + lane_p; m < m1; m += PS) {
-        const int wo = m % Wo, ho = (m / Wo) % Ho, n = m / (Wo * Ho);
-        const float gv = bf2f(dy[(size_t)m * Co + g * COG + j]);
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-          if (t >= T) break;
-          const int hi = ho * s - p + t / KW, wi = wo * s - p + t % KW;
-          if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-            acc[t] += gv * bf2f(x[(((size_t)n * H + hi) * W + wi) * C + g * CG + c]);
-        }
-      }
-    }
-    __shared__ float red[256][TMAX + 1];
-#pragma unroll
-    for (int t = 0; t < TMAX; ++t) red[threadIdx.x][t] = acc[t];
-    __syncthreads();
-    if (lane_p == 0 && active) {
-      for (int t = 0; t < T && t < TMAX; ++t) {
-        float v = 0.f;
-        for (int q = 0; q < PS; ++q) v += red[threadIdx.x + q * (256 / PS)][t];
-        atomicAdd(dw + ((size_t)(g * COG + j) * T + t) * CG + c, v);
-      }
-    }
-    __syncthreads();
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -476,60 +305,32 @@ static inline int grid_of(size_t n) {
   return (int)g;
 }
 
-#define GCONV_DISPATCH(CGV, COGV, BODY)                                            \
-  if (CGV == 4 && COGV == 4) { constexpr int CG_ = 4, COG_ = 4; BODY; return; }     \
-  if (CGV == 8 && COGV == 8) { constexpr int CG_ = 8, COG_ = 8; BODY; return; }     \
-  if (CGV == 16 && COGV == 16) { constexpr int CG_ = 16, COG_ = 16; BODY; return; } \
-  if (CGV == 32 && COGV == 32) { constexpr int CG_ = 32, COG_ = 32; BODY; return; }
-
-void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
-                             int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
-  const int CG = C / G, COG = Co / G;
-  const int P = N * Ho * Wo;
-  if (KH * KW <= 9) {
-    GCONV_DISPATCH(CG, COG,
-                   hipLaunchKernelGGL((gconv_fwd_t<CG_, COG_>), dim3((P + 255) / 256, G), dim3(256),
-                                      CG_ * COG_ * KH * KW * 4, s, x, w, y, N, H, W, C, Ho, Wo, Co, KH, KW, stride,
-                                      pad))
-  }
+void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  if (launch_gconv_mfma_fwd(x, w, y, frag, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s)) return;
   const size_t total = (size_t)N * Ho * Wo * (Co / 8);
   hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, s, x, w, y, N, H, W, C, Ho, Wo, Co, G, KH,
                      KW, stride, pad);
 }
-void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
-                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
-  const int CG = C / G, COG = Co / G;
-  const int P = N * H * W;
-  if (KH * KW <= 9) {
-    GCONV_DISPATCH(CG, COG,
-                   hipLaunchKernelGGL((gconv_dgrad_t<CG_, COG_>), dim3((P + 255) / 256, G), dim3(256),
-                                      CG_ * COG_ * KH * KW * 4, s, dy, w, dx, N, H, W, C, Ho, Wo, Co, KH, KW, stride,
-                                      pad))
-  }
+void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C,
+                               int Ho, int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  if (launch_gconv_mfma_dgrad(dy, w, dx, frag, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s)) return;
   const size_t total = (size_t)N * H * W * (C / 8);
   hipLaunchKernelGGL(gconv_dgrad_kernel, dim3(grid_of(total)), dim3(256), 0, s, dy, w, dx, N, H, W, C, Ho, Wo, Co, G,
                      KH, KW, stride, pad);
 }
-void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Ho, int Wo,
-                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
-  const int CG = C / G, COG = Co / G;
+void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
+                               int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
+                               int pad, hipStream_t s) {
+  if (launch_gconv_mfma_wgrad(dy, x, dw, part, splits, zero, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s)) return;
+  hipMemsetAsync(dw, 0, sizeof(float) * (size_t)Co * KH * KW * (C / G), s);
   const int M = N * Ho * Wo;
-  if (KH * KW <= 9) {
-    // ~2048 workgroups in total over (splits x groups)
-    int splits = 2048 / G;
-    if (splits < 1) splits = 1;
-    if (splits > (M + 127) / 128) splits = (M + 127) / 128;
-    const int rps = (M + splits - 1) / splits;
-    GCONV_DISPATCH(CG, COG,
-                   hipLaunchKernelGGL((gconv_wgrad_t<CG_, COG_>), dim3(splits, G), dim3(256), 0, s, dy, x, dw, N, H,
-                                      W, C, Ho, Wo, Co, KH, KW, stride, pad, rps))
-  }
   const int nw = Co * KH * KW * (C / G);
-  int splits = 2048 / ((nw + 255) / 256);
-  if (splits < 1) splits = 1;
-  if (splits > (M + 63) / 64) splits = (M + 63) / 64;
-  const int rps = (M + splits - 1) / splits;
-  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((nw + 255) / 256, splits), dim3(256), 0, s, dy, x, dw, N, H, W, C, Ho,
+  int nsplit = 2048 / ((nw + 255) / 256);
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > (M + 63) / 64) nsplit = (M + 63) / 64;
+  const int rps = (M + nsplit - 1) / nsplit;
+  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((nw + 255) / 256, nsplit), dim3(256), 0, s, dy, x, dw, N, H, W, C, Ho,
                      Wo, Co, G, KH, KW, stride, pad, rps);
 }
 void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,

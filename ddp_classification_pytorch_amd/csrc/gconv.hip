@@ -1,0 +1,565 @@
+// Grouped convolution on the matrix cores (ResNeXt-50 32x4d, BASELINE.json
+// config 4; reference: torchvision resnext50_32x4d as
+// built by BASELINE/train.py `--model`).
+//
+// The group widths of ResNeXt (CG = 4, 8, 16, 32 channels) are far below an
+// MFMA tile, so channels are processed in "super-groups" of SG = 16 or 32
+// channels (SG a multiple of CG).  Inside a super-group the grouped conv is a
+// dense SG x (T*SG) GEMM whose weight is block-diagonal: the zero blocks cost
+// MFMA issue slots (cheap: the op is memory-bound) but let every operand be a
+// plain 16x16x32 bf16 fragment.
+//
+// One workgroup = 256 consecutive destination pixels (linear n,y,x order) of
+// one super-group.  The source rows those pixels touch (a contiguous range of
+// global rows n*Hs+h) are staged once in LDS with 16-byte loads, so every tap
+// re-reads LDS instead of L2.  Pixel index 0 of the LDS image is a zero pixel
+// that out-of-range taps point at ("pad, don't mask").
+//
+//   fwd  : dst = y  [N,Ho,Wo,C], src = x  rows  y*s + (kh-p)
+//   dgrad: dst = dx [N,H,W,C],   src = dy rows (y + (p-kh)) / s when divisible
+//   wgrad: A = dy^T and B = gathered x, both read with ds_read_b64_tr_b16 from
+//          LDS images [pixel][SG]; per-split partials reduced deterministically.
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+namespace {
+
+constexpr int GP = 256;  // destination pixels per workgroup / wgrad chunk
+constexpr int GT = 9;    // max taps
+
+struct GconvParams {
+  const bf16* src;  // gathered image [N][Hs][Ws][C]
+  const bf16* w;    // [C][T][CG] grouped weight (bf16)
+  bf16* dst;        // fwd / dgrad output [N][Hd][Wd][C]
+  const bf16* dy;   // wgrad: [N][Hd][Wd][C]
+  float* part;      // wgrad: [splits][C][T][CG]
+  const bf16* wfrag;  // fwd/dgrad: fragment-ordered block-diagonal weight (gconv_frag_kernel)
+  const bf16* zero;   // >= 16 bytes of zeros (global)
+  int nbuf;           // wgrad: 2 = double-buffered chunks
+  int Hs, Ws, Hd, Wd, C, CG, T;
+  int ss, sd;       // src row = (dst_row*ss + oh) / sd, sd in {1, 2}
+  int M;            // N*Hd*Wd
+  int nsg, ntiles;  // super-groups, total tiles (pixel blocks x nsg)
+  int rows_per_split, bufb;  // wgrad: pixels per split, LDS bytes per chunk buffer
+  int ohmin, ohmax;
+  FastDiv div_wd, div_hd;
+  int8_t oh[GT + 1], ow[GT + 1];
+};
+
+__device__ __forceinline__ int floor_sd(int v, int sd) { return sd == 1 ? v : (v >> 1); }
+
+// contiguous global-row range [R_lo, R_lo + NR) of src rows touched by dst pixels [m0, m1]
+__device__ __forceinline__ void halo_rows(const GconvParams& p, int m0, int m1, int& R_lo, int& NR) {
+  const uint32_t q0 = fdiv((uint32_t)m0, p.div_wd), q1 = fdiv((uint32_t)m1, p.div_wd);
+  const int n0 = (int)fdiv(q0, p.div_hd), n1 = (int)fdiv(q1, p.div_hd);
+  const int y0 = (int)q0 - n0 * p.Hd, y1 = (int)q1 - n1 * p.Hd;
+  const int rlo = max(0, floor_sd(y0 * p.ss + p.ohmin, p.sd));
+  const int rhi = min(p.Hs - 1, floor_sd(y1 * p.ss + p.ohmax, p.sd));
+  R_lo = n0 * p.Hs + rlo;
+  NR = n1 * p.Hs + rhi - R_lo + 1;
+}
+
+// stage NR*Ws pixels x SG channels of super-group sg at LDS pixel 1.. with
+// LDS-DMA (global_load_lds: lane data lands at wave base + 16*lane, and the
+// image is laid out in exactly the enumeration order); zero pixel at 0.
+template <int SG>
+__device__ __forceinline__ void stage_halo(const GconvParams& p, char* img, int sg, int R_lo, int NR) {
+  constexpr int CH = SG / 8;
+  const int total = NR * p.Ws * CH;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bf16* base = p.src + (size_t)R_lo * p.Ws * p.C + sg * SG;
+  for (int e0 = wave * 64; e0 < total; e0 += 256) {
+    const int e = e0 + lane;
+    if (e < total)
+      __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)(e / CH) * p.C + (e % CH) * 8),
+                                       LDS_PTR(void, img + SG * 2 + e0 * 16), 16, 0, 0);
+  }
+}
+
+template <int SG>
+__device__ __forceinline__ void zero_pixel(char* img) {
+  if (threadIdx.x < SG / 8) *(bf16x8*)(img + threadIdx.x * 16) = bf16x8{};
+}
+
+struct PixGeo {
+  int rb;   // (n*Hs - R_lo) : row base relative to the halo
+  int yy, xx;
+  bool ok;
+};
+
+__device__ __forceinline__ PixGeo pix_geo(const GconvParams& p, int m, int R_lo) {
+  PixGeo g;
+  g.ok = m < p.M;
+  const uint32_t mm = g.ok ? (uint32_t)m : 0u;
+  const uint32_t q = fdiv(mm, p.div_wd);
+  const int x = (int)(mm - q * p.Wd);
+  const int n = (int)fdiv(q, p.div_hd);
+  const int y = (int)q - n * p.Hd;
+  g.rb = n * p.Hs - R_lo;
+  g.yy = y * p.ss;
+  g.xx = x * p.ss;
+  return g;
+}
+
+// LDS pixel index of tap (oh, ow) for a destination pixel, 0 = zero pixel
+__device__ __forceinline__ int tap_idx(const GconvParams& p, const PixGeo& g, int oh, int ow, bool tap_ok) {
+  int h = g.yy + oh, w = g.xx + ow;
+  bool ok = g.ok && tap_ok;
+  if (p.sd != 1) {
+    ok = ok && (((h | w) & 1) == 0);
+    h >>= 1;
+    w >>= 1;
+  }
+  ok = ok && (unsigned)h < (unsigned)p.Hs && (unsigned)w < (unsigned)p.Ws;
+  return ok ? 1 + (g.rb + h) * p.Ws + w : 0;
+}
+
+// A fragment of the block-diagonal dense weight: 8 k-values (tap t, channels c0..c0+7)
+// of row `row`.  DGRAD=false: row = output channel, k channel = input channel;
+// DGRAD=true: row = input channel, k channel = output channel.
+template <int SG, bool DGRAD>
+__device__ __forceinline__ bf16x8 w_frag(const GconvParams& p, int sg, int row, int t, int c0) {
+  bf16x8 v{};
+  if (t >= p.T) return v;
+  const int T = p.T, CG = p.CG;
+  const int grow = row / CG;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    if (c / CG != grow) continue;
+    const int co = DGRAD ? c : row;   // output channel (local)
+    const int ci = DGRAD ? row : c;   // input channel (local)
+    v[e] = p.w[((size_t)(sg * SG + co) * T + t) * CG + (ci % CG)];
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// fwd / dgrad: D[row = channel][col = pixel] = W_bd[row][k] * B[k][pixel]
+// ---------------------------------------------------------------------------
+template <int SG, bool DGRAD>
+__global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) {
+  constexpr int NRT = SG / 16;                 // 16-row tiles of the output channels
+  constexpr int TPS = SG == 16 ? 2 : 1;        // taps per k-step (32 k per MFMA)
+  constexpr int NST = (GT + TPS - 1) / TPS;    // max k-steps
+  constexpr int CPT = 4;                       // 16-pixel column tiles per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = (int)xcd_remap(blockIdx.x, p.ntiles);
+  const int sg = tile % p.nsg, pb = tile / p.nsg;
+  const int m0 = pb * GP, m1 = min(p.M, m0 + GP) - 1;
+  int R_lo, NR;
+  halo_rows(p, m0, m1, R_lo, NR);
+  stage_halo<SG>(p, smem, sg, R_lo, NR);
+  zero_pixel<SG>(smem);
+
+  const int kc = lane >> 4;                    // k-chunk of 8 within the 32-wide k-step
+  const int chunk = SG == 16 ? (kc & 1) : kc;  // 16-byte chunk of the source pixel
+  const int nst = (p.T + TPS - 1) / TPS;
+
+  // lane-private tap list + weight fragments (registers for the whole block)
+  int8_t toh[NST], tow[NST];
+  bool tok[NST];
+  bf16x8 a[NST][NRT];
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    const int t0 = st * TPS;
+    const int t = SG == 16 ? ((kc >> 1) ? t0 + 1 : t0) : t0;
+    toh[st] = SG == 16 ? ((kc >> 1) ? p.oh[t0 + 1] : p.oh[t0]) : p.oh[t0];
+    tow[st] = SG == 16 ? ((kc >> 1) ? p.ow[t0 + 1] : p.ow[t0]) : p.ow[t0];
+    tok[st] = t < p.T;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+      a[st][rt] = st < nst ? *(const bf16x8*)(p.wfrag + ((size_t)((sg * nst + st) * NRT + rt) * 64 + lane) * 8)
+                           : bf16x8{};
+  }
+
+  PixGeo g[CPT];
+#pragma unroll
+  for (int ct = 0; ct < CPT; ++ct) g[ct] = pix_geo(p, m0 + wave * 64 + ct * 16 + (lane & 15), R_lo);
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[NRT][CPT];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CPT; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    if (st < nst) {  // uniform
+      bf16x8 b[CPT];
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct) {
+        const int idx = tap_idx(p, g[ct], toh[st], tow[st], tok[st]);
+        b[ct] = *LDS_PTR(bf16x8, smem + idx * (SG * 2) + chunk * 16);
+      }
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CPT; ++ct)
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st][rt], b[ct], acc[rt][ct], 0, 0, 0);
+    }
+  }
+
+  // lane holds pixel column lane&15, channels (lane>>4)*4 .. +3 of each row tile
+#pragma unroll
+  for (int ct = 0; ct < CPT; ++ct) {
+    const int m = m0 + wave * 64 + ct * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[rt][ct][r]);
+      *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = o;
+    }
+  }
+}
+
+// fragment-ordered block-diagonal weight: [sg][st][rt][lane][8]
+template <int SG, bool DGRAD>
+__global__ void gconv_frag_kernel(const GconvParams p, bf16* __restrict__ out) {
+  constexpr int NRT = SG / 16;
+  constexpr int TPS = SG == 16 ? 2 : 1;
+  const int nst = (p.T + TPS - 1) / TPS;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.nsg * nst * NRT * 64) return;
+  const int lane = i & 63, rt = (i >> 6) % NRT, st = ((i >> 6) / NRT) % nst, sg = ((i >> 6) / NRT) / nst;
+  const int kc = lane >> 4;
+  const int t = st * TPS + (SG == 16 ? (kc >> 1) : 0);
+  const int chunk = SG == 16 ? (kc & 1) : kc;
+  *(bf16x8*)(out + (size_t)i * 8) = w_frag<SG, DGRAD>(p, sg, rt * 16 + (lane & 15), t, chunk * 8);
+}
+
+// 8 consecutive rows (k) x 16 columns of a [row][SG] bf16 LDS image, transposed:
+// lane (l&15) receives column col0 + (l&15); rows are given per lane (ra: rows 0-3, rb: 4-7)
+__device__ __forceinline__ bf16x8 tr8(const char* img_a, const char* img_b, int lane) {
+  (void)lane;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img_a));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img_b));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// ---------------------------------------------------------------------------
+// wgrad: D[j][t, c] = sum_m dy[m][j] * x[src(m,t)][c] per super-group
+// ---------------------------------------------------------------------------
+template <int SG>
+__global__ void __launch_bounds__(256) gconv_wgrad_kernel(const GconvParams p) {
+  constexpr int NRT = SG / 16;
+  constexpr int NTG = NRT * NRT;          // tile groups (row tile x column half), 9 taps each
+  constexpr int KSPLIT = 4 / NTG;         // waves sharing one tile group split the k-steps
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CH = SG / 8;
+  constexpr int DYB = GP * SG * 2;        // dy image [GP][SG] at the start of each buffer
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = (int)xcd_remap(blockIdx.x, p.ntiles);
+  const int sg = tile % p.nsg, split = tile / p.nsg;
+  const int tg = wave % NTG, kslot = wave / NTG;
+  const int rt = tg % NRT, chh = tg / NRT;
+  const int q = (lane & 15) >> 2, pp = lane & 3;
+  const int mstart = split * p.rows_per_split;
+  const int mend = min(p.M, mstart + p.rows_per_split);
+  const int nchunks = (mend - mstart + GP - 1) / GP;
+  const int bufb = p.bufb;
+
+  bool tok[GT];
+  int8_t toh[GT], tow[GT];
+#pragma unroll
+  for (int t = 0; t < GT; ++t) {
+    tok[t] = t < p.T;
+    toh[t] = p.oh[t];
+    tow[t] = p.ow[t];
+  }
+
+  // LDS-DMA of one chunk (dy rows + source halo) into buffer `buf`
+  auto issue = [&](int m0c, char* buf) -> int {
+    const int m1c = min(mend, m0c + GP) - 1;
+    int R_lo, NR;
+    halo_rows(p, m0c, m1c, R_lo, NR);
+    stage_halo<SG>(p, buf + DYB, sg, R_lo, NR);
+#pragma unroll
+    for (int e0 = wave * 64; e0 < GP * CH; e0 += 256) {
+      const int e = e0 + lane;
+      const int m = m0c + e / CH;
+      const bf16* g = m <= m1c ? p.dy + (size_t)m * p.C + sg * SG + (e % CH) * 8 : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, buf + e0 * 16), 16, 0, 0);
+    }
+    return R_lo;
+  };
+
+  f32x4 acc[GT];
+#pragma unroll
+  for (int t = 0; t < GT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  zero_pixel<SG>(smem + DYB);
+  if (p.nbuf == 2) zero_pixel<SG>(smem + bufb + DYB);
+  int R_cur = issue(mstart, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int ci = 0; ci < nchunks; ++ci) {
+    const int m0 = mstart + ci * GP;
+    const int m1 = min(mend, m0 + GP) - 1;
+    char* cur = smem + (p.nbuf == 2 ? (ci & 1) * bufb : 0);
+    int R_next = 0;
+    if (p.nbuf == 2 && ci + 1 < nchunks) R_next = issue(m0 + GP, smem + ((ci + 1) & 1) * bufb);
+    const char* dyimg = cur;
+    const char* img = cur + DYB;
+    for (int ks = kslot; ks < GP / 32; ks += KSPLIT) {
+      const int ra = ks * 32 + 8 * (lane >> 4) + q, rb = ra + 4;
+      const int col = rt * 16 + 4 * pp;
+      const bf16x8 af = tr8(dyimg + ra * (SG * 2) + col * 2, dyimg + rb * (SG * 2) + col * 2, lane);
+      const PixGeo ga = pix_geo(p, m0 + ra, R_cur);
+      const PixGeo gb = pix_geo(p, m0 + rb, R_cur);
+      const bool oka = m0 + ra <= m1, okb = m0 + rb <= m1;
+      const int bcol = (chh * 16 + 4 * pp) * 2;
+#pragma unroll
+      for (int t = 0; t < GT; ++t) {
+        if (t >= p.T) continue;  // uniform
+        const int ia = oka ? tap_idx(p, ga, toh[t], tow[t], tok[t]) : 0;
+        const int ib = okb ? tap_idx(p, gb, toh[t], tow[t], tok[t]) : 0;
+        const bf16x8 bf = tr8(img + ia * (SG * 2) + bcol, img + ib * (SG * 2) + bcol, lane);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+      }
+    }
+    if (p.nbuf == 1 && ci + 1 < nchunks) {
+      __syncthreads();
+      R_next = issue(m0 + GP, smem);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    R_cur = R_next;
+  }
+
+  // D tile (row tile rt, column half chh, tap t): lane holds column c = chh*16 + (lane&15),
+  // rows j = rt*16 + (lane>>4)*4 + r.  Waves that split the k-steps are summed in LDS.
+  float* part = p.part + (size_t)split * p.C * p.T * p.CG;
+  const int c = chh * 16 + (lane & 15);
+  if (KSPLIT > 1) {
+    float* red = (float*)smem;  // [KSPLIT][GT][64][4]
+#pragma unroll
+    for (int t = 0; t < GT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((kslot * GT + t) * 64 + lane) * 4 + r] = acc[t][r];
+    __syncthreads();
+    if (kslot != 0) return;
+#pragma unroll
+    for (int t = 0; t < GT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+        for (int k = 0; k < KSPLIT; ++k) s += red[((k * GT + t) * 64 + lane) * 4 + r];
+        acc[t][r] = s;
+      }
+  }
+#pragma unroll
+  for (int t = 0; t < GT; ++t) {
+    if (t >= p.T) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = rt * 16 + (lane >> 4) * 4 + r;
+      if (j / p.CG != c / p.CG) continue;
+      part[((size_t)(sg * SG + j) * p.T + t) * p.CG + (c % p.CG)] = acc[t][r];
+    }
+  }
+}
+
+__global__ void partial_reduce_kernel(const float* __restrict__ part, int splits, int n, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  int k = 0;
+  for (; k + 4 <= splits; k += 4)
+    s += (part[(size_t)k * n + i] + part[(size_t)(k + 1) * n + i]) +
+         (part[(size_t)(k + 2) * n + i] + part[(size_t)(k + 3) * n + i]);
+  for (; k < splits; ++k) s += part[(size_t)k * n + i];
+  out[i] = s;
+}
+
+// --- host side ------------------------------------------------------------
+int pick_sg(int C, int CG) {
+  if (CG <= 16 && 16 % CG == 0 && C % 16 == 0) return 16;
+  if (CG == 32 && C % 32 == 0) return 32;
+  return 0;
+}
+
+GconvParams make_params(int Hs, int Ws, int Hd, int Wd, int N, int C, int CG, int KH, int KW, int ss, int sd,
+                        const int* oh, const int* ow) {
+  GconvParams p{};
+  p.Hs = Hs;
+  p.Ws = Ws;
+  p.Hd = Hd;
+  p.Wd = Wd;
+  p.C = C;
+  p.CG = CG;
+  p.T = KH * KW;
+  p.ss = ss;
+  p.sd = sd;
+  p.M = N * Hd * Wd;
+  p.div_wd = make_fastdiv(Wd);
+  p.div_hd = make_fastdiv(Hd);
+  p.ohmin = 1 << 30;
+  p.ohmax = -(1 << 30);
+  for (int t = 0; t <= GT; ++t) {
+    p.oh[t] = t < p.T ? (int8_t)oh[t] : 0;
+    p.ow[t] = t < p.T ? (int8_t)ow[t] : 0;
+  }
+  for (int t = 0; t < p.T; ++t) {
+    p.ohmin = std::min(p.ohmin, oh[t]);
+    p.ohmax = std::max(p.ohmax, oh[t]);
+  }
+  return p;
+}
+
+// exact max halo rows over all 256-pixel blocks (cached per geometry)
+int max_halo_rows(const GconvParams& p, int N) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int, int, int, int, int, int>, int> cache;
+  const auto key = std::make_tuple(N, p.Hs, p.Ws, p.Hd, p.Wd, p.ss, p.sd, p.ohmin, p.ohmax);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  auto fl = [&](int v) { return p.sd == 1 ? v : (v >= 0 ? v / 2 : -((-v + 1) / 2)); };
+  int best = 1;
+  for (int m0 = 0; m0 < p.M; m0 += GP) {
+    const int m1 = std::min(p.M, m0 + GP) - 1;
+    const int q0 = m0 / p.Wd, q1 = m1 / p.Wd;
+    const int n0 = q0 / p.Hd, n1 = q1 / p.Hd;
+    const int y0 = q0 - n0 * p.Hd, y1 = q1 - n1 * p.Hd;
+    const int rlo = std::max(0, fl(y0 * p.ss + p.ohmin));
+    const int rhi = std::min(p.Hs - 1, fl(y1 * p.ss + p.ohmax));
+    best = std::max(best, n1 * p.Hs + rhi - (n0 * p.Hs + rlo) + 1);
+  }
+  cache[key] = best;
+  return best;
+}
+
+template <typename K>
+void allow_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024) hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+constexpr size_t kMaxLds = 160 * 1024;
+
+template <int SG, bool DGRAD>
+bool launch_gather(GconvParams p, int N, bf16* frag, hipStream_t s) {
+  constexpr int TPS = SG == 16 ? 2 : 1;
+  p.nsg = p.C / SG;
+  const int npb = (p.M + GP - 1) / GP;
+  p.ntiles = npb * p.nsg;
+  const size_t lds = (size_t)(1 + max_halo_rows(p, N) * p.Ws) * SG * 2;
+  if (lds > kMaxLds) return false;
+  const int nfrag = p.nsg * ((p.T + TPS - 1) / TPS) * (SG / 16) * 64;
+  hipLaunchKernelGGL((gconv_frag_kernel<SG, DGRAD>), dim3((nfrag + 255) / 256), dim3(256), 0, s, p, frag);
+  p.wfrag = frag;
+  allow_lds(gconv_gather_kernel<SG, DGRAD>, lds);
+  hipLaunchKernelGGL((gconv_gather_kernel<SG, DGRAD>), dim3(p.ntiles), dim3(256), lds, s, p);
+  return true;
+}
+
+}  // namespace
+
+int gconv_frag_elems(int C, int G, int KH, int KW) {
+  const int SG = pick_sg(C, C / G);
+  if (SG == 0 || KH * KW > GT) return 0;
+  const int TPS = SG == 16 ? 2 : 1;
+  return (C / SG) * ((KH * KW + TPS - 1) / TPS) * (SG / 16) * 64 * 8;
+}
+
+bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  const int CG = C / G;
+  const int SG = pick_sg(C, CG);
+  if (SG == 0 || Co != C || KH * KW > GT || frag == nullptr) return false;
+  int oh[GT], ow[GT];
+  for (int t = 0; t < KH * KW; ++t) {
+    oh[t] = t / KW - pad;
+    ow[t] = t % KW - pad;
+  }
+  GconvParams p = make_params(H, W, Ho, Wo, N, C, CG, KH, KW, stride, 1, oh, ow);
+  p.src = x;
+  p.w = w;
+  p.dst = y;
+  return SG == 16 ? launch_gather<16, false>(p, N, frag, s) : launch_gather<32, false>(p, N, frag, s);
+}
+
+bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+  const int CG = C / G;
+  const int SG = pick_sg(C, CG);
+  if (SG == 0 || Co != C || KH * KW > GT || stride > 2 || frag == nullptr) return false;
+  int oh[GT], ow[GT];
+  for (int t = 0; t < KH * KW; ++t) {
+    oh[t] = pad - t / KW;
+    ow[t] = pad - t % KW;
+  }
+  GconvParams p = make_params(Ho, Wo, H, W, N, C, CG, KH, KW, 1, stride, oh, ow);
+  p.src = dy;
+  p.w = w;
+  p.dst = dx;
+  return SG == 16 ? launch_gather<16, true>(p, N, frag, s) : launch_gather<32, true>(p, N, frag, s);
+}
+
+int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G) {
+  const int SG = pick_sg(C, C / G);
+  if (SG == 0) return 0;
+  const int M = N * Ho * Wo;
+  const int nsg = C / SG;
+  const int chunks = (M + GP - 1) / GP;
+  int splits = std::max(1, 2048 / nsg);
+  splits = std::min(splits, chunks);
+  const int cps = (chunks + splits - 1) / splits;  // chunks per split
+  return (chunks + cps - 1) / cps;
+}
+
+bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
+                             int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
+                             int pad, hipStream_t s) {
+  const int CG = C / G;
+  const int SG = pick_sg(C, CG);
+  if (SG == 0 || Co != C || KH * KW > GT || splits <= 0) return false;
+  int oh[GT], ow[GT];
+  for (int t = 0; t < KH * KW; ++t) {
+    oh[t] = t / KW - pad;
+    ow[t] = t % KW - pad;
+  }
+  GconvParams p = make_params(H, W, Ho, Wo, N, C, CG, KH, KW, stride, 1, oh, ow);
+  p.src = x;
+  p.dy = dy;
+  p.part = part;
+  p.zero = zero;
+  p.nsg = C / SG;
+  const int chunks = (p.M + GP - 1) / GP;
+  const int cps = (chunks + splits - 1) / splits;
+  p.rows_per_split = cps * GP;  // chunk starts stay multiples of GP (the halo bound's blocks)
+  p.ntiles = splits * p.nsg;
+  const size_t bufb = ((size_t)GP * SG * 2 + (size_t)(1 + max_halo_rows(p, N) * p.Ws) * SG * 2 + 15) / 16 * 16;
+  const size_t red = (size_t)(4 / ((SG / 16) * (SG / 16))) * GT * 64 * 4 * 4;
+  p.bufb = (int)bufb;
+  p.nbuf = (2 * bufb <= kMaxLds && cps > 1) ? 2 : 1;
+  const size_t lds = std::max(p.nbuf * bufb, red);
+  if (lds > kMaxLds) return false;
+  if (SG == 16) {
+    allow_lds(gconv_wgrad_kernel<16>, lds);
+    hipLaunchKernelGGL(gconv_wgrad_kernel<16>, dim3(p.ntiles), dim3(256), lds, s, p);
+  } else {
+    allow_lds(gconv_wgrad_kernel<32>, lds);
+    hipLaunchKernelGGL(gconv_wgrad_kernel<32>, dim3(p.ntiles), dim3(256), lds, s, p);
+  }
+  const int n = C * KH * KW * CG;
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, splits, n, dw);
+  return true;
+}
+
+}  // namespace dcp

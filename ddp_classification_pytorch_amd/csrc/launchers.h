@@ -20,12 +20,25 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16*
                      const float* bias, int relu, const bf16* zero, hipStream_t stream);
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
                   const TapList& taps, float* dw, const bf16* zero, int num_cu, hipStream_t stream);
-void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo,
-                             int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
-void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
-                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
-void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, int N, int H, int W, int C, int Ho, int Wo,
-                               int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+// frag: gconv_frag_elems(...) bf16 workspace (MFMA path; may be null -> direct kernels)
+void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C,
+                               int Ho, int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+// dw is fully written; part = workspace of gconv_mfma_wgrad_splits(...) x Co*KH*KW*(C/G) floats
+void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
+                               int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
+                               int pad, hipStream_t s);
+// MFMA super-group kernels (gconv.hip); return false for shapes they do not cover
+int gconv_frag_elems(int C, int G, int KH, int KW);
+bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G);
+bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
+                             int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
+                             int pad, hipStream_t s);
 
 int bn_stats_partials(int M, int C, bool from_slabs);
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s);

@@ -307,6 +307,27 @@ def test_nested_eval_counts(K):
     assert torch.equal(cnt.cpu(), ref)
 
 
+@pytest.mark.parametrize("N,H,W,C,G,KH,stride,pad", [
+    (2, 14, 14, 128, 32, 3, 1, 1),   # CG=4  (super-group 16, 4 groups block-diagonal)
+    (3, 13, 11, 256, 32, 3, 2, 1),   # CG=8, odd spatial, stride 2, M not a multiple of 256
+    (2, 28, 28, 512, 32, 3, 2, 1),   # CG=16
+    (4, 7, 7, 1024, 32, 3, 1, 1),    # CG=32 (super-group 32), blocks span many images
+    (3, 14, 14, 1024, 32, 3, 2, 1),  # CG=32 stride 2: the largest halo (>64 KB LDS)
+    (2, 9, 9, 64, 16, 1, 1, 0),      # 1x1 grouped
+    (2, 10, 10, 128, 2, 3, 1, 1),    # CG=64: direct-kernel fallback
+])
+def test_grouped_conv_shapes(K, N, H, W, C, G, KH, stride, pad):
+    x = rnd(N, H, W, C)
+    w = rnd(C, KH, KH, C // G, scale=0.3)
+    y = K.grouped_conv_fwd(x.to(DEV), w.to(DEV), G, stride, pad)
+    assert relerr(y, _ref.grouped_conv_fwd(x.float(), w.float(), G, stride, pad)) < 1e-2
+    dy = rnd(*y.shape)
+    dx = K.grouped_conv_dgrad(dy.to(DEV), w.to(DEV), H, W, G, stride, pad)
+    assert relerr(dx, _ref.grouped_conv_dgrad(dy.float(), w.float(), H, W, G, stride, pad)) < 1e-2
+    dw = K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), KH, KH, G, stride, pad)
+    assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), KH, KH, G, stride, pad)) < 5e-3
+
+
 def test_grouped_and_dw_and_se(K):
     x = rnd(2, 14, 14, 128)
     w = rnd(128, 3, 3, 4, scale=0.3)

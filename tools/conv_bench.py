@@ -5,6 +5,7 @@ torch channels_last bf16) on the 23 unique ResNet-50 conv shapes (SURVEY.md
 per-step totals weighted by each shape's multiplicity in ResNet-50.
 
     python tools/conv_bench.py [--batch 256] [--iters 20] [--no-miopen]
+    python tools/conv_bench.py --grouped [--batch 128]   # ResNeXt-50 32x4d grouped 3x3 convs
 """
 import argparse
 import json
@@ -28,6 +29,10 @@ R50 = [
     (2048, 512, 1, 1, 7, 2), (512, 512, 3, 1, 7, 2),
 ]
 
+# ResNeXt-50 32x4d grouped 3x3 convs: (C, stride, H_in, count), groups = 32
+RX50_GROUPED = [(128, 1, 56, 3), (256, 2, 56, 1), (256, 1, 28, 3), (512, 2, 28, 1), (512, 1, 14, 5),
+                (1024, 2, 14, 1), (1024, 1, 7, 2)]
+
 
 def timeit(fn, iters):
     for _ in range(3):
@@ -48,7 +53,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--grouped", action="store_true", help="ResNeXt-50 grouped convs instead of ResNet-50")
     a = ap.parse_args()
+    if a.grouped:
+        return grouped(a)
     K = _ext.hip_ops()
     dev = torch.device("cuda", 0)
     N = a.batch
@@ -95,6 +103,43 @@ def main():
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"batch": N, "rows": rows, "totals_us": tot}, f, indent=1)
+
+
+def grouped(a):
+    K = _ext.hip_ops()
+    dev = torch.device("cuda", 0)
+    N, G = a.batch, 32
+    tot = [0.0] * 6
+    print(f"{'shape':28s} {'fwd us':>8s} {'dgrad':>8s} {'wgrad':>8s} {'GB/s fwd':>9s} | "
+          f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s}")
+    for C, s, H, cnt in RX50_GROUPED:
+        Ho = (H + 2 - 3) // s + 1
+        x = torch.randn(N, H, H, C, device=dev).bfloat16()
+        w = (torch.randn(C, 3, 3, C // G, device=dev) / (9 * C // G) ** 0.5).bfloat16()
+        dy = torch.randn(N, Ho, Ho, C, device=dev).bfloat16()
+        t = [timeit(lambda: K.grouped_conv_fwd(x, w, G, s, 1), a.iters),
+             timeit(lambda: K.grouped_conv_dgrad(dy, w, H, H, G, s, 1), a.iters),
+             timeit(lambda: K.grouped_conv_wgrad(dy, x, 3, 3, G, s, 1), a.iters)]
+        mi = [0.0, 0.0, 0.0]
+        if not a.no_miopen:
+            xc, dyc = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
+            wc = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            mi[0] = timeit(lambda: F.conv2d(xc, wc, stride=s, padding=1, groups=G), a.iters)
+            mi[1] = timeit(lambda: torch.ops.aten.convolution_backward(
+                dyc, xc, wc, None, [s, s], [1, 1], [1, 1], False, [0, 0], G, [True, False, False]), a.iters)
+            mi[2] = timeit(lambda: torch.ops.aten.convolution_backward(
+                dyc, xc, wc, None, [s, s], [1, 1], [1, 1], False, [0, 0], G, [False, True, False]), a.iters)
+        gbs = (x.numel() + dy.numel()) * 2 / t[0] / 1e3
+        name = f"C{C} s{s} {H}->{Ho} x{cnt}"
+        print(f"{name:28s} {t[0]:8.1f} {t[1]:8.1f} {t[2]:8.1f} {gbs:9.0f} | {mi[0]:8.1f} {mi[1]:8.1f} {mi[2]:8.1f}",
+              flush=True)
+        for i, v in enumerate(t + mi):
+            tot[i] += cnt * v
+    print("per-step totals (ms): ours fwd/dgrad/wgrad = " + "/".join(f"{v / 1e3:.2f}" for v in tot[:3]) +
+          f" sum {sum(tot[:3]) / 1e3:.2f}")
+    if not a.no_miopen:
+        print("                      miopen            = " + "/".join(f"{v / 1e3:.2f}" for v in tot[3:]) +
+              f" sum {sum(tot[3:]) / 1e3:.2f}")
 
 
 if __name__ == "__main__":
