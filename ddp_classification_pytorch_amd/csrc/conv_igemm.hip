@@ -56,7 +56,9 @@ __device__ __forceinline__ uint32_t swz128(uint32_t r, uint32_t c) {
   return r * 128u + ((c ^ ((r >> 1) & 7u)) << 4);
 }
 
-template <int BN>
+// EPI: 0 = bf16 store, 1 = store + per-64-row BN statistics, 2 = bias / activation (linear heads)
+// FAST: Cs % 64 == 0, one tap per 64-deep k-tile
+template <int BN, int EPI, bool FAST>
 __global__ void __launch_bounds__(256)
 tap_gemm_kernel(const TapGemmParams p) {
   constexpr int BM = 128;                 // pixel rows per block
@@ -110,14 +112,13 @@ tap_gemm_kernel(const TapGemmParams p) {
     b_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
   }
 
-  const bool fast = (p.cpt & 7) == 0;  // Cs % 64 == 0: one tap per k-tile
   const int tiles_per_tap = p.cpt >> 3;
   const int kc_total = p.ntaps * p.cpt;
 
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
-    if (fast) {
+    if constexpr (FAST) {
       const int t = kt / tiles_per_tap;
       const int cbase = (kt - t * tiles_per_tap) * 64;
       const int dy = p.dy[t], dx = p.dx[t];
@@ -205,14 +206,89 @@ tap_gemm_kernel(const TapGemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue: bias/ReLU, bf16 store (8 B per lane), BN partial stats ----
-  const int co_lane = n0 + wn * (BN / 2) + (lane >> 4) * 4;
-  float s1[TN][4], s2[TN][4];
+  if constexpr (EPI != 2) {
+    // ---- epilogue through LDS: the k-loop ended with a barrier and no loads in flight ----
+    // tile image E[BM pixels][BN channels] bf16, 16-byte chunks XOR-swizzled by (pixel>>1)
+    constexpr int RB = BN * 2, NCH = BN / 8;
+    char* E = smem;
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+        *LDS_PTR(bf16x4, E + off) = o;
+      }
+    }
+    __syncthreads();
+    // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels
+    {
+      constexpr int R = 256 / NCH;
+      const int c = tid % NCH, pr0 = tid / NCH;
+      const bool cok = n0 + c * 8 < p.Co;
+#pragma unroll
+      for (int k = 0; k < BM / R; ++k) {
+        const int pl = pr0 + k * R;
+        const int m = m0 + pl;
+        const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+        if (m < p.M && cok) {
+          uint32_t drow;
+          if (p.ds == 1) {
+            drow = (uint32_t)m * (uint32_t)p.Co;
+          } else {
+            const uint32_t q = fdiv(m, p.div_wy);
+            const uint32_t x = m - q * p.Wy;
+            const uint32_t n = fdiv(q, p.div_hy);
+            const uint32_t y = q - n * p.Hy;
+            drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+          }
+          *(bf16x8*)(p.dst + drow + n0 + c * 8) = v;
+        }
+      }
+    }
+    if constexpr (EPI == 1) {
+      // Per 64-row tile and channel: (mean, M2) by a Welford pass over the bf16-rounded
+      // outputs (no E[x^2]-E[x]^2 cancellation); merged later with Chan's formula.
+      const int ch = tid % BN, h = tid / BN;
+      const int co = n0 + ch;
+      const int nvalid = min(64, p.M - (m0 + h * 64));
+      if (h < 2 && co < p.Co && nvalid > 0) {
+        const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
+        float mean = 0.f, m2 = 0.f;
+        if (nvalid == 64) {
+#pragma unroll
+          for (int r = 0; r < 64; ++r) {
+            const int pl = h * 64 + r;
+            const uint32_t off = pl * RB + (coff ^ ((((uint32_t)pl >> 1) & (NCH - 1)) << 4));
+            const float x = bf2f(*LDS_PTR(bf16, E + off));
+            const float d = x - mean;
+            mean += d * (1.f / (float)(r + 1));
+            m2 += d * (x - mean);
+          }
+        } else {
+          for (int r = 0; r < nvalid; ++r) {
+            const int pl = h * 64 + r;
+            const uint32_t off = pl * RB + (coff ^ ((((uint32_t)pl >> 1) & (NCH - 1)) << 4));
+            const float x = bf2f(*LDS_PTR(bf16, E + off));
+            const float d = x - mean;
+            mean += d / (float)(r + 1);
+            m2 += d * (x - mean);
+          }
+        }
+        const size_t rb = (size_t)(m0 / 64 + h);
+        p.stats[(rb * 2 + 0) * p.Co + co] = mean;
+        p.stats[(rb * 2 + 1) * p.Co + co] = m2;
+      }
+    }
+    return;
+  }
 
+  // ---- register epilogue (linear heads): bias / activation, 8-byte stores ----
+  const int co_lane = n0 + wn * (BN / 2) + (lane >> 4) * 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -241,61 +317,6 @@ tap_gemm_kernel(const TapGemmParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
       if (mok && co < p.Co) *(bf16x4*)(p.dst + drow + co) = o;
-      if (p.stats) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s1[j][r] += mok ? bf2f(o[r]) : 0.f;
-      }
-    }
-  }
-  if (p.stats) {
-    // Per 64-row wave tile and channel: (mean, M2) with M2 around the tile mean
-    // (two passes over the register-resident tile), merged later with Chan's
-    // formula -- no E[x^2]-E[x]^2 cancellation.
-    const int nvalid = min(64, p.M - (m0 + wm * 64));
-    const float inv_n = nvalid > 0 ? 1.f / nvalid : 0.f;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-        s1[j][r] *= inv_n;  // tile mean
-      }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-      const bool mok = m < p.M;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int co = co_lane + j * 16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = acc[j][i][r];
-          if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
-          if (p.relu == 1) t = fmaxf(t, 0.f);
-          else if (p.relu == 2) t = 1.f / (1.f + __expf(-t));
-          const float d = bf2f(f2bf(t)) - s1[j][r];
-          s2[j][r] += mok ? d * d : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) s2[j][r] += __shfl_xor(s2[j][r], o, 64);
-      }
-    const int rb = m0 / 64 + wm;
-    if ((lane & 15) == 0 && nvalid > 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int co = co_lane + j * 16;
-        if (co < p.Co) {
-          *(f32x4*)(p.stats + ((size_t)rb * 2 + 0) * p.Co + co) = f32x4{s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
-          *(f32x4*)(p.stats + ((size_t)rb * 2 + 1) * p.Co + co) = f32x4{s2[j][0], s2[j][1], s2[j][2], s2[j][3]};
-        }
-      }
     }
   }
 }
@@ -469,13 +490,22 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   }
   if (p.M == 0) return;
   const int ntm = (p.M + 127) / 128;
+  const int epi = (bias != nullptr || relu != 0) ? 2 : (stats != nullptr ? 1 : 0);
+  const bool fast = (p.cpt & 7) == 0;
+#define DCP_TAPGEMM(BN_, EPI_, FAST_)                                                                 \
+  hipLaunchKernelGGL((tap_gemm_kernel<BN_, EPI_, FAST_>), dim3(ntm * ((Co + BN_ - 1) / BN_)), dim3(256), \
+                     2 * (128 + BN_) * 128, stream, p)
+#define DCP_TAPGEMM_EPI(BN_, FAST_)                 \
+  if (epi == 0) DCP_TAPGEMM(BN_, 0, FAST_);         \
+  else if (epi == 1) DCP_TAPGEMM(BN_, 1, FAST_);    \
+  else DCP_TAPGEMM(BN_, 2, FAST_);
   if (Co <= 64) {
-    const int ntn = (Co + 63) / 64;
-    hipLaunchKernelGGL(tap_gemm_kernel<64>, dim3(ntm * ntn), dim3(256), 2 * (128 + 64) * 128, stream, p);
+    if (fast) { DCP_TAPGEMM_EPI(64, true) } else { DCP_TAPGEMM_EPI(64, false) }
   } else {
-    const int ntn = (Co + 127) / 128;
-    hipLaunchKernelGGL(tap_gemm_kernel<128>, dim3(ntm * ntn), dim3(256), 2 * (128 + 128) * 128, stream, p);
+    if (fast) { DCP_TAPGEMM_EPI(128, true) } else { DCP_TAPGEMM_EPI(128, false) }
   }
+#undef DCP_TAPGEMM_EPI
+#undef DCP_TAPGEMM
 }
 
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,

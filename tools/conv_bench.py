@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--json", default=None)
     ap.add_argument("--grouped", action="store_true", help="ResNeXt-50 grouped convs instead of ResNet-50")
+    ap.add_argument("--only", default=None, help="comma-separated shape indices to run")
     a = ap.parse_args()
     if a.grouped:
         return grouped(a)
@@ -64,7 +65,10 @@ def main():
     rows = []
     print(f"{'shape':34s} {'fwd us':>8s} {'TF':>6s} {'dgrad':>8s} {'TF':>6s} {'wgrad':>8s} {'TF':>6s} | "
           f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s}")
-    for Ci, Co, k, s, H, cnt in R50:
+    only = {int(i) for i in a.only.split(",")} if a.only else None
+    for idx, (Ci, Co, k, s, H, cnt) in enumerate(R50):
+        if only is not None and idx not in only:
+            continue
         p = k // 2
         Ho = (H + 2 * p - k) // s + 1
         flop = 2.0 * N * Ho * Ho * Co * Ci * k * k
