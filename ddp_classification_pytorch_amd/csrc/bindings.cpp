@@ -165,10 +165,13 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   TORCH_CHECK(x.size(0) == N, "batch mismatch");
   TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_wgrad needs channel multiples of 8");
   TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "wgrad geometry");
-  auto dw = at::zeros({Co, KH, KW, C}, f32_like(dy));
+  auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
+  const int ncu = num_cus(dy.get_device());
+  const int splits = dcp::wgrad_splits(N * Ho * Wo, Co, KH * KW * C, KH * KW, ncu, nullptr);
+  auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
   dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
-                    zero_page(dy.get_device()), num_cus(dy.get_device()), cur_stream());
+                    part.data_ptr<float>(), zero_page(dy.get_device()), ncu, cur_stream());
   return dw;
 }
 
@@ -199,12 +202,15 @@ Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
   CHECK_ACT(x);
   const int B = dy.size(0), Np = dy.size(1), K = x.size(1);
   TORCH_CHECK(x.size(0) == B && K % 8 == 0 && Np % 8 == 0, "linear_wgrad shapes");
-  auto dw = at::zeros({Np, K}, f32_like(dy));
+  auto dw = at::empty({Np, K}, f32_like(dy));
   dcp::TapList t;
   t.n = 1;
   t.dy[0] = t.dx[0] = t.widx[0] = 0;
-  dcp::launch_wgrad(bp(dy), B, 1, 1, Np, bp(x), 1, 1, K, 1, t, dw.data_ptr<float>(), zero_page(dy.get_device()),
-                    num_cus(dy.get_device()), cur_stream());
+  const int ncu = num_cus(dy.get_device());
+  const int splits = dcp::wgrad_splits(B, Np, K, 1, ncu, nullptr);
+  auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
+  dcp::launch_wgrad(bp(dy), B, 1, 1, Np, bp(x), 1, 1, K, 1, t, dw.data_ptr<float>(), part.data_ptr<float>(),
+                    zero_page(dy.get_device()), ncu, cur_stream());
   return dw;
 }
 
@@ -702,7 +708,13 @@ void cdr_mask(const Tensor& table, const Tensor& chunks, const Tensor& state, do
 
 }  // namespace
 
+void set_tuning(int64_t idx, int64_t value) {
+  TORCH_CHECK(idx >= 0 && idx < 8, "tuning index");
+  dcp::g_tune[idx] = (int)value;
+}
+
 TORCH_LIBRARY(dcp, m) {
+  m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);

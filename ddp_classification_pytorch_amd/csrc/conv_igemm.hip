@@ -28,10 +28,15 @@
 // with both operands m-major in memory; its LDS images are [m][...] rows read
 // with the gfx950 transpose read `ds_read_b64_tr_b16`, split-K over m with
 // fp32 atomics into the (zeroed) gradient.
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.cuh"
 #include "launchers.h"
 
 namespace dcp {
+
+int g_tune[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
@@ -47,20 +52,108 @@ struct TapGemmParams {
   int relu;          // fused activation on the stored output: 0 none, 1 ReLU, 2 sigmoid (linear heads)
   const float* bias; // optional per-output-channel bias (linear heads)
   FastDiv div_wy, div_hy, div_cpt;
-  int8_t dy[kMaxTaps], dx[kMaxTaps];
-  uint8_t widx[kMaxTaps];
+  // per tap: dy (int8) | dx (int8) << 8 | weight tap index << 16.  Dword entries so a
+  // wave-uniform lookup is one s_load_dword (byte arrays compile to vector loads, whose
+  // vmcnt wait would drain the LDS-DMA ring).
+  int tap[kMaxTaps];
+  int ablate;  // tuning experiments only: 1 = no staging in the k-loop, 2 = no MFMA
+  int cvar;    // tuning experiments only: compute-loop variant
 };
+
+__device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
+__device__ __forceinline__ int tap_dx(int v) { return (int)(int8_t)((v >> 8) & 0xff); }
+__device__ __forceinline__ int tap_w(int v) { return (v >> 16) & 0xffff; }
 
 // byte offset of logical 16B chunk `c` of row `r` in a 128-byte-row image
 __device__ __forceinline__ uint32_t swz128(uint32_t r, uint32_t c) {
   return r * 128u + ((c ^ ((r >> 1) & 7u)) << 4);
 }
 
+// Per 64-row tile and channel of the LDS output image E[rows][BN] (16-byte chunks
+// XOR-swizzled by row>>1): (mean, M2) of the bf16-rounded outputs, two passes over
+// register-resident values (no E[x^2]-E[x]^2 cancellation); merged later with
+// Chan's formula.  Thread -> (channel, 64-row tile); NT tiles.
+template <int BN, int NT>
+__device__ __forceinline__ void tile_stats(const TapGemmParams& p, const char* E, int m0, int n0, int tid) {
+  constexpr int RB = BN * 2, NCH = BN / 8;
+  const int ch = tid % BN, h = tid / BN;
+  const int co = n0 + ch;
+  const int nvalid = min(64, p.M - (m0 + h * 64));
+  if (h >= NT || co >= p.Co || nvalid <= 0) return;
+  const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
+  float v[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    const uint32_t pl = h * 64 + r;
+    v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + (coff ^ (((pl >> 1) & (NCH - 1)) << 4))));
+  }
+  float s[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 64; ++r) s[r & 7] += r < nvalid ? v[r] : 0.f;
+  const float mean = ((s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]))) / (float)nvalid;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    const float d = v[r] - mean;
+    s[r & 7] += r < nvalid ? d * d : 0.f;
+  }
+  const float m2 = (s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]));
+  const size_t rb = (size_t)(m0 / 64 + h);
+  p.stats[(rb * 2 + 0) * p.Co + co] = mean;
+  p.stats[(rb * 2 + 1) * p.Co + co] = m2;
+}
+
+// vmcnt(n) with a wave-uniform runtime n in [0, 31] (a scalar branch to an immediate wait)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 // EPI: 0 = bf16 store, 1 = store + per-64-row BN statistics, 2 = bias / activation (linear heads)
 // FAST: Cs % 64 == 0, one tap per 64-deep k-tile
-template <int BN, int EPI, bool FAST>
+// NS: LDS stages.  NS = 2: double buffer, vmcnt(0) + barrier per k-tile (several blocks per
+// CU hide the latency).  NS > 2 (FAST only): a ring whose LDS-DMA loads stay in flight across
+// the raw s_barrier, drained by a counted vmcnt -- for deep-K shapes at one block per CU.
+template <int BN, int EPI, bool FAST, int NS = 2>
 __global__ void __launch_bounds__(256)
 tap_gemm_kernel(const TapGemmParams p) {
+  static_assert(NS == 2 || FAST, "the LDS ring needs the one-tap-per-k-tile path");
   constexpr int BM = 128;                 // pixel rows per block
   constexpr int A_BYTES = BM * 128;       // 64 k (bf16) per row
   constexpr int B_BYTES = BN * 128;
@@ -121,8 +214,9 @@ tap_gemm_kernel(const TapGemmParams p) {
     if constexpr (FAST) {
       const int t = kt / tiles_per_tap;
       const int cbase = (kt - t * tiles_per_tap) * 64;
-      const int dy = p.dy[t], dx = p.dx[t];
-      const uint32_t wofs = (uint32_t)p.widx[t] * p.Cs + cbase;
+      const int tv = p.tap[t];
+      const int dy = tap_dy(tv), dx = tap_dx(tv);
+      const uint32_t wofs = (uint32_t)tap_w(tv) * p.Cs + cbase;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
@@ -145,8 +239,8 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         bool ok = a_ok[i] && kc < kc_total;
-        const int tt = ok ? t : 0;
-        const int hi = a_ys[i] + p.dy[tt], wi = a_xs[i] + p.dx[tt];
+        const int tv = p.tap[ok ? t : 0];
+        const int hi = a_ys[i] + tap_dy(tv), wi = a_xs[i] + tap_dx(tv);
         ok = ok && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + ci0 : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
@@ -158,7 +252,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         const bool ok = b_ok[i] && kc < kc_total;
-        const bf16* g = ok ? p.wt + b_row[i] + (uint32_t)p.widx[ok ? t : 0] * p.Cs + ci0 : p.zero;
+        const bf16* g = ok ? p.wt + b_row[i] + (uint32_t)tap_w(p.tap[ok ? t : 0]) * p.Cs + ci0 : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
                                          LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
       }
@@ -172,16 +266,7 @@ tap_gemm_kernel(const TapGemmParams p) {
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = p.nkt;
-  if (nkt > 0) {
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
+  auto compute = [&](const char* As, const char* Bs) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t c = s * 4 + (lane >> 4);
@@ -202,7 +287,35 @@ tap_gemm_kernel(const TapGemmParams p) {
         for (int i = 0; i < 4; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if constexpr (NS == 2) {
+    if (nkt > 0) {
+      stage(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nkt && !(p.ablate & 1)) stage(kt + 1, buf ^ 1);
+      const char* As = smem + buf * STAGE;
+      if (!(p.ablate & 2)) compute(As, As + A_BYTES);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    constexpr int LPT = 4 + BI;  // LDS-DMA instructions per thread per k-tile
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+      if (i < nkt) stage(i, i);
+    for (int kt = 0; kt < nkt; ++kt) {
+      // tiles issued after kt: kt+1 .. min(kt+NS-2, nkt-1)
+      wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));
+      __builtin_amdgcn_s_barrier();  // tile kt landed for every wave; tile kt-1's slot is free
+      asm volatile("" ::: "memory");
+      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      const char* As = smem + (kt % NS) * STAGE;
+      compute(As, As + A_BYTES);
+    }
     __syncthreads();
   }
 
@@ -250,40 +363,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         }
       }
     }
-    if constexpr (EPI == 1) {
-      // Per 64-row tile and channel: (mean, M2) by a Welford pass over the bf16-rounded
-      // outputs (no E[x^2]-E[x]^2 cancellation); merged later with Chan's formula.
-      const int ch = tid % BN, h = tid / BN;
-      const int co = n0 + ch;
-      const int nvalid = min(64, p.M - (m0 + h * 64));
-      if (h < 2 && co < p.Co && nvalid > 0) {
-        const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
-        float mean = 0.f, m2 = 0.f;
-        if (nvalid == 64) {
-#pragma unroll
-          for (int r = 0; r < 64; ++r) {
-            const int pl = h * 64 + r;
-            const uint32_t off = pl * RB + (coff ^ ((((uint32_t)pl >> 1) & (NCH - 1)) << 4));
-            const float x = bf2f(*LDS_PTR(bf16, E + off));
-            const float d = x - mean;
-            mean += d * (1.f / (float)(r + 1));
-            m2 += d * (x - mean);
-          }
-        } else {
-          for (int r = 0; r < nvalid; ++r) {
-            const int pl = h * 64 + r;
-            const uint32_t off = pl * RB + (coff ^ ((((uint32_t)pl >> 1) & (NCH - 1)) << 4));
-            const float x = bf2f(*LDS_PTR(bf16, E + off));
-            const float d = x - mean;
-            mean += d / (float)(r + 1);
-            m2 += d * (x - mean);
-          }
-        }
-        const size_t rb = (size_t)(m0 / 64 + h);
-        p.stats[(rb * 2 + 0) * p.Co + co] = mean;
-        p.stats[(rb * 2 + 1) * p.Co + co] = m2;
-      }
-    }
+    if constexpr (EPI == 1) tile_stats<BN, BM / 64>(p, E, m0, n0, tid);
     return;
   }
 
@@ -322,16 +402,200 @@ tap_gemm_kernel(const TapGemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// 8-wave variant for the common one-tap-per-k-tile shapes with Co >= 128:
+// 256 pixel rows x 128 output channels per workgroup (the weight tile is shared
+// by twice the rows: 6 instead of 8 LDS-DMA instructions per thread per 64-deep
+// k-tile for the same 32 MFMAs per wave), 3 LDS stages (144 KB) so a tile's loads
+// are issued two k-tiles ahead and stay in flight across the raw barrier, drained
+// by a counted vmcnt.  One workgroup (2 waves per SIMD) per CU.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ void __launch_bounds__(512)
+tap_gemm8_kernel(const TapGemmParams p) {
+  constexpr int BM = 256, BN = 128, NS = 3;
+  constexpr int A_BYTES = BM * 128;       // pixel rows x 64 k (bf16)
+  constexpr int B_BYTES = BN * 128;       // channel rows x 64 k
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int TN = 4;
+  constexpr int LPT = 6;                  // LDS-DMA instructions per thread per k-tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;  // 64-pixel group, 64-channel group
+
+  const uint32_t ntn = (p.Co + BN - 1) / BN;
+  const uint32_t ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  uint32_t a_pix[4];
+  int a_ys[4], a_xs[4];
+  uint32_t a_chunk[4];
+  bool a_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (wave * 4 + i) * 8 + (lane >> 3);
+    const int m = m0 + r;
+    a_ok[i] = m < p.M;
+    const uint32_t mm = a_ok[i] ? m : 0;
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const uint32_t x = mm - q * p.Wy;
+    const uint32_t n = fdiv(q, p.div_hy);
+    const uint32_t y = q - n * p.Hy;
+    a_pix[i] = n * (uint32_t)(p.Hs * p.Ws);
+    a_ys[i] = y * p.ss;
+    a_xs[i] = x * p.ss;
+    a_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+  }
+  uint32_t b_row[2], b_chunk[2];
+  bool b_ok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 2 + i) * 8 + (lane >> 3);
+    b_ok[i] = (n0 + r) < p.Co;
+    b_row[i] = (uint32_t)(n0 + r) * p.ldw;
+    b_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+  }
+  const int tiles_per_tap = p.cpt >> 3;
+
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+    const int t = kt / tiles_per_tap;
+    const int cbase = (kt - t * tiles_per_tap) * 64;
+    const int tv = p.tap[t];
+    const int dy = tap_dy(tv), dx = tap_dx(tv);
+    const uint32_t wofs = (uint32_t)tap_w(tv) * p.Cs + cbase;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
+      const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+      const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8 : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16* g = b_ok[i] ? p.wt + b_row[i] + wofs + b_chunk[i] * 8 : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, Bs + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = p.nkt;
+  stage(0, 0);
+  if (nkt > 1) stage(1, 1);
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_vmcnt(kt + 1 < nkt ? LPT : 0);  // tile kt landed (tile kt+1 may stay in flight)
+    if (!(p.ablate & 4)) __builtin_amdgcn_s_barrier();  // ... for every wave; tile kt-1's slot is free
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nkt && !(p.ablate & 1)) stage(kt + 2, (kt + 2) % NS);
+    const char* As = smem + (kt % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+    if (p.ablate & 2) {
+    } else if (p.cvar == 0) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t c = s * 4 + (lane >> 4);
+        bf16x8 wf[TN], af[4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+      }
+    } else {
+      // all 16 fragments of the k-tile in flight at once; counted lgkmcnt waits per MFMA group
+      bf16x8 wf[2][TN], af[2][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t c = s * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[s][j] = *(const bf16x8*)(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[s][i] = *(const bf16x8*)(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
+      }
+      if (p.cvar == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
+      if (p.cvar == 2) __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue through LDS (as tap_gemm_kernel): E[256 pixels][128 channels] ----
+  constexpr int RB = BN * 2, NCH = BN / 8;
+  char* E = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const uint32_t cl = wn * 64 + j * 16 + (lane >> 4) * 4;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+      const uint32_t off = pl * RB + (((cl >> 3) ^ ((pl >> 1) & (NCH - 1))) << 4) + ((cl >> 2) & 1) * 8;
+      *LDS_PTR(bf16x4, E + off) = o;
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int R = 512 / NCH;
+    const int c = tid % NCH, pr0 = tid / NCH;
+    const bool cok = n0 + c * 8 < p.Co;
+#pragma unroll
+    for (int k = 0; k < BM / R; ++k) {
+      const int pl = pr0 + k * R;
+      const int m = m0 + pl;
+      const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+      if (m < p.M && cok) {
+        uint32_t drow;
+        if (p.ds == 1) {
+          drow = (uint32_t)m * (uint32_t)p.Co;
+        } else {
+          const uint32_t q = fdiv(m, p.div_wy);
+          const uint32_t x = m - q * p.Wy;
+          const uint32_t n = fdiv(q, p.div_hy);
+          const uint32_t y = q - n * p.Hy;
+          drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+        }
+        *(bf16x8*)(p.dst + drow + n0 + c * 8) = v;
+      }
+    }
+  }
+  if constexpr (EPI == 1) tile_stats<BN, 4>(p, E, m0, n0, tid);
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
 struct WgradParams {
   const bf16* dy;    // [M][Co]
   const bf16* src;   // [N][Hs][Ws][Cs]
-  float* dw;         // [Co][T*Cs] fp32, accumulated
+  float* dw;         // [Co][T*Cs] fp32, accumulated atomically (part == nullptr)
+  float* part;       // [splits][Co][T*Cs] fp32 per-split partials (plain stores), or nullptr
   const bf16* zero;
   int Hs, Ws, Cs, Ho, Wo, ss;
   int Co, M, ldw;    // ldw = T*Cs
   int cpt, kc_total, rows_per_split;
+  int ablate;  // tuning experiments only: 8 = skip the atomic flush
   FastDiv div_wo, div_ho, div_cpt;
   int8_t dy_t[kMaxTaps], dx_t[kMaxTaps];
 };
@@ -459,7 +723,10 @@ wgrad_kernel(const WgradParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (co < p.Co) unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
+        if (co < p.Co && !(p.ablate & 8)) {
+          if (p.part) p.part[((size_t)blockIdx.y * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
+          else unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
+        }
       }
     }
   }
@@ -468,6 +735,20 @@ wgrad_kernel(const WgradParams p) {
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+template <int BN, int EPI, bool FAST, int NS>
+static void launch_tg(const TapGemmParams& p, int grid, hipStream_t stream) {
+  const size_t lds = (size_t)NS * (128 + BN) * 128;
+  if (lds > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds);
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS>), dim3(grid), dim3(256), lds, stream, p);
+}
+
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
@@ -483,34 +764,131 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   p.nkt = (taps.n * p.cpt + 7) / 8;
   p.relu = relu; p.bias = bias;
   p.div_wy = make_fastdiv(Wy); p.div_hy = make_fastdiv(Hy); p.div_cpt = make_fastdiv(p.cpt);
-  for (int i = 0; i < taps.n; ++i) {
-    p.dy[i] = (int8_t)taps.dy[i];
-    p.dx[i] = (int8_t)taps.dx[i];
-    p.widx[i] = (uint8_t)taps.widx[i];
-  }
+  for (int i = 0; i < taps.n; ++i)
+    p.tap[i] = (taps.dy[i] & 0xff) | ((taps.dx[i] & 0xff) << 8) | ((taps.widx[i] & 0xffff) << 16);
   if (p.M == 0) return;
   const int ntm = (p.M + 127) / 128;
   const int epi = (bias != nullptr || relu != 0) ? 2 : (stats != nullptr ? 1 : 0);
   const bool fast = (p.cpt & 7) == 0;
-#define DCP_TAPGEMM(BN_, EPI_, FAST_)                                                                 \
-  hipLaunchKernelGGL((tap_gemm_kernel<BN_, EPI_, FAST_>), dim3(ntm * ((Co + BN_ - 1) / BN_)), dim3(256), \
-                     2 * (128 + BN_) * 128, stream, p)
-#define DCP_TAPGEMM_EPI(BN_, FAST_)                 \
-  if (epi == 0) DCP_TAPGEMM(BN_, 0, FAST_);         \
-  else if (epi == 1) DCP_TAPGEMM(BN_, 1, FAST_);    \
-  else DCP_TAPGEMM(BN_, 2, FAST_);
-  if (Co <= 64) {
-    if (fast) { DCP_TAPGEMM_EPI(64, true) } else { DCP_TAPGEMM_EPI(64, false) }
-  } else {
-    if (fast) { DCP_TAPGEMM_EPI(128, true) } else { DCP_TAPGEMM_EPI(128, false) }
+  // config: BN (64/128 output channels per tile) and NS (LDS stages); g_tune overrides the
+  // heuristic (tuning experiments only)
+  const int env_bn = g_tune[0], env_ns = g_tune[1];
+  p.ablate = g_tune[2];
+  p.cvar = g_tune[4];
+  int bn = Co <= 64 ? 64 : 128, ns = 2;
+  if (env_bn > 0 && fast) bn = env_bn;
+  if (env_ns > 0 && fast) ns = env_ns;
+  if (!fast) ns = 2;
+  const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
+  if (fast && Co >= 128 && epi != 2 && use8) {
+    const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
+    constexpr size_t lds8 = 3 * (256 + 128) * 128;
+    static bool attr8 = false;
+    if (!attr8) {
+      hipFuncSetAttribute((const void*)tap_gemm8_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
+      hipFuncSetAttribute((const void*)tap_gemm8_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
+      attr8 = true;
+    }
+    if (epi == 1) hipLaunchKernelGGL(tap_gemm8_kernel<1>, dim3(grid8), dim3(512), lds8, stream, p);
+    else hipLaunchKernelGGL(tap_gemm8_kernel<0>, dim3(grid8), dim3(512), lds8, stream, p);
+    return;
   }
-#undef DCP_TAPGEMM_EPI
-#undef DCP_TAPGEMM
+  const int grid = ntm * ((Co + bn - 1) / bn);
+#define DCP_TG_NS(BN_, EPI_, FAST_)                                           \
+  if (ns == 2) launch_tg<BN_, EPI_, FAST_, 2>(p, grid, stream);               \
+  else if (ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3>(p, grid, stream); \
+  else launch_tg<BN_, EPI_, (FAST_ || true), 4>(p, grid, stream);
+#define DCP_TG_EPI(BN_, FAST_)                     \
+  if (epi == 0) { DCP_TG_NS(BN_, 0, FAST_) }       \
+  else if (epi == 1) { DCP_TG_NS(BN_, 1, FAST_) }  \
+  else { DCP_TG_NS(BN_, 2, FAST_) }
+  if (bn == 64) {
+    if (fast) { DCP_TG_EPI(64, true) } else { DCP_TG_EPI(64, false) }
+  } else {
+    if (fast) { DCP_TG_EPI(128, true) } else { DCP_TG_EPI(128, false) }
+  }
+#undef DCP_TG_EPI
+#undef DCP_TG_NS
+}
+
+// Deterministic split-K reduction, two levels: a workgroup sums a chunk of up to 64
+// splits for 64 float4 columns (4 sub-lanes per column, 16 independent loads each,
+// fixed-order LDS combine), then one pass adds the <= ceil(splits/64) chunk sums.
+__global__ void __launch_bounds__(256) split_reduce1_kernel(const float4* __restrict__ part, int splits, int n4,
+                                                            float4* __restrict__ out) {
+  __shared__ float4 red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int k0 = blockIdx.y * 64;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+#pragma unroll 4
+    for (int k = k0 + sub; k < min(splits, k0 + 64); k += 4) {
+      const float4 v = part[(size_t)k * n4 + col];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && col < n4) {
+    float4 t = red[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float4 v = red[q][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    out[(size_t)blockIdx.y * n4 + col] = t;
+  }
+}
+
+__global__ void split_reduce2_kernel(const float4* __restrict__ part, int rows, int n4, float4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 s = part[i];
+  for (int k = 1; k < rows; ++k) {
+    const float4 v = part[(size_t)k * n4 + i];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  out[i] = s;
+}
+
+// out[i] = sum_k part[k][i]; n % 4 == 0.  part must hold splits*n + ceil(splits/64)*n floats
+// when splits > 64 (the chunk sums are written behind the partials).
+void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream) {
+  const int n4 = n / 4;
+  const int chunks = (splits + 63) / 64;
+  if (chunks == 1) {
+    hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, 1), dim3(256), 0, stream, (const float4*)part,
+                       splits, n4, (float4*)out);
+    return;
+  }
+  float* tmp = const_cast<float*>(part) + (size_t)splits * n;
+  hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
+                     splits, n4, (float4*)tmp);
+  hipLaunchKernelGGL(split_reduce2_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float4*)tmp, chunks, n4,
+                     (float4*)out);
+}
+
+// split-K plan of the weight-gradient GEMM, >= 256 rows per split: ~2 blocks per CU for
+// 1x1 convs / linears (fewer, longer splits: less partial-slab traffic), ~4 for k x k
+// (measured per shape with tools/conv_bench.py --cfgs "5=2,5=4")
+int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split) {
+  const int ntm = (Co + 127) / 128, ntn = (ldw + 127) / 128;
+  const int tiles = ntm * ntn;
+  const int target = (g_tune[5] > 0 ? g_tune[5] : (taps == 1 ? 2 : 4)) * num_cu;
+  int splits = (target + tiles - 1) / tiles;
+  int max_splits = (M + 255) / 256;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int rps = (M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  splits = (M + rps - 1) / rps;
+  if (rows_per_split) *rows_per_split = rps;
+  return splits;
 }
 
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
                   const bf16* src, int Hs, int Ws, int Cs, int ss,
-                  const TapList& taps, float* dw, const bf16* zero, int num_cu, hipStream_t stream) {
+                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream) {
   WgradParams p;
   p.dy = dy; p.src = src; p.dw = dw; p.zero = zero;
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs; p.Ho = Ho; p.Wo = Wo; p.ss = ss;
@@ -521,19 +899,20 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
-  const int ntm = (Co + 127) / 128, ntn = (p.ldw + 127) / 128;
-  const int tiles = ntm * ntn;
-  // split-K over m: aim for ~4 waves of blocks over the chip, >= 256 rows per split
-  const int target = 4 * num_cu;
-  int splits = (target + tiles - 1) / tiles;
-  int max_splits = (p.M + 255) / 256;
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  int rps = (p.M + splits - 1) / splits;
-  rps = (rps + 63) / 64 * 64;
-  splits = (p.M + rps - 1) / rps;
+  const int tiles = ((Co + 127) / 128) * ((p.ldw + 127) / 128);
+  p.ablate = g_tune[2];
+  if (g_tune[6] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
+  int rps = 0;
+  const int splits = wgrad_splits(p.M, Co, p.ldw, taps.n, num_cu, &rps);
   p.rows_per_split = rps;
+  // partials: plain stores + one deterministic reduce (memory-side float atomics cost
+  // ~1/4 of the kernel); a single split writes the gradient directly
+  p.part = (part != nullptr && splits > 1) ? part : nullptr;
+  if (splits == 1) {
+    p.part = dw;  // split 0 stores straight into dw
+  }
   hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, splits), dim3(256), 4 * 64 * 256, stream, p);
+  if (part != nullptr && splits > 1) launch_split_reduce(part, splits, Co * p.ldw, dw, stream);
 }
 
 }  // namespace dcp

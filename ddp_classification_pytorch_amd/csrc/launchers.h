@@ -8,6 +8,10 @@ typedef __bf16 bf16;
 
 namespace dcp {
 
+// tuning switches for in-process A/B experiments (tools/conv_bench.py --cfgs); all 0 = defaults
+// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant, [5] wgrad blocks per CU, [6] wgrad atomics
+extern int g_tune[8];
+
 constexpr int kMaxTaps = 64;
 
 struct TapList {
@@ -18,8 +22,12 @@ struct TapList {
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream);
+// partial-slab split-K weight gradient: dw is fully written when part != nullptr
+// (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw
+int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split);
+void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream);
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
-                  const TapList& taps, float* dw, const bf16* zero, int num_cu, hipStream_t stream);
+                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream);
 // frag: gconv_frag_elems(...) bf16 workspace (MFMA path; may be null -> direct kernels)
 void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
                              int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);

@@ -55,9 +55,13 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--grouped", action="store_true", help="ResNeXt-50 grouped convs instead of ResNet-50")
     ap.add_argument("--only", default=None, help="comma-separated shape indices to run")
+    ap.add_argument("--cfgs", default=None,
+                    help="in-process A/B of tuning configs: 'idx=val;idx=val,idx=val,...' (g_tune slots)")
     a = ap.parse_args()
     if a.grouped:
         return grouped(a)
+    if a.cfgs:
+        return ab(a)
     K = _ext.hip_ops()
     dev = torch.device("cuda", 0)
     N = a.batch
@@ -107,6 +111,52 @@ def main():
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"batch": N, "rows": rows, "totals_us": tot}, f, indent=1)
+
+
+def _apply(K, cfg):
+    for i in range(8):
+        K.set_tuning(i, 0)
+    for kv in filter(None, cfg.split(";")):
+        i, v = kv.split("=")
+        K.set_tuning(int(i), int(v))
+
+
+def ab(a):
+    """Time every shape under each tuning config in ONE process (interleaved, so the
+    clock / box variance between runs does not decide the comparison)."""
+    K = _ext.hip_ops()
+    dev = torch.device("cuda", 0)
+    N = a.batch
+    cfgs = a.cfgs.split(",")
+    only = {int(i) for i in a.only.split(",")} if a.only else None
+    tot = [[0.0] * 3 for _ in cfgs]
+    print(f"{'shape':30s} " + " | ".join(f"{c:>22s}" for c in cfgs))
+    for idx, (Ci, Co, k, s, H, cnt) in enumerate(R50):
+        if only is not None and idx not in only:
+            continue
+        p = k // 2
+        Ho = (H + 2 * p - k) // s + 1
+        x = torch.randn(N, H, H, Ci, device=dev).bfloat16()
+        w = (torch.randn(Co, k, k, Ci, device=dev) / (k * k * Ci) ** 0.5)
+        wb, wt = K.weight_prep(w, 0, True)
+        dy = torch.randn(N, Ho, Ho, Co, device=dev).bfloat16()
+        res = [[0.0] * 3 for _ in cfgs]
+        for rep in range(3):
+            for ci, cfg in enumerate(cfgs):
+                _apply(K, cfg)
+                t = [timeit(lambda: K.conv_fwd(x, wb, s, p, True), a.iters),
+                     timeit(lambda: K.conv_dgrad(dy, wt, H, H, s, p), a.iters) if Ci > 8 else 0.0,
+                     timeit(lambda: K.conv_wgrad(dy, x, k, k, s, p), a.iters)]
+                for j in range(3):
+                    res[ci][j] = t[j] if rep == 0 else min(res[ci][j], t[j])
+        for ci in range(len(cfgs)):
+            for j in range(3):
+                tot[ci][j] += cnt * res[ci][j]
+        name = f"{Ci}->{Co} k{k} s{s} {H}->{Ho} x{cnt}"
+        print(f"{name:30s} " + " | ".join(f"{r[0]:6.1f} {r[1]:6.1f} {r[2]:6.1f}" for r in res), flush=True)
+    _apply(K, "")
+    print("per-step totals (ms): " + " | ".join(
+        f"{c}: " + "/".join(f"{v / 1e3:.2f}" for v in t) + f" = {sum(t) / 1e3:.2f}" for c, t in zip(cfgs, tot)))
 
 
 def grouped(a):
