@@ -58,7 +58,7 @@ def parse(argv=None):
 
 
 CONFIGS = {
-    "r50": dict(model="resnet50", batch=256, image_size=224, num_classes=1000),
+    "r50": dict(model="resnet50", batch=512, image_size=224, num_classes=1000),
     "arcface": dict(model="resnet50", batch=256, image_size=112, num_classes=10000),
     "resnext": dict(model="resnext50_32x4d", batch=128, image_size=224, num_classes=1000),
     "r101": dict(model="resnet101", batch=512, image_size=224, num_classes=1000),

@@ -732,6 +732,136 @@ wgrad_kernel(const WgradParams p) {
   }
 }
 
+// 256 x 256 weight-gradient tile (8 waves, each 64 co x 128 cols): half the LDS-DMA
+// and transposed-read instructions per MFMA of the 128 x 128 kernel above; images are
+// [64 pixels][256 bf16] (512-byte rows) with the same 32-byte-piece XOR swizzle.
+__device__ __forceinline__ uint32_t swz512(uint32_t r, uint32_t c) {
+  return r * 512u + ((c ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3))) << 4);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag512(const char* img, uint32_t row0, uint32_t col0, int lane) {
+  const uint32_t q = (lane & 15) >> 2, pp = lane & 3;
+  const uint32_t col = col0 + pp * 4;
+  const uint32_t o1 = swz512(row0 + q, col >> 3) + (col & 7) * 2;
+  const uint32_t o2 = swz512(row0 + 4 + q, col >> 3) + (col & 7) * 2;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o1));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o2));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ void __launch_bounds__(512)
+wgrad256_kernel(const WgradParams p) {
+  constexpr int BK = 64;
+  constexpr int IMG = BK * 512;   // 64 rows x 256 bf16
+  constexpr int STAGE = 2 * IMG;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;   // 64-co group, 128-col group
+  const int ntm = (p.Co + 255) / 256;
+  const int ntn = (p.ldw + 255) / 256;
+  const uint32_t tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tn = tile % ntn, tmi = tile / ntn;
+  const int co0 = tmi * 256, kcol0 = tn * 256;
+  const int mstart = blockIdx.y * p.rows_per_split;
+  const int mend = min(p.M, mstart + p.rows_per_split);
+  const int nkt = (mend - mstart + BK - 1) / BK;
+
+  // load slots: 4 per image per thread; wave instruction i covers rows (wave*4+i)*2 .. +1
+  uint32_t a_col[4];
+  bool a_cok[4];
+  int b_dy[4], b_dx[4];
+  uint32_t b_ci[4];
+  bool b_cok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t r = (wave * 4 + i) * 2 + (lane >> 5);
+    const uint32_t c = (lane & 31) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
+    a_col[i] = co0 + c * 8;
+    a_cok[i] = (int)a_col[i] < p.Co;
+    const int kc = kcol0 / 8 + c;
+    b_cok[i] = kc < p.kc_total;
+    const int t = b_cok[i] ? (int)fdiv(kc, p.div_cpt) : 0;
+    b_ci[i] = (kc - t * p.cpt) * 8;
+    b_dy[i] = p.dy_t[t];
+    b_dx[i] = p.dx_t[t];
+  }
+
+  auto stage = [&](int kt, int buf) {
+    char* Ai = smem + buf * STAGE;
+    char* Bi = Ai + IMG;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (wave * 4 + i) * 2 + (lane >> 5);
+      const int m = mstart + kt * BK + r;
+      const bool mok = m < mend;
+      const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 4 + i) * 1024), 16, 0, 0);
+      const uint32_t mm = mok ? m : 0;
+      const uint32_t q = fdiv(mm, p.div_wo);
+      const uint32_t x = mm - q * p.Wo;
+      const uint32_t n = fdiv(q, p.div_ho);
+      const uint32_t y = q - n * p.Ho;
+      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const char* Ai = smem + buf * STAGE;
+    const char* Bi = Ai + IMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t row0 = s * 32 + 8 * (lane >> 4);
+      bf16x8 af[4], bfr[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag512(Ai, row0, wm * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bfr[j] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nkt == 0) return;
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kcol = kcol0 + wn * 128 + j * 16 + (lane & 15);
+      if (kcol >= p.ldw) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < p.Co) {
+          if (p.part) p.part[((size_t)blockIdx.y * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
+          else unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
@@ -871,10 +1001,15 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
 // split-K plan of the weight-gradient GEMM, >= 256 rows per split: ~2 blocks per CU for
 // 1x1 convs / linears (fewer, longer splits: less partial-slab traffic), ~4 for k x k
 // (measured per shape with tools/conv_bench.py --cfgs "5=2,5=4")
+static bool wgrad_big(int Co, int ldw) { return g_tune[7] != 2 && Co >= 256 && ldw >= 256; }
+
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split) {
-  const int ntm = (Co + 127) / 128, ntn = (ldw + 127) / 128;
+  const bool big = wgrad_big(Co, ldw);
+  const int bt = big ? 256 : 128;
+  const int ntm = (Co + bt - 1) / bt, ntn = (ldw + bt - 1) / bt;
   const int tiles = ntm * ntn;
-  const int target = (g_tune[5] > 0 ? g_tune[5] : (taps == 1 ? 2 : 4)) * num_cu;
+  const int per_cu = big ? 1 : (taps == 1 ? 2 : 4);
+  const int target = (g_tune[5] > 0 ? g_tune[5] : per_cu) * num_cu;
   int splits = (target + tiles - 1) / tiles;
   int max_splits = (M + 255) / 256;
   if (splits > max_splits) splits = max_splits;
@@ -899,7 +1034,9 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
-  const int tiles = ((Co + 127) / 128) * ((p.ldw + 127) / 128);
+  const bool big = wgrad_big(Co, p.ldw);
+  const int bt = big ? 256 : 128;
+  const int tiles = ((Co + bt - 1) / bt) * ((p.ldw + bt - 1) / bt);
   p.ablate = g_tune[2];
   if (g_tune[6] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
   int rps = 0;
@@ -911,7 +1048,17 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   if (splits == 1) {
     p.part = dw;  // split 0 stores straight into dw
   }
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, splits), dim3(256), 4 * 64 * 256, stream, p);
+  if (big) {
+    constexpr int lds = 4 * 64 * 512;
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)wgrad256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles, splits), dim3(512), lds, stream, p);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, splits), dim3(256), 4 * 64 * 256, stream, p);
+  }
   if (part != nullptr && splits > 1) launch_split_reduce(part, splits, Co * p.ldw, dw, stream);
 }
 

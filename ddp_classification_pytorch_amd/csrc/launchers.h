@@ -9,7 +9,7 @@ typedef __bf16 bf16;
 namespace dcp {
 
 // tuning switches for in-process A/B experiments (tools/conv_bench.py --cfgs); all 0 = defaults
-// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant, [5] wgrad blocks per CU, [6] wgrad atomics
+// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant, [5] wgrad blocks per CU, [6] wgrad atomics, [7] 256-tile wgrad (0 auto, 1 on, 2 off)
 extern int g_tune[8];
 
 constexpr int kMaxTaps = 64;
