@@ -107,7 +107,8 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
 }
 
 // dy [N,Ho,Wo,Co], wt [C,KH,KW,Co] (transposed weight) -> dx [N,H,W,C]
-Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                  const optional<Tensor>& add) {
   CHECK_ACT(dy);
   CHECK_ACT(wt);
   const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
@@ -129,8 +130,14 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
         t.dx[i] = pad - kw;
         t.widx[i] = i;
       }
+    const bf16* addp = nullptr;
+    if (add.has_value()) {
+      CHECK_ACT(*add);
+      TORCH_CHECK(add->sizes() == dx.sizes(), "conv_dgrad add shape");
+      addp = bp(*add);
+    }
     dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr,
-                         nullptr, 0, z, st);
+                         nullptr, 0, z, st, addp);
     return dx;
   }
   // stride 2: four parity classes of the input grid
@@ -153,6 +160,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
       dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, Hy, Wy, 1, 2, ph, pw, t,
                            nullptr, nullptr, 0, z, st);
     }
+  if (add.has_value()) dx.add_(*add);
   return dx;
 }
 
@@ -716,7 +724,7 @@ void set_tuning(int64_t idx, int64_t value) {
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
-  m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad) -> Tensor", &conv_dgrad);
+  m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, int act) -> Tensor", &linear_fwd);
   m.def("linear_wgrad(Tensor dy, Tensor x) -> Tensor", &linear_wgrad);

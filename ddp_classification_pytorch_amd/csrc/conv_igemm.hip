@@ -51,6 +51,7 @@ struct TapGemmParams {
   int ntaps, cpt, nkt, ldw;
   int relu;          // fused activation on the stored output: 0 none, 1 ReLU, 2 sigmoid (linear heads)
   const float* bias; // optional per-output-channel bias (linear heads)
+  const bf16* addsrc;  // optional: added to the stored output (same layout as dst; fused residual-gradient sum)
   FastDiv div_wy, div_hy, div_cpt;
   // per tap: dy (int8) | dx (int8) << 8 | weight tap index << 16.  Dword entries so a
   // wave-uniform lookup is one s_load_dword (byte arrays compile to vector loads, whose
@@ -359,7 +360,13 @@ tap_gemm_kernel(const TapGemmParams p) {
             const uint32_t y = q - n * p.Hy;
             drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
           }
-          *(bf16x8*)(p.dst + drow + n0 + c * 8) = v;
+          bf16x8 o = v;
+          if (p.addsrc) {
+            const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
+          }
+          *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
         }
       }
     }
@@ -576,7 +583,13 @@ tap_gemm8_kernel(const TapGemmParams p) {
           const uint32_t y = q - n * p.Hy;
           drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
         }
-        *(bf16x8*)(p.dst + drow + n0 + c * 8) = v;
+        bf16x8 o = v;
+        if (p.addsrc) {
+          const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
+        }
+        *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
       }
     }
   }
@@ -883,9 +896,9 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                      const TapList& taps, float* stats, const float* bias, int relu,
-                     const bf16* zero, hipStream_t stream) {
+                     const bf16* zero, hipStream_t stream, const bf16* addsrc) {
   TapGemmParams p;
-  p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero;
+  p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
   p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;

@@ -21,7 +21,7 @@ struct TapList {
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
-                     const float* bias, int relu, const bf16* zero, hipStream_t stream);
+                     const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr);
 // partial-slab split-K weight gradient: dw is fully written when part != nullptr
 // (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split);

@@ -36,11 +36,11 @@ class Conv2d(nn.Module):
         fan_out = self.out_channels * self.kernel_size * self.kernel_size // self.groups
         nn.init.normal_(self.weight, 0.0, math.sqrt(2.0 / fan_out))
 
-    def forward(self, x, stats=False):
-        """Returns (y, bn_stat_slabs_or_None)."""
+    def forward(self, x, stats=False, link=None):
+        """Returns (y, bn_stat_slabs_or_None).  `link`: residual-gradient hand-off (ops.functional.ResidualLink)."""
         if self.groups > 1:
             return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding), None
-        y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda)
+        y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda, link)
         return y, (slabs if stats and x.is_cuda else None)
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
@@ -79,14 +79,24 @@ class BatchNorm2d(nn.Module):
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
         self.process_group = None  # set by parallel.convert_sync_batchnorm
         self.frozen = False
+        self._nbt_pending = 0
 
-    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01):
+    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None):
         stats = self.training and not self.frozen
         if stats:
-            self.num_batches_tracked.add_(1)
+            self._nbt_pending += 1  # folded into num_batches_tracked lazily (no per-step device add)
         return Fn.batch_norm_act(x, slabs, self.weight, self.bias, self.running_mean, self.running_var, stats,
                                  self.momentum, self.eps, act=act, slope=slope, residual=residual,
-                                 group=self.process_group if stats else None)
+                                 group=self.process_group if stats else None, link=link)
+
+    def flush_batches_tracked(self):
+        if self._nbt_pending:
+            self.num_batches_tracked.add_(self._nbt_pending)
+            self._nbt_pending = 0
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self.flush_batches_tracked()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
 
     def extra_repr(self):
         return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, sync={self.process_group is not None}"

@@ -40,7 +40,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         t = _train_stats(self.bn1)
-        y, s = self.conv1(x, stats=t)
+        link = Fn.ResidualLink() if self.downsample is None else None
+        y, s = self.conv1(x, stats=t, link=link)
         y = self.bn1(y, s, act="relu")
         y, s = self.conv2(y, stats=t)
         if self.downsample is not None:
@@ -48,7 +49,7 @@ class BasicBlock(nn.Module):
             r = self.downsample[1](r, rs, act="none")
         else:
             r = x
-        return self.bn2(y, s, act="relu", residual=r)
+        return self.bn2(y, s, act="relu", residual=r, link=link)
 
 
 class Bottleneck(nn.Module):
@@ -67,7 +68,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         t = _train_stats(self.bn1)
-        y, s = self.conv1(x, stats=t)
+        # identity blocks: the residual gradient is summed in conv1's dgrad epilogue
+        link = Fn.ResidualLink() if self.downsample is None else None
+        y, s = self.conv1(x, stats=t, link=link)
         y = self.bn1(y, s, act="relu")
         y, s = self.conv2(y, stats=t)
         y = self.bn2(y, s, act="relu")
@@ -77,7 +80,7 @@ class Bottleneck(nn.Module):
             r = self.downsample[1](r, rs, act="none")
         else:
             r = x
-        return self.bn3(y, s, act="relu", residual=r)
+        return self.bn3(y, s, act="relu", residual=r, link=link)
 
 
 class ResNet(nn.Module):

@@ -43,7 +43,7 @@ def conv_fwd(x, w, stride, pad, stats):
     return y, torch.empty(0, device=x.device)
 
 
-def conv_dgrad(dy, wt, H, W, stride, pad):
+def conv_dgrad(dy, wt, H, W, stride, pad, add=None):
     # wt: [C,KH,KW,Co] (transposed); recover w [Co,KH,KW,C]
     w = wt.permute(3, 1, 2, 0)
     N = dy.shape[0]
@@ -54,7 +54,10 @@ def conv_dgrad(dy, wt, H, W, stride, pad):
     op_w = W - ((Wo - 1) * stride - 2 * pad + KW)
     dx = F.conv_transpose2d(_nchw(_f(dy)), _w_oihw(_f(w)), stride=stride, padding=pad, output_padding=(op_h, op_w))
     assert dx.shape == (N, C, H, W)
-    return _nhwc(dx).to(dy.dtype)
+    dx = _nhwc(dx)
+    if add is not None:
+        dx = dx + _f(add)
+    return dx.to(dy.dtype)
 
 
 def conv_wgrad(dy, x, KH, KW, stride, pad):

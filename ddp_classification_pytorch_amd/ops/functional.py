@@ -67,12 +67,27 @@ def prepared_weight(w: torch.Tensor, co_pad: int = 0, transposed: bool = True):
 
 
 # ----------------------------------------------------------------------------- convolution
+class ResidualLink:
+    """Hands the identity-path gradient of a residual block from the block's last
+    BN+add+ReLU backward to the backward of the block's FIRST conv, which adds it in
+    its dgrad epilogue (one fused pass instead of a separate bf16 add kernel over the
+    block-input gradient).  Only for blocks whose residual is the raw block input.
+    Autograd order guarantees the BN backward runs first (the first conv's output
+    gradient depends on it)."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _Conv2d(Function):
     @staticmethod
-    def forward(ctx, x, weight, wb, wt, stride, pad, stats):
+    def forward(ctx, x, weight, wb, wt, stride, pad, stats, link):
         y, slabs = K(x).conv_fwd(x, wb, stride, pad, stats)
         ctx.save_for_backward(x, wt)
         ctx.geo = (weight.shape[1], weight.shape[2], stride, pad)
+        ctx.link = link
         ctx.mark_non_differentiable(slabs)
         return y, slabs
 
@@ -82,20 +97,28 @@ class _Conv2d(Function):
         KH, KW, stride, pad = ctx.geo
         dy = dy.contiguous()
         k = K(dy)
+        add = None
+        if ctx.link is not None:
+            add, ctx.link.grad = ctx.link.grad, None
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
+            if add is not None:
+                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add.contiguous())
+            else:
+                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
         if ctx.needs_input_grad[1]:
             dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
-def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False):
-    """NHWC conv; returns (y, bn_stat_slabs).  weight: fp32 [Co,KH,KW,Ci]."""
+def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
+           link: "ResidualLink | None" = None):
+    """NHWC conv; returns (y, bn_stat_slabs).  weight: fp32 [Co,KH,KW,Ci].
+    `link`: the block's ResidualLink when this is the first conv of a residual block."""
     if weight.shape[3] != x.shape[3]:  # stem: input channels zero-padded to a multiple of 8
         weight = F.pad(weight, (0, x.shape[3] - weight.shape[3]))
     wb, wt = prepared_weight(weight, 0, True)
-    return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats)
+    return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link)
 
 
 class _GroupedConv2d(Function):
@@ -186,7 +209,7 @@ class BNConfig:
 
 class _BNAct(Function):
     @staticmethod
-    def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig):
+    def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig, link):
         k = K(x)
         C = x.shape[-1]
         count = x.numel() // C
@@ -205,6 +228,7 @@ class _BNAct(Function):
         ctx.cfg = cfg
         ctx.count = count
         ctx.has_res = res is not None
+        ctx.link = link
         return y
 
     @staticmethod
@@ -227,16 +251,19 @@ class _BNAct(Function):
                                   float(ctx.count), cfg.act, cfg.slope, want_dres)
         dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
         dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
-        return dx, None, dgamma, dbeta, (dres if want_dres else None), None, None, None
+        if want_dres and ctx.link is not None:
+            ctx.link.grad = dres  # summed into the block input gradient by the first conv's dgrad
+            want_dres = False
+        return dx, None, dgamma, dbeta, (dres if want_dres else None), None, None, None, None
 
 
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
-                   slope=0.01, residual=None, group=None):
+                   slope=0.01, residual=None, group=None, link=None):
     world = dist.get_world_size(group) if group is not None else 1
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
     if slabs is None or (slabs.numel() == 0):
         slabs = None
-    return _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg)
+    return _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link)
 
 
 # ----------------------------------------------------------------------------- pooling

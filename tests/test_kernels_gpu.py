@@ -307,6 +307,21 @@ def test_nested_eval_counts(K):
     assert torch.equal(cnt.cpu(), ref)
 
 
+@pytest.mark.parametrize("Ci,Co,k,s", [(256, 64, 1, 1), (64, 128, 3, 1), (128, 64, 3, 2)])
+def test_conv_dgrad_fused_add(K, Ci, Co, k, s):
+    """dgrad epilogue that adds the identity-path gradient (ResidualLink)."""
+    N, H = 2, 14
+    p = k // 2
+    Ho = (H + 2 * p - k) // s + 1
+    w = torch.randn(Co, k, k, Ci) / (k * k * Ci) ** 0.5
+    _, wt = K.weight_prep(w.to(DEV), 0, True)
+    dy = rnd(N, Ho, Ho, Co)
+    add = rnd(N, H, H, Ci)
+    dx = K.conv_dgrad(dy.to(DEV), wt, H, H, s, p, add.to(DEV))
+    ref = _ref.conv_dgrad(dy.float(), w.bfloat16().float().permute(3, 1, 2, 0), H, H, s, p).float() + add.float()
+    assert relerr(dx, ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,C,G,KH,stride,pad", [
     (2, 14, 14, 128, 32, 3, 1, 1),   # CG=4  (super-group 16, 4 groups block-diagonal)
     (3, 13, 11, 256, 32, 3, 2, 1),   # CG=8, odd spatial, stride 2, M not a multiple of 256
