@@ -79,7 +79,7 @@ dcp::TapList fwd_taps(int KH, int KW, int pad) {
   return t;
 }
 
-// x [N,H,W,C] bf16, w [Co,KH,KW,C] bf16 -> y [N,Ho,Wo,Co], stats slabs [ceil(M/64),2,Co]
+// x [N,H,W,C] bf16, w [Co,KH,KW,C] bf16 -> y [N,Ho,Wo,Co], stats slabs [ceil(M/128),2,Co]
 std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad, bool stats) {
   CHECK_ACT(x);
   CHECK_ACT(w);
@@ -96,7 +96,7 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
   const int M = N * Ho * Wo;
   Tensor slabs;
   if (stats)
-    slabs = at::empty({(M + 63) / 64, 2, Co}, f32_like(x));
+    slabs = at::empty({(M + 127) / 128, 2, Co}, f32_like(x));
   else
     slabs = at::empty({0}, f32_like(x));
   const auto taps = fwd_taps(KH, KW, pad);
@@ -302,7 +302,7 @@ Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
   const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
   if (from_slabs)
-    TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 63) / 64 && slabs->size(1) == 2 && slabs->size(2) == C,
+    TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 127) / 128 && slabs->size(1) == 2 && slabs->size(2) == C,
                 "slab shape");
   auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
   auto out = at::empty({1, 3, C}, f32_like(x));
@@ -716,6 +716,15 @@ void cdr_mask(const Tensor& table, const Tensor& chunks, const Tensor& state, do
 
 }  // namespace
 
+// entries: int64 [E, 7] packed WPEntry table; blocks: int32 [B, 2] (entry, tile) -- both device tensors
+void mt_weight_prep(const Tensor& entries, const Tensor& blocks) {
+  CHECK_DEV(entries);
+  CHECK_DEV(blocks);
+  TORCH_CHECK(entries.scalar_type() == at::kLong && entries.dim() == 2 && entries.size(1) == 7, "entries [E,7] int64");
+  TORCH_CHECK(blocks.scalar_type() == at::kInt && blocks.dim() == 2 && blocks.size(1) == 2, "blocks [B,2] int32");
+  dcp::launch_mt_weight_prep(entries.data_ptr(), blocks.data_ptr(), (int)blocks.size(0), cur_stream());
+}
+
 void set_tuning(int64_t idx, int64_t value) {
   TORCH_CHECK(idx >= 0 && idx < 8, "tuning index");
   dcp::g_tune[idx] = (int)value;
@@ -723,6 +732,7 @@ void set_tuning(int64_t idx, int64_t value) {
 
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
+  m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);

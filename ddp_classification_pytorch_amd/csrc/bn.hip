@@ -11,7 +11,7 @@
 // ResNets feed BN inputs whose mean is large against their spread (post-ReLU
 // inputs to 1x1 convs) and E[x^2]-E[x]^2 in fp32 loses the variance.
 // Pipeline per BN layer (training):
-//   conv epilogue    -> per-64-row tile (mean, M2) slabs            (conv_igemm.hip)
+//   conv epilogue    -> per-128-row slab (mean, M2)                 (conv_igemm.hip)
 //   bn_slab_partial  -> per-split (n, mean, M2) partials  } bn_stats -> [1][3][C]
 //   bn_merge         -> one (n, mean, M2) per channel     }   (SyncBN: all_gather -> [W][3][C])
 //   bn_finalize      -> merge W entries; mean, invstd, scale, shift; running-stat update
@@ -54,7 +54,7 @@ struct Welford {
   }
 };
 
-// conv slabs [R][2][C] = per-64-row tile (mean, M2); tile r holds min(64, M-64r) rows.
+// conv slabs [R][2][C] = per-128-row slab (mean, M2); slab r holds min(128, M-128r) rows.
 // out[blockIdx.y][3][C] = (n, mean, M2) over this split's tiles.
 __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __restrict__ slabs, int R, int M, int C,
                                                               int tiles_per_split, float* __restrict__ out) {
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __res
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     for (int r = r0 + w; r < r1; r += 4) {
-      const float nb = (float)min(64, M - 64 * r);
+      const float nb = (float)min(128, M - 128 * r);
       a.merge(nb, slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
     }
   }
@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
 // ---------------------------------------------------------------------------
 int bn_stats_partials(int M, int C, bool from_slabs) {
   if (from_slabs) {
-    const int R = (M + 63) / 64;
+    const int R = (M + 127) / 128;
     int splits = (R + 31) / 32;
     return splits > 64 ? 64 : (splits < 1 ? 1 : splits);
   }
@@ -501,7 +501,7 @@ int bn_stats_partials(int M, int C, bool from_slabs) {
 // part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
   if (slabs) {
-    const int R = (M + 63) / 64;
+    const int R = (M + 127) / 128;
     const int P = bn_stats_partials(M, C, true);
     const int tps = (R + P - 1) / P;
     hipLaunchKernelGGL(bn_slab_partial_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps, part);

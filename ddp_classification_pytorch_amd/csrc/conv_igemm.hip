@@ -42,7 +42,7 @@ struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
   const bf16* wt;    // [Co][T][Cs]
   bf16* dst;         // [N][Hd][Wd][Co]
-  float* stats;      // [ceil(M/64)][2][Co] per-64-row tile (mean, M2) or nullptr
+  float* stats;      // [ceil(M/128)][2][Co] per-128-row slab (mean, M2) or nullptr
   const bf16* zero;  // >= 16 bytes of zeros
   int Hs, Ws, Cs;
   int Hy, Wy, ss;
@@ -70,41 +70,63 @@ __device__ __forceinline__ uint32_t swz128(uint32_t r, uint32_t c) {
   return r * 128u + ((c ^ ((r >> 1) & 7u)) << 4);
 }
 
-// Per 64-row tile and channel of the LDS output image E[rows][BN] (16-byte chunks
-// XOR-swizzled by row>>1): (mean, M2) of the bf16-rounded outputs, two passes over
-// register-resident values (no E[x^2]-E[x]^2 cancellation); merged later with
-// Chan's formula.  Thread -> (channel, 64-row tile); NT tiles.
+// Per 128-row slab and channel of the LDS output image E[rows][BN] (16-byte chunks
+// XOR-swizzled by row>>1): (mean, M2) of the bf16-rounded outputs.  A thread takes one
+// channel x 64 rows with two passes over register-resident values (no E[x^2]-E[x]^2
+// cancellation), then the two 64-row halves of a slab are merged with Chan's formula
+// through LDS (scratch behind the image).  NT = 64-row tiles in the block (even).
 template <int BN, int NT>
-__device__ __forceinline__ void tile_stats(const TapGemmParams& p, const char* E, int m0, int n0, int tid) {
+__device__ __forceinline__ void tile_stats(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
   constexpr int RB = BN * 2, NCH = BN / 8;
+  static_assert(NT % 2 == 0, "slabs pair 64-row tiles");
+  float* xch = (float*)(E + NT * 64 * RB);  // [NT/2][3][BN]
   const int ch = tid % BN, h = tid / BN;
   const int co = n0 + ch;
-  const int nvalid = min(64, p.M - (m0 + h * 64));
-  if (h >= NT || co >= p.Co || nvalid <= 0) return;
-  const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
-  float v[64];
+  const bool active = h < NT && co < p.Co;
+  const int nvalid = active ? max(0, min(64, p.M - (m0 + h * 64))) : 0;
+  float mean = 0.f, m2 = 0.f;
+  if (nvalid > 0) {
+    const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
+    float v[64];
 #pragma unroll
-  for (int r = 0; r < 64; ++r) {
-    const uint32_t pl = h * 64 + r;
-    v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + (coff ^ (((pl >> 1) & (NCH - 1)) << 4))));
+    for (int r = 0; r < 64; ++r) {
+      const uint32_t pl = h * 64 + r;
+      v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + (coff ^ (((pl >> 1) & (NCH - 1)) << 4))));
+    }
+    float s[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) s[r & 7] += r < nvalid ? v[r] : 0.f;
+    mean = ((s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]))) / (float)nvalid;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) {
+      const float d = v[r] - mean;
+      s[r & 7] += r < nvalid ? d * d : 0.f;
+    }
+    m2 = (s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]));
   }
-  float s[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s[k] = 0.f;
-#pragma unroll
-  for (int r = 0; r < 64; ++r) s[r & 7] += r < nvalid ? v[r] : 0.f;
-  const float mean = ((s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]))) / (float)nvalid;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s[k] = 0.f;
-#pragma unroll
-  for (int r = 0; r < 64; ++r) {
-    const float d = v[r] - mean;
-    s[r & 7] += r < nvalid ? d * d : 0.f;
+  if (active && (h & 1)) {
+    xch[((h >> 1) * 3 + 0) * BN + ch] = (float)nvalid;
+    xch[((h >> 1) * 3 + 1) * BN + ch] = mean;
+    xch[((h >> 1) * 3 + 2) * BN + ch] = m2;
   }
-  const float m2 = (s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]));
-  const size_t rb = (size_t)(m0 / 64 + h);
-  p.stats[(rb * 2 + 0) * p.Co + co] = mean;
-  p.stats[(rb * 2 + 1) * p.Co + co] = m2;
+  __syncthreads();
+  if (active && !(h & 1) && nvalid > 0) {
+    const float nb = xch[((h >> 1) * 3 + 0) * BN + ch];
+    if (nb > 0.f) {
+      const float mb = xch[((h >> 1) * 3 + 1) * BN + ch], m2b = xch[((h >> 1) * 3 + 2) * BN + ch];
+      const float na = (float)nvalid, n = na + nb;
+      const float d = mb - mean;
+      mean += d * (nb / n);
+      m2 += m2b + d * d * (na * nb / n);
+    }
+    const size_t rb = (size_t)(m0 / 128 + (h >> 1));
+    p.stats[(rb * 2 + 0) * p.Co + co] = mean;
+    p.stats[(rb * 2 + 1) * p.Co + co] = m2;
+  }
 }
 
 // vmcnt(n) with a wave-uniform runtime n in [0, 31] (a scalar branch to an immediate wait)

@@ -119,6 +119,8 @@ void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const 
                      hipStream_t s);
 
 void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16* wb, bf16* wt, hipStream_t s);
+// entries: packed {w, wb, wt, Co, T, Ci_src, Ci, Cp, tci, tco, pad} (56 B each); blocks: int2 (entry, tile)
+void launch_mt_weight_prep(const void* entries, const void* blocks, int nblocks, hipStream_t s);
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s);
 void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);

@@ -35,6 +35,47 @@ __global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restric
   }
 }
 
+// Multi-tensor weight_prep: every conv / linear weight of the model in ONE launch
+// (one block per (weight, tap, 64x64 tile) from a host-built block list), run once
+// per optimizer step instead of one launch per layer.  Source rows may be narrower
+// than the destination (stem: Ci_src = 3 zero-padded to Ci = 8).
+struct WPEntry {
+  const float* w;
+  bf16* wb;
+  bf16* wt;
+  int Co, T, Ci_src, Ci, Cp, tci, tco, pad_;
+};
+
+__global__ void __launch_bounds__(256) mt_weight_prep_kernel(const WPEntry* __restrict__ entries,
+                                                             const int2* __restrict__ blocks) {
+  __shared__ float tile[64][65];
+  const int2 b = blocks[blockIdx.x];
+  const WPEntry e = entries[b.x];
+  const int per_t = e.tci * e.tco;
+  const int t = b.y / per_t, rr = b.y - t * per_t;
+  const int co0 = (rr / e.tci) * 64, ci0 = (rr % e.tci) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int co = co0 + r, ci = ci0 + tx;
+    float v = 0.f;
+    if (co < e.Co && ci < e.Ci_src) v = e.w[((size_t)co * e.T + t) * e.Ci_src + ci];
+    tile[r][tx] = v;
+    if (co < e.Cp && ci < e.Ci) e.wb[((size_t)co * e.T + t) * e.Ci + ci] = f2bf(v);
+  }
+  if (!e.wt) return;
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (ci < e.Ci && co < e.Cp) e.wt[((size_t)ci * e.T + t) * e.Cp + co] = f2bf(tile[tx][r]);
+  }
+}
+
+void launch_mt_weight_prep(const void* entries, const void* blocks, int nblocks, hipStream_t s) {
+  if (nblocks <= 0) return;
+  hipLaunchKernelGGL(mt_weight_prep_kernel, dim3(nblocks), dim3(256), 0, s, (const WPEntry*)entries,
+                     (const int2*)blocks);
+}
+
 // src: [N][C][H][W] (nchw) or [N][H][W][C]; dtype u8 (is_u8) or fp32
 // dst: [N][H][W][Cp] bf16 = (src*in_scale - mean[c]) / std[c], zero for c >= C
 __global__ void __launch_bounds__(256) to_nhwc_kernel(const void* __restrict__ src, int is_u8, int nchw, int N,

@@ -14,6 +14,8 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import weakref
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -47,13 +49,22 @@ def bump_weight_generation():
     _GEN[0] += 1
 
 
-def prepared_weight(w: torch.Tensor, co_pad: int = 0, transposed: bool = True):
-    """(bf16 copy padded to co_pad rows, transposed copy) of a fp32 master, cached per version."""
-    key = (w._version, _GEN[0], w.data_ptr(), co_pad, transposed)
+def prepared_weight(w: torch.Tensor, co_pad: int = 0, transposed: bool = True, ci: int = 0):
+    """(bf16 copy padded to co_pad rows, transposed copy) of a fp32 master, cached per version.
+
+    On the GPU every registered weight lives in a persistent bf16 buffer and all stale
+    ones are refreshed together by ONE multi-tensor launch (the first prepared_weight
+    call after an optimizer step re-converts the whole model).  ``ci`` zero-pads the
+    input-channel (last) dim (the stem's 3 -> 8)."""
+    if w.is_cuda and w.dtype == torch.float32 and w.is_contiguous():
+        return _MT.get(w, co_pad, transposed, ci)
+    key = (w._version, _GEN[0], w.data_ptr(), co_pad, transposed, ci)
     cached = getattr(w, "_dcp_prep", None)
     if cached is not None and cached[0] == key:
         return cached[1], cached[2]
     wd = w.detach()
+    if ci and ci != wd.shape[-1]:
+        wd = F.pad(wd, (0, ci - wd.shape[-1]))
     if not wd.is_contiguous():
         wd = wd.contiguous()
     wb, wt = K(wd).weight_prep(wd, co_pad, transposed)
@@ -64,6 +75,81 @@ def prepared_weight(w: torch.Tensor, co_pad: int = 0, transposed: bool = True):
     except Exception:  # non-leaf / functional tensors cannot carry attributes
         pass
     return wb, wt
+
+
+class _MTWeightCache:
+    """Persistent bf16 (and transposed) copies of the fp32 master weights, refreshed in
+    one `mt_weight_prep` launch per step from a packed device table of
+    {fp32 src, bf16 dst, bf16 dst^T, shape} entries plus a (entry, tile) block list,
+    both built once per set of stale weights and reused every step."""
+
+    def __init__(self):
+        self.entries = {}   # (id(w), co_pad, transposed, ci) -> entry dict
+        self.tables = {}    # tuple of entry ids -> (entries tensor, blocks tensor)
+
+    @staticmethod
+    def _stamp(w):
+        return (w._version, _GEN[0], w.data_ptr())
+
+    def get(self, w, co_pad, transposed, ci):
+        ek = (id(w), co_pad, bool(transposed), ci)
+        e = self.entries.get(ek)
+        if e is None or e["ref"]() is not w:
+            e = self._register(w, co_pad, transposed, ci)
+            self.entries[ek] = e
+        if e["stamp"] != self._stamp(w):
+            self.refresh()
+        return e["wb"], e["wt"]
+
+    def _register(self, w, co_pad, transposed, ci):
+        Co, Ci_src = w.shape[0], w.shape[-1]
+        mid = tuple(w.shape[1:-1])
+        T = 1
+        for d in mid:
+            T *= d
+        Ci = ci or Ci_src
+        Cp = co_pad or Co
+        wb = torch.empty((Cp,) + mid + (Ci,), dtype=torch.bfloat16, device=w.device)
+        wt = (torch.empty((Ci,) + mid + (Cp,), dtype=torch.bfloat16, device=w.device) if transposed
+              else torch.empty(0, dtype=torch.bfloat16, device=w.device))
+        return {"ref": weakref.ref(w), "wb": wb, "wt": wt, "stamp": None,
+                "shape": (Co, T, Ci_src, Ci, Cp), "transposed": bool(transposed)}
+
+    def refresh(self):
+        stale = []
+        for k in list(self.entries):
+            e = self.entries[k]
+            w = e["ref"]()
+            if w is None:
+                del self.entries[k]
+                continue
+            if e["stamp"] != self._stamp(w):
+                stale.append((k, e, w))
+        if not stale:
+            return
+        tkey = tuple(k for k, _, _ in stale) + tuple(w.data_ptr() for _, _, w in stale)
+        tab = self.tables.get(tkey)
+        if tab is None:
+            rows, blocks = [], []
+            for i, (_, e, w) in enumerate(stale):
+                Co, T, Ci_src, Ci, Cp = e["shape"]
+                tci, tco = (Ci + 63) // 64, (Cp + 63) // 64
+                wt_ptr = e["wt"].data_ptr() if e["transposed"] else 0
+                rows.append([w.data_ptr(), e["wb"].data_ptr(), wt_ptr, Co | (T << 32), Ci_src | (Ci << 32),
+                             Cp | (tci << 32), tco])
+                blocks.extend((i, t) for t in range(T * tci * tco))
+            dev = stale[0][2].device
+            ent = torch.tensor(rows, dtype=torch.int64).to(dev)
+            blk = torch.tensor(blocks, dtype=torch.int32).to(dev)
+            if len(self.tables) > 16:
+                self.tables.clear()
+            tab = self.tables[tkey] = (ent, blk)
+        _ext.hip_ops().mt_weight_prep(*tab)
+        for _, e, w in stale:
+            e["stamp"] = self._stamp(w)
+
+
+_MT = _MTWeightCache()
 
 
 # ----------------------------------------------------------------------------- convolution
@@ -116,7 +202,9 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0,
     """NHWC conv; returns (y, bn_stat_slabs).  weight: fp32 [Co,KH,KW,Ci].
     `link`: the block's ResidualLink when this is the first conv of a residual block."""
     if weight.shape[3] != x.shape[3]:  # stem: input channels zero-padded to a multiple of 8
-        weight = F.pad(weight, (0, x.shape[3] - weight.shape[3]))
+        wb, wt = prepared_weight(weight, 0, True, ci=x.shape[3])
+        weight = F.pad(weight, (0, x.shape[3] - weight.shape[3]))  # autograd view for the padded dW
+        return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link)
     wb, wt = prepared_weight(weight, 0, True)
     return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link)
 
