@@ -52,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--num-classes", type=int, default=None)
     ap.add_argument("--syncbn", action="store_true", help="cross-replica BN (reference default); off = local BN")
     ap.add_argument("--bucket-cap-mb", type=float, default=100.0)
+    ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                    help="DDP gradient all-reduce precision (bf16 = bf16_compress_hook: half the xGMI bytes)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     return ap.parse_args(argv)
@@ -92,10 +94,17 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl" on ROCm).  DCP_DIST_BACKEND=gloo lets tests run
+    # several ranks on one GPU (RCCL refuses duplicate devices).
+    backend = os.environ.get("DCP_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     _ext.hip_ops()  # fail loudly if the gfx950 library is missing
@@ -104,6 +113,10 @@ def main(argv=None):
     model = build_bench_model(a).to(dev)
     if world > 1:
         model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb)
+        if a.grad_comm == "bf16":
+            from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+
+            model.register_comm_hook(None, default_hooks.bf16_compress_hook)
     opt = FusedSGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
 
     B, S = a.batch, a.image_size
@@ -179,6 +192,8 @@ def main(argv=None):
                 "num_classes": a.num_classes,
                 "parallelism": f"dp{world}",
                 "syncbn": bool(a.syncbn),
+                "grad_comm": a.grad_comm,
+                "bucket_cap_mb": a.bucket_cap_mb,
                 "optimizer": "fused SGD momentum 0.9 wd 1e-4",
                 "final_loss": round(loss_v, 4),
             },
