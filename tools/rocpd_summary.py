@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Per-kernel summary of a rocprofv3 SQLite (rocpd) database.
+
+    python tools/rocpd_summary.py gpurun_out/prof/run_results.db --steps 11 [--csv out.csv]
+
+Groups dispatches by kernel name, prints calls, total / mean time, share of
+the GPU-busy time and the per-training-step time (total / --steps, the
+number of steps the profiled program ran including warm-up), plus the
+busy-time and wall span of the whole trace.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import re
+import sqlite3
+import sys
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(.*\)$", "", name) if not name.startswith("void at::") else name.split("(")[0]
+    return name[:110]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("db")
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--csv", default=None)
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args(argv)
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, start, end from kernels").fetchall()
+    if not rows:
+        print("no kernel dispatches", file=sys.stderr)
+        return 1
+    agg = {}
+    for name, s, e in rows:
+        k = short(name)
+        d = agg.setdefault(k, [0, 0.0, 1e30, 0.0])
+        dur = (e - s) / 1e3
+        d[0] += 1
+        d[1] += dur
+        d[2] = min(d[2], dur)
+        d[3] = max(d[3], dur)
+    busy = sum(v[1] for v in agg.values())
+    span = (max(r[2] for r in rows) - min(r[1] for r in rows)) / 1e3
+    out = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    hdr = ["kernel", "calls", "total_us", "mean_us", "min_us", "max_us", "pct_busy", "us_per_step"]
+    table = [[k, v[0], round(v[1], 1), round(v[1] / v[0], 2), round(v[2], 2), round(v[3], 2),
+              round(100 * v[1] / busy, 2), round(v[1] / a.steps, 1)] for k, v in out]
+    print(f"# dispatches={len(rows)} gpu_busy_ms={busy / 1e3:.2f} trace_span_ms={span / 1e3:.2f} "
+          f"steps={a.steps} busy_ms_per_step={busy / 1e3 / a.steps:.2f}")
+    print("%-90s %6s %11s %9s %6s %9s" % ("kernel", "calls", "total_us", "mean_us", "%busy", "us/step"))
+    for r in table[: a.top]:
+        print("%-90s %6d %11.1f %9.2f %6.2f %9.1f" % (r[0][:90], r[1], r[2], r[3], r[6], r[7]))
+    if a.csv:
+        with open(a.csv, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(hdr)
+            w.writerows(table)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
