@@ -164,6 +164,65 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
   return dx;
 }
 
+// Stride-1 dgrad fused with the backward reduction of the BN(+ReLU)(+residual) layer that
+// produced this conv's input (y = that layer's BN input).  Returns the activation-masked
+// input gradient g' [N,H,W,C] and the per-channel sums [2,C] = (sum g', sum g'*xhat).
+std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int64_t pad, const optional<Tensor>& add,
+                                         const Tensor& y, const optional<Tensor>& res, const Tensor& scale,
+                                         const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act) {
+  CHECK_ACT(dy);
+  CHECK_ACT(wt);
+  CHECK_ACT(y);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int C = wt.size(0), KH = wt.size(1), KW = wt.size(2);
+  TORCH_CHECK(wt.size(3) == Co, "transposed weight Co mismatch");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_dgrad_bn needs channel multiples of 8");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(3) == C, "conv_dgrad_bn: BN input shape");
+  const int H = y.size(1), W = y.size(2);
+  TORCH_CHECK(H + 2 * pad - KH + 1 == Ho && W + 2 * pad - KW + 1 == Wo, "conv_dgrad_bn: stride-1 geometry");
+  TORCH_CHECK(act == 0 || act == 1, "conv_dgrad_bn: act must be none or ReLU");
+  for (const Tensor* t : {&scale, &shift, &mean, &invstd}) {
+    CHECK_DEV(*t);
+    CHECK_F32(*t);
+    CHECK_CONTIG(*t);
+    TORCH_CHECK(t->numel() == C, "conv_dgrad_bn: per-channel vector size");
+  }
+  auto dx = at::empty({N, H, W, C}, bf16_like(dy));
+  const bf16* addp = nullptr;
+  if (add.has_value()) {
+    CHECK_ACT(*add);
+    TORCH_CHECK(add->sizes() == dx.sizes(), "conv_dgrad_bn add shape");
+    addp = bp(*add);
+  }
+  const bf16* resp = nullptr;
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == dx.sizes(), "conv_dgrad_bn residual shape");
+    resp = bp(*res);
+  }
+  const int M = N * H * W;
+  const int ntm = (M + 127) / 128;
+  auto part = at::empty({ntm, 2, C}, f32_like(dy));
+  auto sums = at::empty({2, C}, f32_like(dy));
+  dcp::TapList t;
+  t.n = KH * KW;
+  TORCH_CHECK(t.n <= dcp::kMaxTaps, "kernel too large");
+  for (int kh = 0; kh < KH; ++kh)
+    for (int kw = 0; kw < KW; ++kw) {
+      const int i = kh * KW + kw;
+      t.dy[i] = pad - kh;
+      t.dx[i] = pad - kw;
+      t.widx[i] = i;
+    }
+  dcp::BnBwdEpi e{bp(y), resp, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act};
+  auto st = cur_stream();
+  dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr, nullptr,
+                       0, zero_page(dy.get_device()), st, addp, &e);
+  dcp::launch_partial_sum(part.data_ptr<float>(), ntm, 2 * C, sums.data_ptr<float>(), st);
+  return {dx, sums};
+}
+
 // dy [N,Ho,Wo,Co], x [N,H,W,C] -> dw fp32 [Co,KH,KW,C]
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
   CHECK_ACT(dy);
@@ -735,6 +794,10 @@ TORCH_LIBRARY(dcp, m) {
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);
+  m.def(
+      "conv_dgrad_bn(Tensor dy, Tensor wt, int pad, Tensor? add, Tensor y, Tensor? res, Tensor scale, Tensor shift, "
+      "Tensor mean, Tensor invstd, int act) -> (Tensor, Tensor)",
+      &conv_dgrad_bn);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, int act) -> Tensor", &linear_fwd);
   m.def("linear_wgrad(Tensor dy, Tensor x) -> Tensor", &linear_wgrad);

@@ -513,6 +513,10 @@ void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* par
   }
 }
 
+void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
+}
+
 int colsum_partials(int M) {
   int g = (M + 255) / 256;
   return g > 128 ? 128 : (g < 1 ? 1 : g);

@@ -59,6 +59,9 @@ struct TapGemmParams {
   int tap[kMaxTaps];
   int ablate;  // tuning experiments only: 1 = no staging in the k-loop, 2 = no MFMA
   int cvar;    // tuning experiments only: compute-loop variant
+  // EPI 3 (stride-1 dgrad): backward of the BN(+ReLU)(+residual) layer that produced this
+  // conv's input, fused into the epilogue (see launchers.h BnBwdEpi)
+  BnBwdEpi bnb;
 };
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
@@ -340,6 +343,84 @@ tap_gemm_kernel(const TapGemmParams p) {
       compute(As, As + A_BYTES);
     }
     __syncthreads();
+  }
+
+  if constexpr (EPI == 3) {
+    // ---- dgrad + fused BN backward (stride 1: dst rows == GEMM rows) ----
+    constexpr int RB = BN * 2, NCH = BN / 8, R = 256 / NCH;
+    char* E = smem;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+        *LDS_PTR(bf16x4, E + off) = o;
+      }
+    }
+    __syncthreads();
+    const int c = tid % NCH, pr0 = tid / NCH;
+    const int cg = n0 + c * 8;
+    const bool cok = cg < p.Co;
+    float sc[8], sh[8], mu[8], s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      sc[e] = cok ? p.bnb.scale[cg + e] : 0.f;
+      sh[e] = cok ? p.bnb.shift[cg + e] : 0.f;
+      mu[e] = cok ? p.bnb.mean[cg + e] : 0.f;
+    }
+#pragma unroll 2
+    for (int k = 0; k < BM / R; ++k) {
+      const int pl = pr0 + k * R;
+      const int m = m0 + pl;
+      if (m < p.M && cok) {
+        const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+        const size_t off = (size_t)m * p.Co + cg;
+        const bf16x8 yv = *(const bf16x8*)(p.bnb.y + off);
+        bf16x8 a, rv;
+        if (p.addsrc) a = *(const bf16x8*)(p.addsrc + off);
+        if (p.bnb.res) rv = *(const bf16x8*)(p.bnb.res + off);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float g = bf2f(v[e]);
+          if (p.addsrc) g = bf2f(f2bf(g + bf2f(a[e])));  // the rounding of the unfused add
+          const float yf = bf2f(yv[e]);
+          float z = yf * sc[e] + sh[e];
+          if (p.bnb.res) z += bf2f(rv[e]);
+          if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
+          o[e] = f2bf(g);
+          const float gr = bf2f(o[e]);
+          s1[e] += gr;
+          s2[e] += gr * (yf - mu[e]);
+        }
+        *(bf16x8*)(p.dst + off) = o;
+      }
+    }
+    // per-tile channel sums: fixed-order reduction over the R row groups (deterministic)
+    float* red = (float*)(smem + BM * RB);  // [2][R][BN]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(0 * R + pr0) * BN + c * 8 + e] = s1[e];
+      red[(1 * R + pr0) * BN + c * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int which = tid / BN, ch = tid - which * BN;
+      if (n0 + ch < p.Co) {
+        float t = 0.f;
+#pragma unroll 4
+        for (int r = 0; r < R; ++r) t += red[(which * R + r) * BN + ch];
+        if (which) t *= p.bnb.invstd[n0 + ch];
+        p.bnb.part[((size_t)tm * 2 + which) * p.Co + n0 + ch] = t;
+      }
+    }
+    return;
   }
 
   if constexpr (EPI != 2) {
@@ -918,9 +999,10 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                      const TapList& taps, float* stats, const float* bias, int relu,
-                     const bf16* zero, hipStream_t stream, const bf16* addsrc) {
+                     const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb) {
   TapGemmParams p;
   p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
+  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
   p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;
@@ -933,7 +1015,14 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     p.tap[i] = (taps.dy[i] & 0xff) | ((taps.dx[i] & 0xff) << 8) | ((taps.widx[i] & 0xffff) << 16);
   if (p.M == 0) return;
   const int ntm = (p.M + 127) / 128;
-  const int epi = (bias != nullptr || relu != 0) ? 2 : (stats != nullptr ? 1 : 0);
+  int epi = (bias != nullptr || relu != 0) ? 2 : (stats != nullptr ? 1 : 0);
+  if (bnb != nullptr) {
+    if (ds != 1 || Hd != Hy || Wd != Wy || stats != nullptr || bias != nullptr || relu != 0) {
+      fprintf(stderr, "launch_tap_gemm: fused BN backward needs a plain stride-1 dgrad\n");
+      abort();
+    }
+    epi = 3;
+  }
   const bool fast = (p.cpt & 7) == 0;
   // config: BN (64/128 output channels per tile) and NS (LDS stages); g_tune overrides the
   // heuristic (tuning experiments only)
@@ -945,7 +1034,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   if (env_ns > 0 && fast) ns = env_ns;
   if (!fast) ns = 2;
   const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
-  if (fast && Co >= 128 && epi != 2 && use8) {
+  if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
     constexpr size_t lds8 = 3 * (256 + 128) * 128;
     static bool attr8 = false;
@@ -966,6 +1055,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
 #define DCP_TG_EPI(BN_, FAST_)                     \
   if (epi == 0) { DCP_TG_NS(BN_, 0, FAST_) }       \
   else if (epi == 1) { DCP_TG_NS(BN_, 1, FAST_) }  \
+  else if (epi == 3) { DCP_TG_NS(BN_, 3, FAST_) }  \
   else { DCP_TG_NS(BN_, 2, FAST_) }
   if (bn == 64) {
     if (fast) { DCP_TG_EPI(64, true) } else { DCP_TG_EPI(64, false) }

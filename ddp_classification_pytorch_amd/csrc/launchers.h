@@ -19,9 +19,27 @@ struct TapList {
   int dy[kMaxTaps], dx[kMaxTaps], widx[kMaxTaps];
 };
 
+// Backward of a training-mode BN + ReLU/identity (+ residual add) fused into the epilogue of
+// the stride-1 dgrad that produces the gradient g of the BN layer's OUTPUT:
+//   dst = g' = g * act'(y*scale + shift [+ res])   (the activation-masked gradient)
+//   part[tile][0][c] = sum g',  part[tile][1][c] = sum g' * (y - mean) * invstd  (per 128-row tile)
+// so the separate BN backward reduction pass (re-reading g and y) disappears.
+struct BnBwdEpi {
+  const bf16* y;        // BN input [M][C]
+  const bf16* res;      // residual added before the activation, or nullptr
+  const float* scale;   // gamma * invstd
+  const float* shift;   // beta - mean * scale
+  const float* mean;
+  const float* invstd;
+  float* part;          // [ceil(M/128)][2][C]
+  int act;              // 0 none, 1 ReLU
+};
+
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
-                     const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr);
+                     const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,
+                     const BnBwdEpi* bnb = nullptr);
+void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s);
 // partial-slab split-K weight gradient: dw is fully written when part != nullptr
 // (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split);

@@ -36,11 +36,13 @@ class Conv2d(nn.Module):
         fan_out = self.out_channels * self.kernel_size * self.kernel_size // self.groups
         nn.init.normal_(self.weight, 0.0, math.sqrt(2.0 / fan_out))
 
-    def forward(self, x, stats=False, link=None):
-        """Returns (y, bn_stat_slabs_or_None).  `link`: residual-gradient hand-off (ops.functional.ResidualLink)."""
+    def forward(self, x, stats=False, link=None, deposit=None):
+        """Returns (y, bn_stat_slabs_or_None).  `link` / `deposit`: block-input gradient
+        hand-off as primary / secondary consumer (ops.functional.GradJoin)."""
         if self.groups > 1:
-            return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding), None
-        y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda, link)
+            y = Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding)
+            return y, None
+        y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda, link, deposit)
         return y, (slabs if stats and x.is_cuda else None)
 
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):

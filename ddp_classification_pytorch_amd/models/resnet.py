@@ -40,16 +40,17 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         t = _train_stats(self.bn1)
-        link = Fn.ResidualLink() if self.downsample is None else None
-        y, s = self.conv1(x, stats=t, link=link)
+        # the block input's second consumer (residual add / downsample conv) hands its
+        # gradient to conv1, which sums it in its dgrad epilogue (strided conv1: no join)
+        join = Fn.GradJoin(1) if self.conv1.stride == 1 else None
+        y, s = self.conv1(x, stats=t, link=join)
         y = self.bn1(y, s, act="relu")
         y, s = self.conv2(y, stats=t)
         if self.downsample is not None:
-            r, rs = self.downsample[0](x, stats=t)
+            r, rs = self.downsample[0](x, stats=t, deposit=join)
             r = self.downsample[1](r, rs, act="none")
-        else:
-            r = x
-        return self.bn2(y, s, act="relu", residual=r, link=link)
+            return self.bn2(y, s, act="relu", residual=r)
+        return self.bn2(y, s, act="relu", residual=x, link=join)
 
 
 class Bottleneck(nn.Module):
@@ -68,19 +69,21 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         t = _train_stats(self.bn1)
-        # identity blocks: the residual gradient is summed in conv1's dgrad epilogue
-        link = Fn.ResidualLink() if self.downsample is None else None
-        y, s = self.conv1(x, stats=t, link=link)
+        # the block input's second consumer (the residual add of an identity block, the
+        # downsample conv of a projection block) hands its gradient to conv1, which sums it
+        # in its dgrad epilogue -- fused there with the backward of the BN that produced x.
+        # The downsample branch runs after conv3 so its backward precedes conv1's.
+        join = Fn.GradJoin(1)
+        y, s = self.conv1(x, stats=t, link=join)
         y = self.bn1(y, s, act="relu")
         y, s = self.conv2(y, stats=t)
         y = self.bn2(y, s, act="relu")
         y, s = self.conv3(y, stats=t)
         if self.downsample is not None:
-            r, rs = self.downsample[0](x, stats=t)
+            r, rs = self.downsample[0](x, stats=t, deposit=join)
             r = self.downsample[1](r, rs, act="none")
-        else:
-            r = x
-        return self.bn3(y, s, act="relu", residual=r, link=link)
+            return self.bn3(y, s, act="relu", residual=r)
+        return self.bn3(y, s, act="relu", residual=x, link=join)
 
 
 class ResNet(nn.Module):

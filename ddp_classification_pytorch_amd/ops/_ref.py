@@ -60,6 +60,19 @@ def conv_dgrad(dy, wt, H, W, stride, pad, add=None):
     return dx.to(dy.dtype)
 
 
+def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act):
+    """Stride-1 dgrad + the backward reduction of the BN(+act)(+res) layer producing its input:
+    -> (activation-masked gradient g', [2, C] = (sum g', sum g' * xhat))."""
+    g = conv_dgrad(dy, wt, y.shape[1], y.shape[2], 1, pad, add)
+    z = _f(y) * scale + shift
+    if res is not None:
+        z = z + _f(res)
+    gm = (_f(g) * _act_d(z, act, 0.0)).to(dy.dtype)
+    xh = (_rows(y) - mean) * invstd
+    gr = _rows(gm)
+    return gm, torch.stack([gr.sum(0), (gr * xh).sum(0)])
+
+
 def conv_wgrad(dy, x, KH, KW, stride, pad):
     Co, C = dy.shape[3], x.shape[3]
     dw = torch.nn.grad.conv2d_weight(_nchw(_f(x)), (Co, C, KH, KW), _nchw(_f(dy)), stride=stride, padding=pad)

@@ -153,27 +153,77 @@ _MT = _MTWeightCache()
 
 
 # ----------------------------------------------------------------------------- convolution
-class ResidualLink:
-    """Hands the identity-path gradient of a residual block from the block's last
-    BN+add+ReLU backward to the backward of the block's FIRST conv, which adds it in
-    its dgrad epilogue (one fused pass instead of a separate bf16 add kernel over the
-    block-input gradient).  Only for blocks whose residual is the raw block input.
-    Autograd order guarantees the BN backward runs first (the first conv's output
-    gradient depends on it)."""
+class GradJoin:
+    """Gradient hand-off for a block input consumed by several ops.
 
-    __slots__ = ("grad",)
+    The ``secondaries`` other consumers (an identity block's last BN+add+ReLU backward,
+    a projection block's downsample-conv dgrad) *deposit* their gradient here instead
+    of returning it to autograd; the block's first conv (the primary consumer) *claims*
+    the sum and adds it in its dgrad epilogue -- no separate bf16 add kernel over the
+    block-input gradient.  A deposit that arrives after the claim is handed back to
+    autograd unchanged, so every backward order stays correct; the primary fuses the
+    producer BN's backward (see :class:`BNSource`) only when all secondaries arrived.
+    """
 
-    def __init__(self):
-        self.grad = None
+    __slots__ = ("grad", "expected", "arrived", "closed")
+
+    def __init__(self, secondaries: int = 1):
+        self.grad, self.expected, self.arrived, self.closed = None, secondaries, 0, False
+
+    def deposit(self, g):
+        if self.closed or g is None:
+            return g
+        self.grad = g if self.grad is None else self.grad + g
+        self.arrived += 1
+        return None
+
+    def claim(self):
+        self.closed = True
+        g, self.grad = self.grad, None
+        return g, self.arrived >= self.expected
+
+
+ResidualLink = GradJoin  # identity-block residual hand-off (one secondary: the last BN's residual)
+
+
+class BNSource:
+    """Attached (as ``_dcp_bnsrc``) to the output z of a training-mode BN(+ReLU)(+residual)
+    layer so that the stride-1 conv consuming z can run that layer's backward reduction in
+    its dgrad epilogue (``conv_dgrad_bn``): the epilogue emits the activation-masked
+    gradient and the per-channel (sum g', sum g' xhat), and the BN backward is left with
+    one elementwise pass -- no separate reduction pass re-reading the gradient and the BN
+    input.  ``fused`` keeps a reference to the masked gradient, which also stops autograd
+    from accumulating another consumer's gradient into that buffer in place; the BN
+    backward uses the fused result only if it receives exactly that buffer."""
+
+    __slots__ = ("tensors", "act", "fused")
+
+    def __init__(self, act: int):
+        self.tensors, self.act, self.fused = None, act, None
+
+    def release(self):
+        self.tensors = self.fused = None
+
+
+_FUSE_BN_BWD = [True]
+
+
+def set_bn_backward_fusion(enabled: bool):
+    """Toggle the dgrad-epilogue BN backward (A/B tests; default on)."""
+    _FUSE_BN_BWD[0] = bool(enabled)
+
+
+def bn_source(x):
+    return getattr(x, "_dcp_bnsrc", None)
 
 
 class _Conv2d(Function):
     @staticmethod
-    def forward(ctx, x, weight, wb, wt, stride, pad, stats, link):
+    def forward(ctx, x, weight, wb, wt, stride, pad, stats, link, bnsrc, deposit):
         y, slabs = K(x).conv_fwd(x, wb, stride, pad, stats)
         ctx.save_for_backward(x, wt)
         ctx.geo = (weight.shape[1], weight.shape[2], stride, pad)
-        ctx.link = link
+        ctx.link, ctx.bnsrc, ctx.deposit = link, bnsrc, deposit
         ctx.mark_non_differentiable(slabs)
         return y, slabs
 
@@ -183,30 +233,45 @@ class _Conv2d(Function):
         KH, KW, stride, pad = ctx.geo
         dy = dy.contiguous()
         k = K(dy)
-        add = None
+        add, complete = None, True
         if ctx.link is not None:
-            add, ctx.link.grad = ctx.link.grad, None
+            add, complete = ctx.link.claim()
+            if add is not None:
+                add = add.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if add is not None:
-                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add.contiguous())
+            src = ctx.bnsrc
+            if src is not None and complete and stride == 1 and src.tensors is not None:
+                y, res, scale, shift, mean, invstd = src.tensors
+                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act)
+                src.fused = (dx, sums)
+            elif add is not None:
+                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add)
             else:
                 dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
+            if ctx.deposit is not None:
+                dx = ctx.deposit.deposit(dx)
         if ctx.needs_input_grad[1]:
             dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
-        return dx, dw, None, None, None, None, None, None
+        ctx.link = ctx.bnsrc = ctx.deposit = None
+        return dx, dw, None, None, None, None, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
-           link: "ResidualLink | None" = None):
+           link: "GradJoin | None" = None, deposit: "GradJoin | None" = None):
     """NHWC conv; returns (y, bn_stat_slabs).  weight: fp32 [Co,KH,KW,Ci].
-    `link`: the block's ResidualLink when this is the first conv of a residual block."""
+
+    `link`: the block's GradJoin when this conv is the primary consumer of the block input
+    (its dgrad epilogue adds the other consumers' gradient); `deposit`: the GradJoin this
+    conv's input gradient is handed to (secondary consumer, e.g. a downsample conv).
+    A stride-1 conv whose input carries a BNSource fuses that BN's backward reduction."""
+    bnsrc = bn_source(x) if (stride == 1 and deposit is None and _FUSE_BN_BWD[0]) else None
     if weight.shape[3] != x.shape[3]:  # stem: input channels zero-padded to a multiple of 8
         wb, wt = prepared_weight(weight, 0, True, ci=x.shape[3])
         weight = F.pad(weight, (0, x.shape[3] - weight.shape[3]))  # autograd view for the padded dW
-        return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link)
+        return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link, None, deposit)
     wb, wt = prepared_weight(weight, 0, True)
-    return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link)
+    return _Conv2d.apply(x, weight, wb, wt, stride, pad, stats, link, bnsrc, deposit)
 
 
 class _GroupedConv2d(Function):
@@ -297,7 +362,7 @@ class BNConfig:
 
 class _BNAct(Function):
     @staticmethod
-    def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig, link):
+    def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig, link, src):
         k = K(x)
         C = x.shape[-1]
         count = x.numel() // C
@@ -317,6 +382,9 @@ class _BNAct(Function):
         ctx.count = count
         ctx.has_res = res is not None
         ctx.link = link
+        ctx.src = src
+        if src is not None:
+            src.tensors = (x, res, scale, shift, mean, invstd)
         return y
 
     @staticmethod
@@ -325,24 +393,41 @@ class _BNAct(Function):
         cfg = ctx.cfg
         dy = dy.contiguous()
         k = K(dy)
-        need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        sums = None
-        local = None
-        if cfg.training_stats or need_affine:
-            local = k.bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, cfg.act, cfg.slope)
+        src, ctx.src = ctx.src, None
+        fused = src.fused if src is not None else None
+        if src is not None:
+            src.release()
+        want_dres = ctx.has_res and ctx.needs_input_grad[4]
+        if fused is not None and fused[0].data_ptr() == dy.data_ptr() and fused[0].shape == dy.shape:
+            # the consuming conv's dgrad epilogue already masked the gradient and reduced it
+            g, local = fused
             sums = local
-            if cfg.training_stats and cfg.group is not None:
+            if cfg.group is not None:
                 sums = local.clone()
                 dist.all_reduce(sums, group=cfg.group)
-        want_dres = ctx.has_res and ctx.needs_input_grad[4]
-        dx, dres = k.bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums if cfg.training_stats else None,
-                                  float(ctx.count), cfg.act, cfg.slope, want_dres)
+            dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
+                                   False)
+            dres = g if want_dres else None
+        else:
+            need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+            sums = None
+            local = None
+            if cfg.training_stats or need_affine:
+                local = k.bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, cfg.act, cfg.slope)
+                sums = local
+                if cfg.training_stats and cfg.group is not None:
+                    sums = local.clone()
+                    dist.all_reduce(sums, group=cfg.group)
+            dx, dres = k.bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums if cfg.training_stats else None,
+                                      float(ctx.count), cfg.act, cfg.slope, want_dres)
+            if not want_dres:
+                dres = None
         dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
         dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
-        if want_dres and ctx.link is not None:
-            ctx.link.grad = dres  # summed into the block input gradient by the first conv's dgrad
-            want_dres = False
-        return dx, None, dgamma, dbeta, (dres if want_dres else None), None, None, None, None
+        if dres is not None and ctx.link is not None:
+            dres = ctx.link.deposit(dres)  # summed into the block input gradient by the first conv's dgrad
+        ctx.link = None
+        return dx, None, dgamma, dbeta, dres, None, None, None, None, None
 
 
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
@@ -351,7 +436,15 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
     if slabs is None or (slabs.numel() == 0):
         slabs = None
-    return _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link)
+    # ReLU / identity only: their masks are idempotent, so a consumer that masked the
+    # gradient early composes with any unfused fallback
+    src = None
+    if training_stats and cfg.act in (0, 1) and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
+        src = BNSource(cfg.act)
+    out = _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link, src)
+    if src is not None:
+        out._dcp_bnsrc = src
+    return out
 
 
 # ----------------------------------------------------------------------------- pooling

@@ -1,0 +1,110 @@
+"""Backward fusion protocol (CPU reference math): the stride-1 conv consuming a BN output
+runs that BN's backward reduction in its dgrad epilogue (BNSource), and a block input's
+secondary consumers hand their gradient to the primary conv (GradJoin).  Gradients must
+equal the unfused path, and every backward order of the join must stay correct."""
+import pytest
+import torch
+
+from ddp_classification_pytorch_amd.models import build_model
+from ddp_classification_pytorch_amd.ops import _ref
+from ddp_classification_pytorch_amd.ops import functional as Fn
+
+
+def _grads(name, fuse, size=32, seed=0):
+    Fn.set_bn_backward_fusion(fuse)
+    try:
+        torch.manual_seed(seed)
+        m = build_model(name, num_classes=10)
+        g = torch.Generator().manual_seed(1)
+        imgs = torch.rand(4, 3, size, size, generator=g, dtype=torch.float32)
+        labels = torch.randint(0, 10, (4,), generator=g)
+        x = Fn.to_device_nhwc(imgs, cpad=8, nchw=True)
+        loss = Fn.cross_entropy(m(x), labels)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.flatten() for p in m.parameters()])
+    finally:
+        Fn.set_bn_backward_fusion(True)
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50", "resnext50_32x4d"])
+def test_fused_bn_backward_matches_unfused(name, monkeypatch):
+    calls = []
+    orig = _ref.conv_dgrad_bn
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(_ref, "conv_dgrad_bn", counting)
+    l1, g1 = _grads(name, True)
+    n_fused = len(calls)
+    l0, g0 = _grads(name, False)
+    assert len(calls) == n_fused  # nothing fused with the switch off
+    assert n_fused > 0
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+
+
+def test_resnet50_fuses_expected_layers(monkeypatch):
+    calls = []
+    orig = _ref.conv_dgrad_bn
+    monkeypatch.setattr(_ref, "conv_dgrad_bn", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    _grads("resnet50", True)
+    # conv2 of the 13 stride-1 blocks, conv3 of all 16, conv1 of the 15 blocks after the first
+    assert len(calls) == 13 + 16 + 15
+
+
+class _Probe(torch.autograd.Function):
+    """Identity whose backward deposits into a GradJoin (a secondary consumer)."""
+
+    @staticmethod
+    def forward(ctx, x, join):
+        ctx.join = join
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.join.deposit(g * 3.0), None
+
+
+@pytest.mark.parametrize("late", [False, True])
+def test_gradjoin_any_order(late):
+    """Deposit before the claim: summed by the primary.  Deposit after the claim: handed
+    back to autograd unchanged."""
+    x = torch.randn(8, requires_grad=True)
+    j = Fn.GradJoin(1)
+    if late:
+        j.claim()  # the primary already ran
+        out = (_Probe.apply(x, j)).sum()
+        out.backward()
+        assert torch.allclose(x.grad, torch.full_like(x, 3.0))
+    else:
+        assert j.deposit(torch.ones(8)) is None
+        add, complete = j.claim()
+        assert complete and torch.equal(add, torch.ones(8))
+        assert j.deposit(torch.ones(8)) is not None  # after the claim: returned unchanged
+
+
+def test_unfused_fallback_when_conv_output_shared():
+    """A BN output consumed by a fusing conv AND another op: the BN backward receives the
+    autograd sum (not the fused buffer) and must take the unfused path -- still exact."""
+    torch.manual_seed(0)
+    from ddp_classification_pytorch_amd.models.layers import BatchNorm2d, Conv2d
+
+    def run(fuse):
+        Fn.set_bn_backward_fusion(fuse)
+        try:
+            torch.manual_seed(0)
+            conv0, bn, conv1 = Conv2d(8, 16, 3, 1, 1), BatchNorm2d(16), Conv2d(16, 16, 1)
+            x = torch.randn(2, 6, 6, 8)
+            y, s = conv0(x)
+            z = bn(y, s, act="relu")
+            out, _ = conv1(z)
+            loss = (out * out).sum() + (z * 0.5).sum()  # second consumer of z
+            loss.backward()
+            return torch.cat([p.grad.flatten() for p in (conv0.weight, bn.weight, bn.bias, conv1.weight)])
+        finally:
+            Fn.set_bn_backward_fusion(True)
+
+    g1, g0 = run(True), run(False)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5

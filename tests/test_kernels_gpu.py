@@ -322,6 +322,41 @@ def test_conv_dgrad_fused_add(K, Ci, Co, k, s):
     assert relerr(dx, ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,Ci,Co,k,add,res,act", [
+    (2, 14, 256, 64, 1, True, True, 1),     # conv1 of an identity block: join add + residual BN3
+    (2, 14, 64, 64, 3, False, False, 1),    # conv2 (3x3 s1) consuming BN1 (BN=64 tile)
+    (2, 14, 128, 512, 1, False, False, 1),  # conv3 consuming BN2, 128-channel tiles
+    (3, 9, 72, 40, 3, True, False, 0),      # ragged M / channels, identity activation
+    (8, 7, 512, 2048, 1, False, True, 1),   # layer4: M = 392 (not a multiple of 128)
+])
+def test_conv_dgrad_bn_fused(K, N, H, Ci, Co, k, add, res, act):
+    """dgrad epilogue fused with the BN(+ReLU)(+residual) backward reduction: the masked
+    gradient and the per-channel (sum g', sum g' xhat) against the fp32 reference."""
+    torch.manual_seed(0)
+    p = k // 2
+    w = torch.randn(Co, k, k, Ci) / (k * k * Ci) ** 0.5
+    _, wt = K.weight_prep(w.to(DEV), 0, True)
+    dy = rnd(N, H, H, Co)
+    y = rnd(N, H, H, Ci, scale=2.0) + 0.5
+    a = rnd(N, H, H, Ci) if add else None
+    r = rnd(N, H, H, Ci) if res else None
+    scale = torch.rand(Ci) + 0.5
+    shift = torch.randn(Ci) * 0.3
+    mean = torch.randn(Ci) * 0.2 + 0.5
+    invstd = torch.rand(Ci) + 0.5
+    d = lambda t: None if t is None else t.to(DEV)
+    g, sums = K.conv_dgrad_bn(dy.to(DEV), wt, p, d(a), y.to(DEV), d(r), scale.to(DEV), shift.to(DEV),
+                              mean.to(DEV), invstd.to(DEV), act)
+    wtr = _ref.weight_prep(w.bfloat16().float(), 0, True)[1]
+    rg, rsums = _ref.conv_dgrad_bn(dy.float(), wtr, p, None if a is None else a.float(), y.float(),
+                                   None if r is None else r.float(), scale, shift, mean, invstd, act)
+    assert relerr(g, rg) < 1e-2
+    # masks can flip where the reference's z sits on 0; the sums are judged loosely but tightly
+    # enough to catch a missing row, channel or tile
+    assert relerr(sums[0], rsums[0]) < 2e-2
+    assert relerr(sums[1], rsums[1]) < 2e-2
+
+
 @pytest.mark.parametrize("N,H,W,C,G,KH,stride,pad", [
     (2, 14, 14, 128, 32, 3, 1, 1),   # CG=4  (super-group 16, 4 groups block-diagonal)
     (3, 13, 11, 256, 32, 3, 2, 1),   # CG=8, odd spatial, stride 2, M not a multiple of 256
