@@ -202,7 +202,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   }
   const int M = N * H * W;
   const int ntm = (M + 127) / 128;
-  auto part = at::empty({ntm, 2, C}, f32_like(dy));
+  // per-tile partials + room for the chunk sums of the two-level deterministic reduce
+  auto part = at::empty({(int64_t)(ntm + (ntm + 63) / 64) * 2 * C}, f32_like(dy));
   auto sums = at::empty({2, C}, f32_like(dy));
   dcp::TapList t;
   t.n = KH * KW;
@@ -219,7 +220,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   auto st = cur_stream();
   dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr, nullptr,
                        0, zero_page(dy.get_device()), st, addp, &e);
-  dcp::launch_partial_sum(part.data_ptr<float>(), ntm, 2 * C, sums.data_ptr<float>(), st);
+  dcp::launch_split_reduce(part.data_ptr<float>(), ntm, 2 * C, sums.data_ptr<float>(), st);
   return {dx, sums};
 }
 

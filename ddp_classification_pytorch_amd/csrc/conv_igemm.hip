@@ -347,25 +347,16 @@ tap_gemm_kernel(const TapGemmParams p) {
 
   if constexpr (EPI == 3) {
     // ---- dgrad + fused BN backward (stride 1: dst rows == GEMM rows) ----
-    constexpr int RB = BN * 2, NCH = BN / 8, R = 256 / NCH;
+    constexpr int RB = BN * 2, NCH = BN / 8, R = 256 / NCH, RPT = BM / R;
     char* E = smem;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
-        *LDS_PTR(bf16x4, E + off) = o;
-      }
-    }
-    __syncthreads();
     const int c = tid % NCH, pr0 = tid / NCH;
     const int cg = n0 + c * 8;
     const bool cok = cg < p.Co;
+    // The HBM-bound part is this thread's BN-input / residual / add-source rows: they are
+    // loaded in batches of RB_ rows, the first batch in flight while the accumulators go
+    // through LDS.  (Batches keep VGPR + AGPR <= 256: two waves per SIMD.)
+    constexpr int RBATCH = RPT >= 4 ? 4 : RPT;
+    const bool has_res = p.bnb.res != nullptr, has_add = p.addsrc != nullptr;
     float sc[8], sh[8], mu[8], s1[8], s2[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -374,32 +365,56 @@ tap_gemm_kernel(const TapGemmParams p) {
       sh[e] = cok ? p.bnb.shift[cg + e] : 0.f;
       mu[e] = cok ? p.bnb.mean[cg + e] : 0.f;
     }
-#pragma unroll 2
-    for (int k = 0; k < BM / R; ++k) {
-      const int pl = pr0 + k * R;
-      const int m = m0 + pl;
-      if (m < p.M && cok) {
-        const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
-        const size_t off = (size_t)m * p.Co + cg;
-        const bf16x8 yv = *(const bf16x8*)(p.bnb.y + off);
-        bf16x8 a, rv;
-        if (p.addsrc) a = *(const bf16x8*)(p.addsrc + off);
-        if (p.bnb.res) rv = *(const bf16x8*)(p.bnb.res + off);
-        bf16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float g = bf2f(v[e]);
-          if (p.addsrc) g = bf2f(f2bf(g + bf2f(a[e])));  // the rounding of the unfused add
-          const float yf = bf2f(yv[e]);
-          float z = yf * sc[e] + sh[e];
-          if (p.bnb.res) z += bf2f(rv[e]);
-          if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
-          o[e] = f2bf(g);
-          const float gr = bf2f(o[e]);
-          s1[e] += gr;
-          s2[e] += gr * (yf - mu[e]);
+    for (int b = 0; b < RPT / RBATCH; ++b) {
+      bf16x8 yv[RBATCH], rv[RBATCH], av[RBATCH];
+#pragma unroll
+      for (int q = 0; q < RBATCH; ++q) {
+        const int m = m0 + pr0 + (b * RBATCH + q) * R;
+        const bool ok = m < p.M && cok;
+        const size_t off = (size_t)(ok ? m : 0) * p.Co + (cok ? cg : 0);
+        yv[q] = ok ? *(const bf16x8*)(p.bnb.y + off) : bf16x8{};
+        if (has_res) rv[q] = ok ? *(const bf16x8*)(p.bnb.res + off) : bf16x8{};
+        if (has_add) av[q] = ok ? *(const bf16x8*)(p.addsrc + off) : bf16x8{};
+      }
+      if (b == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+            const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+            *LDS_PTR(bf16x4, E + off) = o;
+          }
         }
-        *(bf16x8*)(p.dst + off) = o;
+        __syncthreads();
+      }
+#pragma unroll
+      for (int q = 0; q < RBATCH; ++q) {
+        const int pl = pr0 + (b * RBATCH + q) * R;
+        const int m = m0 + pl;
+        if (m < p.M && cok) {
+          const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float g = bf2f(v[e]);
+            if (has_add) g = bf2f(f2bf(g + bf2f(av[q][e])));  // the rounding of the unfused add
+            const float yf = bf2f(yv[q][e]);
+            float z = yf * sc[e] + sh[e];
+            if (has_res) z += bf2f(rv[q][e]);
+            if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
+            o[e] = f2bf(g);
+            const float gr = bf2f(o[e]);
+            s1[e] += gr;
+            s2[e] += gr * (yf - mu[e]);
+          }
+          *(bf16x8*)(p.dst + (size_t)m * p.Co + cg) = o;
+        }
       }
     }
     // per-tile channel sums: fixed-order reduction over the R row groups (deterministic)
