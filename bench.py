@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from ddp_classification_pytorch_amd import _ext  # noqa: E402
-from ddp_classification_pytorch_amd.models import build_model  # noqa: E402
+from ddp_classification_pytorch_amd.models import build_model, input_layout  # noqa: E402
 from ddp_classification_pytorch_amd.ops import functional as Fn  # noqa: E402
 from ddp_classification_pytorch_amd.optim import FusedSGD  # noqa: E402
 from ddp_classification_pytorch_amd.parallel import ddp as pddp  # noqa: E402
@@ -127,10 +127,10 @@ def main(argv=None):
     mean = torch.tensor(IMAGENET_MEAN, device=dev)
     std = torch.tensor(IMAGENET_STD, device=dev)
 
-    cpad = 3 if a.model.startswith("tresnet") else 8
+    layout = input_layout(model)  # e.g. ResNets: 2x2 space-to-depth input of the s2d stem
 
     def step():
-        x = Fn.to_device_nhwc(images, mean, std, cpad=cpad, nchw=True, in_scale=1.0 / 255.0)
+        x = Fn.to_device_nhwc(images, mean, std, nchw=True, in_scale=1.0 / 255.0, **layout)
         if a.config == "arcface":
             loss, _ = model(x, labels)
         else:

@@ -106,6 +106,27 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
   return {y, slabs};
 }
 
+// forward with an explicit output grid (asymmetric padding: output (oy, ox) reads input rows
+// oy*stride + kh - pad, columns ox*stride + kw - pad; out-of-range taps read zeros)
+std::tuple<Tensor, Tensor> conv_fwd_geo(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad, int64_t Ho,
+                                        int64_t Wo, bool stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(3) == x.size(3), "conv_fwd_geo shapes");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0 && KH * KW <= dcp::kMaxTaps && pad >= 0 && pad < 64, "conv_fwd_geo geometry");
+  TORCH_CHECK(Ho > 0 && Wo > 0 && (Ho - 1) * stride - pad < H && (Wo - 1) * stride - pad < W, "conv_fwd_geo grid");
+  auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
+  const int M = N * Ho * Wo;
+  Tensor slabs = stats ? at::empty({(M + 127) / 128, 2, Co}, f32_like(x)) : at::empty({0}, f32_like(x));
+  const auto taps = fwd_taps(KH, KW, pad);
+  dcp::launch_tap_gemm(bp(x), N, H, W, C, bp(w), Co, KH * KW, bpm(y), Ho, Wo, Ho, Wo, stride, 1, 0, 0, taps,
+                       stats ? slabs.data_ptr<float>() : nullptr, nullptr, 0, zero_page(x.get_device()),
+                       cur_stream());
+  return {y, slabs};
+}
+
 // dy [N,Ho,Wo,Co], wt [C,KH,KW,Co] (transposed weight) -> dx [N,H,W,C]
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   const optional<Tensor>& add) {
@@ -233,6 +254,25 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   TORCH_CHECK(x.size(0) == N, "batch mismatch");
   TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_wgrad needs channel multiples of 8");
   TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "wgrad geometry");
+  auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
+  const auto taps = fwd_taps(KH, KW, pad);
+  const int ncu = num_cus(dy.get_device());
+  const int splits = dcp::wgrad_splits(N * Ho * Wo, Co, KH * KW * C, KH * KW, ncu, nullptr);
+  auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
+  dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
+                    part.data_ptr<float>(), zero_page(dy.get_device()), ncu, cur_stream());
+  return dw;
+}
+
+// weight gradient for conv_fwd_geo's geometry (output grid taken from dy)
+Tensor conv_wgrad_geo(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(x.size(0) == N && C % 8 == 0 && Co % 8 == 0 && KH * KW <= dcp::kMaxTaps, "conv_wgrad_geo shapes");
+  TORCH_CHECK(pad >= 0 && pad < 64 && (Ho - 1) * stride - pad < H && (Wo - 1) * stride - pad < W,
+              "conv_wgrad_geo grid");
   auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
   const int ncu = num_cus(dy.get_device());
@@ -483,6 +523,72 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& idx, int64_t H, int64_t W, in
   return dx;
 }
 
+static void check_bn_vecs(std::initializer_list<const Tensor*> ts, int C) {
+  for (const Tensor* t : ts) {
+    CHECK_DEV(*t);
+    CHECK_F32(*t);
+    CHECK_CONTIG(*t);
+    TORCH_CHECK(t->numel() == C, "per-channel vector size");
+  }
+}
+
+static bool bn_pool_ok(int C) { return C % 8 == 0 && 256 % (C / 8) == 0; }
+
+// max pool of act(x*scale + shift) (the stem BN-apply + ReLU + pool in one pass) -> (y, argmax)
+std::tuple<Tensor, Tensor> bn_act_maxpool(const Tensor& x, const Tensor& scale, const Tensor& shift, int64_t act,
+                                          int64_t k, int64_t s, int64_t p) {
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(bn_pool_ok(C) && k * k <= 255 && (act == 0 || act == 1), "bn_act_maxpool shapes");
+  check_bn_vecs({&scale, &shift}, C);
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  auto idx = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  dcp::launch_maxpool_fwd(bp(x), bpm(y), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s, p, cur_stream(),
+                          scale.data_ptr<float>(), shift.data_ptr<float>(), (int)act);
+  return {y, idx};
+}
+
+// backward reduction of BN(+act) -> max pool: [2, C] = (sum g', sum g' * xhat)
+Tensor maxpool_bn_bwd_reduce(const Tensor& dy, const Tensor& idx, const Tensor& x, const Tensor& scale,
+                             const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act, int64_t k,
+                             int64_t s, int64_t p) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2);
+  TORCH_CHECK(bn_pool_ok(C) && dy.size(0) == N && dy.size(3) == C && idx.sizes() == dy.sizes(), "maxpool_bn shapes");
+  TORCH_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "maxpool_bn geometry");
+  check_bn_vecs({&scale, &shift, &mean, &invstd}, C);
+  auto part = at::empty({dcp::maxpool_bn_bwd_blocks(), 2, C}, f32_like(x));
+  auto sums = at::empty({2, C}, f32_like(x));
+  dcp::launch_maxpool_bn_bwd(bp(dy), idx.data_ptr<uint8_t>(), bp(x), N, H, W, C, Ho, Wo, k, s, p,
+                             scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                             invstd.data_ptr<float>(), (int)act, part.data_ptr<float>(), sums.data_ptr<float>(),
+                             nullptr, 0.f, nullptr, cur_stream());
+  return sums;
+}
+
+// elementwise pass: dx of the BN input from the pooled gradient and the global sums
+Tensor maxpool_bn_bwd_elemt(const Tensor& dy, const Tensor& idx, const Tensor& x, const Tensor& scale,
+                            const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act,
+                            const Tensor& sums, double count, int64_t k, int64_t s, int64_t p) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Ho = dy.size(1), Wo = dy.size(2);
+  TORCH_CHECK(bn_pool_ok(C) && dy.size(0) == N && dy.size(3) == C && idx.sizes() == dy.sizes(), "maxpool_bn shapes");
+  TORCH_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "maxpool_bn geometry");
+  check_bn_vecs({&scale, &shift, &mean, &invstd}, C);
+  TORCH_CHECK(sums.numel() == 2 * C && sums.is_contiguous(), "sums [2, C]");
+  auto dx = at::empty_like(x);
+  dcp::launch_maxpool_bn_bwd(bp(dy), idx.data_ptr<uint8_t>(), bp(x), N, H, W, C, Ho, Wo, k, s, p,
+                             scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                             invstd.data_ptr<float>(), (int)act, nullptr, nullptr, sums.data_ptr<float>(),
+                             (float)(1.0 / count), bpm(dx), cur_stream());
+  return dx;
+}
+
 Tensor gap_fwd(const Tensor& x) {
   CHECK_ACT(x);
   const int N = x.size(0), C = x.size(-1);
@@ -531,6 +637,23 @@ Tensor to_nhwc(const Tensor& src, bool nchw, int64_t cpad, double in_scale, cons
   auto y = at::empty({N, H, W, Cp}, src.options().dtype(at::kBFloat16));
   dcp::launch_to_nhwc(src.data_ptr(), src.scalar_type() == at::kByte, nchw, N, C, H, W, Cp, (float)in_scale,
                       fp(mean), fp(stdv), bpm(y), cur_stream());
+  return y;
+}
+
+// image batch -> space-to-depth 2x2 NHWC input of the s2d stem [N, H/2, W/2, 16]
+Tensor to_nhwc_s2d(const Tensor& src, bool nchw, double in_scale, const optional<Tensor>& mean,
+                   const optional<Tensor>& stdv) {
+  CHECK_DEV(src);
+  CHECK_CONTIG(src);
+  TORCH_CHECK(src.scalar_type() == at::kByte || src.scalar_type() == at::kFloat, "to_nhwc_s2d input u8 or fp32");
+  const int N = src.size(0);
+  const int C = nchw ? src.size(1) : src.size(3);
+  const int H = nchw ? src.size(2) : src.size(1);
+  const int W = nchw ? src.size(3) : src.size(2);
+  TORCH_CHECK(C <= 4 && H % 2 == 0 && W % 2 == 0, "to_nhwc_s2d needs <= 4 channels and even H, W");
+  auto y = at::empty({N, H / 2, W / 2, 16}, src.options().dtype(at::kBFloat16));
+  dcp::launch_to_nhwc_s2d(src.data_ptr(), src.scalar_type() == at::kByte, nchw, N, C, H, W, (float)in_scale, fp(mean),
+                          fp(stdv), bpm(y), cur_stream());
   return y;
 }
 
@@ -829,10 +952,24 @@ TORCH_LIBRARY(dcp, m) {
       &bn_bwd_elemt);
   m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)", &maxpool_fwd);
   m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int p) -> Tensor", &maxpool_bwd);
+  m.def("bn_act_maxpool(Tensor x, Tensor scale, Tensor shift, int act, int k, int s, int p) -> (Tensor, Tensor)",
+        &bn_act_maxpool);
+  m.def(
+      "maxpool_bn_bwd_reduce(Tensor dy, Tensor idx, Tensor x, Tensor scale, Tensor shift, Tensor mean, "
+      "Tensor invstd, int act, int k, int s, int p) -> Tensor",
+      &maxpool_bn_bwd_reduce);
+  m.def(
+      "maxpool_bn_bwd_elemt(Tensor dy, Tensor idx, Tensor x, Tensor scale, Tensor shift, Tensor mean, "
+      "Tensor invstd, int act, Tensor sums, float count, int k, int s, int p) -> Tensor",
+      &maxpool_bn_bwd_elemt);
   m.def("gap_fwd(Tensor x) -> Tensor", &gap_fwd);
   m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &gap_bwd);
   m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
   m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
+  m.def("to_nhwc_s2d(Tensor src, bool nchw, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc_s2d);
+  m.def("conv_fwd_geo(Tensor x, Tensor w, int stride, int pad, int Ho, int Wo, bool stats) -> (Tensor, Tensor)",
+        &conv_fwd_geo);
+  m.def("conv_wgrad_geo(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad_geo);
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor", &act_bwd);
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);
   m.def("nested_eval(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval);

@@ -28,6 +28,7 @@
 // with both operands m-major in memory; its LDS images are [m][...] rows read
 // with the gfx950 transpose read `ds_read_b64_tr_b16`, split-K over m with
 // fp32 atomics into the (zeroed) gradient.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -760,10 +761,14 @@ wgrad_kernel(const WgradParams p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int ntm = (p.Co + 127) / 128;
   const int ntn = (p.ldw + 127) / 128;
-  const uint32_t tile = xcd_remap(blockIdx.x, ntm * ntn);
+  // 1-D grid over (split, tile): consecutive logical ids -- the tiles of one split, which
+  // share its dY rows and input pixels -- land on the same XCD (one L2), so each XCD
+  // streams its own contiguous range of rows from HBM once
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t split = lid / (ntm * ntn), tile = lid % (ntm * ntn);
   const int tn = tile % ntn, tmi = tile / ntn;
   const int co0 = tmi * 128, kcol0 = tn * 128;
-  const int mstart = blockIdx.y * p.rows_per_split;
+  const int mstart = split * p.rows_per_split;
   const int mend = min(p.M, mstart + p.rows_per_split);
   const int nkt = (mend - mstart + BK - 1) / BK;
 
@@ -855,7 +860,7 @@ wgrad_kernel(const WgradParams p) {
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
         if (co < p.Co && !(p.ablate & 8)) {
-          if (p.part) p.part[((size_t)blockIdx.y * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
+          if (p.part) p.part[((size_t)split * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
           else unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
         }
       }
@@ -891,10 +896,11 @@ wgrad256_kernel(const WgradParams p) {
   const int wm = wave & 3, wn = wave >> 2;   // 64-co group, 128-col group
   const int ntm = (p.Co + 255) / 256;
   const int ntn = (p.ldw + 255) / 256;
-  const uint32_t tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);  // see wgrad_kernel
+  const uint32_t split = lid / (ntm * ntn), tile = lid % (ntm * ntn);
   const int tn = tile % ntn, tmi = tile / ntn;
   const int co0 = tmi * 256, kcol0 = tn * 256;
-  const int mstart = blockIdx.y * p.rows_per_split;
+  const int mstart = split * p.rows_per_split;
   const int mend = min(p.M, mstart + p.rows_per_split);
   const int nkt = (mend - mstart + BK - 1) / BK;
 
@@ -985,7 +991,7 @@ wgrad256_kernel(const WgradParams p) {
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
         if (co < p.Co) {
-          if (p.part) p.part[((size_t)blockIdx.y * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
+          if (p.part) p.part[((size_t)split * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
           else unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
         }
       }
@@ -998,12 +1004,20 @@ wgrad256_kernel(const WgradParams p) {
 // ---------------------------------------------------------------------------
 template <int BN, int EPI, bool FAST, int NS>
 static void launch_tg(const TapGemmParams& p, int grid, hipStream_t stream) {
-  const size_t lds = (size_t)NS * (128 + BN) * 128;
-  if (lds > 64 * 1024) {
+  // LDS: the stages the k-loop actually uses (short-K shapes -- 1x1 convs with 64 input
+  // channels -- need one, which lets more workgroups share a CU) or the epilogue image
+  const size_t stage = (size_t)(128 + BN) * 128;
+  const size_t full = (size_t)NS * stage;
+  size_t epi = 0;
+  if (EPI == 0) epi = (size_t)128 * 2 * BN;
+  if (EPI == 1) epi = (size_t)128 * 2 * BN + 12 * BN;
+  if (EPI == 3) epi = (size_t)128 * 2 * BN + 16384;
+  const size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
+  if (full > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds);
+                          (int)full);
       attr = true;
     }
   }
@@ -1110,17 +1124,6 @@ __global__ void __launch_bounds__(256) split_reduce1_kernel(const float4* __rest
   }
 }
 
-__global__ void split_reduce2_kernel(const float4* __restrict__ part, int rows, int n4, float4* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  float4 s = part[i];
-  for (int k = 1; k < rows; ++k) {
-    const float4 v = part[(size_t)k * n4 + i];
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-  }
-  out[i] = s;
-}
-
 // out[i] = sum_k part[k][i]; n % 4 == 0.  part must hold splits*n + ceil(splits/64)*n floats
 // when splits > 64 (the chunk sums are written behind the partials).
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream) {
@@ -1134,8 +1137,9 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
   float* tmp = const_cast<float*>(part) + (size_t)splits * n;
   hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
                      splits, n4, (float4*)tmp);
-  hipLaunchKernelGGL(split_reduce2_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream, (const float4*)tmp, chunks, n4,
-                     (float4*)out);
+  // second level: 4 waves per 64 columns split the chunk rows (a thread-per-column loop over
+  // ~200 chunk rows left narrow reductions -- BN sums of 2C columns -- latency bound)
+  launch_partial_sum(tmp, chunks, n, out, stream);
 }
 
 // split-K plan of the weight-gradient GEMM, >= 256 rows per split: ~2 blocks per CU for
@@ -1195,9 +1199,9 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
       hipFuncSetAttribute((const void*)wgrad256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr = true;
     }
-    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles, splits), dim3(512), lds, stream, p);
+    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * splits), dim3(512), lds, stream, p);
   } else {
-    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, splits), dim3(256), 4 * 64 * 256, stream, p);
+    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * splits), dim3(256), 4 * 64 * 256, stream, p);
   }
   if (part != nullptr && splits > 1) launch_split_reduce(part, splits, Co * p.ldw, dw, stream);
 }

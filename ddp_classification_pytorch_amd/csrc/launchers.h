@@ -86,7 +86,15 @@ void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const f
                          int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s);
 
 void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
-                        int s, int p, hipStream_t st);
+                        int s, int p, hipStream_t st, const float* scale = nullptr, const float* shift = nullptr,
+                        int act = 0);
+// backward of BN(+act) -> max pool: dx == nullptr -> reduction pass (part: maxpool_bn_bwd_blocks() x 2 x C
+// scratch, sums_out [2][C]); else the elementwise pass with the global `sums`
+int maxpool_bn_bwd_blocks();
+void launch_maxpool_bn_bwd(const bf16* dy, const uint8_t* idx, const bf16* x, int N, int H, int W, int C, int Ho,
+                           int Wo, int k, int s, int p, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, int act, float* part, float* sums_out, const float* sums,
+                           float inv_count, bf16* dx, hipStream_t st);
 void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st);
 void launch_gap_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t st);
@@ -141,6 +149,9 @@ void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16*
 void launch_mt_weight_prep(const void* entries, const void* blocks, int nblocks, hipStream_t s);
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s);
+// space-to-depth 2x2 input of the s2d stem: dst [N][H/2][W/2][16], channel (py*2+px)*4 + c (c < 3 real)
+void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
+                        const float* mean, const float* stdv, bf16* dst, hipStream_t s);
 void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,

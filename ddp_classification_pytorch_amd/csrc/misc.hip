@@ -190,8 +190,75 @@ void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16*
   hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, s, w, Co, T, Ci, Co_pad, wb, wt);
 }
 
+// One thread per OUTPUT pixel, 16-byte stores: dst [N][H/S][W/S][S*S*Cq] with channel
+// (py*S + px)*Cq + c = normalised src[n][c][i*S+py][j*S+px] (c < C, else 0).  S = 2 is the
+// space-to-depth input of the 4x4 stride-1 form of the 7x7/2 stem (models/resnet.py).
+template <int S, int CQ>
+__global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict__ src, int is_u8, int nchw, int N,
+                                                          int C, int H, int W, float in_scale,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ stdv, bf16* __restrict__ dst) {
+  constexpr int OC = S * S * CQ;
+  const int Ho = H / S, Wo = W / S;
+  const size_t total = (size_t)N * Ho * Wo;
+  float mu[CQ], is[CQ];
+#pragma unroll
+  for (int c = 0; c < CQ; ++c) {
+    mu[c] = (c < C && mean) ? mean[c] : 0.f;
+    is[c] = (c < C && stdv) ? 1.f / stdv[c] : 1.f;
+  }
+  for (size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x; pix < total;
+       pix += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(pix % Wo);
+    const size_t q = pix / Wo;
+    const int i = (int)(q % Ho);
+    const size_t n = q / Ho;
+    bf16 o[OC];
+#pragma unroll
+    for (int py = 0; py < S; ++py)
+#pragma unroll
+      for (int px = 0; px < S; ++px) {
+        const size_t y = (size_t)i * S + py, x = (size_t)j * S + px;
+#pragma unroll
+        for (int c = 0; c < CQ; ++c) {
+          float v = 0.f;
+          if (c < C) {
+            const size_t si = nchw ? ((n * C + c) * H + y) * W + x : ((n * H + y) * W + x) * C + c;
+            const float raw = is_u8 ? (float)((const uint8_t*)src)[si] : ((const float*)src)[si];
+            v = (raw * in_scale - mu[c]) * is[c];
+          }
+          o[(py * S + px) * CQ + c] = f2bf(v);
+        }
+      }
+#pragma unroll
+    for (int k = 0; k < OC / 8; ++k) {
+      bf16x8 w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = o[k * 8 + e];
+      *(bf16x8*)(dst + pix * OC + k * 8) = w;
+    }
+  }
+}
+
+void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
+                        const float* mean, const float* stdv, bf16* dst, hipStream_t s) {
+  size_t total = (size_t)N * (H / 2) * (W / 2);
+  size_t g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL((to_nhwc_pix_kernel<2, 4>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
+                     in_scale, mean, stdv, dst);
+}
+
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s) {
+  if (Cp == 8 && C <= 8) {
+    size_t total = (size_t)N * H * W;
+    size_t g = (total + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL((to_nhwc_pix_kernel<1, 8>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
+                       in_scale, mean, stdv, dst);
+    return;
+  }
   size_t total = (size_t)N * H * W * Cp;
   size_t g = (total + 255) / 256;
   if (g > 8192) g = 8192;

@@ -3,30 +3,61 @@
 // Replaces the ATen max-pool (stem, NESTED/model/imagenet_resnet.py:111),
 // average pool (:116 AvgPool2d(7) / torchvision AdaptiveAvgPool2d) and
 // TResNet's SpaceToDepth stem (timm).
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.cuh"
 #include "launchers.h"
 
 namespace dcp {
 
+// 32-bit decode of a flat (pixel, 8-channel chunk) index i = ((n*H + y)*W + x)*cpr + ch with
+// magic-number divisions (64-bit integer division is emulated on the GPU and dominated these
+// memory-bound kernels); flat indices < 2^31 are checked on the host
+struct PixDiv {
+  FastDiv cpr, w, h;
+  __device__ __forceinline__ void decode(uint32_t i, int& ch, int& x, int& y, int& n) const {
+    const uint32_t pix = fdiv(i, cpr);
+    ch = (int)(i - pix * cpr.d);
+    const uint32_t q = fdiv(pix, w);
+    x = (int)(pix - q * w.d);
+    const uint32_t nn = fdiv(q, h);
+    y = (int)(q - nn * h.d);
+    n = (int)nn;
+  }
+};
+
+static inline PixDiv make_pixdiv(int cpr, int W, int H) {
+  return PixDiv{make_fastdiv(cpr), make_fastdiv(W), make_fastdiv(H)};
+}
+
 // max pool k x k / stride s / pad p; 8 channels per thread; argmax as window index
+// With `scale` != nullptr the input is a BN layer's INPUT and every window element is first
+// mapped through bf16(act(x*scale + shift)) (act: 0 none, 1 ReLU): the stem's BN-apply + ReLU
+// fused into the pool, so the full-resolution activation is never written (it is recomputed
+// from x in the backward, maxpool_bn_bwd_kernel).
+// KK/SS/PP > 0: compile-time window geometry (the ResNet stem's 3x3/2 pad 1: divisions by the
+// stride become shifts); 0: runtime k, s, p
+template <int KK, int SS, int PP>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H, int W, int C,
-                                                          int Ho, int Wo, int k, int s, int p) {
+                                                          int Ho, int Wo, int k_, int s_, int p_,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int act, PixDiv dv) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_, p = KK ? PP : p_;
   const int cpr = C >> 3;
-  const size_t total = (size_t)N * Ho * Wo * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int ch = (int)(i % cpr);
-    size_t pix = i / cpr;
-    const int wo = (int)(pix % Wo);
-    pix /= Wo;
-    const int ho = (int)(pix % Ho);
-    const int n = (int)(pix / Ho);
-    float best[8];
+  const uint32_t total = (uint32_t)N * Ho * Wo * cpr;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int ch, wo, ho, n;
+    dv.decode(i, ch, wo, ho, n);
+    float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       best[q] = -INFINITY;
       bi[q] = 0;
+      sc[q] = scale ? scale[ch * 8 + q] : 1.f;
+      sh[q] = scale ? shift[ch * 8 + q] : 0.f;
     }
     for (int kh = 0; kh < k; ++kh) {
       const int hi = ho * s - p + kh;
@@ -34,10 +65,15 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
       for (int kw = 0; kw < k; ++kw) {
         const int wi = wo * s - p + kw;
         if ((unsigned)wi >= (unsigned)W) continue;
-        const bf16x8 v = *(const bf16x8*)(x + (((size_t)n * H + hi) * W + wi) * C + ch * 8);
+        const bf16x8 v = *(const bf16x8*)(x + ((uint32_t)(n * H + hi) * W + wi) * C + ch * 8);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const float f = bf2f(v[q]);
+          float f = bf2f(v[q]);
+          if (scale) {
+            f = f * sc[q] + sh[q];
+            if (act == 1) f = fmaxf(f, 0.f);
+            f = bf2f(f2bf(f));  // the bf16 activation the unfused BN kernel would have stored
+          }
           if (f > best[q]) {
             best[q] = f;
             bi[q] = (uint8_t)(kh * k + kw);
@@ -60,18 +96,16 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
 
 // gather form of the max-pool backward: every input pixel sums the output
 // gradients whose window argmax points at it (deterministic, no atomics)
+template <int KK, int SS, int PP>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
                                                           bf16* __restrict__ dx, int N, int H, int W, int C, int Ho,
-                                                          int Wo, int k, int s, int p) {
+                                                          int Wo, int k_, int s_, int p_, PixDiv dv) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_, p = KK ? PP : p_;
   const int cpr = C >> 3;
-  const size_t total = (size_t)N * H * W * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int ch = (int)(i % cpr);
-    size_t pix = i / cpr;
-    const int wi = (int)(pix % W);
-    pix /= W;
-    const int hi = (int)(pix % H);
-    const int n = (int)(pix / H);
+  const uint32_t total = (uint32_t)N * H * W * cpr;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int ch, wi, hi, n;
+    dv.decode(i, ch, wi, hi, n);
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.f;
@@ -86,7 +120,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
         const int kw = wi - (wo * s - p);
         if (kw < 0 || kw >= k) continue;
-        const size_t o = (((size_t)n * Ho + ho) * Wo + wo) * C + ch * 8;
+        const uint32_t o = ((uint32_t)(n * Ho + ho) * Wo + wo) * C + ch * 8;
         const uint64_t packed = *(const uint64_t*)(idx + o);
         const bf16x8 g = *(const bf16x8*)(dy + o);
         const uint8_t want = (uint8_t)(kh * k + kw);
@@ -99,6 +133,104 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
     *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+// Backward of BN(+act) followed by the max pool, from the pooled gradient dy and the window
+// argmax: every input pixel gathers its gradient g from the <= ceil(k/s)^2 windows whose argmax
+// points at it, masks it with act'(x*scale + shift), then
+//   PASS 0: per-workgroup partial (sum g', sum g' * (x - mean) * invstd)  -> part[block][2][C]
+//   PASS 1: dx = a*g' + b*x + c with the BN coefficients folded from the global sums
+// (the unfused chain wrote the full-resolution pool gradient and read it twice).
+// Requires 256 % (C/8) == 0 so each thread keeps one 8-channel chunk for the whole grid stride.
+template <int PASS, int KK, int SS, int PP>
+__global__ void __launch_bounds__(256) maxpool_bn_bwd_kernel(const bf16* __restrict__ dy,
+                                                             const uint8_t* __restrict__ idx,
+                                                             const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                             int Ho, int Wo, int k_, int s_, int p_,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, int act,
+                                                             const float* __restrict__ sums, float inv_count,
+                                                             float* __restrict__ part, bf16* __restrict__ dx,
+                                                             PixDiv dv) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_, p = KK ? PP : p_;
+  const int cpr = C >> 3;
+  const int ch = threadIdx.x % cpr;
+  float sc[8], sh[8], mu[8], ca[8], cb[8], cc[8], s1[8], s2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = ch * 8 + q;
+    sc[q] = scale[c];
+    sh[q] = shift[c];
+    mu[q] = mean[c];
+    s1[q] = s2[q] = 0.f;
+    if (PASS == 1) {
+      const float is = invstd[c];
+      const float a2 = sums[c] * inv_count, a3 = sums[C + c] * inv_count * is;
+      ca[q] = sc[q];
+      cb[q] = -sc[q] * a3;
+      cc[q] = -sc[q] * a2 + sc[q] * a3 * mu[q];
+    }
+  }
+  const uint32_t total = (uint32_t)N * H * W * cpr;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int chd, wi, hi, n;
+    dv.decode(i, chd, wi, hi, n);
+    float g[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] = 0.f;
+    const int ho_lo = max(0, (hi + p - k + s) / s);
+    const int ho_hi = min(Ho - 1, (hi + p) / s);
+    const int wo_lo = max(0, (wi + p - k + s) / s);
+    const int wo_hi = min(Wo - 1, (wi + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int kh = hi - (ho * s - p);
+      if (kh < 0 || kh >= k) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int kw = wi - (wo * s - p);
+        if (kw < 0 || kw >= k) continue;
+        const uint32_t o = ((uint32_t)(n * Ho + ho) * Wo + wo) * C + ch * 8;
+        const uint64_t packed = *(const uint64_t*)(idx + o);
+        const bf16x8 gv = *(const bf16x8*)(dy + o);
+        const uint8_t want = (uint8_t)(kh * k + kw);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (((packed >> (8 * q)) & 0xff) == want) g[q] += bf2f(gv[q]);
+      }
+    }
+    const bf16x8 xv = *(const bf16x8*)(x + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float xf = bf2f(xv[q]);
+      float gq = bf2f(f2bf(g[q]));  // the bf16 pool gradient of the unfused chain
+      if (act == 1 && !(xf * sc[q] + sh[q] > 0.f)) gq = 0.f;
+      if (PASS == 0) {
+        s1[q] += gq;
+        s2[q] += gq * (xf - mu[q]);
+      } else {
+        o[q] = f2bf(ca[q] * gq + cb[q] * xf + cc[q]);
+      }
+    }
+    if (PASS == 1) *(bf16x8*)(dx + i * 8) = o;
+  }
+  if (PASS == 0) {
+    __shared__ float red[2][256][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[0][threadIdx.x][q] = s1[q];
+      red[1][threadIdx.x][q] = s2[q] * invstd[ch * 8 + q];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < cpr * 8 * 2) {
+      const int which = threadIdx.x / (cpr * 8), c = threadIdx.x % (cpr * 8);
+      const int cch = c >> 3, q = c & 7;
+      float t = 0.f;
+      for (int r = cch; r < 256; r += cpr) t += red[which][r][q];
+      part[((size_t)blockIdx.x * 2 + which) * C + c] = t;
+    }
   }
 }
 
@@ -169,18 +301,67 @@ static inline int ew_grid2(size_t n) {
   return (int)g;
 }
 
+static void check_flat(size_t elems) {
+  if (elems >= (1ull << 31)) {
+    fprintf(stderr, "pool kernels: tensor of %zu elements exceeds the 32-bit index range\n", elems);
+    abort();
+  }
+}
+
 void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
-                        int s, int p, hipStream_t st) {
+                        int s, int p, hipStream_t st, const float* scale, const float* shift, int act) {
   const size_t total = (size_t)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid2(total)), dim3(256), 0, st, x, y, idx, N, H, W, C, Ho, Wo, k,
-                     s, p);
+  check_flat((size_t)N * H * W * C);
+  check_flat((size_t)N * Ho * Wo * C);
+  const PixDiv dv = make_pixdiv(C / 8, Wo, Ho);
+  if (k == 3 && s == 2 && p == 1)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<3, 2, 1>), dim3(ew_grid2(total)), dim3(256), 0, st, x, y, idx, N, H, W, C,
+                       Ho, Wo, k, s, p, scale, shift, act, dv);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<0, 0, 0>), dim3(ew_grid2(total)), dim3(256), 0, st, x, y, idx, N, H, W, C,
+                       Ho, Wo, k, s, p, scale, shift, act, dv);
+}
+
+int maxpool_bn_bwd_blocks() { return 2048; }
+
+void launch_maxpool_bn_bwd(const bf16* dy, const uint8_t* idx, const bf16* x, int N, int H, int W, int C, int Ho,
+                           int Wo, int k, int s, int p, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, int act, float* part, float* sums_out, const float* sums,
+                           float inv_count, bf16* dx, hipStream_t st) {
+  const size_t total = (size_t)N * H * W * (C / 8);
+  check_flat((size_t)N * H * W * C);
+  const PixDiv dv = make_pixdiv(C / 8, W, H);
+  const bool stem = k == 3 && s == 2 && p == 1;
+  if (dx == nullptr) {
+    const int g = maxpool_bn_bwd_blocks();
+    if (stem)
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<0, 3, 2, 1>), dim3(g), dim3(256), 0, st, dy, idx, x, N, H, W, C, Ho,
+                         Wo, k, s, p, scale, shift, mean, invstd, act, nullptr, 0.f, part, nullptr, dv);
+    else
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<0, 0, 0, 0>), dim3(g), dim3(256), 0, st, dy, idx, x, N, H, W, C, Ho,
+                         Wo, k, s, p, scale, shift, mean, invstd, act, nullptr, 0.f, part, nullptr, dv);
+    launch_partial_sum(part, g, 2 * C, sums_out, st);
+  } else {
+    if (stem)
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 3, 2, 1>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, x, N,
+                         H, W, C, Ho, Wo, k, s, p, scale, shift, mean, invstd, act, sums, inv_count, nullptr, dx, dv);
+    else
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 0, 0, 0>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, x, N,
+                         H, W, C, Ho, Wo, k, s, p, scale, shift, mean, invstd, act, sums, inv_count, nullptr, dx, dv);
+  }
 }
 
 void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st) {
   const size_t total = (size_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo,
-                     k, s, p);
+  check_flat((size_t)N * H * W * C);
+  const PixDiv dv = make_pixdiv(C / 8, W, H);
+  if (k == 3 && s == 2 && p == 1)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<3, 2, 1>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, dx, N, H, W,
+                       C, Ho, Wo, k, s, p, dv);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<0, 0, 0>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, dx, N, H, W,
+                       C, Ho, Wo, k, s, p, dv);
 }
 
 void launch_gap_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t st) {

@@ -45,8 +45,8 @@ class DevicePrefetcher:
     """Wraps a loader of (uint8 HWC images, labels[, index]) and yields
     (NHWC activations, labels[, index]) on ``device``."""
 
-    def __init__(self, loader, device, mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8):
-        self.loader, self.device, self.cpad = loader, torch.device(device), cpad
+    def __init__(self, loader, device, mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8, s2d=False):
+        self.loader, self.device, self.cpad, self.s2d = loader, torch.device(device), cpad, s2d
         self.mean = torch.tensor(mean, dtype=torch.float32, device=self.device)
         self.std = torch.tensor(std, dtype=torch.float32, device=self.device)
         self.cuda = self.device.type == "cuda"
@@ -63,7 +63,8 @@ class DevicePrefetcher:
         imgs, labels = batch[0], batch[1]
         imgs = imgs.to(self.device, non_blocking=True)
         labels = labels.to(self.device, non_blocking=True)
-        x = Fn.to_device_nhwc(imgs, self.mean, self.std, cpad=self.cpad, nchw=False, in_scale=1.0 / 255.0)
+        x = Fn.to_device_nhwc(imgs, self.mean, self.std, cpad=self.cpad, nchw=False, in_scale=1.0 / 255.0,
+                              s2d=self.s2d and imgs.shape[1] % 2 == 0 and imgs.shape[2] % 2 == 0)
         rest = tuple(b.to(self.device, non_blocking=True) for b in batch[2:])
         return (x, labels) + rest
 
@@ -96,9 +97,10 @@ class SyntheticLoader:
     """``steps`` batches of on-device random uint8 images (cycling over ``pool`` distinct batches)."""
 
     def __init__(self, batch_size, steps, size=224, num_classes=1000, device="cuda", pool=2, seed=0,
-                 mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8, return_index=False):
+                 mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8, return_index=False, s2d=False):
         self.device = torch.device(device)
         self.steps, self.cpad, self.return_index, self.batch_size = steps, cpad, return_index, batch_size
+        self.s2d = s2d and size % 2 == 0
         g = torch.Generator(device="cpu")
         g.manual_seed(seed)
         self.imgs = [torch.randint(0, 256, (batch_size, size, size, 3), dtype=torch.uint8, generator=g).to(self.device)
@@ -114,7 +116,8 @@ class SyntheticLoader:
     def __iter__(self):
         for i in range(self.steps):
             k = i % len(self.imgs)
-            x = Fn.to_device_nhwc(self.imgs[k], self.mean, self.std, cpad=self.cpad, nchw=False, in_scale=1 / 255.0)
+            x = Fn.to_device_nhwc(self.imgs[k], self.mean, self.std, cpad=self.cpad, nchw=False, in_scale=1 / 255.0,
+                                  s2d=self.s2d)
             if self.return_index:
                 idx = torch.arange(k * self.batch_size, (k + 1) * self.batch_size, device=self.device)
                 yield x, self.labels[k], idx

@@ -95,11 +95,12 @@ def build_data(args, rt: Runtime, drop_last_train=False):
         tr, va = WithIndex(tr), WithIndex(va)
     mean, std = norm_stats(args.dataset if "CIFAR" in args.dataset.upper() else "imagenet")
     cpad = 3 if str(args.model).startswith("tresnet") else 8
+    s2d = str(args.model).startswith(("resnet", "resnext"))  # ImageNet ResNets: space-to-depth stem input
     tr_s = ShardSampler(tr, rt.world, rt.rank, shuffle=True, seed=args.seed, drop_last=drop_last_train)
     va_s = ShardSampler(va, rt.world, rt.rank, shuffle=False, seed=args.seed)
     workers = args.workers if args.data != "synthetic" else min(args.workers, 2)
     tr_l = build_loader(tr, args.batchsize, tr_s, workers=workers, drop_last=drop_last_train,
                         worker_init_fn=worker_init_fn)
     va_l = build_loader(va, args.batchsize, va_s, workers=workers, drop_last=False, worker_init_fn=worker_init_fn)
-    return (DevicePrefetcher(tr_l, rt.device, mean, std, cpad), DevicePrefetcher(va_l, rt.device, mean, std, cpad),
+    return (DevicePrefetcher(tr_l, rt.device, mean, std, cpad, s2d), DevicePrefetcher(va_l, rt.device, mean, std, cpad, s2d),
             tr, va)

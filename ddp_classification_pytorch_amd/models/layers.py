@@ -91,6 +91,19 @@ class BatchNorm2d(nn.Module):
                                  self.momentum, self.eps, act=act, slope=slope, residual=residual,
                                  group=self.process_group if stats else None, link=link)
 
+    def forward_pool(self, x, slabs=None, act="relu", k=3, s=2, p=1):
+        """BN + act + k x k / s max pool.  Training-mode statistics with a ReLU/identity
+        activation and a channel count the fused kernel covers run as ONE fused op
+        (the full-resolution activation is never stored); otherwise BN then pool."""
+        C = x.shape[-1]
+        if (self.training and not self.frozen and act in ("relu", "none") and C % 8 == 0 and 256 % (C // 8) == 0
+                and torch.is_grad_enabled()):
+            self._nbt_pending += 1
+            return Fn.batch_norm_act_maxpool(x, slabs, self.weight, self.bias, self.running_mean, self.running_var,
+                                             self.momentum, self.eps, act=act, k=k, s=s, p=p,
+                                             group=self.process_group)
+        return Fn.max_pool2d(self(x, slabs, act=act), k, s, p)
+
     def flush_batches_tracked(self):
         if self._nbt_pending:
             self.num_batches_tracked.add_(self._nbt_pending)

@@ -90,14 +90,19 @@ class ResNet(nn.Module):
     """num_classes=0 -> feature extractor returning pooled features [N, C]."""
 
     def __init__(self, block, layers, num_classes=1000, variant="imagenet", groups=1, width_per_group=64,
-                 zero_init_residual=False, in_chans=3):
+                 zero_init_residual=False, in_chans=3, stem_s2d=True):
         super().__init__()
         self.variant = variant
         self.groups, self.base_width = groups, width_per_group
         self.inplanes = 64
         self.in_chans = in_chans
+        # 7x7/2 stem computed as a 4x4/1 conv over the 2x2 space-to-depth input
+        # (ops.functional.stem_conv_s2d); the parameter keeps the torchvision 7x7 layout
+        self.stem_s2d = bool(stem_s2d) and variant == "imagenet" and in_chans <= 4
         if variant == "imagenet":
             self.conv1 = Conv2d(in_chans, 64, 7, 2, 3)
+            if self.stem_s2d:
+                self.register_buffer("_stem_w16", torch.zeros(64, 4, 4, 16), persistent=False)
         elif variant == "cifar":
             self.conv1 = Conv2d(in_chans, 64, 3, 1, 1)
         else:
@@ -129,11 +134,19 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward_features(self, x):
-        """x: NHWC [N,H,W,8] -> pooled features [N, feat_dim]."""
-        y, s = self.conv1(x, stats=_train_stats(self.bn1))
-        y = self.bn1(y, s, act="relu")
+        """x: NHWC [N,H,W,8] (or the s2d stem's [N,H/2,W/2,16]) -> pooled features [N, feat_dim]."""
+        t = _train_stats(self.bn1)
+        if self.stem_s2d and (x.shape[-1] == 16 or (x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0)):
+            if x.shape[-1] != 16:
+                x = Fn.nhwc_to_s2d(x)
+            y, s = Fn.stem_conv_s2d(x, self.conv1.weight, self._stem_w16, stats=t)
+            s = s if (t and x.is_cuda) else None
+        else:
+            y, s = self.conv1(x, stats=t)
         if self.variant == "imagenet":
-            y = Fn.max_pool2d(y, 3, 2, 1)
+            y = self.bn1.forward_pool(y, s, act="relu", k=3, s=2, p=1)  # BN + ReLU + max pool, one fused op
+        else:
+            y = self.bn1(y, s, act="relu")
         y = self.layer1(y)
         y = self.layer2(y)
         y = self.layer3(y)

@@ -73,6 +73,28 @@ def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act):
     return gm, torch.stack([gr.sum(0), (gr * xh).sum(0)])
 
 
+def _pad_geo(xc, KH, KW, stride, pad, Ho, Wo):
+    """NCHW input padded by `pad` at the top/left and padded/cropped at the bottom/right to
+    exactly (Ho-1)*stride + K rows/columns (the explicit output grid of conv_fwd_geo)."""
+    H, W = xc.shape[2], xc.shape[3]
+    Hp, Wp = (Ho - 1) * stride + KH, (Wo - 1) * stride + KW
+    xc = F.pad(xc, (pad, max(0, Wp - pad - W), pad, max(0, Hp - pad - H)))
+    return xc[:, :, :Hp, :Wp]
+
+
+def conv_fwd_geo(x, w, stride, pad, Ho, Wo, stats):
+    xc = _pad_geo(_nchw(_f(x)), w.shape[1], w.shape[2], stride, pad, Ho, Wo)
+    y = F.conv2d(xc, _w_oihw(_f(w)), stride=stride)
+    return _nhwc(y).to(x.dtype), torch.empty(0, device=x.device)
+
+
+def conv_wgrad_geo(dy, x, KH, KW, stride, pad):
+    Co, C, Ho, Wo = dy.shape[3], x.shape[3], dy.shape[1], dy.shape[2]
+    xc = _pad_geo(_nchw(_f(x)), KH, KW, stride, pad, Ho, Wo)
+    dw = torch.nn.grad.conv2d_weight(xc, (Co, C, KH, KW), _nchw(_f(dy)), stride=stride)
+    return dw.permute(0, 2, 3, 1).contiguous()
+
+
 def conv_wgrad(dy, x, KH, KW, stride, pad):
     Co, C = dy.shape[3], x.shape[3]
     dw = torch.nn.grad.conv2d_weight(_nchw(_f(x)), (Co, C, KH, KW), _nchw(_f(dy)), stride=stride, padding=pad)
@@ -249,6 +271,20 @@ def maxpool_bwd(dy, idx, H, W, k, s, p):
     return _nhwc(dx.view(N, C, H, W)).to(dy.dtype)
 
 
+def bn_act_maxpool(x, scale, shift, act, k, s, p):
+    return maxpool_fwd(bn_act(x, None, scale, shift, act, 0.0), k, s, p)
+
+
+def maxpool_bn_bwd_reduce(dy, idx, x, scale, shift, mean, invstd, act, k, s, p):
+    g = maxpool_bwd(dy, idx, x.shape[1], x.shape[2], k, s, p)
+    return bn_bwd_reduce(g, x, None, scale, shift, mean, invstd, act, 0.0)
+
+
+def maxpool_bn_bwd_elemt(dy, idx, x, scale, shift, mean, invstd, act, sums, count, k, s, p):
+    g = maxpool_bwd(dy, idx, x.shape[1], x.shape[2], k, s, p)
+    return bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, count, act, 0.0, False)[0]
+
+
 def gap_fwd(x):
     N, C = x.shape[0], x.shape[-1]
     return _f(x).reshape(N, -1, C).mean(1).to(x.dtype)
@@ -280,6 +316,12 @@ def to_nhwc(src, nchw, cpad, in_scale, mean, std):
     if cpad > C:
         x = F.pad(x, (0, cpad - C))
     return x.contiguous()
+
+
+def to_nhwc_s2d(src, nchw, in_scale, mean, std):
+    x = to_nhwc(src, nchw, 4, in_scale, mean, std)
+    N, H, W, _ = x.shape
+    return x.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 16).contiguous()
 
 
 def act_bwd(dy, y, act):

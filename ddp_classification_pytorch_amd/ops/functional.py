@@ -225,10 +225,13 @@ class _Conv2d(Function):
         ctx.geo = (weight.shape[1], weight.shape[2], stride, pad)
         ctx.link, ctx.bnsrc, ctx.deposit = link, bnsrc, deposit
         ctx.mark_non_differentiable(slabs)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics slabs
         return y, slabs
 
     @staticmethod
     def backward(ctx, dy, _dslabs):
+        if dy is None:
+            return (None,) * 10
         x, wt = ctx.saved_tensors
         KH, KW, stride, pad = ctx.geo
         dy = dy.contiguous()
@@ -447,6 +450,61 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     return out
 
 
+class _BNActPool(Function):
+    """Training-mode BN + ReLU/identity + k x k max pool (the ResNet stem tail) without the
+    full-resolution activation: forward pools act(bn(x)) on the fly; backward gathers the
+    pooled gradient per input pixel and runs the BN reduction and elementwise passes on it."""
+
+    @staticmethod
+    def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig, pool):
+        k = K(x)
+        C = x.shape[-1]
+        count = x.numel() // C
+        st = k.bn_stats(x, slabs)
+        if cfg.group is not None:
+            gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
+            dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+            st = gathered
+            count = count * cfg.world
+        mean, invstd, scale, shift = k.bn_finalize(st, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps)
+        y, idx = k.bn_act_maxpool(x, scale, shift, cfg.act, *pool)
+        ctx.save_for_backward(x, idx, scale, shift, mean, invstd)
+        ctx.cfg, ctx.count, ctx.pool = cfg, count, pool
+        ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, dy, _didx):
+        if dy is None:
+            return (None,) * 8
+        x, idx, scale, shift, mean, invstd = ctx.saved_tensors
+        cfg = ctx.cfg
+        dy = dy.contiguous()
+        k = K(dy)
+        local = k.maxpool_bn_bwd_reduce(dy, idx, x, scale, shift, mean, invstd, cfg.act, *ctx.pool)
+        sums = local
+        if cfg.group is not None:
+            sums = local.clone()
+            dist.all_reduce(sums, group=cfg.group)
+        dx = k.maxpool_bn_bwd_elemt(dy, idx, x, scale, shift, mean, invstd, cfg.act, sums, float(ctx.count),
+                                    *ctx.pool)
+        dgamma = local[1] if ctx.needs_input_grad[2] else None
+        dbeta = local[0] if ctx.needs_input_grad[3] else None
+        return dx, None, dgamma, dbeta, None, None, None, None
+
+
+def batch_norm_act_maxpool(x, slabs, gamma, beta, run_mean, run_var, momentum, eps, act="relu", k=3, s=2, p=1,
+                           group=None):
+    """Training-mode BN(+act) followed by a max pool, fused (returns the pooled activations)."""
+    world = dist.get_world_size(group) if group is not None else 1
+    cfg = BNConfig(True, momentum, eps, ACT[act], 0.0, group, world)
+    if slabs is None or slabs.numel() == 0:
+        slabs = None
+    y, _ = _BNActPool.apply(x, slabs, gamma, beta, run_mean, run_var, cfg, (k, s, p))
+    return y
+
+
 # ----------------------------------------------------------------------------- pooling
 class _MaxPool(Function):
     @staticmethod
@@ -546,11 +604,14 @@ class _XEnt(Function):
         ctx.save_for_backward(logits, labels)
         ctx.C, ctx.smoothing, ctx.reduction = C, smoothing, reduction
         ctx.mark_non_differentiable(rank)
+        ctx.set_materialize_grads(False)
         loss = loss_rows.mean() if reduction == "mean" else loss_rows.sum()
         return loss, rank
 
     @staticmethod
     def backward(ctx, g, _grank):
+        if g is None:
+            return None, None, None, None, None
         logits, labels = ctx.saved_tensors
         B = logits.shape[0]
         scale = 1.0 / B if ctx.reduction == "mean" else 1.0
@@ -640,10 +701,13 @@ class _ArcFace(Function):
         ctx.save_for_backward(xn, inv_x, wn, inv_w, cos, labels, dphi)
         ctx.cfg = (C, D, s, m, easy)
         ctx.mark_non_differentiable(rank, logits)
+        ctx.set_materialize_grads(False)
         return loss_rows.mean(), rank, logits
 
     @staticmethod
     def backward(ctx, g, _grank, _glogits):
+        if g is None:
+            return (None,) * 7
         xn, inv_x, wn, inv_w, cos, labels, dphi = ctx.saved_tensors
         C, D, s, m, easy = ctx.cfg
         k = K(cos)
@@ -666,15 +730,67 @@ def arcface_loss(x, weight, labels, s=30.0, m=0.5, easy_margin=True, return_logi
 
 
 # ----------------------------------------------------------------------------- misc
-def to_device_nhwc(images: torch.Tensor, mean=None, std=None, cpad: int = 8, nchw: bool = True, in_scale: float = 1.0):
+def to_device_nhwc(images: torch.Tensor, mean=None, std=None, cpad: int = 8, nchw: bool = True, in_scale: float = 1.0,
+                   s2d: bool = False):
     """Image batch (uint8 or fp32, NCHW/NHWC, already on the target device) -> normalised
-    NHWC activations with channels zero-padded to ``cpad``."""
+    NHWC activations with channels zero-padded to ``cpad``; ``s2d=True`` emits the 2x2
+    space-to-depth layout [N, H/2, W/2, 16] of the s2d stem (:func:`stem_conv_s2d`)."""
     if mean is not None and not torch.is_tensor(mean):
         mean = torch.tensor(mean, dtype=torch.float32, device=images.device)
     if std is not None and not torch.is_tensor(std):
         std = torch.tensor(std, dtype=torch.float32, device=images.device)
-    out = K(images).to_nhwc(images.contiguous(), nchw, cpad, in_scale, mean, std)
+    if s2d:
+        out = K(images).to_nhwc_s2d(images.contiguous(), nchw, in_scale, mean, std)
+    else:
+        out = K(images).to_nhwc(images.contiguous(), nchw, cpad, in_scale, mean, std)
     return out.to(act_dtype(images.device)) if not images.is_cuda else out
+
+
+# ----------------------------------------------------------------------------- space-to-depth stem
+def nhwc_to_s2d(x: torch.Tensor) -> torch.Tensor:
+    """[N, H, W, C>=4] NHWC image activations (channels >= 3 zero) -> [N, H/2, W/2, 16]."""
+    N, H, W, _ = x.shape
+    return (x[..., :4].reshape(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5)
+            .reshape(N, H // 2, W // 2, 16).contiguous())
+
+
+def stem_s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Co, 7, 7, C<=4] weight of a 7x7 / stride-2 / pad-3 conv -> [Co, 4, 4, 16] weight of the
+    equivalent 4x4 / stride-1 conv over the 2x2 space-to-depth input (top/left pad 2):
+    w'[co][ta][tb][(py*2+px)*4 + c] = w[co][2ta+py-1][2tb+px-1][c] (zero outside 0..6).
+    Differentiable, so autograd maps the 4x4 weight gradient back onto the 7x7 master."""
+    co, _, _, c = w.shape
+    w8 = F.pad(w, (0, 4 - c, 1, 0, 1, 0))  # [co, 8, 8, 4], kernel index u = k + 1
+    return w8.reshape(co, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(co, 4, 4, 16)
+
+
+class _StemS2D(Function):
+    @staticmethod
+    def forward(ctx, x, w16, wb, stats):
+        y, slabs = K(x).conv_fwd_geo(x, wb, 1, 2, x.shape[1], x.shape[2], stats)
+        ctx.save_for_backward(x)
+        ctx.mark_non_differentiable(slabs)
+        ctx.set_materialize_grads(False)
+        return y, slabs
+
+    @staticmethod
+    def backward(ctx, dy, _dslabs):
+        if dy is None:
+            return None, None, None, None
+        (x,) = ctx.saved_tensors
+        dw = K(dy).conv_wgrad_geo(dy.contiguous(), x, 4, 4, 1, 2) if ctx.needs_input_grad[1] else None
+        return None, dw, None, None
+
+
+def stem_conv_s2d(x16: torch.Tensor, weight: torch.Tensor, buf: torch.Tensor, stats: bool = False):
+    """The ResNet 7x7/2 stem as a 4x4/1 implicit GEMM over the space-to-depth input:
+    K = 16 taps x 16 channels = 256 (4 MFMA k-tiles) instead of 49 taps x 8 padded
+    channels = 392 (7 k-tiles).  ``buf``: persistent fp32 [Co,4,4,16] holding the
+    transformed master weight (its bf16 copy rides the multi-tensor weight cache)."""
+    with torch.no_grad():
+        buf.copy_(stem_s2d_weight(weight.detach()))
+    wb, _ = prepared_weight(buf, 0, False)
+    return _StemS2D.apply(x16, stem_s2d_weight(weight), wb, bool(stats and x16.is_cuda))
 
 
 class _PrefixMask(Function):

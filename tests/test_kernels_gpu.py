@@ -425,6 +425,62 @@ def test_to_nhwc(K):
     yr = _ref.to_nhwc(img, True, 8, 1 / 255.0, mean, std)
     assert y.shape == (2, 20, 24, 8)
     assert relerr(y, yr) < 1e-2
+    # NHWC uint8 source (the data-loader path) and fp32 source
+    imh = img.permute(0, 2, 3, 1).contiguous()
+    assert relerr(K.to_nhwc(imh.to(DEV), False, 8, 1 / 255.0, mean.to(DEV), std.to(DEV)), yr) < 1e-2
+    imf = torch.randn(2, 3, 20, 24)
+    assert relerr(K.to_nhwc(imf.to(DEV), True, 8, 1.0, None, None), _ref.to_nhwc(imf, True, 8, 1.0, None, None)) < 1e-2
+
+
+@pytest.mark.parametrize("nchw", [True, False])
+def test_to_nhwc_s2d(K, nchw):
+    img = torch.randint(0, 256, (3, 3, 20, 24), dtype=torch.uint8)
+    if not nchw:
+        img = img.permute(0, 2, 3, 1).contiguous()
+    mean = torch.tensor([0.485, 0.456, 0.406])
+    std = torch.tensor([0.229, 0.224, 0.225])
+    y = K.to_nhwc_s2d(img.to(DEV), nchw, 1 / 255.0, mean.to(DEV), std.to(DEV))
+    yr = _ref.to_nhwc_s2d(img, nchw, 1 / 255.0, mean, std)
+    assert y.shape == (3, 10, 12, 16)
+    assert relerr(y, yr) < 1e-2
+    assert (y.view(-1, 4, 4)[:, :, 3] == 0).all()  # the pad channel of every phase
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,k,pad", [(4, 112, 16, 64, 4, 2), (2, 9, 16, 72, 4, 2), (3, 15, 64, 64, 3, 1)])
+def test_conv_geo(K, N, H, Ci, Co, k, pad):
+    """explicit-grid conv (the s2d stem: 4x4 taps, top/left pad 2, output grid = input grid)"""
+    torch.manual_seed(0)
+    x = rnd(N, H, H, Ci)
+    w = rnd(Co, k, k, Ci, scale=(k * k * Ci) ** -0.5)
+    y, slabs = K.conv_fwd_geo(x.to(DEV), w.to(DEV), 1, pad, H, H, True)
+    yr, _ = _ref.conv_fwd_geo(x.float(), w.float(), 1, pad, H, H, False)
+    assert relerr(y, yr) < 1e-2
+    assert slabs.shape == ((N * H * H + 127) // 128, 2, Co)
+    dy = rnd(N, H, H, Co)
+    dw = K.conv_wgrad_geo(dy.to(DEV), x.to(DEV), k, k, 1, pad)
+    assert relerr(dw, _ref.conv_wgrad_geo(dy.float(), x.float(), k, k, 1, pad)) < 1e-2
+
+
+def test_s2d_stem_gpu_matches_plain_stem():
+    """The s2d stem (4x4/1 over the space-to-depth input) vs the plain 7x7/2 conv on the HIP
+    kernels: same output and, for the same upstream gradient, the same 7x7 weight gradient."""
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    img = torch.randint(0, 256, (8, 3, 64, 64), dtype=torch.uint8, device=DEV)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    x8 = Fn.to_device_nhwc(img, mean, std, in_scale=1 / 255.0)
+    x16 = Fn.to_device_nhwc(img, mean, std, in_scale=1 / 255.0, s2d=True)
+    assert torch.equal(x16, Fn.nhwc_to_s2d(x8))
+    w = (torch.randn(64, 7, 7, 3, device=DEV) * 0.05).requires_grad_(True)
+    y1, _ = Fn.stem_conv_s2d(x16, w, torch.zeros(64, 4, 4, 16, device=DEV))
+    y0, _ = Fn.conv2d(x8, w, 2, 3)
+    assert y1.shape == y0.shape
+    assert relerr(y1, y0) < 1e-2
+    g = torch.randn_like(y0.float()).bfloat16()
+    (g1,) = torch.autograd.grad(y1, w, g)
+    (g0,) = torch.autograd.grad(y0, w, g)
+    assert relerr(g1, g0) < 1e-2
 
 
 @pytest.mark.parametrize("shape,stride", [((8, 2, 2, 512), 1), ((8, 4, 4, 256), 2), ((4, 8, 8, 64), 1)])
@@ -472,3 +528,27 @@ def test_bn_stats_large_mean_stable(K):
     mean, invstd, _, _ = K.bn_finalize(two, None, None, None, None, 0.1, 0.0)
     var = sr[0, 2] / sr[0, 0]
     assert relerr(invstd, 1 / var.sqrt()) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 32, 64), (3, 17, 15, 64), (2, 12, 10, 128)])
+def test_bn_act_maxpool_fused(K, shape):
+    """stem BN + ReLU + 3x3/2 max pool fused: forward pooled values / argmax and both backward
+    passes against the unfused reference chain."""
+    N, H, W, C = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, C, scale=2.0) + 0.3
+    scale, shift = torch.rand(C) + 0.5, torch.randn(C) * 0.3
+    mean, invstd = torch.randn(C) * 0.2, torch.rand(C) + 0.5
+    d = lambda t: t.to(DEV)
+    y, idx = K.bn_act_maxpool(d(x), d(scale), d(shift), 1, 3, 2, 1)
+    yr, idxr = _ref.bn_act_maxpool(x.float(), scale, shift, 1, 3, 2, 1)
+    assert relerr(y, yr) < 1e-2
+    assert (idx.cpu() == idxr).float().mean().item() > 0.99  # ties on the bf16 grid may pick another max
+    dy = rnd(*y.shape)
+    sums = K.maxpool_bn_bwd_reduce(d(dy), idx, d(x), d(scale), d(shift), d(mean), d(invstd), 1, 3, 2, 1)
+    sr = _ref.maxpool_bn_bwd_reduce(dy.float(), idx.cpu(), x.float(), scale, shift, mean, invstd, 1, 3, 2, 1)
+    assert relerr(sums, sr) < 5e-3  # the kernel rounds the gathered pool gradient to bf16, as the unfused chain
+    cnt = float(N * H * W)
+    dx = K.maxpool_bn_bwd_elemt(d(dy), idx, d(x), d(scale), d(shift), d(mean), d(invstd), 1, sums, cnt, 3, 2, 1)
+    dxr = _ref.maxpool_bn_bwd_elemt(dy.float(), idx.cpu(), x.float(), scale, shift, mean, invstd, 1, sr, cnt, 3, 2, 1)
+    assert relerr(dx, dxr) < 2e-2
