@@ -82,9 +82,12 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        t0 = time.perf_counter()
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        # MIOpen's find pass at a new batch can run minutes: keep the log moving
+        print(f"warmup step {i}: {time.perf_counter() - t0:.1f}s", flush=True)
     t = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
