@@ -411,6 +411,31 @@ Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   return out;
 }
 
+// local (single-rank) BN: statistics + finalize without the [1,3,C] round trip -> (mean, invstd,
+// scale, shift); running stats updated in place.  Same numbers as bn_finalize(bn_stats(x)).
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, const optional<Tensor>& slabs,
+                                                             const optional<Tensor>& gamma,
+                                                             const optional<Tensor>& beta,
+                                                             const optional<Tensor>& run_mean,
+                                                             const optional<Tensor>& run_var, double momentum,
+                                                             double eps) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
+  const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
+  if (from_slabs)
+    TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 127) / 128 && slabs->size(1) == 2 && slabs->size(2) == C,
+                "slab shape");
+  auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
+  auto coef = at::empty({4, C}, f32_like(x));
+  float* cp = coef.data_ptr<float>();
+  dcp::launch_bn_stats_finalize(bp(x), from_slabs ? slabs->data_ptr<float>() : nullptr, M, C, part.data_ptr<float>(),
+                                (float)eps, fp(gamma), fp(beta), cp, cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean),
+                                fpm(run_var), (float)momentum, cur_stream());
+  return {coef[0], coef[1], coef[2], coef[3]};
+}
+
 Tensor colsum(const Tensor& x) {
   CHECK_ACT(x);
   const int C = x.size(-1);
@@ -933,6 +958,10 @@ TORCH_LIBRARY(dcp, m) {
         &grouped_conv_wgrad);
   m.def("bn_stats(Tensor x, Tensor? slabs) -> Tensor", &bn_stats);
   m.def("colsum(Tensor x) -> Tensor", &colsum);
+  m.def(
+      "bn_stats_finalize(Tensor x, Tensor? slabs, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, "
+      "float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      &bn_stats_finalize);
   m.def(
       "bn_finalize(Tensor stats, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, float momentum, "
       "float eps) -> (Tensor, Tensor, Tensor, Tensor)",

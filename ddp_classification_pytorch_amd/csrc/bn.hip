@@ -134,9 +134,9 @@ __global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* _
   }
 }
 
-// partials [P][3][C] -> out [3][C]; one workgroup per 64 channels, 4 waves split P
-__global__ void __launch_bounds__(256) bn_merge_kernel(const float* __restrict__ part, int P, int C,
-                                                       float* __restrict__ out) {
+// partials [P][3][C] -> (n, mean, M2) of channel blockIdx.x*64 + lane, complete in wave 0;
+// one workgroup per 64 channels, 4 waves split P
+__device__ __forceinline__ Welford merge_partials(const float* __restrict__ part, int P, int C) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
@@ -149,12 +149,56 @@ __global__ void __launch_bounds__(256) bn_merge_kernel(const float* __restrict__
   red[1][w][lane] = a.mean;
   red[2][w][lane] = a.m2;
   __syncthreads();
-  if (w == 0 && c < C) {
+  if (w == 0)
     for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+  return a;
+}
+
+// partials [P][3][C] -> out [3][C]
+__global__ void __launch_bounds__(256) bn_merge_kernel(const float* __restrict__ part, int P, int C,
+                                                       float* __restrict__ out) {
+  const Welford a = merge_partials(part, P, C);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) == 0 && c < C) {
     out[c] = a.n;
     out[C + c] = a.mean;
     out[2 * C + c] = a.m2;
   }
+}
+
+// merged (n, mean, M2) of channel c -> mean, invstd, scale, shift (+ running stats)
+__device__ __forceinline__ void finalize_channel(const Welford& a, int c, float eps, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float* __restrict__ mean,
+                                                 float* __restrict__ invstd, float* __restrict__ scale,
+                                                 float* __restrict__ shift, float* __restrict__ run_mean,
+                                                 float* __restrict__ run_var, float momentum) {
+  const float var = a.n > 0.f ? a.m2 / a.n : 0.f;
+  const float is = rsqrtf(var + eps);
+  mean[c] = a.mean;
+  invstd[c] = is;
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - a.mean * g * is;
+  if (run_mean) {
+    const float unb = a.n > 1.f ? a.m2 / (a.n - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * a.mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// local BN (one rank): partials [P][3][C] -> mean, invstd, scale, shift in one launch
+// (bn_merge + bn_finalize with W = 1; bit-identical to the two-kernel path)
+__global__ void __launch_bounds__(256) bn_merge_finalize_kernel(
+    const float* __restrict__ part, int P, int C, float eps, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
+    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+  const Welford m = merge_partials(part, P, C);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  Welford a{0.f, 0.f, 0.f};
+  a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
 }
 
 // [P][K] -> [K] column sums; one workgroup per 64 columns, 4 waves x 4-deep unroll over P
@@ -191,19 +235,7 @@ __global__ void bn_finalize_kernel(const float* __restrict__ st, int W, int C, f
   Welford a{0.f, 0.f, 0.f};
   for (int w = 0; w < W; ++w)
     a.merge(st[((size_t)w * 3 + 0) * C + c], st[((size_t)w * 3 + 1) * C + c], st[((size_t)w * 3 + 2) * C + c]);
-  const float var = a.n > 0.f ? a.m2 / a.n : 0.f;
-  const float is = rsqrtf(var + eps);
-  mean[c] = a.mean;
-  invstd[c] = is;
-  const float g = gamma ? gamma[c] : 1.f;
-  const float b = beta ? beta[c] : 0.f;
-  scale[c] = g * is;
-  shift[c] = b - a.mean * g * is;
-  if (run_mean) {
-    const float unb = a.n > 1.f ? a.m2 / (a.n - 1.f) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * a.mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
-  }
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
 }
 
 // eval / frozen BN: scale = gamma / sqrt(var + eps), shift = beta - mean*scale
@@ -498,19 +530,31 @@ int bn_stats_partials(int M, int C, bool from_slabs) {
   return g > 256 ? 256 : (g < 1 ? 1 : g);
 }
 
-// part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
-void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
+// first level of the statistics: part[P][3][C] from the conv slabs or the raw activations
+static int launch_stat_partials(const bf16* x, const float* slabs, int M, int C, float* part, hipStream_t s) {
+  const int P = bn_stats_partials(M, C, slabs != nullptr);
   if (slabs) {
     const int R = (M + 127) / 128;
-    const int P = bn_stats_partials(M, C, true);
     const int tps = (R + P - 1) / P;
     hipLaunchKernelGGL(bn_slab_partial_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps, part);
-    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
   } else {
-    const int P = bn_stats_partials(M, C, false);
     hipLaunchKernelGGL(chan_welford_partial_kernel, dim3(P), dim3(256), 3 * 2048 * 4, s, x, M, C, part);
-    hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
   }
+  return P;
+}
+
+// part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
+void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
+  const int P = launch_stat_partials(x, slabs, M, C, part, s);
+  hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
+}
+
+void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
+                              const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
+                              float* shift, float* rm, float* rv, float momentum, hipStream_t s) {
+  const int P = launch_stat_partials(x, slabs, M, C, part, s);
+  hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, eps, gamma, beta,
+                     mean, invstd, scale, shift, rm, rv, momentum);
 }
 
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s) {

@@ -68,6 +68,9 @@ bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* pa
 
 int bn_stats_partials(int M, int C, bool from_slabs);
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s);
+void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
+                              const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
+                              float* shift, float* rm, float* rv, float momentum, hipStream_t s);
 int colsum_partials(int M);
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s);
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,

@@ -188,6 +188,10 @@ def bn_finalize(stats, gamma, beta, run_mean, run_var, momentum, eps):
     return mu.float(), invstd.float(), scale.float(), shift.float()
 
 
+def bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, momentum, eps):
+    return bn_finalize(bn_stats(x, slabs), gamma, beta, run_mean, run_var, momentum, eps)
+
+
 def bn_eval_coeff(gamma, beta, run_mean, run_var, eps):
     invstd = torch.rsqrt(run_var.float() + eps)
     g = gamma.float() if gamma is not None else torch.ones_like(invstd)

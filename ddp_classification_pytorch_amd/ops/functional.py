@@ -363,6 +363,20 @@ class BNConfig:
         self.world = world
 
 
+def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
+    """Training-mode BN coefficients -> (mean, invstd, scale, shift, count).  Local BN runs the
+    statistics and the finalize as one launch pair; SyncBN all-gathers the per-rank
+    (n, mean, M2) between them."""
+    count = x.numel() // x.shape[-1]
+    if cfg.group is None:
+        return (*k.bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
+    st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
+    gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
+    dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+    count = count * cfg.world  # DistributedSampler keeps per-rank batches equal
+    return (*k.bn_finalize(gathered, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
+
+
 class _BNAct(Function):
     @staticmethod
     def forward(ctx, x, slabs, gamma, beta, res, run_mean, run_var, cfg: BNConfig, link, src):
@@ -370,13 +384,7 @@ class _BNAct(Function):
         C = x.shape[-1]
         count = x.numel() // C
         if cfg.training_stats:
-            st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
-            if cfg.group is not None:
-                gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
-                dist.all_gather_into_tensor(gathered, st, group=cfg.group)
-                st = gathered
-                count = count * cfg.world  # DistributedSampler keeps per-rank batches equal
-            mean, invstd, scale, shift = k.bn_finalize(st, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps)
+            mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
         else:
             mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
         y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
@@ -458,15 +466,7 @@ class _BNActPool(Function):
     @staticmethod
     def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig, pool):
         k = K(x)
-        C = x.shape[-1]
-        count = x.numel() // C
-        st = k.bn_stats(x, slabs)
-        if cfg.group is not None:
-            gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
-            dist.all_gather_into_tensor(gathered, st, group=cfg.group)
-            st = gathered
-            count = count * cfg.world
-        mean, invstd, scale, shift = k.bn_finalize(st, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps)
+        mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
         y, idx = k.bn_act_maxpool(x, scale, shift, cfg.act, *pool)
         ctx.save_for_backward(x, idx, scale, shift, mean, invstd)
         ctx.cfg, ctx.count, ctx.pool = cfg, count, pool

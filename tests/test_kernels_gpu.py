@@ -552,3 +552,23 @@ def test_bn_act_maxpool_fused(K, shape):
     dx = K.maxpool_bn_bwd_elemt(d(dy), idx, d(x), d(scale), d(shift), d(mean), d(invstd), 1, sums, cnt, 3, 2, 1)
     dxr = _ref.maxpool_bn_bwd_elemt(dy.float(), idx.cpu(), x.float(), scale, shift, mean, invstd, 1, sr, cnt, 3, 2, 1)
     assert relerr(dx, dxr) < 2e-2
+
+
+@pytest.mark.parametrize("slab", [False, True])
+def test_bn_stats_finalize_fused_bitwise(K, slab):
+    """Local-BN one-launch-pair path == bn_finalize(bn_stats(.)) bit for bit, running stats too."""
+    torch.manual_seed(0)
+    x = rnd(4, 14, 14, 64).to(DEV)
+    slabs = None
+    if slab:
+        w = rnd(128, 1, 1, 64, scale=0.125)
+        x, slabs = K.conv_fwd(x, w.to(DEV), 1, 0, True)
+    C = x.shape[-1]
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rm1, rv1 = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    ref = K.bn_finalize(K.bn_stats(x, slabs), g, b, rm1, rv1, 0.1, 1e-5)
+    out = K.bn_stats_finalize(x, slabs, g, b, rm2, rv2, 0.1, 1e-5)
+    for r, o in zip(ref, out):
+        assert torch.equal(r, o)
+    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
