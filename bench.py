@@ -107,7 +107,12 @@ def main(argv=None):
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    _ext.hip_ops()  # fail loudly if the gfx950 library is missing
+    kops = _ext.hip_ops()  # fail loudly if the gfx950 library is missing
+    # A/B experiments only: DCP_TUNE="idx=value,..." sets the kernel-config overrides
+    # (conv_igemm.hip g_tune: 0 BN tile, 1 LDS stages, 3 8-wave kernel)
+    for kv in filter(None, os.environ.get("DCP_TUNE", "").split(",")):
+        i, v = kv.split("=")
+        kops.set_tuning(int(i), int(v))
 
     torch.manual_seed(1234 + rank)
     model = build_bench_model(a).to(dev)
