@@ -51,7 +51,7 @@ def parse(argv=None):
     ap.add_argument("--image-size", type=int, default=None)
     ap.add_argument("--num-classes", type=int, default=None)
     ap.add_argument("--syncbn", action="store_true", help="cross-replica BN (reference default); off = local BN")
-    ap.add_argument("--bucket-cap-mb", type=float, default=100.0)
+    ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="DDP gradient all-reduce precision (bf16 = bf16_compress_hook: half the xGMI bytes)")
     ap.add_argument("--lr", type=float, default=0.1)

@@ -43,7 +43,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--dist-backend", default=None, help="nccl (=RCCL) on GPU, gloo on CPU")
     a("--syncbn", dest="syncbn", action="store_true", default=None, help="cross-replica BN (reference default)")
     a("--no-syncbn", dest="syncbn", action="store_false")
-    a("--bucket-cap-mb", type=float, default=100.0)
+    a("--bucket-cap-mb", type=float, default=25.0)
     a("--first-bucket-mb", type=float, default=4.0)
     a("--device", default=None, help="cuda (default when available) or cpu")
     # data
