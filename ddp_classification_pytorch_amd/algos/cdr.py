@@ -86,19 +86,24 @@ def run(args):
     from ..engine.runtime import build_data, setup
     from ..ops import functional as Fn
     from ..optim import MultiStepLR, build_optimizer
+    from ..parallel.ddp import wrap_ddp
     import os
 
     rt = setup(args)
     rotate_results_file(os.path.join(args.out_dir, "results_cdr.txt"))
     train_data, val_data, _, _ = build_data(args, rt)
     model = build_classifier(args, log_softmax=True).to(rt.device)
+    # one process per GPU: gradients are all-reduced by DDP before the mask, so every rank
+    # selects the same critical parameters from the global-batch gradient
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb)
     opt = build_optimizer("sgd", model.parameters(), args.lr, args.momentum, 0.0)
     sched = MultiStepLR(opt, milestones=args.milestones, gamma=args.gamma)
     C = args.num_classes
     state = {"epoch": 0}
 
     def fwd_train(batch):
-        return Fn.cross_entropy(model(batch[0]), batch[1], C, return_rank=True)
+        return Fn.cross_entropy(net(batch[0]), batch[1], C, return_rank=True)
 
     def fwd_eval(batch):
         return Fn.cross_entropy_rows(model(batch[0]), batch[1], C)
@@ -113,7 +118,7 @@ def run(args):
             return super().train_epoch(epoch)
 
     loop = _Loop(args, rt, {"model": model}, opt, sched, train_data, val_data, fwd_train, fwd_eval,
-                 post_backward=post_backward, scheduler_before_epoch=True)
+                 post_backward=post_backward, scheduler_before_epoch=True, train_modules=[net])
     best = loop.run()
     hist = loop.logger.history.get("val/top1", [])
     if rt.is_main and hist:  # the reference crashes on an empty list here (CDR/main.py:381)

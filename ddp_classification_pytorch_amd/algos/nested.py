@@ -35,6 +35,7 @@ from ..models.heads import NetClassifier
 from ..models.nested import NetFeat
 from ..ops import functional as Fn
 from ..optim import FusedSGD, MultiStepLR
+from ..parallel.ddp import wrap_ddp
 from ..utils.misc import AverageMeter, ProgressBar
 
 
@@ -125,6 +126,13 @@ def run(args):
                         weight_decay=args.weight_decay)
     opt_cls = FusedSGD(net_cls.parameters(), lr=1e-4, momentum=args.momentum, weight_decay=args.weight_decay)
     opts = [opt_feat, opt_cls]
+    # DDP over both networks (the reference runs NESTED single-GPU).  Frozen-BN gamma/beta stop
+    # requiring grad in train(freeze_bn=True), which must happen before DDP registers the
+    # parameters it all-reduces.
+    net_feat.train(True, freeze_bn=args.freeze_bn)
+    ddp_kw = dict(syncbn=False, bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
+    feat_net = wrap_ddp(net_feat, rt.local_rank, **ddp_kw)
+    cls_net = wrap_ddp(net_cls, rt.local_rank, **ddp_kw)
     rng = np.random.RandomState(args.seed + rt.rank)
     bar = ProgressBar(stream=None) if rt.is_main else None
 
@@ -144,7 +152,7 @@ def run(args):
             for o in opts:
                 for g in o.param_groups:
                     g["lr"] = lr
-            _step(net_feat, net_cls, opts, batch[0], batch[1], dist_k, args.dropout, nb_cls, rng)
+            _step(feat_net, cls_net, opts, batch[0], batch[1], dist_k, args.dropout, nb_cls, rng)
             if args.max_steps_per_epoch and n_iter >= args.max_steps_per_epoch:
                 n_iter = args.warmup_iters
                 break
@@ -186,7 +194,7 @@ def run(args):
         for i, batch in enumerate(train_data):
             if i >= n_steps:
                 break
-            loss, rank = _step(net_feat, net_cls, opts, batch[0], batch[1], dist_k, args.dropout, nb_cls, rng)
+            loss, rank = _step(feat_net, cls_net, opts, batch[0], batch[1], dist_k, args.dropout, nb_cls, rng)
             if (i + 1) % args.log_interval == 0 or i + 1 == n_steps:
                 B = rank.numel()
                 losses.update(loss.item(), B)

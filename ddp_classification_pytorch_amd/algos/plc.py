@@ -29,6 +29,7 @@ from ..engine.loop import ClassificationLoop
 from ..engine.runtime import build_data, setup
 from ..ops import functional as Fn
 from ..optim import FusedSGD
+from ..parallel.ddp import wrap_ddp
 
 
 def label_noise(targets, eta, noise_type=0, factor=1.2, rng=None):
@@ -98,9 +99,11 @@ def prob_correction(y_noise, f_x, random_state=0, current_delta=0.3, delta_incre
     return y, current_delta
 
 
-def eta_approximation(model, loader, n, num_classes, device, epochs=1, lr=0.01, log=print):
-    """Train ``model`` and return softmax posteriors [n, C] for every dataset index
-    (batches must yield (x, y, index))."""
+def eta_approximation(model, loader, n, num_classes, device, epochs=1, lr=0.01, log=print, net=None):
+    """Train ``model`` (forward through ``net``, its DDP wrapper, when given) and return
+    softmax posteriors [n, C] for every dataset index (batches must yield (x, y, index));
+    under DDP every rank fills the rows of its own shard and the table is all-reduced."""
+    net = net if net is not None else model
     opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, nesterov=True, weight_decay=5e-4)
     eta = torch.zeros(n, num_classes)
     for ep in range(epochs):
@@ -109,7 +112,7 @@ def eta_approximation(model, loader, n, num_classes, device, epochs=1, lr=0.01, 
         for x, y, idx in loader:
             if y.numel() == 1:
                 continue
-            logits = model(x)
+            logits = net(x)
             loss, rank = Fn.cross_entropy(logits, y, num_classes, return_rank=True)
             opt.zero_grad(set_to_none=True)
             loss.backward()
@@ -119,6 +122,13 @@ def eta_approximation(model, loader, n, num_classes, device, epochs=1, lr=0.01, 
             if ep == epochs - 1:
                 eta[idx.cpu()] = torch.softmax(logits.detach().float(), 1).cpu()
         log(f"Epoch [{ep + 1}|{epochs}] \t Train Acc {100.0 * correct / max(total, 1):.3f}")
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        # disjoint shards (plus identical DistributedSampler padding rows): sum and renormalise
+        dev = next(model.parameters()).device
+        e, c = eta.to(dev), (eta.sum(1) > 0).to(dev, torch.float32)
+        dist.all_reduce(e)
+        dist.all_reduce(c)
+        eta = (e / c.clamp_min(1).unsqueeze(1)).cpu()
     return eta
 
 
@@ -148,6 +158,8 @@ def run(args):
     logger = MetricsLogger(args.out_dir if rt.is_main else None)
     train_data, val_data, train_set, _ = build_data(args, rt)
     model = build_classifier(args).to(rt.device)
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb)
     opt = FusedSGD(model.parameters(), lr=args.lr, momentum=args.momentum, nesterov=True,
                    weight_decay=args.weight_decay)
     C = args.num_classes
@@ -159,7 +171,7 @@ def run(args):
     if args.plc_eta_epochs > 0:
         # synthetic feature-dependent noise from a posterior estimate (PLC/utils.py:149-288)
         eta = eta_approximation(model, train_data, n, C, rt.device, epochs=args.plc_eta_epochs, lr=args.lr,
-                                log=logger.line)
+                                log=logger.line, net=net)
         noisy, _ = label_noise(labels.cpu().numpy(), eta, args.plc_noise_type, rng=np.random.RandomState(args.seed))
         noisy = torch.as_tensor(noisy, device=rt.device)
         changed = int((noisy != labels).sum())
@@ -169,13 +181,13 @@ def run(args):
 
     def fwd_train(batch):
         x, idx = batch[0], batch[2]
-        return Fn.cross_entropy(model(x), labels[idx], C, return_rank=True)
+        return Fn.cross_entropy(net(x), labels[idx], C, return_rank=True)
 
     def fwd_eval(batch):
         return Fn.cross_entropy_rows(model(batch[0]), batch[1], C)
 
     loop = ClassificationLoop(args, rt, {"model": model}, opt, None, train_data, val_data, fwd_train, fwd_eval,
-                              logger=logger)
+                              logger=logger, train_modules=[net])
     for epoch in range(args.epochs):
         tr = loop.train_epoch(epoch)
         f_x = posteriors(model, train_data, n, C)

@@ -60,14 +60,26 @@ def barrier():
         dist.barrier()
 
 
+def _world():
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
 def save_checkpoint(path, models: dict, optimizers: dict = None, schedulers: dict = None, **extra):
-    """Rank-0 atomic write; all ranks sync on a barrier afterwards."""
+    """Rank-0 atomic write; all ranks sync on a barrier afterwards.  Every rank's RNG
+    state is gathered into the file (ranks are seeded seed+rank, so their augmentation /
+    dropout / nested-K streams differ) and :func:`load_checkpoint` restores each rank's own."""
+    per_rank = None
+    if _world() > 1:
+        per_rank = [None] * _world()
+        dist.all_gather_object(per_rank, rng_state())
     if is_rank0():
         os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
         state = {"models": {k: _unwrap(m).state_dict() for k, m in models.items()},
                  "optimizers": {k: o.state_dict() for k, o in (optimizers or {}).items()},
                  "schedulers": {k: s.state_dict() for k, s in (schedulers or {}).items()},
                  "rng": rng_state(), "format": "dcp-ckpt-v1"}
+        if per_rank is not None:
+            state["rng_per_rank"] = per_rank
         state.update(extra)
         tmp = f"{path}.tmp.{os.getpid()}"
         torch.save(state, tmp)
@@ -96,7 +108,14 @@ def load_checkpoint(path, models: dict, optimizers: dict = None, schedulers: dic
     for k, s in (schedulers or {}).items():
         if k in state["schedulers"]:
             s.load_state_dict(state["schedulers"][k])
-    if restore_rng and "rng" in state:
-        set_rng_state(state["rng"])
+    if restore_rng:
+        per_rank = state.get("rng_per_rank")
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        if per_rank is not None and len(per_rank) == _world():
+            set_rng_state(per_rank[rank])
+        elif "rng" in state and _world() == 1:
+            set_rng_state(state["rng"])
+        # a different world size than the one that wrote the file: keep this rank's own
+        # (seed + rank) stream rather than giving every rank rank 0's
     Fn.bump_weight_generation()
-    return {k: v for k, v in state.items() if k not in ("models", "optimizers", "schedulers", "rng")}
+    return {k: v for k, v in state.items() if k not in ("models", "optimizers", "schedulers", "rng", "rng_per_rank")}

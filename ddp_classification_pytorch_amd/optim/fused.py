@@ -64,40 +64,49 @@ class FusedSGD(torch.optim.Optimizer):
             if not params:
                 continue
             mom = group["momentum"]
-            first = False
+            # torch.optim.SGD initialises each momentum buffer to that parameter's first
+            # gradient: parameters seen for the first time step with first=True in their own
+            # launch, so a late-arriving gradient never resets the others' momentum
+            fresh = set()
             for p in params:
                 st = self.state[p]
                 if mom != 0 and "momentum_buffer" not in st:
                     st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    first = True
-            if params[0].is_cuda:
-                entries = []
-                for p in params:
-                    if not (p.is_contiguous() and p.grad.is_contiguous()):
-                        raise RuntimeError("FusedSGD needs contiguous params and grads")
-                    if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
-                        raise RuntimeError("FusedSGD expects fp32 master params and grads")
-                    buf = self.state[p].get("momentum_buffer")
-                    entries.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr() if buf is not None else 0, 0, 0,
-                                    p.numel()))
-                table, chunks = self._tables.setdefault(gi, _TableCache()).get(entries, params[0].device)
-                _ext.hip_ops().mt_sgd(table, chunks, group["lr"], mom, group["dampening"], group["weight_decay"],
-                                      group["nesterov"], first, group["grad_scale"])
-            else:
-                for p in params:
-                    g = p.grad * group["grad_scale"]
-                    if group["weight_decay"]:
-                        g = g + group["weight_decay"] * p
-                    if mom:
-                        buf = self.state[p]["momentum_buffer"]
-                        if first:
-                            buf.copy_(g)
-                        else:
-                            buf.mul_(mom).add_(g, alpha=1 - group["dampening"])
-                        g = g + mom * buf if group["nesterov"] else buf
-                    p.add_(g, alpha=-group["lr"])
+                    fresh.add(p)
+            for first, sub in ((True, [p for p in params if p in fresh]), (False, [p for p in params if p not in fresh])):
+                if sub:
+                    self._update(gi, group, sub, first)
         Fn.bump_weight_generation()
         return loss
+
+    def _update(self, gi, group, params, first):
+        mom = group["momentum"]
+        if params[0].is_cuda:
+            entries = []
+            for p in params:
+                if not (p.is_contiguous() and p.grad.is_contiguous()):
+                    raise RuntimeError("FusedSGD needs contiguous params and grads")
+                if p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                    raise RuntimeError("FusedSGD expects fp32 master params and grads")
+                buf = self.state[p].get("momentum_buffer")
+                entries.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr() if buf is not None else 0, 0, 0,
+                                p.numel()))
+            table, chunks = self._tables.setdefault((gi, first), _TableCache()).get(entries, params[0].device)
+            _ext.hip_ops().mt_sgd(table, chunks, group["lr"], mom, group["dampening"], group["weight_decay"],
+                                  group["nesterov"], first, group["grad_scale"])
+            return
+        for p in params:
+            g = p.grad * group["grad_scale"]
+            if group["weight_decay"]:
+                g = g + group["weight_decay"] * p
+            if mom:
+                buf = self.state[p]["momentum_buffer"]
+                if first:
+                    buf.copy_(g)
+                else:
+                    buf.mul_(mom).add_(g, alpha=1 - group["dampening"])
+                g = g + mom * buf if group["nesterov"] else buf
+            p.add_(g, alpha=-group["lr"])
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -125,30 +134,38 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] += 1
-            step = self.state[params[0]]["step"]
-            b1, b2 = group["betas"]
-            if params[0].is_cuda:
-                entries = []
-                for p in params:
-                    st = self.state[p]
-                    entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
-                                    st["exp_avg_sq"].data_ptr(), 0, p.numel()))
-                table, chunks = self._tables.setdefault(gi, _TableCache()).get(entries, params[0].device)
-                _ext.hip_ops().mt_adam(table, chunks, group["lr"], b1, b2, group["eps"], group["weight_decay"], step,
-                                       group["decoupled"], group["grad_scale"])
-            else:
-                bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
-                for p in params:
-                    st = self.state[p]
-                    g = p.grad * group["grad_scale"]
-                    if group["weight_decay"]:
-                        if group["decoupled"]:
-                            p.mul_(1 - group["lr"] * group["weight_decay"])
-                        else:
-                            g = g + group["weight_decay"] * p
-                    st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
-                    st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
-                    denom = st["exp_avg_sq"].sqrt() / math.sqrt(bc2) + group["eps"]
-                    p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / bc1)
+            # bias correction is per parameter (torch.optim.Adam): one launch per distinct step count
+            by_step = {}
+            for p in params:
+                by_step.setdefault(self.state[p]["step"], []).append(p)
+            for step, sub in sorted(by_step.items()):
+                self._update(gi, group, sub, step)
         Fn.bump_weight_generation()
         return loss
+
+    def _update(self, gi, group, params, step):
+        b1, b2 = group["betas"]
+        if params[0].is_cuda:
+            entries = []
+            for p in params:
+                st = self.state[p]
+                entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
+                                st["exp_avg_sq"].data_ptr(), 0, p.numel()))
+            table, chunks = self._tables.setdefault((gi, len(params), params[0].data_ptr()),
+                                                    _TableCache()).get(entries, params[0].device)
+            _ext.hip_ops().mt_adam(table, chunks, group["lr"], b1, b2, group["eps"], group["weight_decay"], step,
+                                   group["decoupled"], group["grad_scale"])
+            return
+        bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+        for p in params:
+            st = self.state[p]
+            g = p.grad * group["grad_scale"]
+            if group["weight_decay"]:
+                if group["decoupled"]:
+                    p.mul_(1 - group["lr"] * group["weight_decay"])
+                else:
+                    g = g + group["weight_decay"] * p
+            st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+            st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+            denom = st["exp_avg_sq"].sqrt() / math.sqrt(bc2) + group["eps"]
+            p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / bc1)

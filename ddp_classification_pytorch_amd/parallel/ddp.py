@@ -5,12 +5,15 @@ Reference: one process per GPU, ``SyncBatchNorm.convert_sync_batchnorm`` +
 ARCFACE/arc_main.py:238-243).
 
 MI355X choices:
-* 25 MB gradient buckets with a small first bucket.  ResNet-50's grads are
+* 25 MiB gradient buckets with a 4 MiB first bucket.  ResNet-50's grads are
   97.5 MB fp32 and most of them sit in layer4, whose gradients are ready
   first.  A 100 MB cap leaves one 89.7 MB bucket that can only start after
-  the stem's wgrad, fully exposed after backward.  25 MB gives
-  [7.8, 30.0, 25.0, 25.3, 9.3] MB: the first four overlap the backward of
-  layers 3..1, and only the 9.3 MB tail (~0.1 ms per xGMI ring) is exposed;
+  the stem's wgrad, fully exposed after backward.  With 25 MiB buckets the
+  all-reduces of layer4..layer2 overlap the backward of the layers below,
+  and only the last (layer1 + stem side) bucket is exposed; the small first
+  bucket starts the first all-reduce as soon as the head/layer4 tail
+  gradients exist.  The layout is pinned by tests/test_ddp_buckets_cpu.py
+  from the Reducer itself (``bucket_layout_mb``);
 * ``gradient_as_bucket_view=True`` (no grad->bucket copies);
 * ``broadcast_buffers=False``: BN running stats are either identical by
   construction (SyncBN) or rank-local (local BN), so the per-forward buffer
@@ -58,24 +61,45 @@ def convert_sync_batchnorm(model: nn.Module, process_group=None) -> nn.Module:
 
 
 def wrap_ddp(model: nn.Module, local_rank: int = None, syncbn: bool = False, bucket_cap_mb: float = 25.0,
-             first_bucket_mb: float = 4.0, find_unused: bool = False, static_graph: bool = False):
+             first_bucket_mb: float = 4.0, find_unused: bool = False, static_graph: bool = False,
+             force: bool = False):
+    """DDP over the default group (RCCL on GPU, gloo on CPU).
+
+    Bucket limits: torch's Reducer honours a separate first-bucket limit only when the
+    DDP constructor sees ``bucket_cap_mb=None`` (its 25 MiB default,
+    torch/nn/parallel/distributed.py:828-834, 1242-1247); an explicit cap is used for the
+    first bucket too.  So the default 25 MiB cap is passed as ``None`` with
+    ``dist._DEFAULT_FIRST_BUCKET_BYTES`` set for the constructor, and any other cap gives
+    uniform buckets.  ``bucket_layout_mb`` reports what was actually built.
+    ``force``: wrap even at world size 1 (tests)."""
     if syncbn:
         convert_sync_batchnorm(model)
-    if not dist.is_initialized() or dist.get_world_size() == 1 and not syncbn:
+    if not force and (not dist.is_initialized() or dist.get_world_size() == 1 and not syncbn):
         return model
-    kw = dict(broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
-              find_unused_parameters=find_unused, static_graph=static_graph)
+    default_cap = abs(float(bucket_cap_mb) - 25.0) < 1e-9
+    kw = dict(broadcast_buffers=False, bucket_cap_mb=None if default_cap else bucket_cap_mb,
+              gradient_as_bucket_view=True, find_unused_parameters=find_unused, static_graph=static_graph)
     if next(model.parameters()).is_cuda:
         kw["device_ids"] = [local_rank if local_rank is not None else torch.cuda.current_device()]
-    # first bucket size: read by the DDP constructor (torch/nn/parallel/distributed.py:1204,1242-1245)
     prev = getattr(dist, "_DEFAULT_FIRST_BUCKET_BYTES", None)
-    dist._DEFAULT_FIRST_BUCKET_BYTES = int(first_bucket_mb * 1024 * 1024)
+    if default_cap and first_bucket_mb:
+        dist._DEFAULT_FIRST_BUCKET_BYTES = int(first_bucket_mb * 1024 * 1024)
     try:
         ddp = nn.parallel.DistributedDataParallel(model, **kw)
     finally:
         if prev is not None:
             dist._DEFAULT_FIRST_BUCKET_BYTES = prev
     return ddp
+
+
+def bucket_layout_mb(ddp: nn.Module):
+    """Gradient bucket sizes (MiB, in all-reduce order) of a DDP module's Reducer.  The
+    layout is final after the first backward (DDP rebuilds buckets in gradient-ready order)."""
+    data = ddp._get_ddp_logging_data()
+    sizes = data.get("rebuilt_bucket_sizes") or data.get("bucket_sizes", "")
+    if isinstance(sizes, str):
+        sizes = [int(v) for v in sizes.split(",") if v.strip()]
+    return [v / 2**20 for v in sizes]
 
 
 def unwrap(model: nn.Module) -> nn.Module:

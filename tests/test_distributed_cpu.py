@@ -123,3 +123,47 @@ def test_entry_point_two_ranks_gloo():
         assert os.path.exists(os.path.join(d, "last.pth"))
         txt = open(os.path.join(d, "output.txt")).read()
         assert "(n=10)" in txt  # exact val count: sampler padding excluded
+
+
+def _workload_worker(rank, world, port, out_dir, workload):
+    """Run a workload under 2 gloo ranks and record, per rank, the final parameters of every
+    module it put under DDP (CDR / NESTED / PLC all-reduce their gradients)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import main as entry
+    from ddp_classification_pytorch_amd.algos import nested, plc
+    from ddp_classification_pytorch_amd.parallel import ddp as pddp
+
+    wrapped = []
+    orig = pddp.wrap_ddp
+
+    def recording_wrap(model, *a, **kw):
+        out = orig(model, *a, **kw)
+        wrapped.append((model, out))
+        return out
+
+    pddp.wrap_ddp = nested.wrap_ddp = plc.wrap_ddp = recording_wrap
+    common = ["--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10", "--batchsize", "4",
+              "--synthetic-train-size", "16", "--synthetic-val-size", "8", "--workers", "0", "--epochs", "1",
+              "--device", "cpu", "--out-dir", os.path.join(out_dir, f"run{rank}"), "--log-interval", "100"]
+    extra = {"cdr": [], "nested": ["--nested", "20", "--warmup-iters", "2"], "plc": ["--plc-eta-epochs", "1"]}
+    entry.main(["--workload", workload] + common + extra[workload])
+    assert wrapped and all(isinstance(d, torch.nn.parallel.DistributedDataParallel) for _, d in wrapped)
+    torch.save([{n: p.detach().clone() for n, p in m.named_parameters()} for m, _ in wrapped],
+               os.path.join(out_dir, f"params{rank}.pt"))
+
+
+@pytest.mark.parametrize("workload", ["cdr", "nested", "plc"])
+def test_noisy_label_workloads_stay_in_sync_under_ddp(workload):
+    """Ranks start from rank 0's weights (DDP broadcast) and apply all-reduced gradients, so
+    after training on different shards (and different seed+rank RNG streams) every rank
+    holds the same model."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_workload_worker, args=(2, _free_port(), d, workload), nprocs=2, join=True)
+        p0 = torch.load(os.path.join(d, "params0.pt"), weights_only=True)
+        p1 = torch.load(os.path.join(d, "params1.pt"), weights_only=True)
+    assert len(p0) == len(p1) >= 1
+    for a, b in zip(p0, p1):
+        assert a.keys() == b.keys()
+        for n in a:
+            assert torch.allclose(a[n], b[n], atol=1e-6, rtol=1e-5), n
