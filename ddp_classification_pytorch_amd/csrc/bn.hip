@@ -55,7 +55,9 @@ struct Welford {
 };
 
 // conv slabs [R][2][C] = per-128-row slab (mean, M2); slab r holds min(128, M-128r) rows.
-// out[blockIdx.y][3][C] = (n, mean, M2) over this split's tiles.
+// out[blockIdx.y][3][C] = (n, mean, M2) over this split's slabs (<= kSlabsPerSplit: 4 waves x
+// 16 merges, each wave's loads issued four slabs ahead of its merge chain).
+constexpr int kSlabsPerSplit = 64;
 __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __restrict__ slabs, int R, int M, int C,
                                                               int tiles_per_split, float* __restrict__ out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -64,7 +66,18 @@ __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __res
   const int r1 = min(R, r0 + tiles_per_split);
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
-    for (int r = r0 + w; r < r1; r += 4) {
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      float mb[4], m2b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
+    }
+    for (; r < r1; r += 4) {
       const float nb = (float)min(128, M - 128 * r);
       a.merge(nb, slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
     }
@@ -135,27 +148,39 @@ __global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* _
 }
 
 // partials [P][3][C] -> (n, mean, M2) of channel blockIdx.x*64 + lane, complete in wave 0;
-// one workgroup per 64 channels, 4 waves split P
+// one workgroup (kMergeWaves waves splitting P) per 64 channels
+constexpr int kMergeWaves = 16;
 __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part, int P, int C) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
-  if (c < C)
-    for (int p = w; p < P; p += 4)
+  if (c < C) {
+    int p = w;
+    for (; p + 3 * kMergeWaves < P; p += 4 * kMergeWaves) {
+      float v[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[u][q] = part[((size_t)(p + u * kMergeWaves) * 3 + q) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a.merge(v[u][0], v[u][1], v[u][2]);
+    }
+    for (; p < P; p += kMergeWaves)
       a.merge(part[((size_t)p * 3 + 0) * C + c], part[((size_t)p * 3 + 1) * C + c],
               part[((size_t)p * 3 + 2) * C + c]);
-  __shared__ float red[3][4][64];
+  }
+  __shared__ float red[3][kMergeWaves][64];
   red[0][w][lane] = a.n;
   red[1][w][lane] = a.mean;
   red[2][w][lane] = a.m2;
   __syncthreads();
   if (w == 0)
-    for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+    for (int k = 1; k < kMergeWaves; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
   return a;
 }
 
 // partials [P][3][C] -> out [3][C]
-__global__ void __launch_bounds__(256) bn_merge_kernel(const float* __restrict__ part, int P, int C,
+__global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_kernel(const float* __restrict__ part, int P, int C,
                                                        float* __restrict__ out) {
   const Welford a = merge_partials(part, P, C);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -189,7 +214,7 @@ __device__ __forceinline__ void finalize_channel(const Welford& a, int c, float 
 
 // local BN (one rank): partials [P][3][C] -> mean, invstd, scale, shift in one launch
 // (bn_merge + bn_finalize with W = 1; bit-identical to the two-kernel path)
-__global__ void __launch_bounds__(256) bn_merge_finalize_kernel(
+__global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_finalize_kernel(
     const float* __restrict__ part, int P, int C, float eps, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
     float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
@@ -522,8 +547,8 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
 int bn_stats_partials(int M, int C, bool from_slabs) {
   if (from_slabs) {
     const int R = (M + 127) / 128;
-    int splits = (R + 31) / 32;
-    return splits > 64 ? 64 : (splits < 1 ? 1 : splits);
+    int splits = (R + kSlabsPerSplit - 1) / kSlabsPerSplit;
+    return splits > 4096 ? 4096 : (splits < 1 ? 1 : splits);
   }
   const int rpi = 256 / (C / 8);
   int g = (M + rpi * 32 - 1) / (rpi * 32);
@@ -546,14 +571,14 @@ static int launch_stat_partials(const bf16* x, const float* slabs, int M, int C,
 // part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
-  hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
+  hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, out);
 }
 
 void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                               float* shift, float* rm, float* rv, float momentum, hipStream_t s) {
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
-  hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, eps, gamma, beta,
+  hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps, gamma, beta,
                      mean, invstd, scale, shift, rm, rv, momentum);
 }
 

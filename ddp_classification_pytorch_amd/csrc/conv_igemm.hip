@@ -234,6 +234,14 @@ tap_gemm_kernel(const TapGemmParams p) {
 
   const int tiles_per_tap = p.cpt >> 3;
   const int kc_total = p.ntaps * p.cpt;
+  // Narrow-channel path: a lane's tap index varies per lane, and a per-lane lookup in the
+  // kernel arguments is a vector memory load whose wait would drain the LDS-DMA ring every
+  // k-tile.  The table is copied once into LDS behind the stages instead (lgkm counter).
+  const int* tap_lds = (const int*)(smem + NS * STAGE);
+  if constexpr (!FAST) {
+    if (tid < p.ntaps) *LDS_PTR(int, smem + NS * STAGE + tid * 4) = p.tap[tid];
+    __syncthreads();
+  }
 
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STAGE;
@@ -266,7 +274,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         bool ok = a_ok[i] && kc < kc_total;
-        const int tv = p.tap[ok ? t : 0];
+        const int tv = *LDS_PTR(const int, tap_lds + (ok ? t : 0));
         const int hi = a_ys[i] + tap_dy(tv), wi = a_xs[i] + tap_dx(tv);
         ok = ok && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + ci0 : p.zero;
@@ -279,7 +287,8 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         const bool ok = b_ok[i] && kc < kc_total;
-        const bf16* g = ok ? p.wt + b_row[i] + (uint32_t)tap_w(p.tap[ok ? t : 0]) * p.Cs + ci0 : p.zero;
+        const bf16* g =
+            ok ? p.wt + b_row[i] + (uint32_t)tap_w(*LDS_PTR(const int, tap_lds + t)) * p.Cs + ci0 : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
                                          LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
       }
@@ -999,6 +1008,150 @@ wgrad256_kernel(const WgradParams p) {
   }
 }
 
+// 64 x 256 weight-gradient tile for Co <= 64 (the stem, stage-1 layers): the 128-row tiles
+// above leave half of every MFMA on zero rows there.  4 waves, each 64 co x 64 cols; the dY
+// image is [64 pixels][64 co] (128-byte rows), the im2col image [64 pixels][256 cols].
+// 128-byte rows put two rows in each 256-byte bank window, so the 32-byte pieces a
+// ds_read_b64_tr_b16 half-wave reads from rows {r..r+3, r+8..r+11} are spread by XOR-ing
+// the piece index with row bits 1 and 3 (conflict-free; chunk pairs stay adjacent).
+__device__ __forceinline__ uint32_t swz128tr(uint32_t r, uint32_t c) {
+  return r * 128u + ((c ^ ((((r >> 1) & 1u) | (((r >> 3) & 1u) << 1)) << 1)) << 4);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag128(const char* img, uint32_t row0, uint32_t col0, int lane) {
+  const uint32_t q = (lane & 15) >> 2, pp = lane & 3;
+  const uint32_t col = col0 + pp * 4;
+  const uint32_t o1 = swz128tr(row0 + q, col >> 3) + (col & 7) * 2;
+  const uint32_t o2 = swz128tr(row0 + 4 + q, col >> 3) + (col & 7) * 2;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o1));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, img + o2));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ void __launch_bounds__(256)
+wgrad64_kernel(const WgradParams p) {
+  constexpr int BK = 64;
+  constexpr int IMGA = BK * 128;  // 64 pixels x 64 co
+  constexpr int IMGB = BK * 512;  // 64 pixels x 256 cols
+  constexpr int STAGE = IMGA + IMGB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (p.ldw + 255) / 256;
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);  // see wgrad_kernel
+  const uint32_t split = lid / ntn;
+  const int tn = lid % ntn;
+  const int kcol0 = tn * 256;
+  const int mstart = split * p.rows_per_split;
+  const int mend = min(p.M, mstart + p.rows_per_split);
+  const int nkt = (mend - mstart + BK - 1) / BK;
+
+  // dY image: 2 LDS-DMA instructions per thread, instruction i covers rows (wave*2+i)*8 .. +7
+  uint32_t a_col[2];
+  bool a_cok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const uint32_t r = (wave * 2 + i) * 8 + (lane >> 3);
+    const uint32_t c = (lane & 7) ^ ((((r >> 1) & 1u) | (((r >> 3) & 1u) << 1)) << 1);
+    a_col[i] = c * 8;
+    a_cok[i] = (int)a_col[i] < p.Co;
+  }
+  // im2col image: 8 instructions per thread, instruction i covers rows (wave*8+i)*2 .. +1
+  int b_dy[8], b_dx[8];
+  uint32_t b_ci[8];
+  bool b_cok[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t r = (wave * 8 + i) * 2 + (lane >> 5);
+    const uint32_t c = (lane & 31) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
+    const int kc = kcol0 / 8 + c;
+    b_cok[i] = kc < p.kc_total;
+    const int t = b_cok[i] ? (int)fdiv(kc, p.div_cpt) : 0;
+    b_ci[i] = (kc - t * p.cpt) * 8;
+    b_dy[i] = p.dy_t[t];
+    b_dx[i] = p.dx_t[t];
+  }
+
+  auto stage = [&](int kt, int buf) {
+    char* Ai = smem + buf * STAGE;
+    char* Bi = Ai + IMGA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wave * 2 + i) * 8 + (lane >> 3);
+      const int m = mstart + kt * BK + r;
+      const bf16* ga = (m < mend && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 2 + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = (wave * 8 + i) * 2 + (lane >> 5);
+      const int m = mstart + kt * BK + r;
+      const bool mok = m < mend;
+      const uint32_t mm = mok ? m : 0;
+      const uint32_t q = fdiv(mm, p.div_wo);
+      const uint32_t x = mm - q * p.Wo;
+      const uint32_t n = fdiv(q, p.div_ho);
+      const uint32_t y = q - n * p.Ho;
+      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 8 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    const char* Ai = smem + buf * STAGE;
+    const char* Bi = Ai + IMGA;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t row0 = s * 32 + 8 * (lane >> 4);
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr_frag128(Ai, row0, i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag512(Bi, row0, wave * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nkt == 0) return;
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kcol = kcol0 + wave * 64 + j * 16 + (lane & 15);
+      if (kcol >= p.ldw) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = i * 16 + (lane >> 4) * 4 + r;
+        if (co < p.Co) {
+          if (p.part) p.part[((size_t)split * p.Co + co) * p.ldw + kcol] = acc[i][j][r];
+          else unsafeAtomicAdd(p.dw + (size_t)co * p.ldw + kcol, acc[i][j][r]);
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
@@ -1012,7 +1165,8 @@ static void launch_tg(const TapGemmParams& p, int grid, hipStream_t stream) {
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
   if (EPI == 1) epi = (size_t)128 * 2 * BN + 12 * BN;
   if (EPI == 3) epi = (size_t)128 * 2 * BN + 16384;
-  const size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
+  size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
+  if (!FAST) lds = std::max(lds, full + kMaxTaps * sizeof(int));  // LDS tap table behind the stages
   if (full > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
@@ -1146,15 +1300,22 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
 // 1x1 convs / linears (fewer, longer splits: less partial-slab traffic), ~4 for k x k
 // (measured per shape with tools/conv_bench.py --cfgs "5=2,5=4")
 static bool wgrad_big(int Co, int ldw) { return g_tune[7] != 2 && Co >= 256 && ldw >= 256; }
+// 64-row tiles: Co <= 64 with enough columns to fill 256-wide tiles at least half
+static bool wgrad_narrow(int Co, int ldw) { return g_tune[7] != 3 && Co <= 64 && ldw >= 128; }
+
+static int wgrad_tiles(int Co, int ldw) {
+  if (wgrad_narrow(Co, ldw)) return (ldw + 255) / 256;
+  const int bt = wgrad_big(Co, ldw) ? 256 : 128;
+  return ((Co + bt - 1) / bt) * ((ldw + bt - 1) / bt);
+}
 
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split) {
   const bool big = wgrad_big(Co, ldw);
-  const int bt = big ? 256 : 128;
-  const int ntm = (Co + bt - 1) / bt, ntn = (ldw + bt - 1) / bt;
-  const int tiles = ntm * ntn;
-  const int per_cu = big ? 1 : (taps == 1 ? 2 : 4);
+  const int tiles = wgrad_tiles(Co, ldw);
+  const int per_cu = (big || wgrad_narrow(Co, ldw)) ? (big ? 1 : 2) : (taps == 1 ? 2 : 4);
   const int target = (g_tune[5] > 0 ? g_tune[5] : per_cu) * num_cu;
-  int splits = (target + tiles - 1) / tiles;
+  // floor: a grid just past a whole number of resident rounds leaves a tail round of one block
+  int splits = target / tiles;
   int max_splits = (M + 255) / 256;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1179,8 +1340,8 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
   const bool big = wgrad_big(Co, p.ldw);
-  const int bt = big ? 256 : 128;
-  const int tiles = ((Co + bt - 1) / bt) * ((p.ldw + bt - 1) / bt);
+  const bool narrow = wgrad_narrow(Co, p.ldw);
+  const int tiles = wgrad_tiles(Co, p.ldw);
   p.ablate = g_tune[2];
   if (g_tune[6] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
   int rps = 0;
@@ -1192,7 +1353,10 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   if (splits == 1) {
     p.part = dw;  // split 0 stores straight into dw
   }
-  if (big) {
+  if (narrow) {
+    constexpr int lds = 2 * 64 * (128 + 512);
+    hipLaunchKernelGGL(wgrad64_kernel, dim3(tiles * splits), dim3(256), lds, stream, p);
+  } else if (big) {
     constexpr int lds = 4 * 64 * 512;
     static bool attr = false;
     if (!attr) {
