@@ -37,7 +37,7 @@
 
 namespace dcp {
 
-int g_tune[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int g_tune[16] = {0};
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
@@ -72,6 +72,17 @@ __device__ __forceinline__ int tap_w(int v) { return (v >> 16) & 0xffff; }
 // byte offset of logical 16B chunk `c` of row `r` in a 128-byte-row image
 __device__ __forceinline__ uint32_t swz128(uint32_t r, uint32_t c) {
   return r * 128u + ((c ^ ((r >> 1) & 7u)) << 4);
+}
+// k-tile images of BK bf16 per row: 128-byte rows (BK = 64) or 64-byte rows (BK = 32); the
+// XOR of the chunk with row bits 1.. makes the 16x16x32 fragment reads (ds_read_b128, 16-lane
+// groups over 16 rows) bank-conflict free in both
+template <int BK>
+__device__ __forceinline__ uint32_t swz_chunk(uint32_t r) {
+  return BK == 64 ? ((r >> 1) & 7u) : ((r >> 1) & 3u);
+}
+template <int BK>
+__device__ __forceinline__ uint32_t swzk(uint32_t r, uint32_t c) {
+  return r * (BK * 2u) + ((c ^ swz_chunk<BK>(r)) << 4);
 }
 
 // Per 128-row slab and channel of the LDS output image E[rows][BN] (16-byte chunks
@@ -177,13 +188,18 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // NS: LDS stages.  NS = 2: double buffer, vmcnt(0) + barrier per k-tile (several blocks per
 // CU hide the latency).  NS > 2 (FAST only): a ring whose LDS-DMA loads stay in flight across
 // the raw s_barrier, drained by a counted vmcnt -- for deep-K shapes at one block per CU.
-template <int BN, int EPI, bool FAST, int NS = 2>
+template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64>
 __global__ void __launch_bounds__(256)
 tap_gemm_kernel(const TapGemmParams p) {
   static_assert(NS == 2 || FAST, "the LDS ring needs the one-tap-per-k-tile path");
+  static_assert(BK == 64 || BK == 32, "k-tile depth");
   constexpr int BM = 128;                 // pixel rows per block
-  constexpr int A_BYTES = BM * 128;       // 64 k (bf16) per row
-  constexpr int B_BYTES = BN * 128;
+  constexpr int ROWB = BK * 2;            // bytes per image row (BK bf16)
+  constexpr int CH = BK / 8;              // 16-byte chunks per row
+  constexpr int RPI = 64 / CH;            // image rows per LDS-DMA wave instruction
+  constexpr int AI = BM / (4 * RPI);      // A-image LDS-DMA instructions per thread per k-tile
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int B_BYTES = BN * ROWB;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int TN = BN / 32;             // 16-wide co subtiles per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -199,14 +215,14 @@ tap_gemm_kernel(const TapGemmParams p) {
   const uint32_t tn = bid % ntn, tm = bid / ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // ---- per-thread A-load rows (4 glds per k-tile) ----
-  uint32_t a_pix[4];   // n*Hs*Ws
-  int a_ys[4], a_xs[4];
-  uint32_t a_chunk[4];
-  bool a_ok[4];
+  // ---- per-thread A-load rows (AI glds per k-tile) ----
+  uint32_t a_pix[AI];   // n*Hs*Ws
+  int a_ys[AI], a_xs[AI];
+  uint32_t a_chunk[AI];
+  bool a_ok[AI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (wave * 4 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * RPI + lane / CH;
     const int m = m0 + r;
     a_ok[i] = m < p.M;
     const uint32_t mm = a_ok[i] ? m : 0;
@@ -217,22 +233,22 @@ tap_gemm_kernel(const TapGemmParams p) {
     a_pix[i] = n * (uint32_t)(p.Hs * p.Ws);
     a_ys[i] = y * p.ss;
     a_xs[i] = x * p.ss;
-    a_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+    a_chunk[i] = (lane % CH) ^ swz_chunk<BK>(r);
   }
   // ---- per-thread B-load rows ----
-  constexpr int BI = BN / 32;  // glds per thread for B
+  constexpr int BI = BN / (4 * RPI);  // glds per thread for B
   uint32_t b_row[BI];
   uint32_t b_chunk[BI];
   bool b_ok[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
-    const int r = (wave * BI + i) * 8 + (lane >> 3);
+    const int r = (wave * BI + i) * RPI + lane / CH;
     b_ok[i] = (n0 + r) < p.Co;
     b_row[i] = (uint32_t)(n0 + r) * p.ldw;
-    b_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
+    b_chunk[i] = (lane % CH) ^ swz_chunk<BK>(r);
   }
 
-  const int tiles_per_tap = p.cpt >> 3;
+  const int tiles_per_tap = p.cpt / CH;
   const int kc_total = p.ntaps * p.cpt;
   // Narrow-channel path: a lane's tap index varies per lane, and a per-lane lookup in the
   // kernel arguments is a vector memory load whose wait would drain the LDS-DMA ring every
@@ -248,18 +264,18 @@ tap_gemm_kernel(const TapGemmParams p) {
     char* Bs = As + A_BYTES;
     if constexpr (FAST) {
       const int t = kt / tiles_per_tap;
-      const int cbase = (kt - t * tiles_per_tap) * 64;
+      const int cbase = (kt - t * tiles_per_tap) * BK;
       const int tv = p.tap[t];
       const int dy = tap_dy(tv), dx = tap_dx(tv);
       const uint32_t wofs = (uint32_t)tap_w(tv) * p.Cs + cbase;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < AI; ++i) {
         const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
         const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8
                            : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
-                                         LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+                                         LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
@@ -269,8 +285,8 @@ tap_gemm_kernel(const TapGemmParams p) {
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int kc = kt * 8 + a_chunk[i];
+      for (int i = 0; i < AI; ++i) {
+        const int kc = kt * CH + a_chunk[i];
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         bool ok = a_ok[i] && kc < kc_total;
@@ -279,11 +295,11 @@ tap_gemm_kernel(const TapGemmParams p) {
         ok = ok && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + ci0 : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
-                                         LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+                                         LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
-        const int kc = kt * 8 + b_chunk[i];
+        const int kc = kt * CH + b_chunk[i];
         const int t = fdiv(kc, p.div_cpt);
         const int ci0 = (kc - t * p.cpt) * 8;
         const bool ok = b_ok[i] && kc < kc_total;
@@ -304,18 +320,18 @@ tap_gemm_kernel(const TapGemmParams p) {
   const int nkt = p.nkt;
   auto compute = [&](const char* As, const char* Bs) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       const uint32_t c = s * 4 + (lane >> 4);
       bf16x8 wf[TN], af[4];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const uint32_t r = wn * (BN / 2) + j * 16 + (lane & 15);
-        wf[j] = *(const bf16x8*)(Bs + swz128(r, c));
+        wf[j] = *(const bf16x8*)(Bs + swzk<BK>(r, c));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t r = wm * 64 + i * 16 + (lane & 15);
-        af[i] = *(const bf16x8*)(As + swz128(r, c));
+        af[i] = *(const bf16x8*)(As + swzk<BK>(r, c));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -339,7 +355,7 @@ tap_gemm_kernel(const TapGemmParams p) {
       __syncthreads();
     }
   } else {
-    constexpr int LPT = 4 + BI;  // LDS-DMA instructions per thread per k-tile
+    constexpr int LPT = AI + BI;  // LDS-DMA instructions per thread per k-tile
 #pragma unroll
     for (int i = 0; i < NS - 1; ++i)
       if (i < nkt) stage(i, i);
@@ -1155,11 +1171,12 @@ wgrad64_kernel(const WgradParams p) {
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-template <int BN, int EPI, bool FAST, int NS>
-static void launch_tg(const TapGemmParams& p, int grid, hipStream_t stream) {
+template <int BN, int EPI, bool FAST, int NS, int BK = 64>
+static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
+  p.nkt = (p.ntaps * p.cpt + BK / 8 - 1) / (BK / 8);
   // LDS: the stages the k-loop actually uses (short-K shapes -- 1x1 convs with 64 input
   // channels -- need one, which lets more workgroups share a CU) or the epilogue image
-  const size_t stage = (size_t)(128 + BN) * 128;
+  const size_t stage = (size_t)(128 + BN) * BK * 2;
   const size_t full = (size_t)NS * stage;
   size_t epi = 0;
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
@@ -1170,12 +1187,12 @@ static void launch_tg(const TapGemmParams& p, int grid, hipStream_t stream) {
   if (full > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)full);
+      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
       attr = true;
     }
   }
-  hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS>), dim3(grid), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK>), dim3(grid), dim3(256), lds, stream, p);
 }
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
@@ -1216,6 +1233,12 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   if (env_bn > 0 && fast) bn = env_bn;
   if (env_ns > 0 && fast) ns = env_ns;
   if (!fast) ns = 2;
+  // 1x1 shapes with K <= 1024 and 128-channel tiles: 32-deep k-tiles in a 3-stage ring (48 KB,
+  // three workgroups per CU, loads two k-tiles ahead across raw barriers) beat the 64-deep double
+  // buffer (two per CU) by 5-20 %; 3x3 and deep-K shapes keep the latter (tools/conv_bench.py
+  // --cfgs "1=3;8=32" per-shape A/B).  g_tune[8] = 32 forces the ring (with [1] = 3 or 4), 64 disables it.
+  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs <= 1024 && bn == 128) ns = 3;
+  const bool bk32 = fast && (ns == 3 || ns == 4) && (g_tune[8] == 32 || (env_ns == 0 && g_tune[8] != 64));
   const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
   if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
@@ -1231,9 +1254,11 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     return;
   }
   const int grid = ntm * ((Co + bn - 1) / bn);
-#define DCP_TG_NS(BN_, EPI_, FAST_)                                           \
-  if (ns == 2) launch_tg<BN_, EPI_, FAST_, 2>(p, grid, stream);               \
-  else if (ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3>(p, grid, stream); \
+#define DCP_TG_NS(BN_, EPI_, FAST_)                                                    \
+  if (bk32 && ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3, 32>(p, grid, stream);  \
+  else if (bk32 && ns == 4) launch_tg<BN_, EPI_, (FAST_ || true), 4, 32>(p, grid, stream); \
+  else if (ns == 2) launch_tg<BN_, EPI_, FAST_, 2>(p, grid, stream);                   \
+  else if (ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3>(p, grid, stream);          \
   else launch_tg<BN_, EPI_, (FAST_ || true), 4>(p, grid, stream);
 #define DCP_TG_EPI(BN_, FAST_)                     \
   if (epi == 0) { DCP_TG_NS(BN_, 0, FAST_) }       \

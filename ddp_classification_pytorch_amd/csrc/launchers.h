@@ -9,8 +9,10 @@ typedef __bf16 bf16;
 namespace dcp {
 
 // tuning switches for in-process A/B experiments (tools/conv_bench.py --cfgs); all 0 = defaults
-// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant, [5] wgrad blocks per CU, [6] wgrad atomics, [7] 256-tile wgrad (0 auto, 1 on, 2 off)
-extern int g_tune[8];
+// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant,
+// [5] wgrad blocks per CU, [6] wgrad atomics, [7] wgrad tile (0 auto, 2 no 256-tile, 3 no 64-row tile),
+// [8] conv k-tile depth (32 with [1] = 3 or 4)
+extern int g_tune[16];
 
 constexpr int kMaxTaps = 64;
 

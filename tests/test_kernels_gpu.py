@@ -572,3 +572,57 @@ def test_bn_stats_finalize_fused_bitwise(K, slab):
     for r, o in zip(ref, out):
         assert torch.equal(r, o)
     assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+
+
+@pytest.mark.parametrize("cfg", [((1, 3), (8, 32)), ((1, 4), (8, 32)), ((1, 3),)])
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
+                                   (3, 9, 11, 64, 72, 3, 1, 1), (2, 56, 56, 64, 256, 1, 1, 0)])
+def test_conv_pipeline_variants(K, cfg, shape):
+    """Every tap-GEMM pipeline variant (k-tile depth 32/64, 2-4 LDS stages) against the
+    fp32 reference: forward with statistics, data gradient, fused BN-backward data gradient."""
+    N, H, W, Ci, Co, k, s, p = shape
+    x = rnd(N, H, W, Ci)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co)
+    wb, wt = K.weight_prep(w.float().to(DEV), 0, True)
+    try:
+        for i, v in cfg:
+            K.set_tuning(i, v)
+        y, slabs = K.conv_fwd(x.to(DEV), wb, s, p, True)
+        dx = K.conv_dgrad(dy.to(DEV), wt, H, W, s, p)
+        torch.cuda.synchronize()
+    finally:
+        for i, _ in cfg:
+            K.set_tuning(i, 0)
+    yr, _ = _ref.conv_fwd(x.float(), w.float(), s, p, False)
+    assert relerr(y, yr) < 1e-2
+    st = K.bn_stats(y, slabs)
+    sr = _ref.bn_stats(y.float().cpu(), None)
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4 and relerr(st[0, 2], sr[0, 2]) < 1e-4
+    dxr = _ref.conv_dgrad(dy.float(), w.float().permute(3, 1, 2, 0), H, W, s, p)
+    assert relerr(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [((1, 3), (8, 32)), ((1, 4), (8, 32))])
+def test_conv_dgrad_bn_pipeline_variants(K, cfg):
+    """The fused BN-backward dgrad epilogue behind the 32-deep ring variants equals the
+    default pipeline's result (same fp32 reference tolerance)."""
+    torch.manual_seed(1)
+    N, H, Ci, Co, k = 2, 14, 256, 128, 3
+    w = torch.randn(Co, k, k, Ci) / (k * k * Ci) ** 0.5
+    _, wt = K.weight_prep(w.to(DEV), 0, True)
+    args = [rnd(N, H, H, Co).to(DEV), wt, 1, rnd(N, H, H, Ci).to(DEV), (rnd(N, H, H, Ci, scale=2.0) + 0.5).to(DEV),
+            rnd(N, H, H, Ci).to(DEV), (torch.rand(Ci) + 0.5).to(DEV), (torch.randn(Ci) * 0.3).to(DEV),
+            (torch.randn(Ci) * 0.2 + 0.5).to(DEV), (torch.rand(Ci) + 0.5).to(DEV), 1]
+    g0, s0 = K.conv_dgrad_bn(*args)
+    try:
+        for i, v in cfg:
+            K.set_tuning(i, v)
+        g1, s1 = K.conv_dgrad_bn(*args)
+        torch.cuda.synchronize()
+    finally:
+        for i, _ in cfg:
+            K.set_tuning(i, 0)
+    assert relerr(g1, g0) < 1e-2
+    assert relerr(s1[0], s0[0]) < 2e-2 and relerr(s1[1], s0[1]) < 2e-2
