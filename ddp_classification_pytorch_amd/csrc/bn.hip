@@ -337,7 +337,7 @@ template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, bf16* __restrict__ y,
-                                                         int M, int C, float slope) {
+                                                         int M, int C, float slope, int nt) {
   const RowTile t(C);
   if (t.slot >= t.rpi) return;
   float sc[8], sh[8];
@@ -363,7 +363,8 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
         if (RES) z += bf2f(r[u][k]);
         o[k] = f2bf(act_f(z, ACT, slope));
       }
-      *(bf16x8*)(y + (size_t)(m + u * step) * C + t.c0) = o;
+      if (nt) __builtin_nontemporal_store(o, (bf16x8*)(y + (size_t)(m + u * step) * C + t.c0));
+      else *(bf16x8*)(y + (size_t)(m + u * step) * C + t.c0) = o;
     }
   }
   for (; m < M; m += step) {
@@ -640,11 +641,19 @@ static inline int rows_grid(int M, int C, int rows_per_thread, int cap) {
     }                                                                                               \
   } while (0)
 
+// Elementwise grid: two rows per thread and no practical cap on the workgroup count.  Measured
+// on the R50 b512 stage-1/2 tensors (tools/ew_bench.py): 5.7-6.0 TB/s against 4.5 TB/s for a
+// 4096-workgroup grid-stride loop over 8 rows per thread -- HBM wants the whole tensor's loads
+// spread over many short-lived waves.  g_tune[9] / [10] override cap / rows (A/B only).
+static inline dim3 ew_grid(int M, int C) {
+  return dim3(rows_grid(M, C, g_tune[10] > 0 ? g_tune[10] : 2, g_tune[9] > 0 ? g_tune[9] : (1 << 20)));
+}
+
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
                        size_t numel, int C, int act, float slope, hipStream_t s) {
   const int M = (int)(numel / C);
-  const dim3 grid(rows_grid(M, C, 8, 4096));
-  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope);
+  const dim3 grid = ew_grid(M, C);
+  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[11]);
 }
 
 int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }
@@ -663,7 +672,7 @@ void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const f
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
                          int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s) {
   const int M = (int)(numel / C);
-  const dim3 grid(rows_grid(M, C, 8, 4096));
+  const dim3 grid = ew_grid(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_elemt_kernel, grid, 0, s, res, act, dy, x, res, scale, shift, mean, invstd, sums,
                        inv_count, M, C, slope, dx, dres);
 }

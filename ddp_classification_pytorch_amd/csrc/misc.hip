@@ -9,6 +9,9 @@
 //   * nested_eval: best-K search of TestNested (NESTED/train.py:103-166, K19)
 //     as a prefix-cumulative classifier, with per-K top-1/top-3 counters and
 //     nothing materialised (the reference builds a [feat_dim, B, C] tensor).
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.cuh"
 #include "launchers.h"
 
@@ -207,12 +210,12 @@ __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict
     mu[c] = (c < C && mean) ? mean[c] : 0.f;
     is[c] = (c < C && stdv) ? 1.f / stdv[c] : 1.f;
   }
-  for (size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x; pix < total;
-       pix += (size_t)gridDim.x * blockDim.x) {
-    const int j = (int)(pix % Wo);
-    const size_t q = pix / Wo;
-    const int i = (int)(q % Ho);
-    const size_t n = q / Ho;
+  // 32-bit index math (the host checks total < 2^31): 64-bit division is emulated on the GPU
+  for (uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x; pix < (uint32_t)total; pix += gridDim.x * blockDim.x) {
+    const int j = (int)(pix % (uint32_t)Wo);
+    const uint32_t q = pix / (uint32_t)Wo;
+    const int i = (int)(q % (uint32_t)Ho);
+    const size_t n = q / (uint32_t)Ho;
     bf16 o[OC];
 #pragma unroll
     for (int py = 0; py < S; ++py)
@@ -235,7 +238,7 @@ __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict
       bf16x8 w;
 #pragma unroll
       for (int e = 0; e < 8; ++e) w[e] = o[k * 8 + e];
-      *(bf16x8*)(dst + pix * OC + k * 8) = w;
+      *(bf16x8*)(dst + (size_t)pix * OC + k * 8) = w;
     }
   }
 }
@@ -243,8 +246,12 @@ __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict
 void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
                         const float* mean, const float* stdv, bf16* dst, hipStream_t s) {
   size_t total = (size_t)N * (H / 2) * (W / 2);
+  if (total >= (1ull << 31)) {
+    fprintf(stderr, "to_nhwc_s2d: %zu output pixels exceed the 32-bit index range\n", total);
+    abort();
+  }
   size_t g = (total + 255) / 256;
-  if (g > 16384) g = 16384;
+  if (g > (1u << 20)) g = 1u << 20;
   hipLaunchKernelGGL((to_nhwc_pix_kernel<2, 4>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
                      in_scale, mean, stdv, dst);
 }
@@ -253,8 +260,12 @@ void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, i
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s) {
   if (Cp == 8 && C <= 8) {
     size_t total = (size_t)N * H * W;
+    if (total >= (1ull << 31)) {
+      fprintf(stderr, "to_nhwc: %zu pixels exceed the 32-bit index range\n", total);
+      abort();
+    }
     size_t g = (total + 255) / 256;
-    if (g > 16384) g = 16384;
+    if (g > (1u << 20)) g = 1u << 20;
     hipLaunchKernelGGL((to_nhwc_pix_kernel<1, 8>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
                        in_scale, mean, stdv, dst);
     return;

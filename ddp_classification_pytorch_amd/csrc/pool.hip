@@ -294,9 +294,11 @@ __global__ void __launch_bounds__(256) s2d_kernel(const bf16* __restrict__ x, bf
   }
 }
 
+// one (pixel, 8-channel chunk) per thread: the memory-bound passes reach HBM rate only with
+// the whole tensor's loads spread over many short-lived waves (see bn.hip ew_grid)
 static inline int ew_grid2(size_t n) {
   size_t g = (n + 255) / 256;
-  if (g > 8192) g = 8192;
+  if (g > (1u << 20)) g = 1u << 20;
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -322,7 +324,7 @@ void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int 
                        Ho, Wo, k, s, p, scale, shift, act, dv);
 }
 
-int maxpool_bn_bwd_blocks() { return 2048; }
+int maxpool_bn_bwd_blocks() { return 8192; }
 
 void launch_maxpool_bn_bwd(const bf16* dy, const uint8_t* idx, const bf16* x, int N, int H, int W, int C, int Ho,
                            int Wo, int k, int s, int p, const float* scale, const float* shift, const float* mean,
