@@ -190,7 +190,8 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
 // input gradient g' [N,H,W,C] and the per-channel sums [2,C] = (sum g', sum g'*xhat).
 std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int64_t pad, const optional<Tensor>& add,
                                          const Tensor& y, const optional<Tensor>& res, const Tensor& scale,
-                                         const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act) {
+                                         const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act,
+                                         const optional<Tensor>& mask) {
   CHECK_ACT(dy);
   CHECK_ACT(wt);
   CHECK_ACT(y);
@@ -221,6 +222,14 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
     TORCH_CHECK(res->sizes() == dx.sizes(), "conv_dgrad_bn residual shape");
     resp = bp(*res);
   }
+  const uint8_t* maskp = nullptr;
+  if (mask.has_value()) {
+    CHECK_DEV(*mask);
+    CHECK_CONTIG(*mask);
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() * 8 == dx.numel(),
+                "conv_dgrad_bn: mask must be uint8 [N,H,W,C/8]");
+    maskp = mask->data_ptr<uint8_t>();
+  }
   const int M = N * H * W;
   const int ntm = (M + 127) / 128;
   // per-tile partials + room for the chunk sums of the two-level deterministic reduce
@@ -237,7 +246,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
       t.widx[i] = i;
     }
   dcp::BnBwdEpi e{bp(y), resp, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
-                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act};
+                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act, maskp};
   auto st = cur_stream();
   dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr, nullptr,
                        0, zero_page(dy.get_device()), st, addp, &e);
@@ -491,6 +500,26 @@ Tensor bn_act(const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
   dcp::launch_bn_act_fwd(bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
                          shift.data_ptr<float>(), bpm(y), x.numel(), C, act, (float)slope, cur_stream());
   return y;
+}
+
+// bn_act plus the activation mask act'(z) > 0 as bits: uint8 [..., C/8], bit e of byte c = channel 8c+e
+std::tuple<Tensor, Tensor> bn_act_mask(const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
+                                       const Tensor& shift, int64_t act, double slope) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && scale.numel() == C, "bn_act_mask shapes (C % 8 == 0, C <= 2048)");
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+  }
+  auto y = at::empty_like(x);
+  std::vector<int64_t> ms = x.sizes().vec();
+  ms.back() = C / 8;
+  auto mask = at::empty(ms, x.options().dtype(at::kByte));
+  dcp::launch_bn_act_fwd(bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
+                         shift.data_ptr<float>(), bpm(y), x.numel(), C, act, (float)slope, cur_stream(),
+                         mask.data_ptr<uint8_t>());
+  return {y, mask};
 }
 
 Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
@@ -945,7 +974,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);
   m.def(
       "conv_dgrad_bn(Tensor dy, Tensor wt, int pad, Tensor? add, Tensor y, Tensor? res, Tensor scale, Tensor shift, "
-      "Tensor mean, Tensor invstd, int act) -> (Tensor, Tensor)",
+      "Tensor mean, Tensor invstd, int act, Tensor? mask=None) -> (Tensor, Tensor)",
       &conv_dgrad_bn);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, int act) -> Tensor", &linear_fwd);
@@ -971,6 +1000,8 @@ TORCH_LIBRARY(dcp, m) {
       "Tensor, Tensor)",
       &bn_eval_coeff);
   m.def("bn_act(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> Tensor", &bn_act);
+  m.def("bn_act_mask(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> (Tensor, Tensor)",
+        &bn_act_mask);
   m.def(
       "bn_bwd_reduce(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, int "
       "act, float slope) -> Tensor",

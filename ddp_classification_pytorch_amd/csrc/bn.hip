@@ -337,7 +337,10 @@ template <int ACT, bool RES>
 __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, bf16* __restrict__ y,
-                                                         int M, int C, float slope, int nt) {
+                                                         int M, int C, float slope, int nt,
+                                                         uint8_t* __restrict__ mask) {
+  // mask != nullptr: also store act'(z) > 0 as one bit per element ([M][C/8] bytes), so the
+  // backward of a BN + residual + ReLU layer reads 1/16 of the residual's bytes for its mask
   const RowTile t(C);
   if (t.slot >= t.rpi) return;
   float sc[8], sh[8];
@@ -357,14 +360,17 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       bf16x8 o;
+      uint32_t bits = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float z = bf2f(v[u][k]) * sc[k] + sh[k];
         if (RES) z += bf2f(r[u][k]);
+        bits |= (z > 0.f ? 1u : 0u) << k;
         o[k] = f2bf(act_f(z, ACT, slope));
       }
       if (nt) __builtin_nontemporal_store(o, (bf16x8*)(y + (size_t)(m + u * step) * C + t.c0));
       else *(bf16x8*)(y + (size_t)(m + u * step) * C + t.c0) = o;
+      if (mask) mask[(size_t)(m + u * step) * t.cpr + t.ch] = (uint8_t)bits;
     }
   }
   for (; m < M; m += step) {
@@ -373,13 +379,16 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
     bf16x8 r;
     if (RES) r = *(const bf16x8*)(res + off);
     bf16x8 o;
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float z = bf2f(v[k]) * sc[k] + sh[k];
       if (RES) z += bf2f(r[k]);
+      bits |= (z > 0.f ? 1u : 0u) << k;
       o[k] = f2bf(act_f(z, ACT, slope));
     }
     *(bf16x8*)(y + off) = o;
+    if (mask) mask[(size_t)m * t.cpr + t.ch] = (uint8_t)bits;
   }
 }
 
@@ -650,10 +659,11 @@ static inline dim3 ew_grid(int M, int C) {
 }
 
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
-                       size_t numel, int C, int act, float slope, hipStream_t s) {
+                       size_t numel, int C, int act, float slope, hipStream_t s, uint8_t* mask) {
   const int M = (int)(numel / C);
   const dim3 grid = ew_grid(M, C);
-  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[11]);
+  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[11],
+                       mask);
 }
 
 int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }

@@ -188,8 +188,10 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // NS: LDS stages.  NS = 2: double buffer, vmcnt(0) + barrier per k-tile (several blocks per
 // CU hide the latency).  NS > 2 (FAST only): a ring whose LDS-DMA loads stay in flight across
 // the raw s_barrier, drained by a counted vmcnt -- for deep-K shapes at one block per CU.
+// three waves per SIMD: the fused BN-backward epilogue otherwise lands one register past the
+// 168-register step and halves to two workgroups per CU
 template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 3)
 tap_gemm_kernel(const TapGemmParams p) {
   static_assert(NS == 2 || FAST, "the LDS ring needs the one-tap-per-k-tile path");
   static_assert(BK == 64 || BK == 32, "k-tile depth");
@@ -371,29 +373,49 @@ tap_gemm_kernel(const TapGemmParams p) {
     __syncthreads();
   }
 
-  if constexpr (EPI == 3) {
+  if constexpr (EPI == 3 || EPI == 4) {
     // ---- dgrad + fused BN backward (stride 1: dst rows == GEMM rows) ----
+    // EPI 4: the activation mask comes as bits (bn_act_mask) instead of being recomputed from
+    // the BN input and the residual -- no residual rows, no scale/shift registers.
+    constexpr bool MASKED = EPI == 4;
     constexpr int RB = BN * 2, NCH = BN / 8, R = 256 / NCH, RPT = BM / R;
     char* E = smem;
     const int c = tid % NCH, pr0 = tid / NCH;
     const int cg = n0 + c * 8;
     const bool cok = cg < p.Co;
-    // The HBM-bound part is this thread's BN-input / residual / add-source rows: they are
-    // loaded in batches of RB_ rows, the first batch in flight while the accumulators go
-    // through LDS.  (Batches keep VGPR + AGPR <= 256: two waves per SIMD.)
+    // accumulators -> LDS image first: the MFMA accumulators are dead before any epilogue row
+    // is loaded, which keeps the register peak (and so the occupancy) at the k-loop's
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+        *LDS_PTR(bf16x4, E + off) = o;
+      }
+    }
+    // The HBM-bound part is this thread's BN-input / residual / add-source rows, loaded in
+    // batches of RBATCH rows (the first batch in flight across the LDS barrier).
     constexpr int RBATCH = RPT >= 4 ? 4 : RPT;
-    const bool has_res = p.bnb.res != nullptr, has_add = p.addsrc != nullptr;
+    const bool has_res = !MASKED && p.bnb.res != nullptr, has_add = p.addsrc != nullptr;
     float sc[8], sh[8], mu[8], s1[8], s2[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s1[e] = s2[e] = 0.f;
-      sc[e] = cok ? p.bnb.scale[cg + e] : 0.f;
-      sh[e] = cok ? p.bnb.shift[cg + e] : 0.f;
+      if (!MASKED) {
+        sc[e] = cok ? p.bnb.scale[cg + e] : 0.f;
+        sh[e] = cok ? p.bnb.shift[cg + e] : 0.f;
+      }
       mu[e] = cok ? p.bnb.mean[cg + e] : 0.f;
     }
 #pragma unroll
     for (int b = 0; b < RPT / RBATCH; ++b) {
       bf16x8 yv[RBATCH], rv[RBATCH], av[RBATCH];
+      uint32_t mk[RBATCH];
 #pragma unroll
       for (int q = 0; q < RBATCH; ++q) {
         const int m = m0 + pr0 + (b * RBATCH + q) * R;
@@ -402,23 +424,9 @@ tap_gemm_kernel(const TapGemmParams p) {
         yv[q] = ok ? *(const bf16x8*)(p.bnb.y + off) : bf16x8{};
         if (has_res) rv[q] = ok ? *(const bf16x8*)(p.bnb.res + off) : bf16x8{};
         if (has_add) av[q] = ok ? *(const bf16x8*)(p.addsrc + off) : bf16x8{};
+        if (MASKED) mk[q] = ok ? p.bnb.mask[off >> 3] : 0u;
       }
-      if (b == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-            const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
-            *LDS_PTR(bf16x4, E + off) = o;
-          }
-        }
-        __syncthreads();
-      }
+      if (b == 0) __syncthreads();
 #pragma unroll
       for (int q = 0; q < RBATCH; ++q) {
         const int pl = pr0 + (b * RBATCH + q) * R;
@@ -431,9 +439,13 @@ tap_gemm_kernel(const TapGemmParams p) {
             float g = bf2f(v[e]);
             if (has_add) g = bf2f(f2bf(g + bf2f(av[q][e])));  // the rounding of the unfused add
             const float yf = bf2f(yv[q][e]);
-            float z = yf * sc[e] + sh[e];
-            if (has_res) z += bf2f(rv[q][e]);
-            if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
+            if (MASKED) {
+              if (p.bnb.act == 1 && !((mk[q] >> e) & 1u)) g = 0.f;
+            } else {
+              float z = yf * sc[e] + sh[e];
+              if (has_res) z += bf2f(rv[q][e]);
+              if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
+            }
             o[e] = f2bf(g);
             const float gr = bf2f(o[e]);
             s1[e] += gr;
@@ -443,8 +455,10 @@ tap_gemm_kernel(const TapGemmParams p) {
         }
       }
     }
-    // per-tile channel sums: fixed-order reduction over the R row groups (deterministic)
-    float* red = (float*)(smem + BM * RB);  // [2][R][BN]
+    // per-tile channel sums: fixed-order reduction over the R row groups (deterministic), in
+    // the LDS image's space once every thread has read its rows (keeps the workgroup at 32 KB)
+    float* red = (float*)smem;  // [2][R][BN]
+    __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       red[(0 * R + pr0) * BN + c * 8 + e] = s1[e];
@@ -1181,7 +1195,7 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   size_t epi = 0;
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
   if (EPI == 1) epi = (size_t)128 * 2 * BN + 12 * BN;
-  if (EPI == 3) epi = (size_t)128 * 2 * BN + 16384;
+  if (EPI == 3 || EPI == 4) epi = (size_t)128 * 2 * BN;  // the sums' [2][256/(BN/8)][BN] fp32 fit the image
   size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
   if (!FAST) lds = std::max(lds, full + kMaxTaps * sizeof(int));  // LDS tap table behind the stages
   if (full > 64 * 1024) {
@@ -1202,7 +1216,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb) {
   TapGemmParams p;
   p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
-  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
   p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;
@@ -1221,7 +1235,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
       fprintf(stderr, "launch_tap_gemm: fused BN backward needs a plain stride-1 dgrad\n");
       abort();
     }
-    epi = 3;
+    epi = bnb->mask != nullptr ? 4 : 3;
   }
   const bool fast = (p.cpt & 7) == 0;
   // config: BN (64/128 output channels per tile) and NS (LDS stages); g_tune overrides the
@@ -1233,12 +1247,13 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   if (env_bn > 0 && fast) bn = env_bn;
   if (env_ns > 0 && fast) ns = env_ns;
   if (!fast) ns = 2;
-  // 1x1 shapes with K <= 1024 and 128-channel tiles: 32-deep k-tiles in a 3-stage ring (48 KB,
-  // three workgroups per CU, loads two k-tiles ahead across raw barriers) beat the 64-deep double
-  // buffer (two per CU) by 5-20 %; 3x3 and deep-K shapes keep the latter (tools/conv_bench.py
-  // --cfgs "1=3;8=32" per-shape A/B).  g_tune[8] = 32 forces the ring (with [1] = 3 or 4), 64 disables it.
-  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs <= 1024 && bn == 128) ns = 3;
-  const bool bk32 = fast && (ns == 3 || ns == 4) && (g_tune[8] == 32 || (env_ns == 0 && g_tune[8] != 64));
+  // 1x1 shapes with K <= 1024 and 128-channel tiles: 32-deep k-tiles, double-buffered (32 KB of
+  // LDS: four workgroups per CU) beat the 64-deep double buffer (two per CU) by 5-25 % and the
+  // 32-deep 3-stage ring by 2-12 %; 3x3 and deep-K shapes keep 64-deep tiles (tools/conv_bench.py
+  // --cfgs "1=2;8=32,1=3;8=32" per-shape A/B).  g_tune[8] = 32 forces 32-deep tiles (with [1]),
+  // 64 disables the heuristic.
+  bool bk32 = fast && g_tune[8] == 32 && ns >= 2 && ns <= 4;
+  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs <= 1024 && bn == 128) bk32 = true;
   const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
   if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
@@ -1255,7 +1270,8 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   }
   const int grid = ntm * ((Co + bn - 1) / bn);
 #define DCP_TG_NS(BN_, EPI_, FAST_)                                                    \
-  if (bk32 && ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3, 32>(p, grid, stream);  \
+  if (bk32 && ns == 2) launch_tg<BN_, EPI_, (FAST_ || true), 2, 32>(p, grid, stream);  \
+  else if (bk32 && ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3, 32>(p, grid, stream);  \
   else if (bk32 && ns == 4) launch_tg<BN_, EPI_, (FAST_ || true), 4, 32>(p, grid, stream); \
   else if (ns == 2) launch_tg<BN_, EPI_, FAST_, 2>(p, grid, stream);                   \
   else if (ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3>(p, grid, stream);          \
@@ -1264,6 +1280,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   if (epi == 0) { DCP_TG_NS(BN_, 0, FAST_) }       \
   else if (epi == 1) { DCP_TG_NS(BN_, 1, FAST_) }  \
   else if (epi == 3) { DCP_TG_NS(BN_, 3, FAST_) }  \
+  else if (epi == 4) { DCP_TG_NS(BN_, 4, FAST_) }  \
   else { DCP_TG_NS(BN_, 2, FAST_) }
   if (bn == 64) {
     if (fast) { DCP_TG_EPI(64, true) } else { DCP_TG_EPI(64, false) }

@@ -35,6 +35,7 @@ struct BnBwdEpi {
   const float* invstd;
   float* part;          // [ceil(M/128)][2][C]
   int act;              // 0 none, 1 ReLU
+  const uint8_t* mask;  // act'(z) > 0 as bits [M][C/8] (bn_act's mask output), or nullptr: recompute z
 };
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
@@ -81,7 +82,7 @@ void launch_bn_finalize(const float* st, int W, int C, float eps, const float* g
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                           float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
-                       int C, int act, float slope, hipStream_t s);
+                       int C, int act, float slope, hipStream_t s, uint8_t* mask = nullptr);
 int bn_bwd_reduce_blocks(int M, int C);
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,

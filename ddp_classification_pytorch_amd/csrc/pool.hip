@@ -3,6 +3,7 @@
 // Replaces the ATen max-pool (stem, NESTED/model/imagenet_resnet.py:111),
 // average pool (:116 AvgPool2d(7) / torchvision AdaptiveAvgPool2d) and
 // TResNet's SpaceToDepth stem (timm).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -344,11 +345,14 @@ void launch_maxpool_bn_bwd(const bf16* dy, const uint8_t* idx, const bf16* x, in
                          Wo, k, s, p, scale, shift, mean, invstd, act, nullptr, 0.f, part, nullptr, dv);
     launch_partial_sum(part, g, 2 * C, sums_out, st);
   } else {
+    // grid-stride over 8192 workgroups: the windows' overlapping dy / argmax reads stay in the
+    // L2 of the XCD walking them (a one-shot grid measured 583 -> 747 us on the R50 stem)
+    const int g = std::min(ew_grid2(total), 8192);
     if (stem)
-      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 3, 2, 1>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, x, N,
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 3, 2, 1>), dim3(g), dim3(256), 0, st, dy, idx, x, N,
                          H, W, C, Ho, Wo, k, s, p, scale, shift, mean, invstd, act, sums, inv_count, nullptr, dx, dv);
     else
-      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 0, 0, 0>), dim3(ew_grid2(total)), dim3(256), 0, st, dy, idx, x, N,
+      hipLaunchKernelGGL((maxpool_bn_bwd_kernel<1, 0, 0, 0>), dim3(g), dim3(256), 0, st, dy, idx, x, N,
                          H, W, C, Ho, Wo, k, s, p, scale, shift, mean, invstd, act, sums, inv_count, nullptr, dx, dv);
   }
 }

@@ -60,14 +60,25 @@ def conv_dgrad(dy, wt, H, W, stride, pad, add=None):
     return dx.to(dy.dtype)
 
 
-def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act):
+def unpack_mask(mask):
+    """[..., C/8] uint8 activation-mask bits (bit e of byte c = channel 8c+e) -> [..., C] float."""
+    bits = (mask.to(torch.int32).unsqueeze(-1) >> torch.arange(8, dtype=torch.int32)) & 1
+    return bits.reshape(*mask.shape[:-1], mask.shape[-1] * 8).float()
+
+
+def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act, mask=None):
     """Stride-1 dgrad + the backward reduction of the BN(+act)(+res) layer producing its input:
-    -> (activation-masked gradient g', [2, C] = (sum g', sum g' * xhat))."""
+    -> (activation-masked gradient g', [2, C] = (sum g', sum g' * xhat)).  ``mask``: the
+    activation mask bits from :func:`bn_act_mask` (then ``res`` is not read)."""
     g = conv_dgrad(dy, wt, y.shape[1], y.shape[2], 1, pad, add)
-    z = _f(y) * scale + shift
-    if res is not None:
-        z = z + _f(res)
-    gm = (_f(g) * _act_d(z, act, 0.0)).to(dy.dtype)
+    if mask is not None:
+        d = unpack_mask(mask) if act == ACT_RELU else torch.ones_like(_f(y))
+    else:
+        z = _f(y) * scale + shift
+        if res is not None:
+            z = z + _f(res)
+        d = _act_d(z, act, 0.0)
+    gm = (_f(g) * d).to(dy.dtype)
     xh = (_rows(y) - mean) * invstd
     gr = _rows(gm)
     return gm, torch.stack([gr.sum(0), (gr * xh).sum(0)])
@@ -221,6 +232,15 @@ def bn_act(x, res, scale, shift, act, slope):
     if res is not None:
         z = z + _f(res)
     return _act(z, act, slope).to(x.dtype)
+
+
+def bn_act_mask(x, res, scale, shift, act, slope):
+    z = _f(x) * scale + shift
+    if res is not None:
+        z = z + _f(res)
+    pos = (z > 0).to(torch.int32).reshape(*z.shape[:-1], z.shape[-1] // 8, 8)
+    mask = (pos << torch.arange(8, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    return _act(z, act, slope).to(x.dtype), mask
 
 
 def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope):

@@ -245,8 +245,10 @@ class _Conv2d(Function):
         if ctx.needs_input_grad[0]:
             src = ctx.bnsrc
             if src is not None and complete and stride == 1 and src.tensors is not None:
-                y, res, scale, shift, mean, invstd = src.tensors
-                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act)
+                y, res, scale, shift, mean, invstd, mask = src.tensors
+                if mask is not None:
+                    res = None  # the activation mask bits replace the residual read
+                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act, mask)
                 src.fused = (dx, sums)
             elif add is not None:
                 dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add)
@@ -387,7 +389,13 @@ class _BNAct(Function):
             mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
         else:
             mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
-        y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
+        mask = None
+        if src is not None and res is not None and cfg.act == 1:
+            # BN + residual + ReLU feeding a fused-backward conv: keep the ReLU mask as bits so
+            # that backward reads 1/16 of the residual's bytes for it
+            y, mask = k.bn_act_mask(x, res, scale, shift, cfg.act, cfg.slope)
+        else:
+            y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
         ctx.save_for_backward(x, res, gamma, scale, shift, mean, invstd)
         ctx.cfg = cfg
         ctx.count = count
@@ -395,7 +403,7 @@ class _BNAct(Function):
         ctx.link = link
         ctx.src = src
         if src is not None:
-            src.tensors = (x, res, scale, shift, mean, invstd)
+            src.tensors = (x, res, scale, shift, mean, invstd, mask)
         return y
 
     @staticmethod

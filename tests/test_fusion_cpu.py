@@ -108,3 +108,25 @@ def test_unfused_fallback_when_conv_output_shared():
 
     g1, g0 = run(True), run(False)
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+
+
+def test_ref_mask_path_matches_residual_path():
+    """CPU reference: the activation-mask form of the fused BN-backward dgrad equals the
+    residual-recompute form (the GPU kernels are checked the same way in test_kernels_gpu)."""
+    import torch
+
+    from ddp_classification_pytorch_amd.ops import _ref
+
+    torch.manual_seed(0)
+    N, H, Ci, Co = 2, 6, 16, 8
+    y, r = torch.randn(N, H, H, Ci) * 2, torch.randn(N, H, H, Ci)
+    scale, shift = torch.rand(Ci) + 0.5, torch.randn(Ci) * 0.3
+    mean, invstd = torch.randn(Ci) * 0.2, torch.rand(Ci) + 0.5
+    z, mask = _ref.bn_act_mask(y, r, scale, shift, 1, 0.0)
+    assert mask.shape == (N, H, H, Ci // 8)
+    assert torch.equal(_ref.unpack_mask(mask), (y * scale + shift + r > 0).float())
+    wt = torch.randn(Ci, 1, 1, Co)
+    dy, add = torch.randn(N, H, H, Co), torch.randn(N, H, H, Ci)
+    g0, s0 = _ref.conv_dgrad_bn(dy, wt, 0, add, y, r, scale, shift, mean, invstd, 1)
+    g1, s1 = _ref.conv_dgrad_bn(dy, wt, 0, add, y, None, scale, shift, mean, invstd, 1, mask)
+    assert torch.allclose(g0, g1) and torch.allclose(s0, s1)

@@ -626,3 +626,28 @@ def test_conv_dgrad_bn_pipeline_variants(K, cfg):
             K.set_tuning(i, 0)
     assert relerr(g1, g0) < 1e-2
     assert relerr(s1[0], s0[0]) < 2e-2 and relerr(s1[1], s0[1]) < 2e-2
+
+
+def test_bn_act_mask_and_masked_dgrad_bn(K):
+    """bn_act_mask's activation bits against the reference, and the fused BN-backward dgrad
+    reading those bits instead of the residual gives the same result as recomputing z."""
+    torch.manual_seed(2)
+    N, H, Ci, Co = 2, 14, 256, 64
+    y = rnd(N, H, H, Ci, scale=2.0)
+    r = rnd(N, H, H, Ci)
+    scale, shift = torch.rand(Ci) + 0.5, torch.randn(Ci) * 0.3
+    mean, invstd = torch.randn(Ci) * 0.2, torch.rand(Ci) + 0.5
+    z, mask = K.bn_act_mask(y.to(DEV), r.to(DEV), scale.to(DEV), shift.to(DEV), 1, 0.0)
+    zr, mr = _ref.bn_act_mask(y, r, scale, shift, 1, 0.0)
+    assert mask.shape == (N, H, H, Ci // 8) and mask.dtype == torch.uint8
+    assert torch.equal(mask.cpu(), mr)
+    assert relerr(z, zr) < 1e-2
+    w = torch.randn(Co, 1, 1, Ci) / Ci ** 0.5
+    _, wt = K.weight_prep(w.to(DEV), 0, True)
+    dy, add = rnd(N, H, H, Co).to(DEV), rnd(N, H, H, Ci).to(DEV)
+    d = lambda t: t.to(DEV)
+    g0, s0 = K.conv_dgrad_bn(dy, wt, 0, add, d(y), d(r), d(scale), d(shift), d(mean), d(invstd), 1)
+    g1, s1 = K.conv_dgrad_bn(dy, wt, 0, add, d(y), None, d(scale), d(shift), d(mean), d(invstd), 1, mask)
+    assert torch.equal(g0, g1)
+    # the two epilogue variants are separate instantiations: FMA contraction of the sums may differ
+    assert relerr(s1, s0) < 1e-5
