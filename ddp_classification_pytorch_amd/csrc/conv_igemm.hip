@@ -789,11 +789,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, uint32_t row0, uint32
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-__global__ void __launch_bounds__(256)
+// BK = pixel rows per k-tile (64, or 32: half the LDS, twice the workgroups per CU)
+template <int BK>
+__global__ void __launch_bounds__(256, 3)
 wgrad_kernel(const WgradParams p) {
-  constexpr int BK = 64;          // m rows per k-tile
-  constexpr int IMG = BK * 256;   // 64 rows x 128 bf16
+  constexpr int IMG = BK * 256;   // BK rows x 128 bf16
   constexpr int STAGE = 2 * IMG;
+  constexpr int SL = BK / 16;     // LDS-DMA instructions per thread per image
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -811,15 +813,15 @@ wgrad_kernel(const WgradParams p) {
   const int mend = min(p.M, mstart + p.rows_per_split);
   const int nkt = (mend - mstart + BK - 1) / BK;
 
-  // per-thread load slots: 4 per image; wave instruction i covers rows (wave*4+i)*4 .. +3
-  uint32_t a_col[4];
-  bool a_cok[4];
-  int b_dy[4], b_dx[4];
-  uint32_t b_ci[4];
-  bool b_cok[4];
+  // per-thread load slots: SL per image; wave instruction i covers rows (wave*SL+i)*4 .. +3
+  uint32_t a_col[SL];
+  bool a_cok[SL];
+  int b_dy[SL], b_dx[SL];
+  uint32_t b_ci[SL];
+  bool b_cok[SL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t r = (wave * 4 + i) * 4 + (lane >> 4);
+  for (int i = 0; i < SL; ++i) {
+    const uint32_t r = (wave * SL + i) * 4 + (lane >> 4);
     const uint32_t c = (lane & 15) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
     a_col[i] = co0 + c * 8;
     a_cok[i] = (int)a_col[i] < p.Co;
@@ -835,12 +837,12 @@ wgrad_kernel(const WgradParams p) {
     char* Ai = smem + buf * STAGE;
     char* Bi = Ai + IMG;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = (wave * 4 + i) * 4 + (lane >> 4);
+    for (int i = 0; i < SL; ++i) {
+      const int r = (wave * SL + i) * 4 + (lane >> 4);
       const int m = mstart + kt * BK + r;
       const bool mok = m < mend;
       const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 4 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * SL + i) * 1024), 16, 0, 0);
       const uint32_t mm = mok ? m : 0;
       const uint32_t q = fdiv(mm, p.div_wo);
       const uint32_t x = mm - q * p.Wo;
@@ -849,7 +851,7 @@ wgrad_kernel(const WgradParams p) {
       const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
       const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
       const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 4 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SL + i) * 1024), 16, 0, 0);
     }
   };
 
@@ -870,7 +872,7 @@ wgrad_kernel(const WgradParams p) {
     const char* Ai = smem + buf * STAGE;
     const char* Bi = Ai + IMG;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       const uint32_t row0 = s * 32 + 8 * (lane >> 4);
       bf16x8 af[4], bfr[4];
 #pragma unroll
@@ -1058,12 +1060,13 @@ __device__ __forceinline__ bf16x8 tr_frag128(const char* img, uint32_t row0, uin
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-__global__ void __launch_bounds__(256)
+template <int BK>
+__global__ void __launch_bounds__(256, 3)
 wgrad64_kernel(const WgradParams p) {
-  constexpr int BK = 64;
-  constexpr int IMGA = BK * 128;  // 64 pixels x 64 co
-  constexpr int IMGB = BK * 512;  // 64 pixels x 256 cols
+  constexpr int IMGA = BK * 128;  // BK pixels x 64 co
+  constexpr int IMGB = BK * 512;  // BK pixels x 256 cols
   constexpr int STAGE = IMGA + IMGB;
+  constexpr int SA = BK / 32, SB = BK / 8;  // LDS-DMA instructions per thread: dY / im2col image
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1076,23 +1079,23 @@ wgrad64_kernel(const WgradParams p) {
   const int mend = min(p.M, mstart + p.rows_per_split);
   const int nkt = (mend - mstart + BK - 1) / BK;
 
-  // dY image: 2 LDS-DMA instructions per thread, instruction i covers rows (wave*2+i)*8 .. +7
-  uint32_t a_col[2];
-  bool a_cok[2];
+  // dY image: SA LDS-DMA instructions per thread, instruction i covers rows (wave*SA+i)*8 .. +7
+  uint32_t a_col[SA];
+  bool a_cok[SA];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const uint32_t r = (wave * 2 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < SA; ++i) {
+    const uint32_t r = (wave * SA + i) * 8 + (lane >> 3);
     const uint32_t c = (lane & 7) ^ ((((r >> 1) & 1u) | (((r >> 3) & 1u) << 1)) << 1);
     a_col[i] = c * 8;
     a_cok[i] = (int)a_col[i] < p.Co;
   }
-  // im2col image: 8 instructions per thread, instruction i covers rows (wave*8+i)*2 .. +1
-  int b_dy[8], b_dx[8];
-  uint32_t b_ci[8];
-  bool b_cok[8];
+  // im2col image: SB instructions per thread, instruction i covers rows (wave*SB+i)*2 .. +1
+  int b_dy[SB], b_dx[SB];
+  uint32_t b_ci[SB];
+  bool b_cok[SB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t r = (wave * 8 + i) * 2 + (lane >> 5);
+  for (int i = 0; i < SB; ++i) {
+    const uint32_t r = (wave * SB + i) * 2 + (lane >> 5);
     const uint32_t c = (lane & 31) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
     const int kc = kcol0 / 8 + c;
     b_cok[i] = kc < p.kc_total;
@@ -1106,15 +1109,15 @@ wgrad64_kernel(const WgradParams p) {
     char* Ai = smem + buf * STAGE;
     char* Bi = Ai + IMGA;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (wave * 2 + i) * 8 + (lane >> 3);
+    for (int i = 0; i < SA; ++i) {
+      const int r = (wave * SA + i) * 8 + (lane >> 3);
       const int m = mstart + kt * BK + r;
       const bf16* ga = (m < mend && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 2 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * SA + i) * 1024), 16, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = (wave * 8 + i) * 2 + (lane >> 5);
+    for (int i = 0; i < SB; ++i) {
+      const int r = (wave * SB + i) * 2 + (lane >> 5);
       const int m = mstart + kt * BK + r;
       const bool mok = m < mend;
       const uint32_t mm = mok ? m : 0;
@@ -1125,7 +1128,7 @@ wgrad64_kernel(const WgradParams p) {
       const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
       const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
       const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 8 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SB + i) * 1024), 16, 0, 0);
     }
   };
 
@@ -1146,7 +1149,7 @@ wgrad64_kernel(const WgradParams p) {
     const char* Ai = smem + buf * STAGE;
     const char* Bi = Ai + IMGA;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 32; ++s) {
       const uint32_t row0 = s * 32 + 8 * (lane >> 4);
       bf16x8 af[4], bfr[4];
 #pragma unroll
@@ -1252,7 +1255,9 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // 32-deep 3-stage ring by 2-12 %; 3x3 and deep-K shapes keep 64-deep tiles (tools/conv_bench.py
   // --cfgs "1=2;8=32,1=3;8=32" per-shape A/B).  g_tune[8] = 32 forces 32-deep tiles (with [1]),
   // 64 disables the heuristic.
-  bool bk32 = fast && g_tune[8] == 32 && ns >= 2 && ns <= 4;
+  // narrow-channel (non-FAST) shapes -- the space-to-depth stem -- take 32-deep tiles double-
+  // buffered only (their taps are looked up per lane; g_tune[13] = 32 / 64 selects, A/B)
+  bool bk32 = (fast && g_tune[8] == 32 && ns >= 2 && ns <= 4) || (!fast && g_tune[13] == 32);
   if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs <= 1024 && bn == 128) bk32 = true;
   const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
   if (fast && Co >= 128 && epi < 2 && use8) {
@@ -1270,7 +1275,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   }
   const int grid = ntm * ((Co + bn - 1) / bn);
 #define DCP_TG_NS(BN_, EPI_, FAST_)                                                    \
-  if (bk32 && ns == 2) launch_tg<BN_, EPI_, (FAST_ || true), 2, 32>(p, grid, stream);  \
+  if (bk32 && ns == 2) launch_tg<BN_, EPI_, FAST_, 2, 32>(p, grid, stream);             \
   else if (bk32 && ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3, 32>(p, grid, stream);  \
   else if (bk32 && ns == 4) launch_tg<BN_, EPI_, (FAST_ || true), 4, 32>(p, grid, stream); \
   else if (ns == 2) launch_tg<BN_, EPI_, FAST_, 2>(p, grid, stream);                   \
@@ -1395,9 +1400,13 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   if (splits == 1) {
     p.part = dw;  // split 0 stores straight into dw
   }
+  // 32 pixel rows per k-tile (g_tune[12] = 32): half the LDS of the 64-row tiles
+  const bool wbk32 = g_tune[12] == 32;
   if (narrow) {
-    constexpr int lds = 2 * 64 * (128 + 512);
-    hipLaunchKernelGGL(wgrad64_kernel, dim3(tiles * splits), dim3(256), lds, stream, p);
+    if (wbk32)
+      hipLaunchKernelGGL(wgrad64_kernel<32>, dim3(tiles * splits), dim3(256), 2 * 32 * (128 + 512), stream, p);
+    else
+      hipLaunchKernelGGL(wgrad64_kernel<64>, dim3(tiles * splits), dim3(256), 2 * 64 * (128 + 512), stream, p);
   } else if (big) {
     constexpr int lds = 4 * 64 * 512;
     static bool attr = false;
@@ -1407,7 +1416,8 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     }
     hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * splits), dim3(512), lds, stream, p);
   } else {
-    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * splits), dim3(256), 4 * 64 * 256, stream, p);
+    if (wbk32) hipLaunchKernelGGL(wgrad_kernel<32>, dim3(tiles * splits), dim3(256), 4 * 32 * 256, stream, p);
+    else hipLaunchKernelGGL(wgrad_kernel<64>, dim3(tiles * splits), dim3(256), 4 * 64 * 256, stream, p);
   }
   if (part != nullptr && splits > 1) launch_split_reduce(part, splits, Co * p.ldw, dw, stream);
 }

@@ -651,3 +651,42 @@ def test_bn_act_mask_and_masked_dgrad_bn(K):
     assert torch.equal(g0, g1)
     # the two epilogue variants are separate instantiations: FMA contraction of the sums may differ
     assert relerr(s1, s0) < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4))])
+@pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
+                                   (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1)])
+def test_conv_wgrad_variants(K, cfg, shape):
+    """Weight gradient with 32-row k-tiles (and another split plan) against the fp32 reference."""
+    N, H, W, Ci, Co, k, s, p = shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy, x = rnd(N, Ho, Wo, Co), rnd(N, H, W, Ci)
+    try:
+        for i, v in cfg:
+            K.set_tuning(i, v)
+        dw = K.conv_wgrad(dy.to(DEV), x.to(DEV), k, k, s, p)
+        torch.cuda.synchronize()
+    finally:
+        for i, _ in cfg:
+            K.set_tuning(i, 0)
+    assert relerr(dw, _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)) < 5e-3
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,k,pad", [(2, 32, 16, 64, 4, 2), (2, 16, 8, 64, 3, 1)])
+def test_narrow_channel_conv_bk32(K, N, H, Ci, Co, k, pad):
+    """Narrow-channel (per-lane tap lookup) convolution with 32-deep k-tiles (g_tune[13] = 32):
+    the space-to-depth stem geometry and a CIFAR-style stem, against the fp32 reference."""
+    x = rnd(N, H, H, Ci)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
+    wb, _ = K.weight_prep(w.float().to(DEV), 0, False)
+    try:
+        K.set_tuning(13, 32)
+        y, slabs = K.conv_fwd_geo(x.to(DEV), wb, 1, pad, H, H, True)
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(13, 0)
+    yr, _ = _ref.conv_fwd_geo(x.float(), w.float(), 1, pad, H, H, False)
+    assert relerr(y, yr) < 1e-2
+    st = K.bn_stats(y, slabs)
+    sr = _ref.bn_stats(y.float().cpu(), None)
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4 and relerr(st[0, 2], sr[0, 2]) < 1e-4
