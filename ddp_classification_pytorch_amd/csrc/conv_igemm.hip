@@ -85,6 +85,21 @@ __device__ __forceinline__ uint32_t swzk(uint32_t r, uint32_t c) {
   return r * (BK * 2u) + ((c ^ swz_chunk<BK>(r)) << 4);
 }
 
+// Epilogue image E[rows][BN] bf16: 16-byte chunks XOR-swizzled by row>>1, and the two 8-byte
+// halves of a chunk swapped on odd rows, so the accumulator writes (ds_write_b64, 16 lanes = 16
+// consecutive rows of one 8-byte half) hit 16 distinct bank slots and the row-chunk reads
+// (ds_read_b128) stay conflict free.  eimg_off8: byte offset of the 4 channels cl..cl+3 of row pl.
+template <int NCH>
+__device__ __forceinline__ uint32_t eimg_off8(uint32_t pl, uint32_t cl) {
+  return pl * (NCH * 16) + (((cl >> 3) ^ ((pl >> 1) & (NCH - 1))) << 4) + ((((cl >> 2) & 1) ^ (pl & 1)) << 3);
+}
+// the 8 channels of chunk c of row pl, in channel order
+template <int NCH>
+__device__ __forceinline__ bf16x8 eimg_chunk(const char* E, uint32_t pl, uint32_t c) {
+  const bf16x8 v = *LDS_PTR(const bf16x8, E + pl * (NCH * 16) + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+  return (pl & 1) ? bf16x8{v[4], v[5], v[6], v[7], v[0], v[1], v[2], v[3]} : v;
+}
+
 // Per 128-row slab and channel of the LDS output image E[rows][BN] (16-byte chunks
 // XOR-swizzled by row>>1): (mean, M2) of the bf16-rounded outputs.  A thread takes one
 // channel x 64 rows with two passes over register-resident values (no E[x^2]-E[x]^2
@@ -106,7 +121,7 @@ __device__ __forceinline__ void tile_stats(const TapGemmParams& p, char* E, int 
 #pragma unroll
     for (int r = 0; r < 64; ++r) {
       const uint32_t pl = h * 64 + r;
-      v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + (coff ^ (((pl >> 1) & (NCH - 1)) << 4))));
+      v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + ((coff ^ (((pl >> 1) & (NCH - 1)) << 4)) ^ ((pl & 1) << 3))));
     }
     float s[8];
 #pragma unroll
@@ -394,7 +409,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+        const uint32_t off = eimg_off8<NCH>(pl, cl);
         *LDS_PTR(bf16x4, E + off) = o;
       }
     }
@@ -432,7 +447,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int pl = pr0 + (b * RBATCH + q) * R;
         const int m = m0 + pl;
         if (m < p.M && cok) {
-          const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+          const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
           bf16x8 o;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -456,21 +471,25 @@ tap_gemm_kernel(const TapGemmParams p) {
       }
     }
     // per-tile channel sums: fixed-order reduction over the R row groups (deterministic), in
-    // the LDS image's space once every thread has read its rows (keeps the workgroup at 32 KB)
-    float* red = (float*)smem;  // [2][R][BN]
+    // the LDS image's space once every thread has read its rows (keeps the workgroup at 32 KB).
+    // Layout [which][e][R x NCH (+4 pad)]: the writes (fixed e, consecutive threads = consecutive
+    // chunks) and the column reads (32 lanes = 4 chunks x 8 elements) are both bank-conflict free.
+    constexpr int SE = R * NCH + 4;
+    float* red = (float*)smem;  // [2][8][SE]
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[(0 * R + pr0) * BN + c * 8 + e] = s1[e];
-      red[(1 * R + pr0) * BN + c * 8 + e] = s2[e];
+      red[(0 * 8 + e) * SE + pr0 * NCH + c] = s1[e];
+      red[(1 * 8 + e) * SE + pr0 * NCH + c] = s2[e];
     }
     __syncthreads();
     if (tid < 2 * BN) {
       const int which = tid / BN, ch = tid - which * BN;
       if (n0 + ch < p.Co) {
+        const float* col = red + (which * 8 + (ch & 7)) * SE + (ch >> 3);
         float t = 0.f;
 #pragma unroll 4
-        for (int r = 0; r < R; ++r) t += red[(which * R + r) * BN + ch];
+        for (int r = 0; r < R; ++r) t += col[r * NCH];
         if (which) t *= p.bnb.invstd[n0 + ch];
         p.bnb.part[((size_t)tm * 2 + which) * p.Co + n0 + ch] = t;
       }
@@ -492,7 +511,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        const uint32_t off = pl * RB + ((((cl >> 3) ^ ((pl >> 1) & (NCH - 1)))) << 4) + ((cl >> 2) & 1) * 8;
+        const uint32_t off = eimg_off8<NCH>(pl, cl);
         *LDS_PTR(bf16x4, E + off) = o;
       }
     }
@@ -506,7 +525,7 @@ tap_gemm_kernel(const TapGemmParams p) {
       for (int k = 0; k < BM / R; ++k) {
         const int pl = pr0 + k * R;
         const int m = m0 + pl;
-        const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+        const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
         if (m < p.M && cok) {
           uint32_t drow;
           if (p.ds == 1) {
@@ -716,7 +735,7 @@ tap_gemm8_kernel(const TapGemmParams p) {
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-      const uint32_t off = pl * RB + (((cl >> 3) ^ ((pl >> 1) & (NCH - 1))) << 4) + ((cl >> 2) & 1) * 8;
+      const uint32_t off = eimg_off8<NCH>(pl, cl);
       *LDS_PTR(bf16x4, E + off) = o;
     }
   }
@@ -729,7 +748,7 @@ tap_gemm8_kernel(const TapGemmParams p) {
     for (int k = 0; k < BM / R; ++k) {
       const int pl = pr0 + k * R;
       const int m = m0 + pl;
-      const bf16x8 v = *LDS_PTR(bf16x8, E + pl * RB + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
+      const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
       if (m < p.M && cok) {
         uint32_t drow;
         if (p.ds == 1) {
@@ -1198,7 +1217,8 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   size_t epi = 0;
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
   if (EPI == 1) epi = (size_t)128 * 2 * BN + 12 * BN;
-  if (EPI == 3 || EPI == 4) epi = (size_t)128 * 2 * BN;  // the sums' [2][256/(BN/8)][BN] fp32 fit the image
+  // image, then the sums' [2][8][256 + 4] fp32 in its space
+  if (EPI == 3 || EPI == 4) epi = std::max((size_t)128 * 2 * BN, (size_t)2 * 8 * 260 * 4);
   size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
   if (!FAST) lds = std::max(lds, full + kMaxTaps * sizeof(int));  // LDS tap table behind the stages
   if (full > 64 * 1024) {
