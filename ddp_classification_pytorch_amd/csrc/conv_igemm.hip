@@ -223,7 +223,8 @@ tap_gemm_kernel(const TapGemmParams p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  // wave-uniform in an SGPR: the LDS-DMA destinations derived from it need no readfirstlane
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
 
   const uint32_t ntn = (p.Co + BN - 1) / BN;
@@ -231,6 +232,41 @@ tap_gemm_kernel(const TapGemmParams p) {
   const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
   const uint32_t tn = bid % ntn, tm = bid / ntn;
   const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- FAST path: per-slot source pointers and tap-validity masks, computed once ----
+  // A k-tile's load is then ptr + a wave-uniform tap offset, selected against the zero page
+  // by one mask bit: ~3 vector instructions per LDS-DMA instead of ~12 (the k-loop was
+  // vector-issue bound on this address arithmetic).  Rows past M / channels past Co read a
+  // clamped valid row: their outputs are never stored nor counted in the statistics.
+  const bf16* fa_ptr[AI];
+  uint32_t fa_vm[AI];
+  const bf16* fb_ptr[BN / (4 * RPI)];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int r = (wave * AI + i) * RPI + lane / CH;
+      const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+      const uint32_t q = fdiv(mm, p.div_wy);
+      const uint32_t x = mm - q * p.Wy;
+      const uint32_t n = fdiv(q, p.div_hy);
+      const uint32_t y = q - n * p.Hy;
+      const int ys = y * p.ss, xs = x * p.ss;
+      fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs +
+                  ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+      uint32_t vm = 0;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int tv = p.tap[t];
+        const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+        vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+      }
+      fa_vm[i] = vm;
+    }
+#pragma unroll
+    for (int i = 0; i < BN / (4 * RPI); ++i) {
+      const int r = (wave * (BN / (4 * RPI)) + i) * RPI + lane / CH;
+      fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+    }
+  }
 
   // ---- per-thread A-load rows (AI glds per k-tile) ----
   uint32_t a_pix[AI];   // n*Hs*Ws
@@ -283,23 +319,19 @@ tap_gemm_kernel(const TapGemmParams p) {
       const int t = kt / tiles_per_tap;
       const int cbase = (kt - t * tiles_per_tap) * BK;
       const int tv = p.tap[t];
-      const int dy = tap_dy(tv), dx = tap_dx(tv);
-      const uint32_t wofs = (uint32_t)tap_w(tv) * p.Cs + cbase;
+      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
+      const long boff = (long)tap_w(tv) * p.Cs + cbase;
+      const uint32_t tbit = 1u << t;
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
-        const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
-        const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8
-                           : p.zero;
+        const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
         __builtin_amdgcn_global_load_lds((const void*)g,
                                          LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
       }
 #pragma unroll
-      for (int i = 0; i < BI; ++i) {
-        const bf16* g = b_ok[i] ? p.wt + b_row[i] + wofs + b_chunk[i] * 8 : p.zero;
-        __builtin_amdgcn_global_load_lds((const void*)g,
+      for (int i = 0; i < BI; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff),
                                          LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
-      }
     } else {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
@@ -786,6 +818,7 @@ struct WgradParams {
   int Co, M, ldw;    // ldw = T*Cs
   int cpt, kc_total, rows_per_split;
   int ablate;  // tuning experiments only: 8 = skip the atomic flush
+  int direct;  // 1x1 stride-1 (no padding): the input pixel of GEMM row m is m
   FastDiv div_wo, div_ho, div_cpt;
   int8_t dy_t[kMaxTaps], dx_t[kMaxTaps];
 };
@@ -862,14 +895,19 @@ wgrad_kernel(const WgradParams p) {
       const bool mok = m < mend;
       const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
       __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * SL + i) * 1024), 16, 0, 0);
-      const uint32_t mm = mok ? m : 0;
-      const uint32_t q = fdiv(mm, p.div_wo);
-      const uint32_t x = mm - q * p.Wo;
-      const uint32_t n = fdiv(q, p.div_ho);
-      const uint32_t y = q - n * p.Ho;
-      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
-      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
-      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      const bf16* gb;
+      if (p.direct) {  // 1x1 stride 1: input pixel m is GEMM row m (no decode)
+        gb = (mok && b_cok[i]) ? p.src + (size_t)m * p.Cs + b_ci[i] : p.zero;
+      } else {
+        const uint32_t mm = mok ? m : 0;
+        const uint32_t q = fdiv(mm, p.div_wo);
+        const uint32_t x = mm - q * p.Wo;
+        const uint32_t n = fdiv(q, p.div_ho);
+        const uint32_t y = q - n * p.Ho;
+        const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+        const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+        gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      }
       __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SL + i) * 1024), 16, 0, 0);
     }
   };
@@ -994,14 +1032,19 @@ wgrad256_kernel(const WgradParams p) {
       const bool mok = m < mend;
       const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
       __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 4 + i) * 1024), 16, 0, 0);
-      const uint32_t mm = mok ? m : 0;
-      const uint32_t q = fdiv(mm, p.div_wo);
-      const uint32_t x = mm - q * p.Wo;
-      const uint32_t n = fdiv(q, p.div_ho);
-      const uint32_t y = q - n * p.Ho;
-      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
-      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
-      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      const bf16* gb;
+      if (p.direct) {  // 1x1 stride 1: input pixel m is GEMM row m (no decode)
+        gb = (mok && b_cok[i]) ? p.src + (size_t)m * p.Cs + b_ci[i] : p.zero;
+      } else {
+        const uint32_t mm = mok ? m : 0;
+        const uint32_t q = fdiv(mm, p.div_wo);
+        const uint32_t x = mm - q * p.Wo;
+        const uint32_t n = fdiv(q, p.div_ho);
+        const uint32_t y = q - n * p.Ho;
+        const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+        const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+        gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      }
       __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 4 + i) * 1024), 16, 0, 0);
     }
   };
@@ -1139,14 +1182,19 @@ wgrad64_kernel(const WgradParams p) {
       const int r = (wave * SB + i) * 2 + (lane >> 5);
       const int m = mstart + kt * BK + r;
       const bool mok = m < mend;
-      const uint32_t mm = mok ? m : 0;
-      const uint32_t q = fdiv(mm, p.div_wo);
-      const uint32_t x = mm - q * p.Wo;
-      const uint32_t n = fdiv(q, p.div_ho);
-      const uint32_t y = q - n * p.Ho;
-      const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
-      const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
-      const bf16* gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      const bf16* gb;
+      if (p.direct) {  // 1x1 stride 1: input pixel m is GEMM row m (no decode)
+        gb = (mok && b_cok[i]) ? p.src + (size_t)m * p.Cs + b_ci[i] : p.zero;
+      } else {
+        const uint32_t mm = mok ? m : 0;
+        const uint32_t q = fdiv(mm, p.div_wo);
+        const uint32_t x = mm - q * p.Wo;
+        const uint32_t n = fdiv(q, p.div_ho);
+        const uint32_t y = q - n * p.Ho;
+        const int hi = (int)y * p.ss + b_dy[i], wi = (int)x * p.ss + b_dx[i];
+        const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
+        gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
+      }
       __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SB + i) * 1024), 16, 0, 0);
     }
   };
@@ -1260,7 +1308,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     }
     epi = bnb->mask != nullptr ? 4 : 3;
   }
-  const bool fast = (p.cpt & 7) == 0;
+  const bool fast = (p.cpt & 7) == 0 && taps.n <= 32;  // FAST: 32-bit tap-validity masks
   // config: BN (64/128 output channels per tile) and NS (LDS stages); g_tune overrides the
   // heuristic (tuning experiments only)
   const int env_bn = g_tune[0], env_ns = g_tune[1];
@@ -1406,6 +1454,7 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
+  p.direct = (taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && Hs == Ho && Ws == Wo) ? 1 : 0;
   const bool big = wgrad_big(Co, p.ldw);
   const bool narrow = wgrad_narrow(Co, p.ldw);
   const int tiles = wgrad_tiles(Co, p.ldw);
