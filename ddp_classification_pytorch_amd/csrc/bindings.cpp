@@ -127,6 +127,25 @@ std::tuple<Tensor, Tensor> conv_fwd_geo(const Tensor& x, const Tensor& w, int64_
   return {y, slabs};
 }
 
+// the space-to-depth ResNet stem: x [N,H,W,16], w [64,4,4,16] -> y [N,H,W,64] (4x4 / stride 1,
+// pad 2 top/left, 1 bottom/right).  Statistics come as first-level BN partials [P,3,64]
+// (n, mean, M2) from the dedicated kernel (stem.hip), or as conv slabs when the geometry
+// falls back to the implicit GEMM; bn_stats / bn_stats_finalize accept either.
+std::tuple<Tensor, Tensor> stem_fwd(const Tensor& x, const Tensor& w, bool stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(3) == x.size(3), "stem_fwd shapes");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  if (!dcp::stem_fwd_supported(H, W, C, w.size(0), w.size(1), w.size(2)))
+    return conv_fwd_geo(x, w, 1, 2, H, W, stats);
+  TORCH_CHECK((int64_t)N * H * W * 64 < (1ll << 32), "tensor too large");
+  auto y = at::empty({N, H, W, 64}, bf16_like(x));
+  Tensor part = stats ? at::empty({dcp::stem_fwd_blocks(N, H), 3, 64}, f32_like(x)) : at::empty({0}, f32_like(x));
+  dcp::launch_stem_fwd(bp(x), bp(w), bpm(y), stats ? part.data_ptr<float>() : nullptr, zero_page(x.get_device()), N,
+                       H, W, cur_stream());
+  return {y, part};
+}
+
 // dy [N,Ho,Wo,Co], wt [C,KH,KW,Co] (transposed weight) -> dx [N,H,W,C]
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   const optional<Tensor>& add) {
@@ -403,18 +422,27 @@ Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t
 // ---------------------------------------------------------------------------
 // batch norm
 // ---------------------------------------------------------------------------
-// per-channel (n, mean, M2) [1,3,C] from conv slabs (if given) or directly from x
+// statistics given as first-level partials [P,3,C] (n, mean, M2) instead of conv slabs [R,2,C]
+bool is_partials(const Tensor& t, int C) {
+  return t.dim() == 3 && t.size(1) == 3 && t.size(2) == C && t.scalar_type() == at::kFloat;
+}
+
+// per-channel (n, mean, M2) [1,3,C] from conv slabs or partials (if given) or directly from x
 Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
   const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
+  auto out = at::empty({1, 3, C}, f32_like(x));
+  if (from_slabs && is_partials(*slabs, C)) {
+    dcp::launch_bn_merge(slabs->data_ptr<float>(), slabs->size(0), C, out.data_ptr<float>(), cur_stream());
+    return out;
+  }
   if (from_slabs)
     TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 127) / 128 && slabs->size(1) == 2 && slabs->size(2) == C,
                 "slab shape");
   auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
-  auto out = at::empty({1, 3, C}, f32_like(x));
   dcp::launch_bn_stats(bp(x), from_slabs ? slabs->data_ptr<float>() : nullptr, M, C, part.data_ptr<float>(),
                        out.data_ptr<float>(), cur_stream());
   return out;
@@ -433,12 +461,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
   const int M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
   const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
+  auto coef = at::empty({4, C}, f32_like(x));
+  float* cp = coef.data_ptr<float>();
+  if (from_slabs && is_partials(*slabs, C)) {
+    dcp::launch_bn_merge_finalize(slabs->data_ptr<float>(), slabs->size(0), C, (float)eps, fp(gamma), fp(beta), cp,
+                                  cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean), fpm(run_var), (float)momentum,
+                                  cur_stream());
+    return {coef[0], coef[1], coef[2], coef[3]};
+  }
   if (from_slabs)
     TORCH_CHECK(slabs->dim() == 3 && slabs->size(0) == (M + 127) / 128 && slabs->size(1) == 2 && slabs->size(2) == C,
                 "slab shape");
   auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
-  auto coef = at::empty({4, C}, f32_like(x));
-  float* cp = coef.data_ptr<float>();
   dcp::launch_bn_stats_finalize(bp(x), from_slabs ? slabs->data_ptr<float>() : nullptr, M, C, part.data_ptr<float>(),
                                 (float)eps, fp(gamma), fp(beta), cp, cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean),
                                 fpm(run_var), (float)momentum, cur_stream());
@@ -1029,6 +1063,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("to_nhwc_s2d(Tensor src, bool nchw, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc_s2d);
   m.def("conv_fwd_geo(Tensor x, Tensor w, int stride, int pad, int Ho, int Wo, bool stats) -> (Tensor, Tensor)",
         &conv_fwd_geo);
+  m.def("stem_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)", &stem_fwd);
   m.def("conv_wgrad_geo(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad_geo);
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor", &act_bwd);
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);

@@ -592,6 +592,17 @@ void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, f
                      mean, invstd, scale, shift, rm, rv, momentum);
 }
 
+void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, out);
+}
+
+void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const float* gamma, const float* beta,
+                              float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
+                              float momentum, hipStream_t s) {
+  hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps,
+                     gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
+}
+
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s) {
   hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
 }

@@ -74,6 +74,16 @@ void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* par
 void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                               float* shift, float* rm, float* rv, float momentum, hipStream_t s);
+// BN statistics from ready first-level partials [P][3][C] (e.g. the stem kernel's)
+void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s);
+void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const float* gamma, const float* beta,
+                              float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
+                              float momentum, hipStream_t s);
+// stem.hip: the space-to-depth stem conv [N][H][W][16] x [64][4][4][16] -> [N][H][W][64]
+bool stem_fwd_supported(int H, int W, int C, int Co, int KH, int KW);
+int stem_fwd_blocks(int N, int H);
+void launch_stem_fwd(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
+                     hipStream_t s);
 int colsum_partials(int M);
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s);
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,

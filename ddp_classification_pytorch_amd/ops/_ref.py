@@ -99,6 +99,11 @@ def conv_fwd_geo(x, w, stride, pad, Ho, Wo, stats):
     return _nhwc(y).to(x.dtype), torch.empty(0, device=x.device)
 
 
+def stem_fwd(x, w, stats):
+    """the space-to-depth stem: 4x4 / stride 1, pad 2 top/left, output grid = input grid"""
+    return conv_fwd_geo(x, w, 1, 2, x.shape[1], x.shape[2], stats)
+
+
 def conv_wgrad_geo(dy, x, KH, KW, stride, pad):
     Co, C, Ho, Wo = dy.shape[3], x.shape[3], dy.shape[1], dy.shape[2]
     xc = _pad_geo(_nchw(_f(x)), KH, KW, stride, pad, Ho, Wo)

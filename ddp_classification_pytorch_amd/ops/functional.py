@@ -775,7 +775,7 @@ def stem_s2d_weight(w: torch.Tensor) -> torch.Tensor:
 class _StemS2D(Function):
     @staticmethod
     def forward(ctx, x, w16, wb, stats):
-        y, slabs = K(x).conv_fwd_geo(x, wb, 1, 2, x.shape[1], x.shape[2], stats)
+        y, slabs = K(x).stem_fwd(x, wb, stats)  # slabs: BN partials [P,3,64] or conv slabs
         ctx.save_for_backward(x)
         ctx.mark_non_differentiable(slabs)
         ctx.set_materialize_grads(False)

@@ -461,6 +461,38 @@ def test_conv_geo(K, N, H, Ci, Co, k, pad):
     assert relerr(dw, _ref.conv_wgrad_geo(dy.float(), x.float(), k, k, 1, pad)) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(4, 112, 112), (3, 30, 48), (2, 8, 16), (2, 9, 9)])
+def test_stem_fwd(K, N, H, W):
+    """dedicated s2d stem kernel (stem.hip; (2, 9, 9) takes the implicit-GEMM fallback): output
+    vs the fp32 conv, its BN partials vs statistics of the stored bf16 output, and BN finalize
+    from the partials vs from the raw activations"""
+    torch.manual_seed(0)
+    x = rnd(N, H, W, 16)
+    w = rnd(64, 4, 4, 16, scale=256 ** -0.5)
+    y, part = K.stem_fwd(x.to(DEV), w.to(DEV), True)
+    yr, _ = _ref.conv_fwd_geo(x.float(), w.float(), 1, 2, H, W, False)
+    assert y.shape == (N, H, W, 64)
+    assert relerr(y, yr) < 1e-2
+    rows = y.double().reshape(-1, 64)
+    if part.shape[1] == 3:
+        assert part.shape == (N * ((H + 15) // 16), 3, 64)
+        n = part[:, 0].double()
+        assert torch.all(n.sum(0) == N * H * W)
+        mu = (n * part[:, 1].double()).sum(0) / n.sum(0)
+        m2 = part[:, 2].double().sum(0) + (n * (part[:, 1].double() - mu) ** 2).sum(0)
+        assert torch.allclose(mu, rows.mean(0), atol=1e-5, rtol=1e-4)
+        assert torch.allclose(m2 / rows.shape[0], rows.var(0, unbiased=False), atol=1e-6, rtol=1e-4)
+    g, b = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV)
+    a = K.bn_stats_finalize(y, part, g, b, None, None, 0.1, 1e-5)
+    r = K.bn_stats_finalize(y, None, g, b, None, None, 0.1, 1e-5)
+    for u, v in zip(a, r):
+        assert torch.allclose(u, v, atol=1e-4, rtol=1e-4)
+    st = K.bn_stats(y, part)
+    assert torch.allclose(st, K.bn_stats(y, None), atol=1e-3, rtol=1e-4)
+    y2, empty = K.stem_fwd(x.to(DEV), w.to(DEV), False)
+    assert torch.equal(y2, y) and empty.numel() == 0
+
+
 def test_s2d_stem_gpu_matches_plain_stem():
     """The s2d stem (4x4/1 over the space-to-depth input) vs the plain 7x7/2 conv on the HIP
     kernels: same output and, for the same upstream gradient, the same 7x7 weight gradient."""
