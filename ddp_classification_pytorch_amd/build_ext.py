@@ -43,6 +43,9 @@ def _torch_paths():
 
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"]
+# per-file extras: the stem kernel's statistics run beside MFMAs, where packed fp32 (which the
+# SLP vectorizer forms from adjacent scalar adds / FMAs) issues slower than scalar fp32
+FILE_FLAGS = {"stem.hip": ["-fno-slp-vectorize"]}
 
 
 def _headers():
@@ -63,6 +66,7 @@ def _compile(src: str, obj: str, torch_inc, force: bool) -> str:
     cmd = [_hipcc()] + COMMON_FLAGS
     if src.endswith(".hip"):
         cmd += [f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-x", "hip"]
+        cmd += FILE_FLAGS.get(os.path.basename(src), [])
     else:
         # host-only translation unit (bindings): torch headers, no device code
         cmd += ["-D_GLIBCXX_USE_CXX11_ABI=1"] + [f"-I{p}" for p in torch_inc]

@@ -12,10 +12,11 @@
 //    channels in separate planes of 16-byte pixels with a 128-pixel pitch, which puts the
 //    16 lanes of every B-fragment read on 16 distinct 16-byte bank groups;
 //  * a wave computes 32 output channels of one whole output row per step (W/16 MFMA tiles
-//    per 16-channel group), stores bf16 straight from the accumulators (8 bytes per lane per
-//    tile) and folds the row into per-channel (n, mean, M2) statistics, merged per workgroup
-//    into part[block][3][64] -- the first level of the BatchNorm statistics (bn.hip), so
-//    bn_stats / bn_stats_finalize skip the slab pass.
+//    per 16-channel group), stages the bf16 row pair in LDS for 16-byte coalesced stores and
+//    accumulates shifted per-channel sums of the fp32 accumulators,
+//    turned into (n, mean, M2) and merged per workgroup into part[block][3][64] -- the first
+//    level of the BatchNorm statistics (bn.hip), so bn_stats / bn_stats_finalize skip the
+//    slab pass.
 #include "common.cuh"
 #include "launchers.h"
 
@@ -41,21 +42,15 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-// sum over the 16 lanes of a DPP row, result in every lane of the row
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0x128>(v);  // row_ror:8
-  v += dpp_f<0x124>(v);  // row_ror:4
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  return v;
-}
 }  // namespace
 
 template <int NSUB>  // W = 16 * NSUB output columns
 __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
   constexpr int W = NSUB * 16;
   static_assert(W + 4 <= kPlanePx, "row does not fit a plane");
-  extern __shared__ __attribute__((aligned(16))) char ring[];  // kSlots * kSlotBytes
+  // [kSlots * kSlotBytes ring][2 * W * 128 B output staging of one row pair]
+  extern __shared__ __attribute__((aligned(16))) char ring[];
+  char* stage = ring + kSlots * kSlotBytes;
   __shared__ float xch[3][kStemCo];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -92,20 +87,24 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
 #pragma unroll
   for (int d = -2; d <= 2; ++d) load_row(r0 + d);
 
-  float sn = 0.f, smean[8], sm2[8];  // this wave's running statistics of channels (j, r)
+  // statistics: per lane and channel, sums of (v - K) and (v - K)^2 over the lane's pixels with
+  // K = the lane's first value of the channel (c = 4 j + r; scalar fp32: packed fp32 beside
+  // MFMAs costs more than it saves)
+  float shf[8], s1[8], s2[8];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) smean[c] = sm2[c] = 0.f;
+  for (int c = 0; c < 8; ++c) shf[c] = s1[c] = s2[c] = 0.f;
 
   const int nsteps = (r1 - r0) >> 1;
   for (int st = 0; st < nsteps; ++st) {
     const int y0 = r0 + 2 * st;
-    // rows y0-2 .. y0+2 landed (issued before the previous step's 2*NSUB stores); the slots
-    // the next prefetch overwrites were last read in the previous step
+    // rows y0-2 .. y0+2 landed: they were issued before the previous step's NSUB output stores
+    // per lane (vmcnt counts loads, stores and LDS-DMA together, in issue order).  After the
+    // barrier every wave is done with the previous step's ring slots and staging reads.
     if (st == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // also publishes the zeroed padding
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NSUB) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSUB) : "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
@@ -136,71 +135,96 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], af[i], acc[j][i], 0, 0, 0);
     }
 
-    // epilogue: lane holds co = (2 cg + j) * 16 + 4 kq + r of pixel i * 16 + l16
-    bf16* yrow = p.y + (size_t)(n * H + yy) * W * kStemCo + (2 * cg) * 16 + kq * 4;
-    bf16x4 o[2][NSUB];
+    // epilogue: lane holds co = (2 cg + j) * 16 + 4 kq + r of pixel i * 16 + l16.  The row pair
+    // is contiguous in memory (2 W pixels x 128 B): staged in LDS in that order, 8-byte slots
+    // of a pixel XOR-swizzled by the pixel index (conflict-free 8-byte writes), then written
+    // by every thread as 16-byte stores, 4 KB per workgroup instruction (8-byte stores from
+    // the accumulators are store-issue bound).
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < NSUB; ++i) {
+        bf16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[j][i][r] = f2bf(acc[j][i][r]);
-        *(bf16x4*)(yrow + (size_t)(i * 16 + l16) * kStemCo + j * 16) = o[j][i];
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        const uint32_t px = rp * W + i * 16 + l16;
+        const uint32_t slot = (((2 * cg + j) * 4 + kq) ^ (px & 15));
+        *(bf16x4*)(stage + px * 128 + slot * 8) = o;
       }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // not __syncthreads: keep the loads in flight
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16* ydst = p.y + (size_t)(n * H + y0) * W * kStemCo;
+#pragma unroll
+    for (int k = 0; k < NSUB; ++k) {
+      const uint32_t q = k * 256 + tid, px = q >> 3, c = q & 7, sw = px & 15;
+      u32x4 v = *(const u32x4*)(stage + px * 128 + ((c ^ (sw >> 1)) << 4));
+      if (sw & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+      *(u32x4*)(ydst + (size_t)q * 8) = v;
+    }
     if (p.part) {
-      // this row's (W, mean, M2) per channel (of the stored bf16 values), merged into the
-      // wave's running statistics with Chan's formula
-      const float nb = (float)W, f = nb / (sn + nb), cross = sn * f;
+      if (st == 0)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int c = 0; c < 8; ++c) shf[c] = acc[c >> 2][0][c & 3];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s1 = 0.f;
+      for (int c = 0; c < 8; ++c)
 #pragma unroll
-          for (int i = 0; i < NSUB; ++i) s1 += bf2f(o[j][i][r]);
-          const float mb = row16_sum(s1) * (1.f / (float)W);
-          float s2 = 0.f;
-#pragma unroll
-          for (int i = 0; i < NSUB; ++i) {
-            const float d = bf2f(o[j][i][r]) - mb;
-            s2 += d * d;
-          }
-          const float m2b = row16_sum(s2);
-          const int c = j * 4 + r;
-          const float d = mb - smean[c];
-          smean[c] += d * f;
-          sm2[c] += m2b + d * d * cross;
+        for (int i = 0; i < NSUB; ++i) {
+          const float d = acc[c >> 2][i][c & 3] - shf[c];
+          s1[c] += d;
+          s2[c] = fmaf(d, d, s2[c]);
         }
-      sn += nb;
     }
   }
 
   if (p.part) {
-    // merge the two row waves of each channel half; lanes l16 == 0 hold their group's channels
+    // lane (n, mean, M2) per channel, merged over the 16 lanes of the pixel group (equal counts),
+    // then across the two row waves of each channel half through LDS
+    float n = (float)(NSUB * nsteps), mean[8], m2[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float a1 = s1[c], a2 = s2[c];
+      mean[c] = shf[c] + a1 / n;
+      m2[c] = fmaxf(a2 - a1 * a1 / n, 0.f);
+    }
+    auto level = [&](auto partner) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float mb = partner(mean[c]), m2b = partner(m2[c]);
+        const float d = mb - mean[c];
+        mean[c] += 0.5f * d;
+        m2[c] += m2b + d * d * (0.5f * n);
+      }
+      n *= 2.f;
+    };
+    level([](float v) { return dpp_f<0x128>(v); });
+    level([](float v) { return dpp_f<0x124>(v); });
+    level([](float v) { return dpp_f<0x4E>(v); });
+    level([](float v) { return dpp_f<0xB1>(v); });
     if (rp == 1 && l16 == 0)
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const int co = (2 * cg + (c >> 2)) * 16 + kq * 4 + (c & 3);
-        xch[0][co] = sn;
-        xch[1][co] = smean[c];
-        xch[2][co] = sm2[c];
+        xch[0][co] = n;
+        xch[1][co] = mean[c];
+        xch[2][co] = m2[c];
       }
     __syncthreads();
     if (rp == 0 && l16 == 0)
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const int co = (2 * cg + (c >> 2)) * 16 + kq * 4 + (c & 3);
-        const float nbb = xch[0][co], nt = sn + nbb;
-        float mean = smean[c], m2 = sm2[c];
+        const float nbb = xch[0][co], nt = n + nbb;
+        float mu = mean[c], q = m2[c];
         if (nbb > 0.f) {
-          const float d = xch[1][co] - mean, f = nbb / nt;
-          mean += d * f;
-          m2 += xch[2][co] + d * d * sn * f;
+          const float d = xch[1][co] - mu, f = nbb / nt;
+          mu += d * f;
+          q += xch[2][co] + d * d * n * f;
         }
         float* out = p.part + (size_t)blockIdx.x * 3 * kStemCo + co;
         out[0] = nt;
-        out[kStemCo] = mean;
-        out[2 * kStemCo] = m2;
+        out[kStemCo] = mu;
+        out[2 * kStemCo] = q;
       }
   }
 }
@@ -218,7 +242,7 @@ void launch_stem_fwd(const bf16* x, const bf16* w, bf16* y, float* part, const b
   const dim3 grid(stem_fwd_blocks(N, H)), block(256);
   switch (W / 16) {
 #define DCP_STEM(NS_) \
-  case NS_: hipLaunchKernelGGL(stem_fwd_kernel<NS_>, grid, block, kSlots * kSlotBytes, s, p); break;
+  case NS_: hipLaunchKernelGGL(stem_fwd_kernel<NS_>, grid, block, kSlots * kSlotBytes + NS_ * 16 * 256, s, p); break;
     DCP_STEM(1) DCP_STEM(2) DCP_STEM(3) DCP_STEM(4) DCP_STEM(5) DCP_STEM(6) DCP_STEM(7)
 #undef DCP_STEM
     default: break;

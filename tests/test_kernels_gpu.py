@@ -464,8 +464,8 @@ def test_conv_geo(K, N, H, Ci, Co, k, pad):
 @pytest.mark.parametrize("N,H,W", [(4, 112, 112), (3, 30, 48), (2, 8, 16), (2, 9, 9)])
 def test_stem_fwd(K, N, H, W):
     """dedicated s2d stem kernel (stem.hip; (2, 9, 9) takes the implicit-GEMM fallback): output
-    vs the fp32 conv, its BN partials vs statistics of the stored bf16 output, and BN finalize
-    from the partials vs from the raw activations"""
+    vs the fp32 conv, its BN partials (taken from the fp32 accumulators) vs statistics of the
+    fp32 conv, and BN finalize from the partials vs from the stored bf16 activations"""
     torch.manual_seed(0)
     x = rnd(N, H, W, 16)
     w = rnd(64, 4, 4, 16, scale=256 ** -0.5)
@@ -473,7 +473,7 @@ def test_stem_fwd(K, N, H, W):
     yr, _ = _ref.conv_fwd_geo(x.float(), w.float(), 1, 2, H, W, False)
     assert y.shape == (N, H, W, 64)
     assert relerr(y, yr) < 1e-2
-    rows = y.double().reshape(-1, 64)
+    rows = yr.double().reshape(-1, 64).to(DEV)
     if part.shape[1] == 3:
         assert part.shape == (N * ((H + 15) // 16), 3, 64)
         n = part[:, 0].double()
@@ -485,10 +485,10 @@ def test_stem_fwd(K, N, H, W):
     g, b = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV)
     a = K.bn_stats_finalize(y, part, g, b, None, None, 0.1, 1e-5)
     r = K.bn_stats_finalize(y, None, g, b, None, None, 0.1, 1e-5)
-    for u, v in zip(a, r):
-        assert torch.allclose(u, v, atol=1e-4, rtol=1e-4)
+    for u, v in zip(a, r):  # partials: fp32 accumulators; reference: the bf16-rounded y
+        assert torch.allclose(u, v, atol=3e-3, rtol=5e-3)
     st = K.bn_stats(y, part)
-    assert torch.allclose(st, K.bn_stats(y, None), atol=1e-3, rtol=1e-4)
+    assert torch.allclose(st, K.bn_stats(y, None), atol=1e-3, rtol=5e-3)  # bf16 rounding of y
     y2, empty = K.stem_fwd(x.to(DEV), w.to(DEV), False)
     assert torch.equal(y2, y) and empty.numel() == 0
 
