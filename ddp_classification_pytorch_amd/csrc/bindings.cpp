@@ -285,7 +285,7 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
   const int ncu = num_cus(dy.get_device());
-  const int splits = dcp::wgrad_splits(N * Ho * Wo, Co, KH * KW * C, KH * KW, ncu, nullptr);
+  const int splits = dcp::wgrad_plan_splits(N, Ho, Wo, Co, H, W, C, stride, taps, ncu);
   auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
   dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
                     part.data_ptr<float>(), zero_page(dy.get_device()), ncu, cur_stream());
@@ -304,7 +304,7 @@ Tensor conv_wgrad_geo(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW,
   auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
   const int ncu = num_cus(dy.get_device());
-  const int splits = dcp::wgrad_splits(N * Ho * Wo, Co, KH * KW * C, KH * KW, ncu, nullptr);
+  const int splits = dcp::wgrad_plan_splits(N, Ho, Wo, Co, H, W, C, stride, taps, ncu);
   auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
   dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
                     part.data_ptr<float>(), zero_page(dy.get_device()), ncu, cur_stream());

@@ -1122,21 +1122,25 @@ __device__ __forceinline__ bf16x8 tr_frag128(const char* img, uint32_t row0, uin
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BK>
+// NJ: 16-column subtiles per wave -- tiles of 64 NJ columns (4: 256; 3: 192, which covers the
+// 576 columns of a 3x3 conv over 64 channels in three full tiles instead of 2.25 tiles of 256).
+// The im2col image keeps its 512-byte row pitch; chunks past the tile are never loaded.
+template <int BK, int NJ>
 __global__ void __launch_bounds__(256, 3)
 wgrad64_kernel(const WgradParams p) {
+  constexpr int TW = 64 * NJ;     // columns per tile
   constexpr int IMGA = BK * 128;  // BK pixels x 64 co
-  constexpr int IMGB = BK * 512;  // BK pixels x 256 cols
+  constexpr int IMGB = BK * 512;  // BK pixels x (256-column pitch)
   constexpr int STAGE = IMGA + IMGB;
   constexpr int SA = BK / 32, SB = BK / 8;  // LDS-DMA instructions per thread: dY / im2col image
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntn = (p.ldw + 255) / 256;
+  const int ntn = (p.ldw + TW - 1) / TW;
   const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);  // see wgrad_kernel
   const uint32_t split = lid / ntn;
   const int tn = lid % ntn;
-  const int kcol0 = tn * 256;
+  const int kcol0 = tn * TW;
   const int mstart = split * p.rows_per_split;
   const int mend = min(p.M, mstart + p.rows_per_split);
   const int nkt = (mend - mstart + BK - 1) / BK;
@@ -1154,13 +1158,14 @@ wgrad64_kernel(const WgradParams p) {
   // im2col image: SB instructions per thread, instruction i covers rows (wave*SB+i)*2 .. +1
   int b_dy[SB], b_dx[SB];
   uint32_t b_ci[SB];
-  bool b_cok[SB];
+  bool b_cok[SB], b_in[SB];
 #pragma unroll
   for (int i = 0; i < SB; ++i) {
     const uint32_t r = (wave * SB + i) * 2 + (lane >> 5);
     const uint32_t c = (lane & 31) ^ (((r & 3u) << 1) | (((r >> 3) & 1u) << 3));
     const int kc = kcol0 / 8 + c;
-    b_cok[i] = kc < p.kc_total;
+    b_in[i] = c < 8 * NJ;
+    b_cok[i] = b_in[i] && kc < p.kc_total;
     const int t = b_cok[i] ? (int)fdiv(kc, p.div_cpt) : 0;
     b_ci[i] = (kc - t * p.cpt) * 8;
     b_dy[i] = p.dy_t[t];
@@ -1195,15 +1200,16 @@ wgrad64_kernel(const WgradParams p) {
         const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
       }
-      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SB + i) * 1024), 16, 0, 0);
+      if (NJ == 4 || b_in[i])
+        __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SB + i) * 1024), 16, 0, 0);
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nkt > 0) {
     stage(0, 0);
@@ -1218,15 +1224,15 @@ wgrad64_kernel(const WgradParams p) {
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       const uint32_t row0 = s * 32 + 8 * (lane >> 4);
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = tr_frag128(Ai, row0, i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag512(Bi, row0, wave * 64 + j * 16, lane);
+      for (int j = 0; j < NJ; ++j) bfr[j] = tr_frag512(Bi, row0, wave * 16 * NJ + j * 16, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1237,8 +1243,8 @@ wgrad64_kernel(const WgradParams p) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kcol = kcol0 + wave * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < NJ; ++j) {
+      const int kcol = kcol0 + wave * 16 * NJ + j * 16 + (lane & 15);
       if (kcol >= p.ldw) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1418,8 +1424,14 @@ static bool wgrad_big(int Co, int ldw) { return g_tune[7] != 2 && Co >= 256 && l
 // 64-row tiles: Co <= 64 with enough columns to fill 256-wide tiles at least half
 static bool wgrad_narrow(int Co, int ldw) { return g_tune[7] != 3 && Co <= 64 && ldw >= 128; }
 
+// 16-column subtiles per wave of the narrow kernel: 192-column tiles where they pad less
+static int wgrad_nj(int ldw) {
+  if (g_tune[14] == 4 || g_tune[14] == 3) return g_tune[14];
+  return ((ldw + 191) / 192) * 3 < ((ldw + 255) / 256) * 4 ? 3 : 4;
+}
+
 static int wgrad_tiles(int Co, int ldw) {
-  if (wgrad_narrow(Co, ldw)) return (ldw + 255) / 256;
+  if (wgrad_narrow(Co, ldw)) return (ldw + 64 * wgrad_nj(ldw) - 1) / (64 * wgrad_nj(ldw));
   const int bt = wgrad_big(Co, ldw) ? 256 : 128;
   return ((Co + bt - 1) / bt) * ((ldw + bt - 1) / bt);
 }
@@ -1441,6 +1453,23 @@ int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_spl
   return splits;
 }
 
+// the 3x3 / stride-1 / pad-1 same-size geometry of wgrad3x3.hip (taps in fwd_taps order)
+static bool is_3x3_same(int Ho, int Wo, int Hs, int Ws, int ss, const TapList& taps) {
+  if (taps.n != 9 || ss != 1 || Hs != Ho || Ws != Wo) return false;
+  for (int i = 0; i < 9; ++i)
+    if (taps.dy[i] != i / 3 - 1 || taps.dx[i] != i % 3 - 1) return false;
+  return true;
+}
+
+int wgrad_plan_splits(int N, int Ho, int Wo, int Co, int Hs, int Ws, int Cs, int ss, const TapList& taps,
+                      int num_cu) {
+  if (is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
+    const int s3 = wgrad3x3_splits(N, Ho, Wo, Cs, Co, num_cu);
+    if (s3 > 0) return s3;
+  }
+  return wgrad_splits(N * Ho * Wo, Co, taps.n * Cs, taps.n, num_cu, nullptr);
+}
+
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
                   const bf16* src, int Hs, int Ws, int Cs, int ss,
                   const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream) {
@@ -1453,6 +1482,15 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   for (int i = 0; i < taps.n; ++i) {
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
+  }
+  if (is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
+    const int s3 = wgrad3x3_splits(N, Ho, Wo, Cs, Co, num_cu);
+    if (s3 > 0) {
+      // part holds wgrad_plan_splits(...) = s3 partial slices (the caller sized it by that plan)
+      launch_wgrad3x3(dy, src, N, Ho, Wo, Cs, Co, part, s3, zero, stream);
+      launch_split_reduce(part, s3, Co * 9 * Cs, dw, stream);
+      return;
+    }
   }
   p.direct = (taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && Hs == Ho && Ws == Wo) ? 1 : 0;
   const bool big = wgrad_big(Co, p.ldw);
@@ -1472,10 +1510,15 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   // 32 pixel rows per k-tile (g_tune[12] = 32): half the LDS of the 64-row tiles
   const bool wbk32 = g_tune[12] == 32;
   if (narrow) {
-    if (wbk32)
-      hipLaunchKernelGGL(wgrad64_kernel<32>, dim3(tiles * splits), dim3(256), 2 * 32 * (128 + 512), stream, p);
+    const int nj = wgrad_nj(p.ldw);
+    if (wbk32 && nj == 4)
+      hipLaunchKernelGGL((wgrad64_kernel<32, 4>), dim3(tiles * splits), dim3(256), 2 * 32 * (128 + 512), stream, p);
+    else if (wbk32)
+      hipLaunchKernelGGL((wgrad64_kernel<32, 3>), dim3(tiles * splits), dim3(256), 2 * 32 * (128 + 512), stream, p);
+    else if (nj == 4)
+      hipLaunchKernelGGL((wgrad64_kernel<64, 4>), dim3(tiles * splits), dim3(256), 2 * 64 * (128 + 512), stream, p);
     else
-      hipLaunchKernelGGL(wgrad64_kernel<64>, dim3(tiles * splits), dim3(256), 2 * 64 * (128 + 512), stream, p);
+      hipLaunchKernelGGL((wgrad64_kernel<64, 3>), dim3(tiles * splits), dim3(256), 2 * 64 * (128 + 512), stream, p);
   } else if (big) {
     constexpr int lds = 4 * 64 * 512;
     static bool attr = false;

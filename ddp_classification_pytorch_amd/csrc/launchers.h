@@ -11,7 +11,9 @@ namespace dcp {
 // tuning switches for in-process A/B experiments (tools/conv_bench.py --cfgs); all 0 = defaults
 // [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant,
 // [5] wgrad blocks per CU, [6] wgrad atomics, [7] wgrad tile (0 auto, 2 no 256-tile, 3 no 64-row tile),
-// [8] conv k-tile depth (32 with [1] = 3 or 4)
+// [8] conv k-tile depth (32 with [1] = 3 or 4), [9]-[11] elementwise grids (bn.hip),
+// [12] wgrad 32-row k-tiles, [13] narrow-channel conv k-tile depth, [14] narrow wgrad
+// subtiles per wave (3 or 4; 0 auto), [15] = 1: no direct 3x3 weight gradient
 extern int g_tune[16];
 
 constexpr int kMaxTaps = 64;
@@ -46,6 +48,13 @@ void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t
 // partial-slab split-K weight gradient: dw is fully written when part != nullptr
 // (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split);
+// splits (partials) of launch_wgrad for this geometry: the direct 3x3 kernel's where it applies
+int wgrad_plan_splits(int N, int Ho, int Wo, int Co, int Hs, int Ws, int Cs, int ss, const TapList& taps,
+                      int num_cu);
+// wgrad3x3.hip: direct 3x3 / stride-1 / pad-1 weight gradient (0 = not applicable)
+int wgrad3x3_splits(int N, int H, int W, int C, int Co, int num_cu);
+void launch_wgrad3x3(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Co, float* part, int splits,
+                     const bf16* zero, hipStream_t stream);
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream);
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
                   const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream);

@@ -685,11 +685,12 @@ def test_bn_act_mask_and_masked_dgrad_bn(K):
     assert relerr(s1, s0) < 1e-5
 
 
-@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4))])
+@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4)), ((14, 4),), ((14, 3),), ((12, 32), (14, 3))])
 @pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
                                    (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1)])
 def test_conv_wgrad_variants(K, cfg, shape):
-    """Weight gradient with 32-row k-tiles (and another split plan) against the fp32 reference."""
+    """Weight gradient with 32-row k-tiles, another split plan, and the narrow (Co <= 64) kernel's
+    256- / 192-column tiles (g_tune[14] = 4 / 3), against the fp32 reference."""
     N, H, W, Ci, Co, k, s, p = shape
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     dy, x = rnd(N, Ho, Wo, Co), rnd(N, H, W, Ci)
@@ -702,6 +703,24 @@ def test_conv_wgrad_variants(K, cfg, shape):
         for i, _ in cfg:
             K.set_tuning(i, 0)
     assert relerr(dw, _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)) < 5e-3
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co", [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (3, 14, 14, 256, 128),
+                                        (2, 7, 7, 128, 64), (2, 13, 17, 64, 192), (1, 9, 112, 64, 64)])
+def test_wgrad3x3_direct(K, N, H, W, Ci, Co):
+    """Direct 3x3 / stride-1 weight gradient (wgrad3x3.hip: strip-staged windows, partial strips,
+    several channel blocks) against the fp32 reference and the implicit-GEMM path (g_tune[15] = 1)."""
+    torch.manual_seed(0)
+    dy, x = rnd(N, H, W, Co), rnd(N, H, W, Ci)
+    dw = K.conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 1, 1)
+    assert relerr(dw, _ref.conv_wgrad(dy.float(), x.float(), 3, 3, 1, 1)) < 5e-3
+    try:
+        K.set_tuning(15, 1)
+        dw_gemm = K.conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 1, 1)
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(15, 0)
+    assert relerr(dw, dw_gemm) < 2e-3
 
 
 @pytest.mark.parametrize("N,H,Ci,Co,k,pad", [(2, 32, 16, 64, 4, 2), (2, 16, 8, 64, 3, 1)])

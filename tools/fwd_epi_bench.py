@@ -34,14 +34,18 @@ def main():
         flops = 2.0 * N * Ho * Ho * Co * k * k * Ci
         row = []
         for stats in (False, True):
-            for abl in (0, 1, 2):
+            for abl in (0, 1, 2, 3):
                 K.set_tuning(2, abl)
                 us = timeit(lambda: K.conv_fwd(x, w, s, k // 2, stats), iters=10)
                 row.append(us)
             K.set_tuning(2, 0)
+        K.set_tuning(8, 64)  # 64-deep k-tiles for every shape (disables the 1x1 BK32 heuristic)
+        bk64 = timeit(lambda: K.conv_fwd(x, w, s, k // 2, True), iters=10)
+        K.set_tuning(8, 0)
         print(f"H={H:3d} {Ci:4d}->{Co:4d} k{k}: plain {row[0]:7.1f}us ({gb / row[0] * 1e3:5.2f} TB/s "
-              f"{flops / row[0] / 1e6:6.0f} TF/s) noload {row[1]:7.1f} nomfma {row[2]:7.1f} | stats {row[3]:7.1f}us "
-              f"({gb / row[3] * 1e3:5.2f} TB/s) noload {row[4]:7.1f} nomfma {row[5]:7.1f}", flush=True)
+              f"{flops / row[0] / 1e6:6.0f} TF/s) noload {row[1]:7.1f} nomfma {row[2]:7.1f} epi-only {row[3]:7.1f} | "
+              f"stats {row[4]:7.1f}us ({gb / row[4] * 1e3:5.2f} TB/s) noload {row[5]:7.1f} nomfma {row[6]:7.1f} "
+              f"epi-only {row[7]:7.1f} | stats bk64 {bk64:7.1f}", flush=True)
         del x, w
     x = torch.randn(N, 112, 112, 16, device="cuda").bfloat16()
     w = (torch.randn(64, 4, 4, 16, device="cuda") / 16).bfloat16()
