@@ -681,9 +681,10 @@ Tensor gap_fwd(const Tensor& x) {
   CHECK_ACT(x);
   const int N = x.size(0), C = x.size(-1);
   const int HW = x.numel() / (N * C);
-  TORCH_CHECK(C % 8 == 0, "gap channels");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && HW > 0, "gap channels");
   auto y = at::empty({N, C}, x.options());
-  dcp::launch_gap_fwd(bp(x), bpm(y), N, HW, C, cur_stream());
+  auto part = at::empty({dcp::hw_splits(N, HW, C), N, C}, f32_like(x));
+  dcp::launch_gap_fwd(bp(x), bpm(y), part.data_ptr<float>(), N, HW, C, cur_stream());
   return y;
 }
 
@@ -817,11 +818,14 @@ std::tuple<Tensor, Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor
   CHECK_ACT(x);
   CHECK_ACT(g);
   const int N = x.size(0), C = x.size(-1);
+  const int HW = x.numel() / (N * C);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && HW > 0 && g.numel() == (int64_t)N * C, "chan_scale_bwd shapes");
   auto dx = at::empty_like(x);
   auto dg = at::empty({N, C}, f32_like(x));
+  auto part = at::empty({dcp::hw_splits(N, HW, C), N, C}, f32_like(x));
   Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
   dcp::launch_chan_scale_bwd(bp(dy), bp(x), bp(g), res.has_value() ? bp(*res) : nullptr, bpm(dx),
-                             dg.data_ptr<float>(), want_dres ? bpm(dres) : nullptr, N, x.numel() / (N * C), C,
+                             dg.data_ptr<float>(), part.data_ptr<float>(), want_dres ? bpm(dres) : nullptr, N, HW, C,
                              relu ? 1 : 0, cur_stream());
   return {dx, dg, dres};
 }

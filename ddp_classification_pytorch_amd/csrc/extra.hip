@@ -256,45 +256,61 @@ __global__ void __launch_bounds__(256) chan_scale_fwd_kernel(const bf16* __restr
   }
 }
 
-// dz = dy * relu'(z);  dx = dz * g ; dg[n][c] = sum_hw dz*x ; dres = dz
-// one thread per (n, 8-channel chunk); recomputes z from x, g, res
+// dz = dy * relu'(z);  dx = dz * g ; dg[n][c] = sum_hw dz*x ; dres = dz  (z recomputed from x,
+// g, res).  Workgroup (n, s) covers rows [HW s / S, HW (s+1) / S) of image n, 256 / (C/8) rows
+// per pass, and writes its dg partial part[s][n][C] (summed by launch_partial_sum): the early
+// SE layers (56x56, 64 channels) have few (n, chunk) pairs but many rows.
 __global__ void __launch_bounds__(256) chan_scale_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                              const bf16* __restrict__ g, const bf16* __restrict__ res,
-                                                             bf16* __restrict__ dx, float* __restrict__ dg,
+                                                             bf16* __restrict__ dx, float* __restrict__ part,
                                                              bf16* __restrict__ dres, int N, int HW, int C,
                                                              int relu) {
-  const int cpr = C >> 3;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * cpr) return;
-  const int n = i / cpr, ch = i - n * cpr;
-  const bf16x8 s = *(const bf16x8*)(g + (size_t)n * C + ch * 8);
+  const int n = blockIdx.x, s = blockIdx.y, S = gridDim.y;
+  const int cpr = C >> 3, rpp = 256 / cpr;
+  const int slot = threadIdx.x / cpr, ch = threadIdx.x - slot * cpr;
+  const int r0 = (int)((long long)HW * s / S), r1 = (int)((long long)HW * (s + 1) / S);
   float acc[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-  for (int t = 0; t < HW; ++t) {
-    const size_t o = ((size_t)n * HW + t) * C + ch * 8;
-    const bf16x8 gv = *(const bf16x8*)(dy + o);
-    const bf16x8 xv = *(const bf16x8*)(x + o);
-    bf16x8 rv;
-    if (res) rv = *(const bf16x8*)(res + o);
-    bf16x8 d, dz8;
+  if (slot < rpp) {
+    const bf16x8 sv = *(const bf16x8*)(g + (size_t)n * C + ch * 8);
+    float sc[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float dz = bf2f(gv[q]);
-      if (relu) {
-        float z = bf2f(xv[q]) * bf2f(s[q]);
-        if (res) z += bf2f(rv[q]);
-        dz = z > 0.f ? dz : 0.f;
+    for (int q = 0; q < 8; ++q) sc[q] = bf2f(sv[q]);
+    for (int t = r0 + slot; t < r1; t += rpp) {
+      const size_t o = ((size_t)n * HW + t) * C + ch * 8;
+      const bf16x8 gv = *(const bf16x8*)(dy + o);
+      const bf16x8 xv = *(const bf16x8*)(x + o);
+      bf16x8 rv;
+      if (res) rv = *(const bf16x8*)(res + o);
+      bf16x8 d, dz8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float dz = bf2f(gv[q]);
+        if (relu) {
+          float z = bf2f(xv[q]) * sc[q];
+          if (res) z += bf2f(rv[q]);
+          dz = z > 0.f ? dz : 0.f;
+        }
+        acc[q] += dz * bf2f(xv[q]);
+        d[q] = f2bf(dz * sc[q]);
+        dz8[q] = f2bf(dz);
       }
-      acc[q] += dz * bf2f(xv[q]);
-      d[q] = f2bf(dz * bf2f(s[q]));
-      dz8[q] = f2bf(dz);
+      *(bf16x8*)(dx + o) = d;
+      if (dres) *(bf16x8*)(dres + o) = dz8;
     }
-    *(bf16x8*)(dx + o) = d;
-    if (dres) *(bf16x8*)(dres + o) = dz8;
   }
+  __shared__ float red[256 * 8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) dg[(size_t)n * C + ch * 8 + q] = acc[q];
+  for (int q = 0; q < 8; ++q) red[threadIdx.x * 8 + q] = acc[q];
+  __syncthreads();
+  if (slot == 0) {
+    for (int k = 1; k < rpp; ++k)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += red[(k * cpr + ch) * 8 + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part[((size_t)s * N + n) * C + ch * 8 + q] = acc[q];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -351,10 +367,11 @@ void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* 
   hipLaunchKernelGGL(chan_scale_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, g, res, y, N, HW, C, relu);
 }
 void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg,
-                           bf16* dres, int N, int HW, int C, int relu, hipStream_t st) {
-  const int n = N * (C / 8);
-  hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3((n + 63) / 64), dim3(64), 0, st, dy, x, g, res, dx, dg, dres, N, HW,
-                     C, relu);
+                           float* part, bf16* dres, int N, int HW, int C, int relu, hipStream_t st) {
+  const int S = hw_splits(N, HW, C);
+  hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3(N, S), dim3(256), 0, st, dy, x, g, res, dx, part, dres, N, HW, C,
+                     relu);
+  launch_partial_sum(part, S, N * C, dg, st);
 }
 
 }  // namespace dcp

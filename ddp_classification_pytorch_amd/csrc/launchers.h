@@ -122,7 +122,10 @@ void launch_maxpool_bn_bwd(const bf16* dy, const uint8_t* idx, const bf16* x, in
                            float inv_count, bf16* dx, hipStream_t st);
 void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int H, int W, int C, int Ho, int Wo,
                         int k, int s, int p, hipStream_t st);
-void launch_gap_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t st);
+// two-level reductions over HW per (n, c) (gap_fwd, chan_scale_bwd): row splits S; the
+// part workspace holds S x N x C floats
+int hw_splits(int N, int HW, int C);
+void launch_gap_fwd(const bf16* x, bf16* y, float* part, int N, int HW, int C, hipStream_t st);
 void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st);
 void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int inverse, hipStream_t st);
 
@@ -188,7 +191,7 @@ void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, i
                        int s, int p, int reflect, hipStream_t st);
 void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* y, int N, int HW, int C, int relu,
                            hipStream_t st);
-void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg,
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg, float* part,
                            bf16* dres, int N, int HW, int C, int relu, hipStream_t st);
 
 }  // namespace dcp

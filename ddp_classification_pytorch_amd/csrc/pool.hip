@@ -248,27 +248,58 @@ __global__ void __launch_bounds__(256) maxpool_bn_bwd_kernel(const bf16* __restr
   }
 }
 
-// global average pool [N][HW][C] -> [N][C] (bf16 out, fp32 accumulate)
-__global__ void __launch_bounds__(256) gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
-                                                      int HW, int C) {
-  const int cpr = C >> 3;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * cpr) return;
-  const int n = i / cpr, ch = i - n * cpr;
-  float acc[8];
+// global average pool [N][HW][C] -> [N][C] (bf16 out, fp32 accumulate), two levels so that
+// early, large-HW layers (TResNet's SE blocks at 56x56 / 64 channels) spread over the chip:
+// workgroup (n, s) sums rows [HW s / S, HW (s+1) / S) of image n -> part[s][n][C]; then
+// gap_final sums the S partials of each (n, c).  C <= 2048 (one 8-channel chunk per thread).
+__device__ __forceinline__ void rows_sum8(const bf16* __restrict__ base, int r0, int r1, int rpp, int C, float* acc) {
+  int r = r0;
+  for (; r + 3 * rpp < r1; r += 4 * rpp) {
+    bf16x8 v[4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-  const bf16* base = x + (size_t)n * HW * C + ch * 8;
-  for (int t = 0; t < HW; ++t) {
-    const bf16x8 v = *(const bf16x8*)(base + (size_t)t * C);
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(base + (size_t)(r + u * rpp) * C);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += bf2f(v[u][q]);
+  }
+  for (; r < r1; r += rpp) {
+    const bf16x8 v = *(const bf16x8*)(base + (size_t)r * C);
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] += bf2f(v[q]);
   }
-  const float inv = 1.f / HW;
-  bf16x8 o;
+}
+
+__global__ void __launch_bounds__(256) gap_partial_kernel(const bf16* __restrict__ x, float* __restrict__ part, int N,
+                                                          int HW, int C) {
+  const int n = blockIdx.x, s = blockIdx.y, S = gridDim.y;
+  const int cpr = C >> 3, rpp = 256 / cpr;
+  const int slot = threadIdx.x / cpr, ch = threadIdx.x - slot * cpr;
+  const int r0 = (int)((long long)HW * s / S), r1 = (int)((long long)HW * (s + 1) / S);
+  float acc[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q] * inv);
-  *(bf16x8*)(y + (size_t)n * C + ch * 8) = o;
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (slot < rpp) rows_sum8(x + (size_t)n * HW * C + ch * 8, r0 + slot, r1, rpp, C, acc);
+  __shared__ float red[256 * 8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[threadIdx.x * 8 + q] = acc[q];
+  __syncthreads();
+  if (slot == 0) {
+    for (int k = 1; k < rpp; ++k)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += red[(k * cpr + ch) * 8 + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) part[((size_t)s * N + n) * C + ch * 8 + q] = acc[q];
+  }
+}
+
+__global__ void __launch_bounds__(256) gap_final_kernel(const float* __restrict__ part, bf16* __restrict__ y, int NC,
+                                                        int S, float inv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NC) return;
+  float t = 0.f;
+  for (int s = 0; s < S; ++s) t += part[(size_t)s * NC + i];
+  y[i] = f2bf(t * inv);
 }
 
 __global__ void __launch_bounds__(256) gap_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N,
@@ -383,9 +414,19 @@ void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int
                        C, Ho, Wo, k, s, p, dv);
 }
 
-void launch_gap_fwd(const bf16* x, bf16* y, int N, int HW, int C, hipStream_t st) {
-  const int n = N * (C / 8);
-  hipLaunchKernelGGL(gap_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, y, N, HW, C);
+// row splits per image of the two-level per-(n, c) reductions over HW: ~2048 workgroups in
+// total, at least 4 passes of rows each
+int hw_splits(int N, int HW, int C) {
+  const int rpp = 256 / (C / 8);
+  int S = (2048 + N - 1) / N;
+  S = std::min(S, std::max(1, HW / (4 * rpp)));
+  return std::max(1, std::min(S, 64));
+}
+
+void launch_gap_fwd(const bf16* x, bf16* y, float* part, int N, int HW, int C, hipStream_t st) {
+  const int S = hw_splits(N, HW, C);
+  hipLaunchKernelGGL(gap_partial_kernel, dim3(N, S), dim3(256), 0, st, x, part, N, HW, C);
+  hipLaunchKernelGGL(gap_final_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, part, y, N * C, S, 1.f / HW);
 }
 
 void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st) {

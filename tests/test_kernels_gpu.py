@@ -179,6 +179,25 @@ def test_bn_matches_torch_batchnorm(K):
     assert relerr(bd.grad, bt.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(3, 56, 56, 64), (2, 7, 7, 2048), (5, 28, 28, 256), (1, 3, 5, 8)])
+def test_hw_reductions_split(K, shape):
+    """global average pool and the SE channel-scale backward as two-level reductions over the
+    rows (hw_splits row splits per image, 256 / (C/8) rows per pass) vs the fp32 reference"""
+    torch.manual_seed(0)
+    N, H, W, C = shape
+    x = rnd(N, H, W, C)
+    assert relerr(K.gap_fwd(x.to(DEV)), _ref.gap_fwd(x.float())) < 1e-2
+    g, dy, r = rnd(N, C), rnd(N, H, W, C), rnd(N, H, W, C)
+    for res, relu in [(None, False), (r, True)]:
+        rd = res.to(DEV) if res is not None else None
+        rf = res.float() if res is not None else None
+        got = K.chan_scale_bwd(dy.to(DEV), x.to(DEV), g.to(DEV), rd, relu, res is not None)
+        want = _ref.chan_scale_bwd(dy.float(), x.float(), g.float(), rf, relu, res is not None)
+        assert relerr(got[0], want[0]) < 1e-2 and relerr(got[1], want[1]) < 1e-3
+        if res is not None:
+            assert relerr(got[2], want[2]) < 1e-2
+
+
 def test_pools(K):
     x = rnd(2, 17, 15, 64)
     y, idx = K.maxpool_fwd(x.to(DEV), 3, 2, 1)
