@@ -60,13 +60,16 @@ def parse(argv=None):
 
 
 CONFIGS = {
-    # per-GPU batch 1024 (43 GB of the 288 GB HBM): 12.7k img/s against 11.9k at 512 on one MI355X
-    # (1536: 12.9k / 65 GB, 2048: 13.0k / 86 GB) -- the larger grids amortise per-kernel latency
+    # per-GPU batch 1024 for every config (sized for 288 GB of HBM; the larger grids amortise
+    # per-kernel latency).  Measured on one MI355X (profiles/meas_r2/batch_sweep.txt):
+    # r50 512 / 1024 / 2048: 11.9k / 12.7k / 13.0k img/s (43 GB at 1024); arcface 256 / 512 / 1024:
+    # 26.6k / 36.6k / 43.9k (11 GB); resnext 128 / 256 / 512 / 1024: 7.5k / 8.7k / 9.5k / 9.9k (56 GB);
+    # r101 512 / 1024 / 1536: 7.7k / 8.4k / 8.6k (64 GB); tresnet 256 / 512 / 1024: 9.4k / 10.9k / 11.7k
     "r50": dict(model="resnet50", batch=1024, image_size=224, num_classes=1000),
-    "arcface": dict(model="resnet50", batch=256, image_size=112, num_classes=10000),
-    "resnext": dict(model="resnext50_32x4d", batch=128, image_size=224, num_classes=1000),
-    "r101": dict(model="resnet101", batch=512, image_size=224, num_classes=1000),
-    "tresnet": dict(model="tresnet_m", batch=256, image_size=224, num_classes=1000),
+    "arcface": dict(model="resnet50", batch=1024, image_size=112, num_classes=10000),
+    "resnext": dict(model="resnext50_32x4d", batch=1024, image_size=224, num_classes=1000),
+    "r101": dict(model="resnet101", batch=1024, image_size=224, num_classes=1000),
+    "tresnet": dict(model="tresnet_m", batch=1024, image_size=224, num_classes=1000),
 }
 METRICS = {
     "r50": "images/sec (whole node), ResNet-50 224px DDP at 1/2/4/8 MI355X",
