@@ -159,6 +159,69 @@ __device__ __forceinline__ void tile_stats(const TapGemmParams& p, char* E, int 
   }
 }
 
+// (mean, M2) per channel of the 128-row slab of the LDS output image E (bf16-rounded outputs),
+// for BM = 128: thread (chunk c = tid % NCH, row group g = tid / NCH) reads whole 16-byte row
+// chunks (8 channels) of rows g, g + G, ...; sums of (v - K) and (v - K)^2 with K = the slab's
+// row 0 (one shift per channel for every thread, so the partial sums add) -> wave shuffles ->
+// LDS behind row 7 of the image -> one thread per channel.  Replaces 64 two-byte reads and a
+// two-pass per thread (tile_stats) with 8 (BN = 128) or 4 (BN = 64) chunk reads.
+template <int BN>
+__device__ __forceinline__ void tile_stats128(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
+  constexpr int NCH = BN / 8, G = 256 / NCH, RPT = 128 / G, RB = BN * 2;
+  const int c = tid % NCH, g = tid / NCH, lane = tid & 63, wave = tid >> 6;
+  const int nvalid = min(128, p.M - m0);
+  float K[8], s1[8], s2[8];
+  {
+    const bf16x8 v = eimg_chunk<NCH>(E, 0, c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      K[e] = bf2f(v[e]);
+      s1[e] = s2[e] = 0.f;
+    }
+  }
+  bf16x8 vv[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) vv[k] = eimg_chunk<NCH>(E, g + G * k, c);
+#pragma unroll
+  for (int k = 0; k < RPT; ++k)
+    if (g + G * k < nvalid)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = bf2f(vv[k][e]) - K[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+#pragma unroll
+  for (int off = NCH; off < 64; off *= 2)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += __shfl_xor(s1[e], off, 64);
+      s2[e] += __shfl_xor(s2[e], off, 64);
+    }
+  __syncthreads();  // every image read (stores, rows above) is done: rows 8.. become scratch
+  float* xch = (float*)(E + 8 * RB);  // [4 waves][2][BN]
+  if (lane < NCH)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xch[(wave * 2 + 0) * BN + c * 8 + e] = s1[e];
+      xch[(wave * 2 + 1) * BN + c * 8 + e] = s2[e];
+    }
+  __syncthreads();
+  if (tid < BN && n0 + tid < p.Co) {
+    float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      S1 += xch[(w * 2 + 0) * BN + tid];
+      S2 += xch[(w * 2 + 1) * BN + tid];
+    }
+    const float k0 = bf2f(eimg_chunk<NCH>(E, 0, tid >> 3)[tid & 7]);
+    const float n = (float)nvalid;
+    const size_t rb = (size_t)(m0 / 128);
+    p.stats[(rb * 2 + 0) * p.Co + n0 + tid] = k0 + S1 / n;
+    p.stats[(rb * 2 + 1) * p.Co + n0 + tid] = fmaxf(S2 - S1 * S1 / n, 0.f);
+  }
+}
+
 // vmcnt(n) with a wave-uniform runtime n in [0, 31] (a scalar branch to an immediate wait)
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
@@ -548,16 +611,21 @@ tap_gemm_kernel(const TapGemmParams p) {
       }
     }
     __syncthreads();
-    // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels
+    // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels.  All the
+    // thread's image chunks are read first, so its stores issue back to back instead of each
+    // waiting for its own LDS read.
     {
       constexpr int R = 256 / NCH;
       const int c = tid % NCH, pr0 = tid / NCH;
       const bool cok = n0 + c * 8 < p.Co;
+      bf16x8 vv[BM / R];
+#pragma unroll
+      for (int k = 0; k < BM / R; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
 #pragma unroll
       for (int k = 0; k < BM / R; ++k) {
         const int pl = pr0 + k * R;
         const int m = m0 + pl;
-        const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
+        const bf16x8 v = vv[k];
         if (m < p.M && cok) {
           uint32_t drow;
           if (p.ds == 1) {
@@ -579,7 +647,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         }
       }
     }
-    if constexpr (EPI == 1) tile_stats<BN, BM / 64>(p, E, m0, n0, tid);
+    if constexpr (EPI == 1) tile_stats128<BN>(p, E, m0, n0, tid);
     return;
   }
 
@@ -1270,7 +1338,7 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   const size_t full = (size_t)NS * stage;
   size_t epi = 0;
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
-  if (EPI == 1) epi = (size_t)128 * 2 * BN + 12 * BN;
+  if (EPI == 1) epi = (size_t)128 * 2 * BN;  // tile_stats128 keeps its scratch inside the image
   // image, then the sums' [2][8][256 + 4] fp32 in its space
   if (EPI == 3 || EPI == 4) epi = std::max((size_t)128 * 2 * BN, (size_t)2 * 8 * 260 * 4);
   size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
@@ -1332,7 +1400,9 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // narrow-channel (non-FAST) shapes -- the space-to-depth stem -- take 32-deep tiles double-
   // buffered only (their taps are looked up per lane; g_tune[13] = 32 / 64 selects, A/B)
   bool bk32 = (fast && g_tune[8] == 32 && ns >= 2 && ns <= 4) || (!fast && g_tune[13] == 32);
-  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs <= 1024 && bn == 128) bk32 = true;
+  // (K = 64, one 64-deep k-tile, measured faster with the 64-deep tile: 487 vs 511 us on the R50
+  // stage-1 expansion at b1024, tools/fwd_epi_bench.py)
+  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
   const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
   if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
