@@ -1001,7 +1001,7 @@ void mt_weight_prep(const Tensor& entries, const Tensor& blocks) {
 }
 
 void set_tuning(int64_t idx, int64_t value) {
-  TORCH_CHECK(idx >= 0 && idx < 16, "tuning index");
+  TORCH_CHECK(idx >= 0 && idx < 32, "tuning index");
   dcp::g_tune[idx] = (int)value;
 }
 

@@ -37,7 +37,7 @@
 
 namespace dcp {
 
-int g_tune[16] = {0};
+int g_tune[32] = {0};
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]

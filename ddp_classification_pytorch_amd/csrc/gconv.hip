@@ -394,6 +394,14 @@ int pick_sg(int C, int CG) {
   return 0;
 }
 
+// weight-gradient super-group: pick_sg's, or 32 channels with g_tune[16] = 32 (A/B only: the
+// 32-channel block-diagonal tiles measured 8% slower on ResNeXt-50, 8.6k vs 9.4k img/s at b512)
+int wgrad_sg(int C, int CG) {
+  const int base = pick_sg(C, CG);
+  if (base != 0 && g_tune[16] == 32 && CG <= 32 && 32 % CG == 0 && C % 32 == 0) return 32;
+  return base;
+}
+
 GconvParams make_params(int Hs, int Ws, int Hd, int Wd, int N, int C, int CG, int KH, int KW, int ss, int sd,
                         const int* oh, const int* ow) {
   GconvParams p{};
@@ -512,7 +520,7 @@ bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag
 }
 
 int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G) {
-  const int SG = pick_sg(C, C / G);
+  const int SG = wgrad_sg(C, C / G);
   if (SG == 0) return 0;
   const int M = N * Ho * Wo;
   const int nsg = C / SG;
@@ -527,7 +535,7 @@ bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* pa
                              int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
                              int pad, hipStream_t s) {
   const int CG = C / G;
-  const int SG = pick_sg(C, CG);
+  const int SG = wgrad_sg(C, CG);
   if (SG == 0 || Co != C || KH * KW > GT || splits <= 0) return false;
   int oh[GT], ow[GT];
   for (int t = 0; t < KH * KW; ++t) {

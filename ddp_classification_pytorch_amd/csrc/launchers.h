@@ -13,8 +13,9 @@ namespace dcp {
 // [5] wgrad blocks per CU, [6] wgrad atomics, [7] wgrad tile (0 auto, 2 no 256-tile, 3 no 64-row tile),
 // [8] conv k-tile depth (32 with [1] = 3 or 4), [9]-[11] elementwise grids (bn.hip),
 // [12] wgrad 32-row k-tiles, [13] narrow-channel conv k-tile depth, [14] narrow wgrad
-// subtiles per wave (3 or 4; 0 auto), [15] = 1: no direct 3x3 weight gradient
-extern int g_tune[16];
+// subtiles per wave (3 or 4; 0 auto), [15] = 1: no direct 3x3 weight gradient,
+// [16] = 32: grouped-conv weight gradient on 32-channel super-groups
+extern int g_tune[32];
 
 constexpr int kMaxTaps = 64;
 

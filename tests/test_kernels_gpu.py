@@ -397,6 +397,20 @@ def test_grouped_conv_shapes(K, N, H, W, C, G, KH, stride, pad):
     assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), KH, KH, G, stride, pad)) < 5e-3
 
 
+@pytest.mark.parametrize("sg", [16, 32])
+def test_grouped_wgrad_supergroups(K, sg):
+    """grouped-conv weight gradient with 16- and 32-channel super-groups (g_tune[16])"""
+    torch.manual_seed(0)
+    x, dy = rnd(2, 14, 14, 128), rnd(2, 14, 14, 128)
+    try:
+        K.set_tuning(16, sg)
+        dw = K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 32, 1, 1)
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(16, 0)
+    assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), 3, 3, 32, 1, 1)) < 5e-3
+
+
 def test_grouped_and_dw_and_se(K):
     x = rnd(2, 14, 14, 128)
     w = rnd(128, 3, 3, 4, scale=0.3)
