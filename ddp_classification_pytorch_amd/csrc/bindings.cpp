@@ -146,6 +146,47 @@ std::tuple<Tensor, Tensor> stem_fwd(const Tensor& x, const Tensor& w, bool stats
   return {y, part};
 }
 
+// Fused backward of the s2d stem conv + BN(+ReLU) + 3x3/2 max pool (stem.hip): from the pooled
+// gradient, its argmax, the conv output z (BN input) and the stem input x16 -> (tot, sums):
+// tot = the block-reduced [G1 (64 x 256), G2 (64 x 256), G3 (256), local sums] and sums [2,64] =
+// (sum g', sum g' xhat).  stem_bwd_dw turns tot and the (all-reduced) sums into dW.
+bool stem_bwd_fusable(const Tensor& z) {
+  return z.dim() == 4 && dcp::stem_bwd_supported(z.size(1), z.size(2), z.size(3), z.size(1) / 2, z.size(2) / 2);
+}
+
+std::tuple<Tensor, Tensor> stem_bn_pool_bwd(const Tensor& dy, const Tensor& idx, const Tensor& z, const Tensor& x16,
+                                            const Tensor& scale, const Tensor& shift, const Tensor& mean,
+                                            const Tensor& invstd, int64_t act) {
+  CHECK_ACT(dy);
+  CHECK_ACT(z);
+  CHECK_ACT(x16);
+  const int N = z.size(0), H = z.size(1), W = z.size(2);
+  TORCH_CHECK(stem_bwd_fusable(z) && x16.dim() == 4 && x16.size(0) == N && x16.size(1) == H && x16.size(2) == W &&
+                  x16.size(3) == 16 && dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) == 64 &&
+                  idx.numel() == dy.numel() && idx.scalar_type() == at::kByte,
+              "stem_bn_pool_bwd shapes");
+  TORCH_CHECK((int64_t)N * H * W * 64 < (1ll << 31), "tensor too large");
+  const int nb = dcp::stem_bwd_blocks(N, H, num_cus(z.get_device()));
+  const int pf = dcp::stem_bwd_part_floats();
+  auto part = at::empty({(int64_t)(nb + (nb + 63) / 64) * pf}, f32_like(z));
+  auto tot = at::empty({pf}, f32_like(z));
+  auto sums = at::empty({2, 64}, f32_like(z));
+  dcp::launch_stem_bwd(bp(z), bp(x16), bp(dy), idx.data_ptr<uint8_t>(), scale.data_ptr<float>(),
+                       shift.data_ptr<float>(), mean.data_ptr<float>(), (int)act, N, H, W, nb, part.data_ptr<float>(),
+                       cur_stream());
+  dcp::launch_split_reduce(part.data_ptr<float>(), nb, pf, tot.data_ptr<float>(), cur_stream());
+  dcp::launch_stem_bwd_sums(tot.data_ptr<float>(), invstd.data_ptr<float>(), sums.data_ptr<float>(), cur_stream());
+  return {tot, sums};
+}
+
+Tensor stem_bwd_dw(const Tensor& tot, const Tensor& sums, const Tensor& scale, const Tensor& invstd, double count) {
+  TORCH_CHECK(tot.numel() == dcp::stem_bwd_part_floats() && sums.numel() == 128, "stem_bwd_dw shapes");
+  auto dw = at::empty({64, 4, 4, 16}, tot.options());
+  dcp::launch_stem_bwd_dw(tot.data_ptr<float>(), sums.data_ptr<float>(), scale.data_ptr<float>(),
+                          invstd.data_ptr<float>(), (float)(1.0 / count), dw.data_ptr<float>(), cur_stream());
+  return dw;
+}
+
 // dy [N,Ho,Wo,Co], wt [C,KH,KW,Co] (transposed weight) -> dx [N,H,W,C]
 Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int64_t stride, int64_t pad,
                   const optional<Tensor>& add) {
@@ -1068,6 +1109,11 @@ TORCH_LIBRARY(dcp, m) {
   m.def("conv_fwd_geo(Tensor x, Tensor w, int stride, int pad, int Ho, int Wo, bool stats) -> (Tensor, Tensor)",
         &conv_fwd_geo);
   m.def("stem_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)", &stem_fwd);
+  m.def("stem_bwd_fusable(Tensor z) -> bool", &stem_bwd_fusable);
+  m.def("stem_bn_pool_bwd(Tensor dy, Tensor idx, Tensor z, Tensor x16, Tensor scale, Tensor shift, Tensor mean, "
+        "Tensor invstd, int act) -> (Tensor, Tensor)",
+        &stem_bn_pool_bwd);
+  m.def("stem_bwd_dw(Tensor tot, Tensor sums, Tensor scale, Tensor invstd, float count) -> Tensor", &stem_bwd_dw);
   m.def("conv_wgrad_geo(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad_geo);
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor", &act_bwd);
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);

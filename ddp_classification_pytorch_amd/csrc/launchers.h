@@ -94,6 +94,17 @@ bool stem_fwd_supported(int H, int W, int C, int Co, int KH, int KW);
 int stem_fwd_blocks(int N, int H);
 void launch_stem_fwd(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
                      hipStream_t s);
+// fused stem backward (BN + ReLU + 3x3/2 max pool + weight gradient): part [blocks][part_floats];
+// reduce it over blocks (launch_split_reduce) -> tot, then sums [2][64] and dw [64][256]
+bool stem_bwd_supported(int H, int W, int C, int Ho, int Wo);
+int stem_bwd_blocks(int N, int H, int num_cu);
+int stem_bwd_part_floats();
+void launch_stem_bwd(const bf16* z, const bf16* x16, const bf16* dy, const uint8_t* idx, const float* scale,
+                     const float* shift, const float* mean, int act, int N, int H, int W, int nblocks, float* part,
+                     hipStream_t s);
+void launch_stem_bwd_sums(const float* tot, const float* invstd, float* sums, hipStream_t s);
+void launch_stem_bwd_dw(const float* tot, const float* sums, const float* scale, const float* invstd, float inv_count,
+                        float* dw, hipStream_t s);
 int colsum_partials(int M);
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s);
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,

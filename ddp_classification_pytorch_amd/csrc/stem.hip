@@ -17,8 +17,11 @@
 //    turned into (n, mean, M2) and merged per workgroup into part[block][3][64] -- the first
 //    level of the BatchNorm statistics (bn.hip), so bn_stats / bn_stats_finalize skip the
 //    slab pass.
+#include <algorithm>
+
 #include "common.cuh"
 #include "launchers.h"
+#include "pool_gather.cuh"
 
 namespace dcp {
 
@@ -227,6 +230,315 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
         out[2 * kStemCo] = q;
       }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused stem backward: BN(+ReLU) backward + 3x3/2 max-pool backward + the stem weight gradient in
+// ONE pass over the stem output, without the BN statistics first.
+//
+// The weight gradient is linear in the conv-output gradient dz, and training-mode BN backward is
+// dz = sc (g' - a2 - a3 (z - mu)) with per-channel a2 = mean(g'), a3 = mean(g' xhat) invstd, where
+// g' is the pooled gradient gathered to the pixel and masked by relu'(z sc + sh).  So
+//   dW[co][k] = sc[co] (G1[co][k] - a3[co] G2[co][k] - a2[co] G3[k])
+//   G1 = sum_px g'[px][co] X[px][k],  G2 = sum_px (z - mu)[px][co] X[px][k],  G3 = sum_px X[px][k]
+// (X: the space-to-depth input patch of k = (ty, tx, c)) -- all three, and the BN sums
+// (sum g', sum g' (z - mu)), accumulate in the same pass; stem_bwd_finalize applies the
+// coefficients once the (possibly all-reduced) sums are known.  This replaces the two
+// maxpool_bn_bwd passes, the full-resolution dz tensor and the stem weight-gradient GEMM.
+//
+// Workgroup: a contiguous range of output rows (n, y).  Per row:
+//  phase E: every (pixel, 8-channel chunk) gathers g' and writes g' and z - mu (bf16) into two
+//    LDS images [128 px][64 ch] (128-byte rows, chunks XOR-swizzled by row bits 1..2);
+//  phase M: wave w owns tap row ty = w: D[128][64] += A^T B over the row's pixels in k-steps of
+//    32, A = {g' (4 x 16 ch), z - mu (4 x 16 ch)} and B = the input row y + w - 2 of an LDS
+//    ring shifted by tx -- both read with ds_read_b64_tr_b16, the 32 pixels of a k-step
+//    assigned to (k group, half) so that every read covers 8 consecutive rows (conflict free);
+//    G3 = sum X is summed from the same B fragments with plain adds.
+//  Input rows stream through a ring of 8 row slots (+ a zero slot) by LDS-DMA, one row ahead.
+namespace {
+constexpr int kSbRing = 132;                 // ring row pixels: 2 pad + W (<= 112) + pad
+constexpr int kSbSlot = kSbRing * 32;        // 16 bf16 channels per pixel
+constexpr int kSbRows = 129;                 // G rows: 64 g', 64 z - mu, 1 (G3 = sum X)
+constexpr int kSbPart = kSbRows * 256 + 128;  // + local BN sums [2][64]
+
+struct StemBwdParams {
+  const bf16* z;       // stem conv output = BN input [N][H][W][64]
+  const bf16* x16;     // stem input [N][H][W][16]
+  const bf16* dy;      // pooled gradient [N][Ho][Wo][64]
+  const uint8_t* idx;  // window argmax [N][Ho][Wo][64]
+  const float* scale;  // BN scale / shift (the ReLU mask), mean (centering)
+  const float* shift;
+  const float* mean;
+  float* part;         // [blocks][kSbPart]
+  int N, H, Ho, Wo, act, rpb;  // rpb: output rows per workgroup
+};
+
+__device__ __forceinline__ uint32_t sb_aoff(uint32_t r, uint32_t col) {
+  return r * 128u + (((col >> 3) ^ (((r >> 1) & 3u) << 1)) << 4) + (col & 7) * 2;
+}
+__device__ __forceinline__ bf16x8 sb_tr(const char* a, const char* b) {
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, a));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, b));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+}  // namespace
+
+template <int NSUB>  // W = 16 NSUB output columns
+// one workgroup per CU: the 36 accumulator tiles (144 registers) stay live across the gather
+// phase, so the kernel takes the full 512-register file (accumulators in AGPRs, no spills)
+__global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
+  constexpr int W = NSUB * 16, NKS = (W + 31) / 32;
+  static_assert(W + 4 <= kSbRing && NKS * 32 <= 128, "row does not fit");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ag = smem;                 // [128 px][64] g'
+  char* Az = smem + 16384;         // [128 px][64] z - mu
+  char* ring = smem + 32768;       // 8 row slots + the zero slot (index 8)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.H;
+  const int g0 = blockIdx.x * p.rpb, g1 = min(p.N * H, g0 + p.rpb);
+
+  // zero: the k-padding rows W..127 of both A images, every ring slot's padding pixels and the
+  // whole zero slot (LDS-DMA only ever writes pixels 2 .. W+1 of slots 0..7)
+  for (int i = tid; i < (128 - W) * 8 * 2; i += 256) {
+    const int img = i / ((128 - W) * 8), j = i - img * ((128 - W) * 8);
+    *(u32x4*)(smem + img * 16384 + (W + j / 8) * 128 + (j & 7) * 16) = u32x4{0, 0, 0, 0};
+  }
+  for (int i = tid; i < 9 * kSbSlot / 16; i += 256) {
+    const int slot = i / (kSbSlot / 16), px = (i - slot * (kSbSlot / 16)) >> 1;
+    if (slot == 8 || px < 2 || px >= W + 2) *(u32x4*)(ring + (size_t)i * 16) = u32x4{0, 0, 0, 0};
+  }
+  // LDS-DMA of input row yy of image n (global row G = n H + yy) into slot G & 7
+  auto load_row = [&](int n, int yy) {
+    if (yy < 0 || yy >= H) return;
+    const int G = n * H + yy;
+    const int e = wave * 64 + lane;  // 16-byte piece of the row: W * 2 pieces
+    char* dst = ring + (G & 7) * kSbSlot + 64 + wave * 1024;
+    if (e < W * 2)
+      __builtin_amdgcn_global_load_lds((const void*)(p.x16 + (size_t)G * W * 16 + e * 8), LDS_PTR(void, dst), 16, 0, 0);
+  };
+  auto slot_of = [&](int n, int yy) -> const char* {
+    return ring + ((yy < 0 || yy >= H) ? 8 : ((n * H + yy) & 7)) * kSbSlot;
+  };
+
+  // per-thread BN constants of its channel chunk (chunk = tid & 7 for every item of the thread)
+  const int c8 = tid & 7;
+  float sc[8], sh[8], mu[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = p.scale[c8 * 8 + e];
+    sh[e] = p.shift[c8 * 8 + e];
+    mu[e] = p.mean[c8 * 8 + e];
+    s1[e] = s2[e] = 0.f;
+  }
+
+  const uint32_t l16 = lane & 15, kq = lane >> 4, q = l16 >> 2, pp = lane & 3;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float g3[4] = {0.f, 0.f, 0.f, 0.f};  // G3 = sum X: plain adds of the B fragments (VALU, beside MFMAs)
+
+  if (g0 < g1) {
+    const int n = g0 / H, y = g0 - n * H;
+#pragma unroll
+    for (int d = -2; d <= 1; ++d) load_row(n, y + d);
+  }
+  // phase-E operands of a row, loaded one row ahead (the gathers' HBM latency then overlaps the
+  // previous row's MFMAs): per item the conv output chunk and the 2 x 2 candidate windows'
+  // argmax bytes and pooled gradients (3x3 / 2 / pad 1 geometry)
+  constexpr int NIT = (W * 8 + 255) / 256;
+  bf16x8 zv[NIT], gv[NIT][4];
+  uint64_t pk[NIT][4];
+  auto load_items = [&](int gg) {
+    const int nn = gg / H, yy = gg - nn * H;
+    const bf16* zrow = p.z + (size_t)gg * W * 64;
+    const int h0 = yy >> 1, h1 = min((yy + 1) >> 1, p.Ho - 1);
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int i = tid + 256 * k;
+      if (i < W * 8) {
+        const int px = i >> 3;
+        zv[k] = *(const bf16x8*)(zrow + px * 64 + c8 * 8);
+        const int w0 = px >> 1, w1 = min((px + 1) >> 1, p.Wo - 1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t o = ((uint32_t)(nn * p.Ho + ((c >> 1) ? h1 : h0)) * p.Wo + ((c & 1) ? w1 : w0)) * 64 + c8 * 8;
+          pk[k][c] = *(const uint64_t*)(p.idx + o);
+          gv[k][c] = *(const bf16x8*)(p.dy + o);
+        }
+      }
+    }
+  };
+  if (g0 < g1) load_items(g0);
+  for (int g = g0; g < g1; ++g) {
+    const int n = g / H, y = g - n * H;
+    // the rows the next output row adds: y + 2 of this image, or rows 0 and 1 of the next
+    if (g + 1 < g1) {
+      if (y + 1 < H) {
+        load_row(n, y + 2);
+      } else {
+        load_row(n + 1, 0);
+        load_row(n + 1, 1);
+      }
+    }
+    // ---- phase E: g' and z - mu of this row into the A images (same masking and rounding as
+    // gather_pool_grad + maxpool_bn_bwd) ----
+    {
+      const int h0 = y >> 1, h1 = (y + 1) >> 1;
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int i = tid + 256 * k;
+        if (i < W * 8) {
+          const int px = i >> 3;
+          const int w0 = px >> 1, w1 = (px + 1) >> 1;
+          bool ok[4];
+          uint32_t want[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int ho = (c >> 1) ? h1 : h0, wo = (c & 1) ? w1 : w0;
+            ok[c] = ho < p.Ho && wo < p.Wo && ((c >> 1) == 0 || h1 != h0) && ((c & 1) == 0 || w1 != w0);
+            want[c] = (uint32_t)((y - (ho * 2 - 1)) * 3 + (px - (wo * 2 - 1)));
+          }
+          bf16x8 go, zo;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float gsum = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (ok[c] && ((pk[k][c] >> (8 * e)) & 0xff) == want[c]) gsum += bf2f(gv[k][c][e]);
+            const float zf = bf2f(zv[k][e]);
+            float gq = bf2f(f2bf(gsum));  // the bf16 pool gradient of the unfused chain
+            if (p.act == 1 && !(zf * sc[e] + sh[e] > 0.f)) gq = 0.f;
+            const float zc = zf - mu[e];
+            s1[e] += gq;
+            s2[e] += gq * zc;
+            go[e] = f2bf(gq);
+            zo[e] = f2bf(zc);
+          }
+          const uint32_t o = px * 128u + ((c8 ^ (((px >> 1) & 3u) << 1)) << 4);
+          *(bf16x8*)(Ag + o) = go;
+          *(bf16x8*)(Az + o) = zo;
+        }
+      }
+    }
+    if (g + 1 < g1) load_items(g + 1);
+    // this row's ring rows were issued before the operands just consumed (vmcnt retires in
+    // issue order), so waiting on those in phase E covered them; the barrier publishes
+    // every wave's rows and images
+    __syncthreads();
+    // ---- phase M ----
+    const char* brow = slot_of(n, y + wave - 2);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const uint32_t base = ks * 32 + (kq >> 1) * 16 + (kq & 1) * 4;
+      const uint32_t ra = base + q, rb = base + 8 + q;  // this lane's pixel rows (k 0-3 / 4-7)
+      bf16x8 bf[4];
+#pragma unroll
+      for (int tx = 0; tx < 4; ++tx)
+        bf[tx] = sb_tr(brow + (ra + tx) * 32 + pp * 8, brow + (rb + tx) * 32 + pp * 8);
+#pragma unroll
+      for (int tx = 0; tx < 4; ++tx)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          g3[tx] += (base + j < (uint32_t)W) ? bf2f(bf[tx][j]) : 0.f;
+          g3[tx] += (base + 8 + j < (uint32_t)W) ? bf2f(bf[tx][4 + j]) : 0.f;
+        }
+      // A tiles one at a time (register pressure: 32 accumulator tiles are live)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const char* img = i < 4 ? Ag : Az;
+        const uint32_t col = (i & 3) * 16 + pp * 4;
+        const bf16x8 af = sb_tr(img + sb_aoff(ra, col), img + sb_aoff(rb, col));
+#pragma unroll
+        for (int tx = 0; tx < 4; ++tx)
+          acc[i][tx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tx], acc[i][tx], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // A images and this row's ring slots are free
+  }
+
+  // ---- partials: G rows (g' 0..63, z - mu 64..127, G3 128) x 256 columns, then BN sums ----
+  float* part = p.part + (size_t)blockIdx.x * kSbPart;
+  const int col = wave * 64 + (int)l16;  // + tx * 16: column (ty = wave, tx, c = l16)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int tx = 0; tx < 4; ++tx)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[(i * 16 + (int)kq * 4 + r) * 256 + col + tx * 16] = acc[i][tx][r];
+#pragma unroll
+  for (int tx = 0; tx < 4; ++tx) {
+    float t = g3[tx];
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    if (kq == 0) part[128 * 256 + col + tx * 16] = t;
+  }
+  float* red = (float*)smem;  // [2][256][8] (the A images are free)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[tid * 8 + e] = s1[e];
+    red[2048 + tid * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int which = tid >> 6, ch = tid & 63;
+    float t = 0.f;
+    for (int u = ch >> 3; u < 256; u += 8) t += red[which * 2048 + u * 8 + (ch & 7)];
+    part[kSbRows * 256 + which * 64 + ch] = t;
+  }
+}
+
+// sums [2][64] = (sum g', sum g' xhat) from the reduced partial
+__global__ void stem_bwd_sums_kernel(const float* __restrict__ tot, const float* __restrict__ invstd,
+                                     float* __restrict__ sums) {
+  const int t = threadIdx.x;
+  if (t < 128) sums[t] = tot[kSbRows * 256 + t] * (t >= 64 ? invstd[t - 64] : 1.f);
+}
+
+// dW[co][k] = sc (G1 - a3 G2 - a2 G3), a2 = sum g' / n, a3 = (sum g' xhat) / n * invstd
+__global__ void stem_bwd_dw_kernel(const float* __restrict__ tot, const float* __restrict__ sums,
+                                   const float* __restrict__ scale, const float* __restrict__ invstd, float inv_count,
+                                   float* __restrict__ dw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * 256) return;
+  const int co = i >> 8, k = i & 255;
+  const float a2 = sums[co] * inv_count, a3 = sums[64 + co] * inv_count * invstd[co];
+  dw[i] = scale[co] * (tot[co * 256 + k] - a3 * tot[(64 + co) * 256 + k] - a2 * tot[128 * 256 + k]);
+}
+
+bool stem_bwd_supported(int H, int W, int C, int Ho, int Wo) {
+  return C == kStemCo && H % 2 == 0 && W % 16 == 0 && W >= 16 && W + 4 <= kSbRing && Ho == H / 2 && Wo == W / 2;
+}
+int stem_bwd_blocks(int N, int H, int num_cu) { return std::min(N * H, num_cu); }
+int stem_bwd_part_floats() { return kSbPart; }
+
+void launch_stem_bwd(const bf16* z, const bf16* x16, const bf16* dy, const uint8_t* idx, const float* scale,
+                     const float* shift, const float* mean, int act, int N, int H, int W, int nblocks, float* part,
+                     hipStream_t s) {
+  StemBwdParams p{z, x16, dy, idx, scale, shift, mean, part, N, H, H / 2, W / 2, act, 0};
+  p.rpb = (N * H + nblocks - 1) / nblocks;
+  constexpr int lds = 32768 + 9 * kSbSlot;
+  switch (W / 16) {
+#define DCP_STEMB(NS_)                                                                                  \
+  case NS_:                                                                                             \
+    hipFuncSetAttribute((const void*)stem_bwd_kernel<NS_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+    hipLaunchKernelGGL(stem_bwd_kernel<NS_>, dim3(nblocks), dim3(256), lds, s, p);                      \
+    break;
+    DCP_STEMB(1) DCP_STEMB(2) DCP_STEMB(3) DCP_STEMB(4) DCP_STEMB(5) DCP_STEMB(6) DCP_STEMB(7)
+#undef DCP_STEMB
+    default: break;
+  }
+}
+
+void launch_stem_bwd_sums(const float* tot, const float* invstd, float* sums, hipStream_t s) {
+  hipLaunchKernelGGL(stem_bwd_sums_kernel, dim3(1), dim3(128), 0, s, tot, invstd, sums);
+}
+
+void launch_stem_bwd_dw(const float* tot, const float* sums, const float* scale, const float* invstd, float inv_count,
+                        float* dw, hipStream_t s) {
+  hipLaunchKernelGGL(stem_bwd_dw_kernel, dim3(64), dim3(256), 0, s, tot, sums, scale, invstd, inv_count, dw);
 }
 
 int stem_fwd_blocks(int N, int H) { return N * ((H + kStemRows - 1) / kStemRows); }

@@ -16,11 +16,18 @@ Input: NHWC activations with the 3 image channels zero-padded to 8
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops import functional as Fn
 from .layers import BatchNorm2d, Conv2d, Linear
+
+
+# the one-op stem (conv + BN + ReLU + max pool, fused one-pass backward, stem.hip stem_bwd);
+# off by default until it measures faster than the unfused chain; DCP_FUSED_STEM=1 switches it on
+_FUSED_STEM = [os.environ.get("DCP_FUSED_STEM", "0") == "1"]
 
 
 def _train_stats(bn: BatchNorm2d) -> bool:
@@ -139,6 +146,14 @@ class ResNet(nn.Module):
         if self.stem_s2d and (x.shape[-1] == 16 or (x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0)):
             if x.shape[-1] != 16:
                 x = Fn.nhwc_to_s2d(x)
+            if (t and self.variant == "imagenet" and _FUSED_STEM[0] and self.bn1.weight is not None
+                    and Fn.stem_bn_pool_fusable(x)):
+                # conv + BN + ReLU + max pool as one op with the one-pass fused backward
+                self.bn1._nbt_pending += 1
+                y = Fn.stem_bn_pool(x, self.conv1.weight, self._stem_w16, self.bn1.weight, self.bn1.bias,
+                                    self.bn1.running_mean, self.bn1.running_var, self.bn1.momentum, self.bn1.eps,
+                                    act="relu", group=self.bn1.process_group)
+                return self._forward_stages(y)
             y, s = Fn.stem_conv_s2d(x, self.conv1.weight, self._stem_w16, stats=t)
             s = s if (t and x.is_cuda) else None
         else:
@@ -147,6 +162,9 @@ class ResNet(nn.Module):
             y = self.bn1.forward_pool(y, s, act="relu", k=3, s=2, p=1)  # BN + ReLU + max pool, one fused op
         else:
             y = self.bn1(y, s, act="relu")
+        return self._forward_stages(y)
+
+    def _forward_stages(self, y):
         y = self.layer1(y)
         y = self.layer2(y)
         y = self.layer3(y)

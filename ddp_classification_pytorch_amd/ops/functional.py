@@ -801,6 +801,66 @@ def stem_conv_s2d(x16: torch.Tensor, weight: torch.Tensor, buf: torch.Tensor, st
     return _StemS2D.apply(x16, stem_s2d_weight(weight), wb, bool(stats and x16.is_cuda))
 
 
+class _StemBNPool(Function):
+    """The ResNet stem as one op: s2d 4x4 conv (statistics from its kernel) + training-mode
+    BN + ReLU + 3x3/2 max pool.  Backward runs the fused stem kernel (stem.hip stem_bwd): the
+    BN / max-pool backward and the stem weight gradient in one pass, the weight gradient
+    formed from G1 = sum g' X, G2 = sum (z - mu) X, G3 = sum X once the BN sums are known, so
+    neither the full-resolution activation gradient nor a second BN-backward pass exists."""
+
+    @staticmethod
+    def forward(ctx, x16, w16, wb, gamma, beta, run_mean, run_var, cfg: BNConfig):
+        k = K(x16)
+        z, part = k.stem_fwd(x16, wb, True)
+        mean, invstd, scale, shift, count = _bn_train_coeff(k, z, part, gamma, beta, run_mean, run_var, cfg)
+        y, idx = k.bn_act_maxpool(z, scale, shift, cfg.act, 3, 2, 1)
+        ctx.save_for_backward(x16, z, idx, scale, shift, mean, invstd)
+        ctx.cfg, ctx.count = cfg, count
+        ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, dy, _didx):
+        if dy is None:
+            return (None,) * 8
+        x16, z, idx, scale, shift, mean, invstd = ctx.saved_tensors
+        cfg = ctx.cfg
+        k = K(dy)
+        tot, local = k.stem_bn_pool_bwd(dy.contiguous(), idx, z, x16, scale, shift, mean, invstd, cfg.act)
+        sums = local
+        if cfg.group is not None:
+            sums = local.clone()
+            dist.all_reduce(sums, group=cfg.group)
+        dw = k.stem_bwd_dw(tot, sums, scale, invstd, float(ctx.count)) if ctx.needs_input_grad[1] else None
+        dgamma = local[1] if ctx.needs_input_grad[3] else None
+        dbeta = local[0] if ctx.needs_input_grad[4] else None
+        return None, dw, None, dgamma, dbeta, None, None, None
+
+
+def stem_bn_pool_fusable(x16: torch.Tensor, act: str = "relu") -> bool:
+    """Whether stem_bn_pool's fused kernels cover this input (GPU, training, ReLU/identity,
+    even H, W a multiple of 16 up to 112)."""
+    if not (x16.is_cuda and x16.dim() == 4 and x16.shape[-1] == 16 and act in ("relu", "none")
+            and torch.is_grad_enabled()):
+        return False
+    z_like = x16.new_empty((1, x16.shape[1], x16.shape[2], 64))
+    return bool(K(x16).stem_bwd_fusable(z_like))
+
+
+def stem_bn_pool(x16, weight, buf, gamma, beta, run_mean, run_var, momentum, eps, act="relu", group=None):
+    """s2d stem conv + training-mode BN + act + 3x3/2 max pool as one autograd op (see
+    _StemBNPool); ``weight`` is the 7x7 master, ``buf`` the persistent [64,4,4,16] fp32 buffer
+    of its s2d form (as stem_conv_s2d)."""
+    world = dist.get_world_size(group) if group is not None else 1
+    cfg = BNConfig(True, momentum, eps, ACT[act], 0.0, group, world)
+    with torch.no_grad():
+        buf.copy_(stem_s2d_weight(weight.detach()))
+    wb, _ = prepared_weight(buf, 0, False)
+    y, _ = _StemBNPool.apply(x16, stem_s2d_weight(weight), wb, gamma, beta, run_mean, run_var, cfg)
+    return y
+
+
 class _PrefixMask(Function):
     @staticmethod
     def forward(ctx, x, keep):

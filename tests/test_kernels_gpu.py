@@ -548,6 +548,42 @@ def test_s2d_stem_gpu_matches_plain_stem():
     assert relerr(g1, g0) < 1e-2
 
 
+@pytest.mark.parametrize("size,batch", [(64, 4), (96, 3), (224, 2)])
+def test_fused_stem_matches_unfused(size, batch):
+    """The one-op stem (stem conv + BN + ReLU + max pool, one-pass fused backward in stem.hip)
+    against the unfused chain (stem conv, BN+ReLU+pool, two-pass BN/pool backward, implicit-GEMM
+    weight gradient) on a ResNet-18: loss, stem / BN1 gradients and a deep layer's gradient."""
+    import copy
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.models import resnet as R
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    m1 = build_model("resnet18", num_classes=10).to(DEV)
+    m0 = copy.deepcopy(m1)
+    img = torch.randint(0, 256, (batch, 3, size, size), dtype=torch.uint8, device=DEV)
+    lab = torch.randint(0, 10, (batch,), device=DEV)
+    mean, std = torch.tensor((0.485, 0.456, 0.406), device=DEV), torch.tensor((0.229, 0.224, 0.225), device=DEV)
+    x = Fn.to_device_nhwc(img, mean, std, nchw=True, in_scale=1 / 255.0, **input_layout(m1))
+    assert Fn.stem_bn_pool_fusable(x)
+    losses = []
+    prev = R._FUSED_STEM[0]
+    for m, fused in ((m1, True), (m0, False)):
+        R._FUSED_STEM[0] = fused
+        try:
+            loss = Fn.cross_entropy(m(x), lab)
+            loss.backward()
+        finally:
+            R._FUSED_STEM[0] = prev
+        losses.append(float(loss))
+    assert abs(losses[0] - losses[1]) < 1e-3 * max(1.0, abs(losses[1]))
+    assert relerr(m1.conv1.weight.grad, m0.conv1.weight.grad) < 2e-2
+    assert relerr(m1.bn1.weight.grad, m0.bn1.weight.grad) < 2e-2
+    assert relerr(m1.bn1.bias.grad, m0.bn1.bias.grad) < 2e-2
+    assert relerr(m1.layer4[1].conv2.weight.grad, m0.layer4[1].conv2.weight.grad) < 2e-2
+    assert torch.allclose(m1.bn1.running_mean, m0.bn1.running_mean, atol=1e-4, rtol=1e-3)
+
+
 @pytest.mark.parametrize("shape,stride", [((8, 2, 2, 512), 1), ((8, 4, 4, 256), 2), ((4, 8, 8, 64), 1)])
 def test_basic_block_vs_fp64(shape, stride):
     import copy
