@@ -374,15 +374,6 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
   if (g0 < g1) load_items(g0);
   for (int g = g0; g < g1; ++g) {
     const int n = g / H, y = g - n * H;
-    // the rows the next output row adds: y + 2 of this image, or rows 0 and 1 of the next
-    if (g + 1 < g1) {
-      if (y + 1 < H) {
-        load_row(n, y + 2);
-      } else {
-        load_row(n + 1, 0);
-        load_row(n + 1, 1);
-      }
-    }
     // ---- phase E: g' and z - mu of this row into the A images (same masking and rounding as
     // gather_pool_grad + maxpool_bn_bwd) ----
     {
@@ -398,16 +389,19 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int ho = (c >> 1) ? h1 : h0, wo = (c & 1) ? w1 : w0;
-            ok[c] = ho < p.Ho && wo < p.Wo && ((c >> 1) == 0 || h1 != h0) && ((c & 1) == 0 || w1 != w0);
+            ok[c] = (ho < p.Ho) & (wo < p.Wo) & (((c >> 1) == 0) | (h1 != h0)) & (((c & 1) == 0) | (w1 != w0));
             want[c] = (uint32_t)((y - (ho * 2 - 1)) * 3 + (px - (wo * 2 - 1)));
           }
           bf16x8 go, zo;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            float gsum = 0.f;
+            float gsum = 0.f;  // branch-free: selects, no divergent blocks around the loads' uses
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-              if (ok[c] && ((pk[k][c] >> (8 * e)) & 0xff) == want[c]) gsum += bf2f(gv[k][c][e]);
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t b = (uint32_t)(pk[k][c] >> (8 * e)) & 0xffu;
+              const bool hit = ok[c] & (b == want[c]);  // non-short-circuit: a select, no branch
+              gsum += hit ? bf2f(gv[k][c][e]) : 0.f;
+            }
             const float zf = bf2f(zv[k][e]);
             float gq = bf2f(f2bf(gsum));  // the bf16 pool gradient of the unfused chain
             if (p.act == 1 && !(zf * sc[e] + sh[e] > 0.f)) gq = 0.f;
@@ -423,11 +417,23 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
         }
       }
     }
-    if (g + 1 < g1) load_items(g + 1);
-    // this row's ring rows were issued before the operands just consumed (vmcnt retires in
-    // issue order), so waiting on those in phase E covered them; the barrier publishes
-    // every wave's rows and images
-    __syncthreads();
+    // Next row's operands, issued after this row's were consumed (phase E's waits then never
+    // cover fresh loads): the input row(s) the next output row adds -- y + 2, or rows 0 and 1
+    // of the next image -- and its gather operands.  The ring rows of THIS row were issued one
+    // row earlier, before the operands phase E just consumed, so (vmcnt retires in issue
+    // order) they have landed.  A raw barrier: __syncthreads() would also drain vmcnt.
+    if (g + 1 < g1) {
+      if (y + 1 < H) {
+        load_row(n, y + 2);
+      } else {
+        load_row(n + 1, 0);
+        load_row(n + 1, 1);
+      }
+      load_items(g + 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     // ---- phase M ----
     const char* brow = slot_of(n, y + wave - 2);
 #pragma unroll
@@ -456,7 +462,10 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
           acc[i][tx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tx], acc[i][tx], 0, 0, 0);
       }
     }
-    __syncthreads();  // A images and this row's ring slots are free
+    // A images and this row's ring slots are free (raw barrier: keep the prefetches in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
 
   // ---- partials: G rows (g' 0..63, z - mu 64..127, G3 128) x 256 columns, then BN sums ----
