@@ -14,7 +14,8 @@ namespace dcp {
 // [8] conv k-tile depth (32 with [1] = 3 or 4), [9]-[11] elementwise grids (bn.hip),
 // [12] wgrad 32-row k-tiles, [13] narrow-channel conv k-tile depth, [14] narrow wgrad
 // subtiles per wave (3 or 4; 0 auto), [15] = 1: no direct 3x3 weight gradient,
-// [16] = 32: grouped-conv weight gradient on 32-channel super-groups
+// [16] = 32: grouped-conv weight gradient on 32-channel super-groups, [17] fused stem backward
+// ablation (timing only: 1 no MFMA phase, 2 no gather phase)
 extern int g_tune[32];
 
 constexpr int kMaxTaps = 64;

@@ -248,13 +248,14 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
 //
 // Workgroup: a contiguous range of output rows (n, y).  Per row:
 //  phase E: every (pixel, 8-channel chunk) gathers g' and writes g' and z - mu (bf16) into two
-//    LDS images [128 px][64 ch] (128-byte rows, chunks XOR-swizzled by row bits 1..2);
-//  phase M: wave w owns tap row ty = w: D[128][64] += A^T B over the row's pixels in k-steps of
-//    32, A = {g' (4 x 16 ch), z - mu (4 x 16 ch)} and B = the input row y + w - 2 of an LDS
+//    LDS images [128 px][64 ch] (128-byte rows, chunks XOR-swizzled by row bits 1..2; two sets
+//    by row parity, so phase E of the next row runs beside phase M of this one);
+//  phase M: wave w owns tap row ty = w & 3 and one A image: D[64][64] += A^T B over the row's
+//    pixels in k-steps of 32, A = g' or z - mu (4 x 16 ch) and B = the input row y + w - 2 of an LDS
 //    ring shifted by tx -- both read with ds_read_b64_tr_b16, the 32 pixels of a k-step
 //    assigned to (k group, half) so that every read covers 8 consecutive rows (conflict free);
 //    G3 = sum X is summed from the same B fragments with plain adds.
-//  Input rows stream through a ring of 8 row slots (+ a zero slot) by LDS-DMA, one row ahead.
+//  Input rows stream through a ring of 8 row slots (+ a zero slot) by LDS-DMA, two rows ahead.
 namespace {
 constexpr int kSbRing = 132;                 // ring row pixels: 2 pad + W (<= 112) + pad
 constexpr int kSbSlot = kSbRing * 32;        // 16 bf16 channels per pixel
@@ -271,10 +272,25 @@ struct StemBwdParams {
   const float* mean;
   float* part;         // [blocks][kSbPart]
   int N, H, Ho, Wo, act, rpb;  // rpb: output rows per workgroup
+  int ablate;                  // A/B timing only (g_tune[17]): 1 no MFMA phase, 2 no gather phase
 };
 
 __device__ __forceinline__ uint32_t sb_aoff(uint32_t r, uint32_t col) {
   return r * 128u + (((col >> 3) ^ (((r >> 1) & 3u) << 1)) << 4) + (col & 7) * 2;
+}
+// 16-byte LDS-DMA per lane (lane-linear destination from the wave-uniform base), issued as
+// inline asm: the compiler then does not track it, so LDS reads are not made to wait for it
+// (it cannot tell ring slots apart and would drain vmcnt, operand prefetches included).  The
+// caller guarantees the data has landed before it is read (see the interval schedule).  M0 is
+// saved and restored around the DMA (the instruction captures it at issue).
+__device__ __forceinline__ void sb_dma16(const void* g, const char* lds) {
+  const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(g), "s"(a)
+      : "memory");
 }
 __device__ __forceinline__ bf16x8 sb_tr(const char* a, const char* b) {
   const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, a));
@@ -284,125 +300,149 @@ __device__ __forceinline__ bf16x8 sb_tr(const char* a, const char* b) {
 }  // namespace
 
 template <int NSUB>  // W = 16 NSUB output columns
-// one workgroup per CU: the 36 accumulator tiles (144 registers) stay live across the gather
-// phase, so the kernel takes the full 512-register file (accumulators in AGPRs, no spills)
-__global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
+// one workgroup of 8 waves per CU (two per SIMD, so the gather phase's dependent VALU chains
+// and the MFMAs of one wave hide behind the other's): wave w owns tap row ty = w & 3 and the g'
+// (w < 4) or the z - mu image (w >= 4): 16 accumulator tiles
+__global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
   constexpr int W = NSUB * 16, NKS = (W + 31) / 32;
   static_assert(W + 4 <= kSbRing && NKS * 32 <= 128, "row does not fit");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ag = smem;                 // [128 px][64] g'
-  char* Az = smem + 16384;         // [128 px][64] z - mu
-  char* ring = smem + 32768;       // 8 row slots + the zero slot (index 8)
+  // A images, double-buffered by row parity: set b at smem + b * 32 KB = {g' [128 px][64],
+  // z - mu [128 px][64]}
+  char* ring = smem + 65536;  // 8 row slots + the zero slot (index 8)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.H;
   const int g0 = blockIdx.x * p.rpb, g1 = min(p.N * H, g0 + p.rpb);
 
-  // zero: the k-padding rows W..127 of both A images, every ring slot's padding pixels and the
-  // whole zero slot (LDS-DMA only ever writes pixels 2 .. W+1 of slots 0..7)
-  for (int i = tid; i < (128 - W) * 8 * 2; i += 256) {
+  // zero: the k-padding rows W..127 of all four A images, every ring slot's padding pixels and
+  // the whole zero slot (LDS-DMA only ever writes pixels 2 .. W+1 of slots 0..7)
+  for (int i = tid; i < (128 - W) * 8 * 4; i += 512) {
     const int img = i / ((128 - W) * 8), j = i - img * ((128 - W) * 8);
     *(u32x4*)(smem + img * 16384 + (W + j / 8) * 128 + (j & 7) * 16) = u32x4{0, 0, 0, 0};
   }
-  for (int i = tid; i < 9 * kSbSlot / 16; i += 256) {
+  for (int i = tid; i < 9 * kSbSlot / 16; i += 512) {
     const int slot = i / (kSbSlot / 16), px = (i - slot * (kSbSlot / 16)) >> 1;
     if (slot == 8 || px < 2 || px >= W + 2) *(u32x4*)(ring + (size_t)i * 16) = u32x4{0, 0, 0, 0};
   }
-  // LDS-DMA of input row yy of image n (global row G = n H + yy) into slot G & 7
+  // LDS-DMA of input row yy of image n (global row G = n H + yy) into slot G & 7 (waves 0..3)
   auto load_row = [&](int n, int yy) {
     if (yy < 0 || yy >= H) return;
     const int G = n * H + yy;
     const int e = wave * 64 + lane;  // 16-byte piece of the row: W * 2 pieces
     char* dst = ring + (G & 7) * kSbSlot + 64 + wave * 1024;
-    if (e < W * 2)
-      __builtin_amdgcn_global_load_lds((const void*)(p.x16 + (size_t)G * W * 16 + e * 8), LDS_PTR(void, dst), 16, 0, 0);
+    if (e < W * 2) sb_dma16(p.x16 + (size_t)G * W * 16 + e * 8, dst);
+  };
+  // the input rows output row gg adds to those of gg - 1: rows 0 and 1 of a new image, else y + 1
+  auto load_new_rows = [&](int gg) {
+    const int nn = gg / H, yy = gg - nn * H;
+    if (yy == 0) {
+      load_row(nn, 0);
+      load_row(nn, 1);
+    } else {
+      load_row(nn, yy + 1);
+    }
   };
   auto slot_of = [&](int n, int yy) -> const char* {
     return ring + ((yy < 0 || yy >= H) ? 8 : ((n * H + yy) & 7)) * kSbSlot;
   };
 
-  // per-thread BN constants of its channel chunk (chunk = tid & 7 for every item of the thread)
+  // BN constants (scale, shift, mean) staged in LDS and re-read per item (24 registers fewer
+  // across the MFMA phase); a thread's items all have channel chunk c8 = tid & 7
+  float* bnc = (float*)(ring + 9 * kSbSlot);
+  if (tid < 192) bnc[tid] = (tid < 64 ? p.scale : tid < 128 ? p.shift : p.mean)[tid & 63];
   const int c8 = tid & 7;
-  float sc[8], sh[8], mu[8], s1[8], s2[8];
+  float s1[8], s2[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = p.scale[c8 * 8 + e];
-    sh[e] = p.shift[c8 * 8 + e];
-    mu[e] = p.mean[c8 * 8 + e];
-    s1[e] = s2[e] = 0.f;
-  }
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
 
   const uint32_t l16 = lane & 15, kq = lane >> 4, q = l16 >> 2, pp = lane & 3;
-  f32x4 acc[8][4];
+  const int ty = wave & 3, half = wave >> 2;
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float g3[4] = {0.f, 0.f, 0.f, 0.f};  // G3 = sum X: plain adds of the B fragments (VALU, beside MFMAs)
 
-  if (g0 < g1) {
-    const int n = g0 / H, y = g0 - n * H;
-#pragma unroll
-    for (int d = -2; d <= 1; ++d) load_row(n, y + d);
-  }
-  // phase-E operands of a row, loaded one row ahead (the gathers' HBM latency then overlaps the
-  // previous row's MFMAs): per item the conv output chunk and the 2 x 2 candidate windows'
-  // argmax bytes and pooled gradients (3x3 / 2 / pad 1 geometry)
-  constexpr int NIT = (W * 8 + 255) / 256;
-  bf16x8 zv[NIT], gv[NIT][4];
-  uint64_t pk[NIT][4];
+  // phase-E operands of a row, loaded a barrier interval ahead (their HBM latency overlaps the
+  // previous interval's MFMAs).  An item is a pixel pair (2j, 2j + 1) x an 8-channel chunk: pixel
+  // 2j lies in pooled column j only, pixel 2j + 1 in columns j and j + 1 (3x3 / 2 / pad 1), and
+  // an even output row in pooled row y / 2 only -- so an item loads 2 (even row) or 4 (odd row)
+  // windows' argmax bytes and pooled gradients instead of 4 per pixel
+  constexpr int NIT = (W * 4 + 511) / 512;
+  bf16x8 zv[NIT][2], gv[NIT][2][2];
+  uint64_t pk[NIT][2][2];
   auto load_items = [&](int gg) {
     const int nn = gg / H, yy = gg - nn * H;
     const bf16* zrow = p.z + (size_t)gg * W * 64;
-    const int h0 = yy >> 1, h1 = min((yy + 1) >> 1, p.Ho - 1);
+    const int h0 = yy >> 1, h1 = min((yy + 1) >> 1, p.Ho - 1);  // even rows: h1 = h0 (masked)
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
-      const int i = tid + 256 * k;
-      if (i < W * 8) {
-        const int px = i >> 3;
-        zv[k] = *(const bf16x8*)(zrow + px * 64 + c8 * 8);
-        const int w0 = px >> 1, w1 = min((px + 1) >> 1, p.Wo - 1);
+      // unpredicated (lanes past the row reload its last item): a masked load would merge into the
+      // live registers through a copy, which waits for the load
+      const int i = min(tid + 512 * k, W * 4 - 1);
+      {
+        const int pr = i >> 3;
+        zv[k][0] = *(const bf16x8*)(zrow + (2 * pr) * 64 + c8 * 8);
+        zv[k][1] = *(const bf16x8*)(zrow + (2 * pr + 1) * 64 + c8 * 8);
+        const int wc1 = min(pr + 1, p.Wo - 1);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const uint32_t o = ((uint32_t)(nn * p.Ho + ((c >> 1) ? h1 : h0)) * p.Wo + ((c & 1) ? w1 : w0)) * 64 + c8 * 8;
-          pk[k][c] = *(const uint64_t*)(p.idx + o);
-          gv[k][c] = *(const bf16x8*)(p.dy + o);
-        }
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const uint32_t o = ((uint32_t)(nn * p.Ho + (r ? h1 : h0)) * p.Wo + (c ? wc1 : pr)) * 64 + c8 * 8;
+            pk[k][r][c] = *(const uint64_t*)(p.idx + o);
+            gv[k][r][c] = *(const bf16x8*)(p.dy + o);
+          }
       }
     }
   };
-  if (g0 < g1) load_items(g0);
-  for (int g = g0; g < g1; ++g) {
-    const int n = g / H, y = g - n * H;
-    // ---- phase E: g' and z - mu of this row into the A images (same masking and rounding as
-    // gather_pool_grad + maxpool_bn_bwd) ----
-    {
-      const int h0 = y >> 1, h1 = (y + 1) >> 1;
+  // ---- phase E of row gg: g' and z - mu into the A images of set gg & 1 (same masking, order
+  // of the window sum and rounding as gather_pool_grad + maxpool_bn_bwd) ----
+  auto phase_e = [&](int gg) {
+    const int y = gg - (gg / H) * H;
+    const int h0 = y >> 1, h1 = (y + 1) >> 1;
+    const bool row1 = (h1 != h0) & (h1 < p.Ho);
+    char* ag = smem + (gg & 1) * 32768;
 #pragma unroll
-      for (int k = 0; k < NIT; ++k) {
-        const int i = tid + 256 * k;
-        if (i < W * 8) {
-          const int px = i >> 3;
-          const int w0 = px >> 1, w1 = (px + 1) >> 1;
-          bool ok[4];
-          uint32_t want[4];
+    for (int k = 0; k < NIT; ++k) {
+      const int i = tid + 512 * k;
+      if (i < W * 4) {
+        const int pr = i >> 3;
+        float sc[8], sh[8], mu[8];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int ho = (c >> 1) ? h1 : h0, wo = (c & 1) ? w1 : w0;
-            ok[c] = (ho < p.Ho) & (wo < p.Wo) & (((c >> 1) == 0) | (h1 != h0)) & (((c & 1) == 0) | (w1 != w0));
-            want[c] = (uint32_t)((y - (ho * 2 - 1)) * 3 + (px - (wo * 2 - 1)));
-          }
+        for (int e = 0; e < 8; e += 4) {
+          *(float4*)&sc[e] = *(const float4*)&bnc[c8 * 8 + e];
+          *(float4*)&sh[e] = *(const float4*)&bnc[64 + c8 * 8 + e];
+          *(float4*)&mu[e] = *(const float4*)&bnc[128 + c8 * 8 + e];
+        }
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const int px = 2 * pr + sp;
+          bool ok[2][2];
+          uint32_t want[2][2];
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const int ho = r ? h1 : h0, wo = pr + c;
+              ok[r][c] = ((r == 0) | row1) & ((c == 0) | ((sp == 1) & (pr + 1 < p.Wo)));
+              want[r][c] = (uint32_t)((y - (ho * 2 - 1)) * 3 + (px - (wo * 2 - 1)));
+            }
           bf16x8 go, zo;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             float gsum = 0.f;  // branch-free: selects, no divergent blocks around the loads' uses
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const uint32_t b = (uint32_t)(pk[k][c] >> (8 * e)) & 0xffu;
-              const bool hit = ok[c] & (b == want[c]);  // non-short-circuit: a select, no branch
-              gsum += hit ? bf2f(gv[k][c][e]) : 0.f;
-            }
-            const float zf = bf2f(zv[k][e]);
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                const uint32_t b = (uint32_t)(pk[k][r][c] >> (8 * e)) & 0xffu;
+                const bool hit = ok[r][c] & (b == want[r][c]);  // non-short-circuit: a select
+                gsum += hit ? bf2f(gv[k][r][c][e]) : 0.f;
+              }
+            const float zf = bf2f(zv[k][sp][e]);
             float gq = bf2f(f2bf(gsum));  // the bf16 pool gradient of the unfused chain
             if (p.act == 1 && !(zf * sc[e] + sh[e] > 0.f)) gq = 0.f;
             const float zc = zf - mu[e];
@@ -412,30 +452,17 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
             zo[e] = f2bf(zc);
           }
           const uint32_t o = px * 128u + ((c8 ^ (((px >> 1) & 3u) << 1)) << 4);
-          *(bf16x8*)(Ag + o) = go;
-          *(bf16x8*)(Az + o) = zo;
+          *(bf16x8*)(ag + o) = go;
+          *(bf16x8*)(ag + 16384 + o) = zo;
         }
       }
     }
-    // Next row's operands, issued after this row's were consumed (phase E's waits then never
-    // cover fresh loads): the input row(s) the next output row adds -- y + 2, or rows 0 and 1
-    // of the next image -- and its gather operands.  The ring rows of THIS row were issued one
-    // row earlier, before the operands phase E just consumed, so (vmcnt retires in issue
-    // order) they have landed.  A raw barrier: __syncthreads() would also drain vmcnt.
-    if (g + 1 < g1) {
-      if (y + 1 < H) {
-        load_row(n, y + 2);
-      } else {
-        load_row(n + 1, 0);
-        load_row(n + 1, 1);
-      }
-      load_items(g + 1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // ---- phase M ----
-    const char* brow = slot_of(n, y + wave - 2);
+  };
+  // ---- phase M of row gg: this wave's A image of set gg & 1 against input row y + ty - 2 ----
+  auto phase_m = [&](int gg) {
+    const int n = gg / H, y = gg - n * H;
+    const char* brow = slot_of(n, y + ty - 2);
+    const char* aimg = smem + (gg & 1) * 32768 + half * 16384;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const uint32_t base = ks * 32 + (kq >> 1) * 16 + (kq & 1) * 4;
@@ -444,25 +471,58 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
 #pragma unroll
       for (int tx = 0; tx < 4; ++tx)
         bf[tx] = sb_tr(brow + (ra + tx) * 32 + pp * 8, brow + (rb + tx) * 32 + pp * 8);
+      if (half == 0)  // wave-uniform
 #pragma unroll
-      for (int tx = 0; tx < 4; ++tx)
+        for (int tx = 0; tx < 4; ++tx)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          g3[tx] += (base + j < (uint32_t)W) ? bf2f(bf[tx][j]) : 0.f;
-          g3[tx] += (base + 8 + j < (uint32_t)W) ? bf2f(bf[tx][4 + j]) : 0.f;
-        }
-      // A tiles one at a time (register pressure: 32 accumulator tiles are live)
+          for (int j = 0; j < 4; ++j) {
+            g3[tx] += (base + j < (uint32_t)W) ? bf2f(bf[tx][j]) : 0.f;
+            g3[tx] += (base + 8 + j < (uint32_t)W) ? bf2f(bf[tx][4 + j]) : 0.f;
+          }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const char* img = i < 4 ? Ag : Az;
-        const uint32_t col = (i & 3) * 16 + pp * 4;
-        const bf16x8 af = sb_tr(img + sb_aoff(ra, col), img + sb_aoff(rb, col));
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t col = i * 16 + pp * 4;
+        const bf16x8 af = sb_tr(aimg + sb_aoff(ra, col), aimg + sb_aoff(rb, col));
 #pragma unroll
         for (int tx = 0; tx < 4; ++tx)
           acc[i][tx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[tx], acc[i][tx], 0, 0, 0);
       }
     }
-    // A images and this row's ring slots are free (raw barrier: keep the prefetches in flight)
+  };
+
+  // Barrier interval t runs phase E of row t + 1 and phase M of row t (A sets by parity), so the
+  // two waves of a SIMD overlap VALU and MFMA: waves 0..3 (which also issue the ring loads) run E
+  // first, waves 4..7 run M first.  Interval t issues the new input rows of row t + 3, then the
+  // gather operands of row t + 2.  Waves 0..3 wait for those operands in phase E of interval t + 1
+  // (vmcnt retires in issue order), so the rows have landed before the barrier ahead of M(t + 3);
+  // in use or in flight are at most input rows G - 2 .. G + 4 (7 of the 8 slots).
+  // Raw barriers: __syncthreads() would also drain vmcnt.
+  if (g0 < g1) {
+    const int n = g0 / H, y = g0 - n * H;
+#pragma unroll
+    for (int d = -2; d <= 1; ++d) load_row(n, y + d);
+    if (g0 + 1 < g1) load_new_rows(g0 + 1);
+    if (g0 + 2 < g1) load_new_rows(g0 + 2);
+    load_items(g0);
+  }
+  // zero fill + BN constants published; the untracked ring DMA of the first three rows landed
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int t = g0 - 1; t < g1; ++t) {
+    const bool doE = t + 1 < g1, doM = t >= g0, doL = t + 2 < g1;
+    // The operand loads have ONE unconditional site for every wave (a clamped row at the end):
+    // loads in wave-dependent or conditional blocks merge into the loop-carried registers through
+    // copies, and a copy of a loading register waits for the load (no prefetch left).  The ring
+    // DMA of the rows of output row t + 3 (untracked, sb_dma16) follows them; waves 0..3 drain it
+    // after phase E of the next interval, two barriers before M(t + 3) reads the rows.
+    if (half != 0 && doM && p.ablate != 1) phase_m(t);
+    if (doE && p.ablate != 2) phase_e(t + 1);
+    // waves 0..3: the previous interval's ring DMA (behind the operands E just consumed) landed
+    if (half == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    load_items(min(t + 2, g1 - 1));
+    if (half == 0 && t + 3 < g1) load_new_rows(t + 3);
+    if (half == 0 && doM && p.ablate != 1) phase_m(t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -470,31 +530,33 @@ __global__ void __launch_bounds__(256, 1) stem_bwd_kernel(StemBwdParams p) {
 
   // ---- partials: G rows (g' 0..63, z - mu 64..127, G3 128) x 256 columns, then BN sums ----
   float* part = p.part + (size_t)blockIdx.x * kSbPart;
-  const int col = wave * 64 + (int)l16;  // + tx * 16: column (ty = wave, tx, c = l16)
+  const int col = ty * 64 + (int)l16;  // + tx * 16: column (ty, tx, c = l16)
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int tx = 0; tx < 4; ++tx)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) part[(i * 16 + (int)kq * 4 + r) * 256 + col + tx * 16] = acc[i][tx][r];
+      for (int r = 0; r < 4; ++r)
+        part[(half * 64 + i * 16 + (int)kq * 4 + r) * 256 + col + tx * 16] = acc[i][tx][r];
+  if (half == 0)
 #pragma unroll
-  for (int tx = 0; tx < 4; ++tx) {
-    float t = g3[tx];
-    t += __shfl_xor(t, 16, 64);
-    t += __shfl_xor(t, 32, 64);
-    if (kq == 0) part[128 * 256 + col + tx * 16] = t;
-  }
-  float* red = (float*)smem;  // [2][256][8] (the A images are free)
+    for (int tx = 0; tx < 4; ++tx) {
+      float t = g3[tx];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if (kq == 0) part[128 * 256 + col + tx * 16] = t;
+    }
+  float* red = (float*)smem;  // [2][512][8] (the A images are free)
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     red[tid * 8 + e] = s1[e];
-    red[2048 + tid * 8 + e] = s2[e];
+    red[4096 + tid * 8 + e] = s2[e];
   }
   __syncthreads();
   if (tid < 128) {
     const int which = tid >> 6, ch = tid & 63;
     float t = 0.f;
-    for (int u = ch >> 3; u < 256; u += 8) t += red[which * 2048 + u * 8 + (ch & 7)];
+    for (int u = ch >> 3; u < 512; u += 8) t += red[which * 4096 + u * 8 + (ch & 7)];
     part[kSbRows * 256 + which * 64 + ch] = t;
   }
 }
@@ -528,12 +590,13 @@ void launch_stem_bwd(const bf16* z, const bf16* x16, const bf16* dy, const uint8
                      hipStream_t s) {
   StemBwdParams p{z, x16, dy, idx, scale, shift, mean, part, N, H, H / 2, W / 2, act, 0};
   p.rpb = (N * H + nblocks - 1) / nblocks;
-  constexpr int lds = 32768 + 9 * kSbSlot;
+  p.ablate = g_tune[17];
+  constexpr int lds = 65536 + 9 * kSbSlot + 768;
   switch (W / 16) {
 #define DCP_STEMB(NS_)                                                                                  \
   case NS_:                                                                                             \
-    hipFuncSetAttribute((const void*)stem_bwd_kernel<NS_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
-    hipLaunchKernelGGL(stem_bwd_kernel<NS_>, dim3(nblocks), dim3(256), lds, s, p);                      \
+    (void)hipFuncSetAttribute((const void*)stem_bwd_kernel<NS_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+    hipLaunchKernelGGL(stem_bwd_kernel<NS_>, dim3(nblocks), dim3(512), lds, s, p);                      \
     break;
     DCP_STEMB(1) DCP_STEMB(2) DCP_STEMB(3) DCP_STEMB(4) DCP_STEMB(5) DCP_STEMB(6) DCP_STEMB(7)
 #undef DCP_STEMB

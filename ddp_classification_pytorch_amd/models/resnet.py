@@ -26,11 +26,10 @@ from .layers import BatchNorm2d, Conv2d, Linear
 
 
 # the one-op stem (conv + BN + ReLU + max pool, fused one-pass backward, stem.hip stem_bwd).
-# Off by default: it removes the full-resolution dz tensor and both BN-backward passes but, at
-# one wave per SIMD (its 32 accumulator tiles stay live), the gather phase is VALU-latency bound
-# -- 3.36 ms against 2.25 ms for the unfused maxpool_bn_bwd x 2 + weight-gradient chain at R50
-# b1024 (profiles/stem_bwd_fused_ab.txt).  DCP_FUSED_STEM=1 switches it on.
-_FUSED_STEM = [os.environ.get("DCP_FUSED_STEM", "0") == "1"]
+# On by default: it removes the full-resolution dz tensor, both BN-backward passes and the stem
+# weight-gradient GEMM -- 1.39 ms against 2.25 ms for the unfused maxpool_bn_bwd x 2 + weight-
+# gradient chain at R50 b1024 (profiles/stem_bwd_fused_ab.txt).  DCP_FUSED_STEM=0 switches it off.
+_FUSED_STEM = [os.environ.get("DCP_FUSED_STEM", "1") == "1"]
 
 
 def _train_stats(bn: BatchNorm2d) -> bool:
