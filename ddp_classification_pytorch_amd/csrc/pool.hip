@@ -61,24 +61,54 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
       sc[q] = scale ? scale[ch * 8 + q] : 1.f;
       sh[q] = scale ? shift[ch * 8 + q] : 0.f;
     }
-    for (int kh = 0; kh < k; ++kh) {
-      const int hi = ho * s - p + kh;
-      if ((unsigned)hi >= (unsigned)H) continue;
-      for (int kw = 0; kw < k; ++kw) {
-        const int wi = wo * s - p + kw;
-        if ((unsigned)wi >= (unsigned)W) continue;
-        const bf16x8 v = *(const bf16x8*)(x + ((uint32_t)(n * H + hi) * W + wi) * C + ch * 8);
+    if constexpr (KK > 0) {
+      // compile-time window: all KK*KK loads issued up front from clamped addresses, taps
+      // outside the image masked afterwards (a branch per tap serialised the loads)
+      bf16x8 v[KK * KK];
+      bool ok[KK * KK];
+#pragma unroll
+      for (int kh = 0; kh < KK; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KK; ++kw) {
+          const int hi = ho * SS - PP + kh, wi = wo * SS - PP + kw;
+          ok[kh * KK + kw] = ((unsigned)hi < (unsigned)H) & ((unsigned)wi < (unsigned)W);
+          const int hc = min(max(hi, 0), H - 1), wc = min(max(wi, 0), W - 1);
+          v[kh * KK + kw] = *(const bf16x8*)(x + ((uint32_t)(n * H + hc) * W + wc) * C + ch * 8);
+        }
+#pragma unroll
+      for (int t = 0; t < KK * KK; ++t)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          float f = bf2f(v[q]);
+          float f = bf2f(v[t][q]);
           if (scale) {
             f = f * sc[q] + sh[q];
             if (act == 1) f = fmaxf(f, 0.f);
             f = bf2f(f2bf(f));  // the bf16 activation the unfused BN kernel would have stored
           }
-          if (f > best[q]) {
-            best[q] = f;
-            bi[q] = (uint8_t)(kh * k + kw);
+          const bool take = ok[t] & (f > best[q]);  // first maximum in window order, as below
+          best[q] = take ? f : best[q];
+          bi[q] = take ? (uint8_t)t : bi[q];
+        }
+    } else {
+      for (int kh = 0; kh < k; ++kh) {
+        const int hi = ho * s - p + kh;
+        if ((unsigned)hi >= (unsigned)H) continue;
+        for (int kw = 0; kw < k; ++kw) {
+          const int wi = wo * s - p + kw;
+          if ((unsigned)wi >= (unsigned)W) continue;
+          const bf16x8 v = *(const bf16x8*)(x + ((uint32_t)(n * H + hi) * W + wi) * C + ch * 8);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float f = bf2f(v[q]);
+            if (scale) {
+              f = f * sc[q] + sh[q];
+              if (act == 1) f = fmaxf(f, 0.f);
+              f = bf2f(f2bf(f));  // the bf16 activation the unfused BN kernel would have stored
+            }
+            if (f > best[q]) {
+              best[q] = f;
+              bi[q] = (uint8_t)(kh * k + kw);
+            }
           }
         }
       }
