@@ -24,6 +24,9 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB_NAME = "_dcp_kernels.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
+# host-only native runtime pieces (no torch, no device code), loaded with ctypes
+HOST_SRC = os.path.join(CSRC, "host")
+LOADER_PATH = os.path.join(HERE, "_dcp_loader.so")
 ARCH = os.environ.get("DCP_OFFLOAD_ARCH", "gfx950")
 
 
@@ -78,7 +81,26 @@ def _compile(src: str, obj: str, torch_inc, force: bool) -> str:
     return f"built {os.path.basename(obj)}"
 
 
+def build_host(force: bool = False, verbose: bool = True) -> str:
+    """The shard loader (`csrc/host/loader.cpp`): plain C++17 + pthreads, C ABI for ctypes."""
+    srcs = sorted(os.path.join(HOST_SRC, f) for f in os.listdir(HOST_SRC) if f.endswith(".cpp"))
+    if force or _stale(LOADER_PATH, srcs + [os.path.abspath(__file__)]):
+        cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
+        if not cxx:
+            raise RuntimeError("no host C++ compiler (g++) found for the shard loader")
+        tmp = LOADER_PATH + f".tmp{os.getpid()}"
+        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-o", tmp] + srcs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"host build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LOADER_PATH)
+        if verbose:
+            print("[dcp-build] linked", LOADER_PATH, flush=True)
+    return LOADER_PATH
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    build_host(force=force, verbose=verbose)
     torch_inc, torch_lib = _torch_paths()
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))

@@ -47,7 +47,10 @@ def build_parser() -> argparse.ArgumentParser:
     a("--first-bucket-mb", type=float, default=4.0)
     a("--device", default=None, help="cuda (default when available) or cpu")
     # data
-    a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic"])
+    a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "shards"])
+    a("--shard-train", dest="shard_train", default=None, help="--data shards: train shard (default <folder>/train.dcps)")
+    a("--shard-val", dest="shard_val", default=None, help="--data shards: val shard (default <folder>/test.dcps)")
+    a("--loader-threads", dest="loader_threads", type=int, default=8, help="native shard loader host threads")
     a("--folder", default="/root/commonfile/foodH/", help="root with train/ and test/ class folders")
     a("--train-dir", "--train_dir", dest="train_dir", default=None)
     a("--val-dir", "--val_dir", dest="val_dir", default=None)

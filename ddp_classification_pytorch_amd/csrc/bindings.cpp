@@ -771,6 +771,33 @@ Tensor to_nhwc(const Tensor& src, bool nchw, int64_t cpad, double in_scale, cons
 }
 
 // image batch -> space-to-depth 2x2 NHWC input of the s2d stem [N, H/2, W/2, 16]
+// Gathered raw records `src` (uint8, device) + per-image boxes `meta` (int64 [B][8], HOST tensor,
+// validated here so no box can address outside its record) -> uint8 [B][Ho][Wo][3].
+Tensor crop_resize(const Tensor& src, const Tensor& meta, int64_t Ho, int64_t Wo) {
+  CHECK_DEV(src);
+  CHECK_CONTIG(src);
+  TORCH_CHECK(src.scalar_type() == at::kByte, "crop_resize src must be uint8");
+  TORCH_CHECK(!meta.is_cuda() && meta.scalar_type() == at::kLong && meta.dim() == 2 && meta.size(1) == 8 &&
+                  meta.is_contiguous(),
+              "crop_resize meta must be a contiguous host int64 [B, 8] tensor");
+  TORCH_CHECK(Ho > 0 && Wo > 0 && Ho <= 8192 && Wo <= 8192, "crop_resize output size");
+  const int64_t B = meta.size(0), nbytes = src.numel();
+  const int64_t* m = meta.data_ptr<int64_t>();
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t* r = m + b * 8;
+    const int64_t off = r[0], H = r[1], W = r[2], y0 = r[3], x0 = r[4], h = r[5], w = r[6];
+    TORCH_CHECK(H > 0 && W > 0 && off >= 0 && off + H * W * 3 <= nbytes, "crop_resize: record ", b,
+                " outside the gathered buffer");
+    TORCH_CHECK(h > 0 && w > 0 && y0 >= 0 && x0 >= 0 && y0 + h <= H && x0 + w <= W, "crop_resize: box of image ", b,
+                " outside its record");
+  }
+  auto out = at::empty({B, Ho, Wo, 3}, src.options());
+  auto md = meta.to(src.device(), /*non_blocking=*/meta.is_pinned());
+  dcp::launch_crop_resize(src.data_ptr<uint8_t>(), md.data_ptr<int64_t>(), (int)B, (int)Ho, (int)Wo,
+                          out.data_ptr<uint8_t>(), cur_stream());
+  return out;
+}
+
 Tensor to_nhwc_s2d(const Tensor& src, bool nchw, double in_scale, const optional<Tensor>& mean,
                    const optional<Tensor>& stdv) {
   CHECK_DEV(src);
@@ -1105,6 +1132,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &gap_bwd);
   m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
   m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
+  m.def("crop_resize(Tensor src, Tensor meta, int Ho, int Wo) -> Tensor", &crop_resize);
   m.def("to_nhwc_s2d(Tensor src, bool nchw, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc_s2d);
   m.def("conv_fwd_geo(Tensor x, Tensor w, int stride, int pad, int Ho, int Wo, bool stats) -> (Tensor, Tensor)",
         &conv_fwd_geo);

@@ -193,6 +193,8 @@ void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, i
 // space-to-depth 2x2 input of the s2d stem: dst [N][H/2][W/2][16], channel (py*2+px)*4 + c (c < 3 real)
 void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
                         const float* mean, const float* stdv, bf16* dst, hipStream_t s);
+// shard-loader augmentation: meta [B][8] = {byte offset, H, W, y0, x0, h, w, flip} -> out [B][Ho][Wo][3]
+void launch_crop_resize(const uint8_t* src, const int64_t* meta, int B, int Ho, int Wo, uint8_t* out, hipStream_t s);
 void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,

@@ -57,6 +57,12 @@ def _datasets(args):
         va = SyntheticImages(n_va, size=size, num_classes=args.num_classes, seed=args.seed + 1,
                              return_index=args.workload == "plc")
         return tr, va
+    if args.data == "shards":
+        from ..data.shards import ShardDataset
+
+        tr = ShardDataset(args.shard_train or os.path.join(args.folder, "train.dcps"), tr_t)
+        va = ShardDataset(args.shard_val or os.path.join(args.folder, "test.dcps"), va_t)
+        return tr, va
     if args.data == "list":
         tr = ListDataset(args.folder, "train", tr_t, seed=args.seed)
         va = ListDataset(args.folder, "val", va_t)
@@ -89,6 +95,25 @@ class WithIndex(torch.utils.data.Dataset):
         return getattr(self.ds, name)
 
 
+def _shard_loaders(args, rt, tr, va, tr_s, va_s, mean, std, cpad, s2d, drop_last_train):
+    """Native loaders (C++ gather + GPU crop/resize) when the transform preset maps onto them;
+    None for presets with rotation/padding (those run the PIL DataLoader over the same shard)."""
+    from ..data.shards import ShardLoader, aug_preset
+
+    try:
+        tr_aug, tr_size = aug_preset(args.transform, True, args.image_size)
+        va_aug, va_size = aug_preset(args.transform, False, args.image_size)
+    except ValueError:
+        return None
+    idx = args.workload == "plc"
+    kw = dict(device=rt.device, threads=args.loader_threads, seed=args.seed, mean=mean, std=std, cpad=cpad,
+              return_index=idx)
+    tr_l = ShardLoader(tr.path, args.batchsize, tr_s, tr_aug, tr_size, drop_last=drop_last_train,
+                       s2d=s2d and tr_size % 2 == 0, **kw)
+    va_l = ShardLoader(va.path, args.batchsize, va_s, va_aug, va_size, s2d=s2d and va_size % 2 == 0, **kw)
+    return tr_l, va_l
+
+
 def build_data(args, rt: Runtime, drop_last_train=False):
     tr, va = _datasets(args)
     if args.workload == "plc" and args.data != "synthetic" and not isinstance(tr, ListDataset):
@@ -98,6 +123,10 @@ def build_data(args, rt: Runtime, drop_last_train=False):
     s2d = str(args.model).startswith(("resnet", "resnext"))  # ImageNet ResNets: space-to-depth stem input
     tr_s = ShardSampler(tr, rt.world, rt.rank, shuffle=True, seed=args.seed, drop_last=drop_last_train)
     va_s = ShardSampler(va, rt.world, rt.rank, shuffle=False, seed=args.seed)
+    if args.data == "shards":
+        native = _shard_loaders(args, rt, tr, va, tr_s, va_s, mean, std, cpad, s2d, drop_last_train)
+        if native is not None:
+            return native + (tr, va)
     workers = args.workers if args.data != "synthetic" else min(args.workers, 2)
     tr_l = build_loader(tr, args.batchsize, tr_s, workers=workers, drop_last=drop_last_train,
                         worker_init_fn=worker_init_fn)

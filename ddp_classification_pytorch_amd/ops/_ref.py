@@ -347,6 +347,35 @@ def to_nhwc(src, nchw, cpad, in_scale, mean, std):
     return x.contiguous()
 
 
+def crop_resize(src, meta, Ho, Wo):
+    """Bilinear crop+resize(+hflip) of gathered uint8 records (see csrc/augment.hip): the same
+    fp32 half-pixel formula as the kernel, rounded half-up."""
+    B = meta.shape[0]
+    out = torch.empty((B, Ho, Wo, 3), dtype=torch.uint8, device=src.device)
+    oy = torch.arange(Ho, dtype=torch.float32)
+    ox = torch.arange(Wo, dtype=torch.float32)
+    for b in range(B):
+        off, H, W, y0, x0, h, w, flip = (int(v) for v in meta[b].tolist())
+        img = src[off:off + H * W * 3].view(H, W, 3)[y0:y0 + h, x0:x0 + w].float()
+        sy = ((oy + 0.5) * (float(h) / Ho) - 0.5).clamp_min(0)
+        sx = ((ox + 0.5) * (float(w) / Wo) - 0.5).clamp_min(0)
+        if flip:
+            sx = sx.flip(0)
+        ya = sy.long().clamp_max(h - 1)
+        xa = sx.long().clamp_max(w - 1)
+        ly = (sy - ya.float()).view(-1, 1, 1)
+        lx = (sx - xa.float()).view(1, -1, 1)
+        yb = (ya + 1).clamp_max(h - 1)
+        xb = (xa + 1).clamp_max(w - 1)
+        a, bb = img[ya][:, xa], img[ya][:, xb]
+        c, d = img[yb][:, xa], img[yb][:, xb]
+        top = a + (bb - a) * lx
+        bot = c + (d - c) * lx
+        v = top + (bot - top) * ly
+        out[b] = torch.floor(v + 0.5).clamp(0, 255).to(torch.uint8)
+    return out
+
+
 def to_nhwc_s2d(src, nchw, in_scale, mean, std):
     x = to_nhwc(src, nchw, 4, in_scale, mean, std)
     N, H, W, _ = x.shape

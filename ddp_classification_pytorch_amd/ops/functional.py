@@ -754,6 +754,13 @@ def to_device_nhwc(images: torch.Tensor, mean=None, std=None, cpad: int = 8, nch
     return out.to(act_dtype(images.device)) if not images.is_cuda else out
 
 
+def crop_resize(src: torch.Tensor, meta: torch.Tensor, Ho: int, Wo: int) -> torch.Tensor:
+    """Gathered raw uint8 records ``src`` (1-D, on the target device) + host int64 ``meta``
+    [B, 8] = {byte offset, H, W, y0, x0, h, w, flip} -> uint8 [B, Ho, Wo, 3]: the resample half of
+    RandomResizedCrop / Resize+CenterCrop + horizontal flip (see data/shards.py)."""
+    return K(src).crop_resize(src, meta, int(Ho), int(Wo))
+
+
 # ----------------------------------------------------------------------------- space-to-depth stem
 def nhwc_to_s2d(x: torch.Tensor) -> torch.Tensor:
     """[N, H, W, C>=4] NHWC image activations (channels >= 3 zero) -> [N, H/2, W/2, 16]."""
