@@ -597,6 +597,28 @@ std::tuple<Tensor, Tensor> bn_act_mask(const Tensor& x, const optional<Tensor>& 
   return {y, mask};
 }
 
+// BN + act over x with a residual that is itself a raw BN input normalised on the fly
+// (projection shortcut: y = act(x*scale + shift + res*rscale + rshift)) plus the act' mask bits.
+std::tuple<Tensor, Tensor> bn2_act_mask(const Tensor& x, const Tensor& res, const Tensor& scale, const Tensor& shift,
+                                        const Tensor& rscale, const Tensor& rshift, int64_t act, double slope) {
+  CHECK_ACT(x);
+  CHECK_ACT(res);
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && scale.numel() == C && shift.numel() == C && rscale.numel() == C &&
+                  rshift.numel() == C && res.sizes() == x.sizes(),
+              "bn2_act_mask shapes (C % 8 == 0, C <= 2048, residual like x)");
+  CHECK_F32(rscale);
+  CHECK_F32(rshift);
+  auto y = at::empty_like(x);
+  std::vector<int64_t> ms = x.sizes().vec();
+  ms.back() = C / 8;
+  auto mask = at::empty(ms, x.options().dtype(at::kByte));
+  dcp::launch_bn_act_fwd(bp(x), bp(res), scale.data_ptr<float>(), shift.data_ptr<float>(), bpm(y), x.numel(), C, act,
+                         (float)slope, cur_stream(), mask.data_ptr<uint8_t>(), rscale.data_ptr<float>(),
+                         rshift.data_ptr<float>());
+  return {y, mask};
+}
+
 Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
                      const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act, double slope) {
   CHECK_ACT(dy);
@@ -1105,6 +1127,9 @@ TORCH_LIBRARY(dcp, m) {
       "bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor run_mean, Tensor run_var, float eps) -> (Tensor, Tensor, "
       "Tensor, Tensor)",
       &bn_eval_coeff);
+  m.def("bn2_act_mask(Tensor x, Tensor res, Tensor scale, Tensor shift, Tensor rscale, Tensor rshift, int act, "
+        "float slope) -> (Tensor, Tensor)",
+        &bn2_act_mask);
   m.def("bn_act(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> Tensor", &bn_act);
   m.def("bn_act_mask(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> (Tensor, Tensor)",
         &bn_act_mask);

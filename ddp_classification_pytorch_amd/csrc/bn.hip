@@ -338,14 +338,25 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, bf16* __restrict__ y,
                                                          int M, int C, float slope, int nt,
-                                                         uint8_t* __restrict__ mask) {
+                                                         uint8_t* __restrict__ mask,
+                                                         const float* __restrict__ rscale,
+                                                         const float* __restrict__ rshift) {
   // mask != nullptr: also store act'(z) > 0 as one bit per element ([M][C/8] bytes), so the
-  // backward of a BN + residual + ReLU layer reads 1/16 of the residual's bytes for its mask
+  // backward of a BN + residual + ReLU layer reads 1/16 of the residual's bytes for its mask.
+  // rscale != nullptr: the residual is itself a raw BN input (a projection shortcut's conv
+  // output) normalised on the fly, res * rscale + rshift -- its BN never writes an activation.
   const RowTile t(C);
   if (t.slot >= t.rpi) return;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8(scale + t.c0, sc);
   load8(shift + t.c0, sh);
+  if (RES && rscale) {
+    load8(rscale + t.c0, rsc);
+    load8(rshift + t.c0, rsh);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rsc[k] = 1.f, rsh[k] = 0.f;
+  }
   const int step = gridDim.x * t.rpi;
   int m = blockIdx.x * t.rpi + t.slot;
   constexpr int U = 4;
@@ -364,7 +375,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float z = bf2f(v[u][k]) * sc[k] + sh[k];
-        if (RES) z += bf2f(r[u][k]);
+        if (RES) z += bf2f(r[u][k]) * rsc[k] + rsh[k];
         bits |= (z > 0.f ? 1u : 0u) << k;
         o[k] = f2bf(act_f(z, ACT, slope));
       }
@@ -383,7 +394,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float z = bf2f(v[k]) * sc[k] + sh[k];
-      if (RES) z += bf2f(r[k]);
+      if (RES) z += bf2f(r[k]) * rsc[k] + rsh[k];
       bits |= (z > 0.f ? 1u : 0u) << k;
       o[k] = f2bf(act_f(z, ACT, slope));
     }
@@ -670,11 +681,12 @@ static inline dim3 ew_grid(int M, int C) {
 }
 
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
-                       size_t numel, int C, int act, float slope, hipStream_t s, uint8_t* mask) {
+                       size_t numel, int C, int act, float slope, hipStream_t s, uint8_t* mask,
+                       const float* rscale, const float* rshift) {
   const int M = (int)(numel / C);
   const dim3 grid = ew_grid(M, C);
   DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[11],
-                       mask);
+                       mask, rscale, rshift);
 }
 
 int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }

@@ -114,7 +114,8 @@ void launch_bn_finalize(const float* st, int W, int C, float eps, const float* g
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                           float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
-                       int C, int act, float slope, hipStream_t s, uint8_t* mask = nullptr);
+                       int C, int act, float slope, hipStream_t s, uint8_t* mask = nullptr,
+                       const float* rscale = nullptr, const float* rshift = nullptr);
 int bn_bwd_reduce_blocks(int M, int C);
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,

@@ -83,8 +83,24 @@ class BatchNorm2d(nn.Module):
         self.frozen = False
         self._nbt_pending = 0
 
-    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None):
+    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None, residual_bn=None):
+        """``residual_bn=(bn, rslabs)``: ``residual`` is the raw input of BatchNorm2d ``bn`` (a
+        projection shortcut), normalised inside this layer's apply pass (Fn.batch_norm_add_bn_act)."""
         stats = self.training and not self.frozen
+        if residual_bn is not None:
+            rbn, rslabs = residual_bn
+            rstats = rbn.training and not rbn.frozen
+            if rstats != stats or rbn.process_group is not self.process_group or link is not None:
+                residual = rbn(residual, rslabs, act="none")  # unfusable combination: BN the shortcut first
+            else:
+                if stats:
+                    self._nbt_pending += 1
+                    rbn._nbt_pending += 1
+                return Fn.batch_norm_add_bn_act(x, slabs, self.weight, self.bias, self.running_mean,
+                                                self.running_var, residual, rslabs, rbn.weight, rbn.bias,
+                                                rbn.running_mean, rbn.running_var, stats, self.momentum, self.eps,
+                                                rbn.momentum, rbn.eps, act=act, slope=slope,
+                                                group=self.process_group if stats else None)
         if stats:
             self._nbt_pending += 1  # folded into num_batches_tracked lazily (no per-step device add)
         return Fn.batch_norm_act(x, slabs, self.weight, self.bias, self.running_mean, self.running_var, stats,

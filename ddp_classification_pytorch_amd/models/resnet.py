@@ -57,8 +57,7 @@ class BasicBlock(nn.Module):
         y, s = self.conv2(y, stats=t)
         if self.downsample is not None:
             r, rs = self.downsample[0](x, stats=t, deposit=join)
-            r = self.downsample[1](r, rs, act="none")
-            return self.bn2(y, s, act="relu", residual=r)
+            return self.bn2(y, s, act="relu", residual=r, residual_bn=(self.downsample[1], rs))
         return self.bn2(y, s, act="relu", residual=x, link=join)
 
 
@@ -90,8 +89,7 @@ class Bottleneck(nn.Module):
         y, s = self.conv3(y, stats=t)
         if self.downsample is not None:
             r, rs = self.downsample[0](x, stats=t, deposit=join)
-            r = self.downsample[1](r, rs, act="none")
-            return self.bn3(y, s, act="relu", residual=r)
+            return self.bn3(y, s, act="relu", residual=r, residual_bn=(self.downsample[1], rs))
         return self.bn3(y, s, act="relu", residual=x, link=join)
 
 

@@ -248,6 +248,10 @@ def bn_act_mask(x, res, scale, shift, act, slope):
     return _act(z, act, slope).to(x.dtype), mask
 
 
+def bn2_act_mask(x, res, scale, shift, rscale, rshift, act, slope):
+    return bn_act_mask(x, _f(res) * rscale + rshift, scale, shift, act, slope)
+
+
 def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope):
     z = _f(x) * scale + shift
     if res is not None:

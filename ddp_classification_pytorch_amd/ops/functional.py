@@ -449,6 +449,109 @@ class _BNAct(Function):
         return dx, None, dgamma, dbeta, dres, None, None, None, None, None
 
 
+def _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
+    if cfg.training_stats:
+        return _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
+    return (*k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps), x.numel() // x.shape[-1])
+
+
+def _bn_backward(k, g, x, scale, shift, mean, invstd, count, cfg: BNConfig, need_affine):
+    """Input gradient (and local [dbeta, dgamma] sums) of a BN layer whose output gradient after
+    the activation is ``g``."""
+    local = sums = None
+    if cfg.training_stats or need_affine:
+        local = k.bn_bwd_reduce(g, x, None, scale, shift, mean, invstd, 0, cfg.slope)
+        sums = local
+        if cfg.training_stats and cfg.group is not None:
+            sums = local.clone()
+            dist.all_reduce(sums, group=cfg.group)
+    dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums if cfg.training_stats else None,
+                           float(count), 0, cfg.slope, False)
+    return dx, local
+
+
+class _BNAddBNAct(Function):
+    """act(BN(x) + BN_r(r)): a bottleneck's last BN fused with its projection shortcut's BN
+    (the ``downsample`` conv output ``r`` is normalised while it is read as the residual, so the
+    shortcut BN never writes an activation).  Backward: the masked gradient
+    ``g`` feeds both BN backwards (the main one through the consuming conv's fused dgrad epilogue
+    when available)."""
+
+    @staticmethod
+    def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
+                cfg: BNConfig, rcfg: BNConfig, src):
+        k = K(x)
+        mean, invstd, scale, shift, count = _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
+        rmean, rinvstd, rscale, rshift, rcount = _bn_coeff(k, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var, rcfg)
+        y, mask = k.bn2_act_mask(x, r, scale, shift, rscale, rshift, cfg.act, cfg.slope)
+        ctx.save_for_backward(x, r, scale, shift, mean, invstd, rscale, rshift, rmean, rinvstd, mask)
+        ctx.cfg, ctx.rcfg, ctx.count, ctx.rcount = cfg, rcfg, count, rcount
+        ctx.src = src
+        if src is not None:
+            # the consuming conv masks the gradient with the bits; the residual is never read there
+            src.tensors = (x, None, scale, shift, mean, invstd, mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, scale, shift, mean, invstd, rscale, rshift, rmean, rinvstd, mask = ctx.saved_tensors
+        cfg, rcfg = ctx.cfg, ctx.rcfg
+        dy = dy.contiguous()
+        k = K(dy)
+        src, ctx.src = ctx.src, None
+        fused = src.fused if src is not None else None
+        if src is not None:
+            src.release()
+        nig = ctx.needs_input_grad
+        if fused is not None and fused[0].data_ptr() == dy.data_ptr() and fused[0].shape == dy.shape:
+            g, local = fused
+            sums = local
+            if cfg.group is not None:
+                sums = local.clone()
+                dist.all_reduce(sums, group=cfg.group)
+            dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
+                                   False)
+        else:
+            rv = k.bn_act(r, None, rscale, rshift, 0, 0.0)  # the shortcut activation, recomputed
+            need_affine = nig[2] or nig[3]
+            local = sums = None
+            if cfg.training_stats or need_affine:
+                local = k.bn_bwd_reduce(dy, x, rv, scale, shift, mean, invstd, cfg.act, cfg.slope)
+                sums = local
+                if cfg.training_stats and cfg.group is not None:
+                    sums = local.clone()
+                    dist.all_reduce(sums, group=cfg.group)
+            dx, g = k.bn_bwd_elemt(dy, x, rv, scale, shift, mean, invstd, sums if cfg.training_stats else None,
+                                   float(ctx.count), cfg.act, cfg.slope, True)
+        dr, rlocal = None, None
+        if nig[6] or nig[8] or nig[9]:
+            dr, rlocal = _bn_backward(k, g, r, rscale, rshift, rmean, rinvstd, ctx.rcount, rcfg, nig[8] or nig[9])
+        dgamma = local[1] if (local is not None and nig[2]) else None
+        dbeta = local[0] if (local is not None and nig[3]) else None
+        rdgamma = rlocal[1] if (rlocal is not None and nig[8]) else None
+        rdbeta = rlocal[0] if (rlocal is not None and nig[9]) else None
+        return (dx, None, dgamma, dbeta, None, None, dr if nig[6] else None, None, rdgamma, rdbeta, None, None,
+                None, None, None)
+
+
+def batch_norm_add_bn_act(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
+                          training_stats, momentum, eps, rmomentum, reps, act="relu", slope=0.01, group=None):
+    """act(BN(x) + BN_r(r)) with both BNs in training or eval mode (see :class:`_BNAddBNAct`)."""
+    world = dist.get_world_size(group) if group is not None else 1
+    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
+    rcfg = BNConfig(training_stats, rmomentum, reps, 0, float(slope), group, world)
+    slabs = None if slabs is None or slabs.numel() == 0 else slabs
+    rslabs = None if rslabs is None or rslabs.numel() == 0 else rslabs
+    src = None
+    if training_stats and cfg.act in (0, 1) and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
+        src = BNSource(cfg.act)
+    out = _BNAddBNAct.apply(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
+                            cfg, rcfg, src)
+    if src is not None:
+        out._dcp_bnsrc = src
+    return out
+
+
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
                    slope=0.01, residual=None, group=None, link=None):
     world = dist.get_world_size(group) if group is not None else 1

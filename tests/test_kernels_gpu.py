@@ -810,3 +810,22 @@ def test_narrow_channel_conv_bk32(K, N, H, Ci, Co, k, pad):
     st = K.bn_stats(y, slabs)
     sr = _ref.bn_stats(y.float().cpu(), None)
     assert relerr(st[0, 1], sr[0, 1]) < 1e-4 and relerr(st[0, 2], sr[0, 2]) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256), (3, 7, 9, 64), (1, 5, 5, 2048)])
+def test_bn2_act_mask_shortcut_bn(K, shape):
+    """BN + ReLU with a projection-shortcut residual normalised on the fly (bn2_act_mask) against
+    the reference, and equal to bn_act_mask over the materialised shortcut activation."""
+    torch.manual_seed(5)
+    C = shape[-1]
+    x, r = rnd(*shape, scale=2.0), rnd(*shape, scale=3.0)
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.3
+    rsc, rsh = torch.rand(C) + 0.2, torch.randn(C) * 0.5
+    d = lambda t: t.to(DEV)
+    y, m = K.bn2_act_mask(d(x), d(r), d(sc), d(sh), d(rsc), d(rsh), 1, 0.0)
+    yr, mr = _ref.bn2_act_mask(x, r, sc, sh, rsc, rsh, 1, 0.0)
+    assert relerr(y, yr) < 1e-2
+    assert (m.cpu() != mr).float().mean().item() < 1e-3  # bits may differ only where z rounds across 0
+    rv = K.bn_act(d(r), None, d(rsc), d(rsh), 0, 0.0)
+    y2, _ = K.bn_act_mask(d(x), rv, d(sc), d(sh), 1, 0.0)
+    assert relerr(y, y2) < 1e-2
