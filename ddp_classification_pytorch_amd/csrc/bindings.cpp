@@ -652,6 +652,30 @@ std::tuple<Tensor, Tensor> bn_bwd_elemt(const Tensor& dy, const Tensor& x, const
   return {dx, dres};
 }
 
+// Both BN input gradients of act(BN(x) + BN_r(r)) from the masked output gradient g (training
+// statistics; sums/rsums are the [2][C] (sum g, sum g*xhat) of each BN).
+std::tuple<Tensor, Tensor> bn2_bwd_elemt(const Tensor& g, const Tensor& x, const Tensor& r, const Tensor& scale,
+                                         const Tensor& mean, const Tensor& invstd, const Tensor& sums,
+                                         const Tensor& rscale, const Tensor& rmean, const Tensor& rinvstd,
+                                         const Tensor& rsums, double count) {
+  CHECK_ACT(g);
+  CHECK_ACT(x);
+  CHECK_ACT(r);
+  const int C = x.size(-1);
+  TORCH_CHECK(g.sizes() == x.sizes() && r.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn2_bwd_elemt shapes");
+  for (const Tensor* t : {&scale, &mean, &invstd, &rscale, &rmean, &rinvstd})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "bn2_bwd_elemt [C] fp32");
+  TORCH_CHECK(sums.numel() == 2 * C && rsums.numel() == 2 * C && sums.is_contiguous() && rsums.is_contiguous(),
+              "bn2_bwd_elemt sums [2][C]");
+  auto dx = at::empty_like(x);
+  auto dr = at::empty_like(r);
+  dcp::launch_bn2_bwd_elemt(bp(g), bp(x), bp(r), scale.data_ptr<float>(), mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), sums.data_ptr<float>(), rscale.data_ptr<float>(),
+                            rmean.data_ptr<float>(), rinvstd.data_ptr<float>(), rsums.data_ptr<float>(),
+                            (float)(1.0 / count), x.numel(), C, bpm(dx), bpm(dr), cur_stream());
+  return {dx, dr};
+}
+
 // ---------------------------------------------------------------------------
 // pooling / layout
 // ---------------------------------------------------------------------------
@@ -1130,6 +1154,9 @@ TORCH_LIBRARY(dcp, m) {
   m.def("bn2_act_mask(Tensor x, Tensor res, Tensor scale, Tensor shift, Tensor rscale, Tensor rshift, int act, "
         "float slope) -> (Tensor, Tensor)",
         &bn2_act_mask);
+  m.def("bn2_bwd_elemt(Tensor g, Tensor x, Tensor r, Tensor scale, Tensor mean, Tensor invstd, Tensor sums, "
+        "Tensor rscale, Tensor rmean, Tensor rinvstd, Tensor rsums, float count) -> (Tensor, Tensor)",
+        &bn2_bwd_elemt);
   m.def("bn_act(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> Tensor", &bn_act);
   m.def("bn_act_mask(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> (Tensor, Tensor)",
         &bn_act_mask);

@@ -564,6 +564,73 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
 }
 
 
+// Both BN backwards of a projection block's output (act(BN(x) + BN_r(r)), see bn2_act_mask)
+// in one pass over the already-masked gradient g: dx = BN'(g, x), dr = BN_r'(g, r).  One read of
+// g instead of two.  Coefficients per channel: d = ca*g + cb*v + cc (training statistics).
+__device__ inline void bn_bwd_coeff8(const float* scale, const float* mean, const float* invstd, const float* sums,
+                                     int C, int c0, float inv_count, float* ca, float* cb, float* cc) {
+  float sc[8], mu[8], is[8], k2[8], k3[8];
+  load8(scale + c0, sc);
+  load8(mean + c0, mu);
+  load8(invstd + c0, is);
+  load8(sums + c0, k2);
+  load8(sums + C + c0, k3);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float a2 = k2[k] * inv_count, a3 = k3[k] * inv_count * is[k];
+    ca[k] = sc[k];
+    cb[k] = -sc[k] * a3;
+    cc[k] = -sc[k] * a2 + sc[k] * a3 * mu[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) bn2_bwd_elemt_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ r, const float* __restrict__ scale,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ sums,
+                                                            const float* __restrict__ rscale,
+                                                            const float* __restrict__ rmean,
+                                                            const float* __restrict__ rinvstd,
+                                                            const float* __restrict__ rsums, float inv_count, int M,
+                                                            int C, bf16* __restrict__ dx, bf16* __restrict__ dr) {
+  const RowTile t(C);
+  if (t.slot >= t.rpi) return;
+  float ca[8], cb[8], cc[8], ra[8], rb[8], rc[8];
+  bn_bwd_coeff8(scale, mean, invstd, sums, C, t.c0, inv_count, ca, cb, cc);
+  bn_bwd_coeff8(rscale, rmean, rinvstd, rsums, C, t.c0, inv_count, ra, rb, rc);
+  const int step = gridDim.x * t.rpi;
+  int m = blockIdx.x * t.rpi + t.slot;
+  constexpr int U = 4;
+  auto body = [&](const bf16x8& g, const bf16x8& v, const bf16x8& w, size_t off) {
+    bf16x8 o, orr;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gv = bf2f(g[k]);
+      o[k] = f2bf(ca[k] * gv + cb[k] * bf2f(v[k]) + cc[k]);
+      orr[k] = f2bf(ra[k] * gv + rb[k] * bf2f(w[k]) + rc[k]);
+    }
+    *(bf16x8*)(dx + off) = o;
+    *(bf16x8*)(dr + off) = orr;
+  };
+  for (; m + (U - 1) * step < M; m += U * step) {
+    bf16x8 g[U], v[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = (size_t)(m + u * step) * C + t.c0;
+      g[u] = *(const bf16x8*)(dy + off);
+      v[u] = *(const bf16x8*)(x + off);
+      w[u] = *(const bf16x8*)(r + off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(g[u], v[u], w[u], (size_t)(m + u * step) * C + t.c0);
+  }
+  for (; m < M; m += step) {
+    const size_t off = (size_t)m * C + t.c0;
+    body(*(const bf16x8*)(dy + off), *(const bf16x8*)(x + off), *(const bf16x8*)(r + off), off);
+  }
+}
+
 // ---------------------------------------------------------------------------
 int bn_stats_partials(int M, int C, bool from_slabs) {
   if (from_slabs) {
@@ -708,6 +775,16 @@ void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const f
   const dim3 grid = ew_grid(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_elemt_kernel, grid, 0, s, res, act, dy, x, res, scale, shift, mean, invstd, sums,
                        inv_count, M, C, slope, dx, dres);
+}
+
+
+void launch_bn2_bwd_elemt(const bf16* dy, const bf16* x, const bf16* r, const float* scale, const float* mean,
+                          const float* invstd, const float* sums, const float* rscale, const float* rmean,
+                          const float* rinvstd, const float* rsums, float inv_count, size_t numel, int C, bf16* dx,
+                          bf16* dr, hipStream_t s) {
+  const int M = (int)(numel / C);
+  hipLaunchKernelGGL(bn2_bwd_elemt_kernel, ew_grid(M, C), dim3(256), 0, s, dy, x, r, scale, mean, invstd, sums,
+                     rscale, rmean, rinvstd, rsums, inv_count, M, C, dx, dr);
 }
 
 }  // namespace dcp

@@ -116,6 +116,10 @@ void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* bet
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
                        int C, int act, float slope, hipStream_t s, uint8_t* mask = nullptr,
                        const float* rscale = nullptr, const float* rshift = nullptr);
+void launch_bn2_bwd_elemt(const bf16* dy, const bf16* x, const bf16* r, const float* scale, const float* mean,
+                          const float* invstd, const float* sums, const float* rscale, const float* rmean,
+                          const float* rinvstd, const float* rsums, float inv_count, size_t numel, int C, bf16* dx,
+                          bf16* dr, hipStream_t s);
 int bn_bwd_reduce_blocks(int M, int C);
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,

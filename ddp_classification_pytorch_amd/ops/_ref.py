@@ -275,6 +275,12 @@ def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope
     return dx.to(dy.dtype), dres
 
 
+def bn2_bwd_elemt(g, x, r, scale, mean, invstd, sums, rscale, rmean, rinvstd, rsums, count):
+    dx, _ = bn_bwd_elemt(g, x, None, scale, torch.zeros_like(scale), mean, invstd, sums, count, 0, 0.0, False)
+    dr, _ = bn_bwd_elemt(g, r, None, rscale, torch.zeros_like(rscale), rmean, rinvstd, rsums, count, 0, 0.0, False)
+    return dx, dr
+
+
 # ----------------------------------------------------------------------------- pooling / layout
 def maxpool_fwd(x, k, s, p):
     y, idx = F.max_pool2d(_nchw(_f(x)), k, s, p, return_indices=True)

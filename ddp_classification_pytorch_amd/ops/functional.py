@@ -509,6 +509,21 @@ class _BNAddBNAct(Function):
             if cfg.group is not None:
                 sums = local.clone()
                 dist.all_reduce(sums, group=cfg.group)
+            if rcfg.training_stats and ctx.rcount == ctx.count:
+                # both input gradients in one pass over g (the shortcut BN's sums first)
+                rlocal = k.bn_bwd_reduce(g, r, None, rscale, rshift, rmean, rinvstd, 0, rcfg.slope)
+                rsums = rlocal
+                if rcfg.group is not None:
+                    rsums = rlocal.clone()
+                    dist.all_reduce(rsums, group=rcfg.group)
+                dx, dr = k.bn2_bwd_elemt(g, x, r, scale, mean, invstd, sums, rscale, rmean, rinvstd, rsums,
+                                         float(ctx.count))
+                dgamma = local[1] if nig[2] else None
+                dbeta = local[0] if nig[3] else None
+                rdgamma = rlocal[1] if nig[8] else None
+                rdbeta = rlocal[0] if nig[9] else None
+                return (dx, None, dgamma, dbeta, None, None, dr if nig[6] else None, None, rdgamma, rdbeta, None,
+                        None, None, None, None)
             dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
                                    False)
         else:

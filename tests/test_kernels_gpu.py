@@ -829,3 +829,19 @@ def test_bn2_act_mask_shortcut_bn(K, shape):
     rv = K.bn_act(d(r), None, d(rsc), d(rsh), 0, 0.0)
     y2, _ = K.bn_act_mask(d(x), rv, d(sc), d(sh), 1, 0.0)
     assert relerr(y, y2) < 1e-2
+
+
+def test_bn2_bwd_elemt_matches_two_passes(K):
+    torch.manual_seed(6)
+    N, H, C = 2, 14, 256
+    g, x, r = rnd(N, H, H, C), rnd(N, H, H, C, scale=2.0), rnd(N, H, H, C, scale=3.0)
+    d = lambda t: t.to(DEV)
+    pr = [torch.rand(C) + 0.5, torch.randn(C) * 0.2, torch.rand(C) + 0.5, torch.randn(2, C) * 5]
+    qr = [torch.rand(C) + 0.2, torch.randn(C) * 0.4, torch.rand(C) + 0.3, torch.randn(2, C) * 7]
+    count = float(N * H * H)
+    dx, dr = K.bn2_bwd_elemt(d(g), d(x), d(r), *[d(t) for t in pr], *[d(t) for t in qr], count)
+    rx, rr = _ref.bn2_bwd_elemt(g, x, r, *pr, *qr, count)
+    assert relerr(dx, rx) < 1e-2 and relerr(dr, rr) < 1e-2
+    z = torch.zeros(C)
+    dx1, _ = K.bn_bwd_elemt(d(g), d(x), None, d(pr[0]), d(z), d(pr[1]), d(pr[2]), d(pr[3]), count, 0, 0.0, False)
+    assert relerr(dx, dx1) < 1e-3
