@@ -90,7 +90,8 @@ class BatchNorm2d(nn.Module):
         if residual_bn is not None:
             rbn, rslabs = residual_bn
             rstats = rbn.training and not rbn.frozen
-            if rstats != stats or rbn.process_group is not self.process_group or link is not None:
+            if (rstats != stats or rbn.process_group is not self.process_group or link is not None
+                    or not Fn.shortcut_bn_fusion()):
                 residual = rbn(residual, rslabs, act="none")  # unfusable combination: BN the shortcut first
             else:
                 if stats:

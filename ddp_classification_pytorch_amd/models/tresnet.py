@@ -77,6 +77,15 @@ class Downsample(nn.Module):
             x = self.pool(x)
         return self.conv(x)
 
+    def raw(self, x):
+        """(conv output, BN statistics slabs, BN module): the shortcut before its BN, for a
+        consumer that normalises it on the fly (BatchNorm2d(residual_bn=...))."""
+        if self.pool is not None:
+            x = self.pool(x)
+        bn = self.conv.bn
+        r, rs = self.conv.conv(x, stats=bn.training and not bn.frozen)
+        return r, (bn, rs)
+
 
 class TBasicBlock(nn.Module):
     expansion = 1
@@ -115,7 +124,8 @@ class TBottleneck(nn.Module):
                            if (stride != 1 or inplanes != planes * 4) else None)
 
     def forward(self, x):
-        shortcut = self.downsample(x) if self.downsample is not None else x
+        # projection shortcut: its BN is applied inside conv3's BN pass (no shortcut activation)
+        shortcut, rbn = self.downsample.raw(x) if self.downsample is not None else (x, None)
         out = self.conv1(x)
         out = self.conv2(out)
         if self.aa is not None:
@@ -123,7 +133,7 @@ class TBottleneck(nn.Module):
         if self.se is not None:
             out = self.se(out)
         y, s = self.conv3.conv(out, stats=self.conv3.bn.training and not self.conv3.bn.frozen)
-        return self.conv3.bn(y, s, act="relu", residual=shortcut)
+        return self.conv3.bn(y, s, act="relu", residual=shortcut, residual_bn=rbn)
 
 
 class TResNet(nn.Module):

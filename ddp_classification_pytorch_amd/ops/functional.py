@@ -208,6 +208,18 @@ class BNSource:
 _FUSE_BN_BWD = [True]
 
 
+_FUSE_SHORTCUT_BN = [True]
+
+
+def set_shortcut_bn_fusion(enabled: bool):
+    """Toggle normalising projection shortcuts inside the block's last BN pass (A/B, tests)."""
+    _FUSE_SHORTCUT_BN[0] = bool(enabled)
+
+
+def shortcut_bn_fusion() -> bool:
+    return _FUSE_SHORTCUT_BN[0]
+
+
 def set_bn_backward_fusion(enabled: bool):
     """Toggle the dgrad-epilogue BN backward (A/B tests; default on)."""
     _FUSE_BN_BWD[0] = bool(enabled)

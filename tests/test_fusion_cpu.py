@@ -130,3 +130,35 @@ def test_ref_mask_path_matches_residual_path():
     g0, s0 = _ref.conv_dgrad_bn(dy, wt, 0, add, y, r, scale, shift, mean, invstd, 1)
     g1, s1 = _ref.conv_dgrad_bn(dy, wt, 0, add, y, None, scale, shift, mean, invstd, 1, mask)
     assert torch.allclose(g0, g1) and torch.allclose(s0, s1)
+
+
+@pytest.mark.parametrize("name,size,cpad", [("resnet50", 64, 8), ("resnet18", 32, 8), ("tresnet_m", 64, 3)])
+def test_shortcut_bn_fusion_matches_unfused(name, size, cpad):
+    """A projection shortcut's BN applied inside the block's last BN pass (Fn.batch_norm_add_bn_act)
+    gives the same loss, parameter gradients and running statistics as the separate BN."""
+    import copy
+
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(3)
+    m1 = build_model(name, num_classes=10)
+    m2 = copy.deepcopy(m1)
+    imgs = torch.randn(3, 3, size, size)
+    labels = torch.randint(0, 10, (3,))
+    out = []
+    for m, fuse in ((m1, True), (m2, False)):
+        Fn.set_shortcut_bn_fusion(fuse)
+        try:
+            x = Fn.to_device_nhwc(imgs, cpad=cpad, nchw=True)
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+        finally:
+            Fn.set_shortcut_bn_fusion(True)
+        out.append(loss.detach())
+    assert torch.allclose(out[0], out[1], rtol=1e-5, atol=1e-6)
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p1.grad, p2.grad, rtol=1e-3, atol=1e-5), n
+    for (n, b1), b2 in zip(m1.named_buffers(), m2.buffers()):
+        if b1.dtype.is_floating_point:
+            assert torch.allclose(b1, b2, rtol=1e-5, atol=1e-6), n
