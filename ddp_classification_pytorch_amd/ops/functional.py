@@ -493,8 +493,21 @@ class _BNAddBNAct(Function):
     def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
                 cfg: BNConfig, rcfg: BNConfig, src):
         k = K(x)
-        mean, invstd, scale, shift, count = _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
-        rmean, rinvstd, rscale, rshift, rcount = _bn_coeff(k, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var, rcfg)
+        if cfg.training_stats and rcfg.training_stats and cfg.group is not None and rcfg.group is cfg.group:
+            # SyncBN: both layers' (n, mean, M2) in ONE all-gather (one small-message latency, not two)
+            C = x.shape[-1]
+            st = torch.cat([k.bn_stats(x, slabs), k.bn_stats(r, rslabs)], dim=2)
+            gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
+            dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+            count = rcount = (x.numel() // C) * cfg.world
+            mean, invstd, scale, shift = k.bn_finalize(gathered[..., :C].contiguous(), gamma, beta, run_mean, run_var,
+                                                       cfg.momentum, cfg.eps)
+            rmean, rinvstd, rscale, rshift = k.bn_finalize(gathered[..., C:].contiguous(), rgamma, rbeta, rrun_mean,
+                                                           rrun_var, rcfg.momentum, rcfg.eps)
+        else:
+            mean, invstd, scale, shift, count = _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
+            rmean, rinvstd, rscale, rshift, rcount = _bn_coeff(k, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
+                                                               rcfg)
         y, mask = k.bn2_act_mask(x, r, scale, shift, rscale, rshift, cfg.act, cfg.slope)
         ctx.save_for_backward(x, r, scale, shift, mean, invstd, rscale, rshift, rmean, rinvstd, mask)
         ctx.cfg, ctx.rcfg, ctx.count, ctx.rcount = cfg, rcfg, count, rcount
@@ -517,17 +530,16 @@ class _BNAddBNAct(Function):
         nig = ctx.needs_input_grad
         if fused is not None and fused[0].data_ptr() == dy.data_ptr() and fused[0].shape == dy.shape:
             g, local = fused
-            sums = local
-            if cfg.group is not None:
-                sums = local.clone()
-                dist.all_reduce(sums, group=cfg.group)
-            if rcfg.training_stats and ctx.rcount == ctx.count:
-                # both input gradients in one pass over g (the shortcut BN's sums first)
+            if rcfg.training_stats and ctx.rcount == ctx.count and rcfg.group is cfg.group:
+                # both input gradients in one pass over g (the shortcut BN's sums first); SyncBN
+                # reduces both layers' sums in one all-reduce
                 rlocal = k.bn_bwd_reduce(g, r, None, rscale, rshift, rmean, rinvstd, 0, rcfg.slope)
-                rsums = rlocal
-                if rcfg.group is not None:
-                    rsums = rlocal.clone()
-                    dist.all_reduce(rsums, group=rcfg.group)
+                sums, rsums = local, rlocal
+                if cfg.group is not None:
+                    both = torch.cat([local, rlocal], dim=1)
+                    dist.all_reduce(both, group=cfg.group)
+                    C = local.shape[1]
+                    sums, rsums = both[:, :C].contiguous(), both[:, C:].contiguous()
                 dx, dr = k.bn2_bwd_elemt(g, x, r, scale, mean, invstd, sums, rscale, rmean, rinvstd, rsums,
                                          float(ctx.count))
                 dgamma = local[1] if nig[2] else None
@@ -536,6 +548,10 @@ class _BNAddBNAct(Function):
                 rdbeta = rlocal[0] if nig[9] else None
                 return (dx, None, dgamma, dbeta, None, None, dr if nig[6] else None, None, rdgamma, rdbeta, None,
                         None, None, None, None)
+            sums = local
+            if cfg.group is not None:
+                sums = local.clone()
+                dist.all_reduce(sums, group=cfg.group)
             dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
                                    False)
         else:

@@ -46,7 +46,8 @@ def _ddp_syncbn_worker(rank, world, port, out_dir):
     dist.all_reduce(lt)
     if rank == 0:
         torch.save({"loss": lt / world, "grads": {n: p.grad.clone() for n, p in model.named_parameters()},
-                    "rm": model.bn1.running_mean.clone(), "rv": model.bn1.running_var.clone()},
+                    "rm": model.bn1.running_mean.clone(), "rv": model.bn1.running_var.clone(),
+                    "bufs": {n: b.clone() for n, b in model.named_buffers() if "running" in n}},
                    os.path.join(out_dir, "ddp.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -83,6 +84,10 @@ def test_ddp_syncbn_equals_single_process_full_batch():
     assert abs(float(got["loss"]) - loss.item()) < 1e-5
     assert torch.allclose(got["rm"], model.bn1.running_mean, atol=1e-6)
     assert torch.allclose(got["rv"], model.bn1.running_var, atol=1e-5)
+    # every BN, including the projection shortcuts normalised inside the block's last BN pass
+    for n, b in model.named_buffers():
+        if "running" in n:
+            assert torch.allclose(got["bufs"][n], b, atol=1e-5), n
     assert err <= 3 * floor + 1e-5, (err, floor)
 
 
