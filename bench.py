@@ -56,6 +56,8 @@ def parse(argv=None):
                     help="DDP gradient all-reduce precision (bf16 = bf16_compress_hook: half the xGMI bytes)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
+    ap.add_argument("--graph", action="store_true",
+                    help="1 GPU: capture the whole step in a HIP graph and replay it (launch-bound small batches)")
     return ap.parse_args(argv)
 
 
@@ -150,8 +152,17 @@ def main(argv=None):
         opt.step()
         return loss
 
-    for _ in range(a.warmup):
-        loss = step()
+    run = step
+    if a.graph:
+        if world > 1:
+            raise SystemExit("--graph is single-GPU only (DDP reducer hooks are not captured)")
+        from ddp_classification_pytorch_amd.engine.graph import GraphedStep
+
+        graphed = GraphedStep(step, warmup=max(1, a.warmup))  # warm-up steps run inside
+        run = graphed
+    else:
+        for _ in range(a.warmup):
+            loss = step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -162,7 +173,7 @@ def main(argv=None):
         prof.__enter__()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss = run()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -201,6 +212,7 @@ def main(argv=None):
                 "image_size": S,
                 "num_classes": a.num_classes,
                 "parallelism": f"dp{world}",
+                "hip_graph": bool(a.graph),
                 "syncbn": bool(a.syncbn),
                 "grad_comm": a.grad_comm,
                 "bucket_cap_mb": a.bucket_cap_mb,

@@ -1,0 +1,44 @@
+"""HIP-graph capture of a whole single-GPU training step (forward, loss, backward, fused
+optimizer step).
+
+At small per-GPU batches (the reference trains with 16-128 images per process,
+BASELINE/main.py:30, CDR/train.sh:4, NESTED/train.py:470) a ResNet-50 step is ~600 kernel
+launches of a few microseconds each and the host launch path, not the GPU, sets the step
+time.  Capturing the step once and replaying it issues the whole dependency chain with one
+``hipGraphLaunch``.  Every op of the step is capture-safe: no host synchronisation, device
+tables (optimizer / weight-prep) built once and cached, outputs from the caching allocator's
+graph pool.
+
+Constraints (checked or documented): inputs and labels must live in the static tensors the
+step closes over (copy new batches into them); hyper-parameters baked into kernel arguments
+(the learning rate) are those at capture time -- recapture after changing them; single
+process (DDP's reducer hooks are not captured here).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class GraphedStep:
+    """``GraphedStep(step_fn, warmup=3)``: runs ``step_fn`` ``warmup`` times on a side stream
+    (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
+    returns the captured step's output tensors (overwritten by every replay)."""
+
+    def __init__(self, step_fn, warmup: int = 3, device=None):
+        if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:
+            raise RuntimeError("GraphedStep captures single-process steps (DDP reducer hooks are not graph-safe)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                step_fn()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = step_fn()
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out
