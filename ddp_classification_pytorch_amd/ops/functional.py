@@ -40,6 +40,23 @@ def round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
+# ----------------------------------------------------------------------------- host tables
+_GRAPH_KEEPALIVE = []
+
+
+def table_to_device(rows, dtype, device) -> torch.Tensor:
+    """Small host table (kernel argument lists: pointers, shapes) -> device tensor, safe under
+    HIP-graph capture: the copy is issued from PINNED memory, and a table uploaded while a
+    stream is capturing keeps its host buffer alive for the graph's lifetime (the captured
+    memcpy node re-reads that buffer on every replay; a pageable temporary would be freed)."""
+    host = torch.tensor(rows, dtype=dtype)
+    if torch.cuda.is_available():
+        host = host.pin_memory()
+        if torch.cuda.is_current_stream_capturing():
+            _GRAPH_KEEPALIVE.append(host)
+    return host.to(device, non_blocking=True)
+
+
 # ----------------------------------------------------------------------------- weight cache
 _GEN = [0]
 
@@ -139,8 +156,8 @@ class _MTWeightCache:
                              Cp | (tci << 32), tco])
                 blocks.extend((i, t) for t in range(T * tci * tco))
             dev = stale[0][2].device
-            ent = torch.tensor(rows, dtype=torch.int64).to(dev)
-            blk = torch.tensor(blocks, dtype=torch.int32).to(dev)
+            ent = table_to_device(rows, torch.int64, dev)
+            blk = table_to_device(blocks, torch.int32, dev)
             if len(self.tables) > 16:
                 self.tables.clear()
             tab = self.tables[tkey] = (ent, blk)

@@ -32,13 +32,14 @@ class _TableCache:
     def get(self, entries, device):
         key = tuple((e[0], e[1], e[2], e[3], e[5]) for e in entries)
         if key != self.key:
-            tab = torch.tensor(entries, dtype=torch.int64).view(-1, 6)
             ch = []
             for i, e in enumerate(entries):
                 n = e[5]
                 ch.extend((i, c) for c in range((n + CHUNK - 1) // CHUNK))
-            self.table = tab.to(device, non_blocking=True)
-            self.chunks = torch.tensor(ch, dtype=torch.int32).view(-1, 2).to(device, non_blocking=True)
+            # graph-capture safe uploads (grads of a captured step live in the graph pool: the
+            # table is rebuilt once during capture and replayed from its pinned host copy)
+            self.table = Fn.table_to_device([list(e) for e in entries], torch.int64, device).view(-1, 6)
+            self.chunks = Fn.table_to_device(ch, torch.int32, device).view(-1, 2)
             self.key = key
         return self.table, self.chunks
 
