@@ -94,6 +94,14 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
   TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)N * Ho * Wo * Co < (1ll << 32), "tensor too large");
   auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
   const int M = N * Ho * Wo;
+  if (stride == 1 && pad == 1 && KH == 3 && KW == 3 && dcp::conv3x3_c64_supported(H, W, C, Co)) {
+    // direct 64 -> 64 channel 3x3 kernel (conv3x3.hip); statistics as (n, mean, M2) partials
+    const int blocks = dcp::conv3x3_c64_blocks(N, H, W, num_cus(x.get_device()));
+    Tensor part = stats ? at::empty({blocks, 3, Co}, f32_like(x)) : at::empty({0}, f32_like(x));
+    dcp::launch_conv3x3_c64(bp(x), bp(w), bpm(y), stats ? part.data_ptr<float>() : nullptr, zero_page(x.get_device()),
+                            N, H, W, blocks, cur_stream());
+    return {y, part};
+  }
   Tensor slabs;
   if (stats)
     slabs = at::empty({(M + 127) / 128, 2, Co}, f32_like(x));
@@ -1114,6 +1122,15 @@ void mt_weight_prep(const Tensor& entries, const Tensor& blocks) {
   dcp::launch_mt_weight_prep(entries.data_ptr(), blocks.data_ptr(), (int)blocks.size(0), cur_stream());
 }
 
+// host int64 table -> int64 device tensor on `device_like`'s device (kernel-argument transport)
+Tensor table_fill(const Tensor& host, const Tensor& device_like) {
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == at::kLong && host.is_contiguous(), "table_fill: host int64");
+  CHECK_DEV(device_like);
+  auto out = at::empty({host.numel()}, device_like.options().dtype(at::kLong));
+  dcp::launch_table_fill(host.data_ptr<int64_t>(), host.numel(), out.data_ptr<int64_t>(), cur_stream());
+  return out;
+}
+
 void set_tuning(int64_t idx, int64_t value) {
   TORCH_CHECK(idx >= 0 && idx < 32, "tuning index");
   dcp::g_tune[idx] = (int)value;
@@ -1121,6 +1138,7 @@ void set_tuning(int64_t idx, int64_t value) {
 
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
+  m.def("table_fill(Tensor host, Tensor device_like) -> Tensor", &table_fill);
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);

@@ -1,0 +1,253 @@
+// Direct 3x3 / stride-1 / pad-1 forward convolution for 64 -> 64 channels (ResNet-50 layer1
+// conv2, ResNet-18/34 layer1), with the BN statistics of the output as per-workgroup
+// (n, mean, M2) partials (SURVEY.md §2.5 K1 + K4).
+//
+// The implicit GEMM (conv_igemm.hip) stages an im2col A tile per tap: every input pixel is
+// fetched into LDS nine times and, with only 64 output channels per tile, each staged byte
+// feeds few MACs -- these layers ran at ~0.45 PFLOP/s.  Here:
+//  * the weights (9 taps x 64 x 64 bf16) live in VGPRs for the whole kernel: wave w holds the
+//    B fragments of output channels 32*(w&1) .. +31 for all taps (36 x 16 bytes per lane);
+//  * a workgroup walks a contiguous range of row strips (R output rows of one image); the
+//    strip's input window -- (R+2) x (W+2) pixels x 128 bytes, zero outside the image -- is
+//    staged ONCE in LDS by LDS-DMA, 16-byte chunks XOR-swizzled by the window pixel's low
+//    three bits so the ds_read_b128 fragment reads of 8 consecutive pixels hit 8 different
+//    bank groups; the nine taps are the same fragments at shifted window pixels;
+//  * per 16-pixel subtile a wave issues 18 fragment reads and 36 MFMAs (16x16x32 bf16, two
+//    output-channel subtiles); waves 0/1 and 2/3 split the subtiles by parity and process two
+//    at a time (four independent accumulator chains);
+//  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
+//    (the numbers the BN normalises), and writes through a per-wave LDS staging tile as 32-byte
+//    row pieces; two workgroups per CU overlap one's window load with the other's MFMAs.
+#include <algorithm>
+
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+namespace {
+constexpr int kC3WinMax = 48 * 1024;        // window bytes per workgroup (two workgroups per CU)
+constexpr int kC3Stage = 4 * 32 * 64;       // per-wave 32 px x 32 ch bf16 staging tiles
+
+struct C3Params {
+  const bf16* x;     // [N][H][W][64]
+  const bf16* w;     // [64][9][64]
+  bf16* y;           // [N][H][W][64]
+  float* part;       // [gridDim.x][3][64] (n, mean, M2) or nullptr
+  const bf16* zero;  // >= 16 zero bytes
+  int H, W;
+  int R, spi;        // rows per strip, strips per image
+  int strips, sps;   // strips in total, strips per workgroup
+  int Wp, xq;        // window pitch (W + 2) and its 16-byte chunk count
+  FastDiv div_wp, div_w, div_spi;
+};
+
+__device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
+  return wpix * 128u + ((c ^ (wpix & 7u)) << 4);
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* win = smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ch = wave & 1, pg = wave >> 1;
+  char* stage = smem + p.xq * 16 + wave * (32 * 64);
+  const int H = p.H, W = p.W, Wp = p.Wp;
+  const uint32_t lr = lane & 15, lg = lane >> 4;
+
+  // B fragments: lane holds co = 32 ch + 16 n + lr, ci = 32 h + 8 lg .. +7 of tap t
+  bf16x8 bw[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bw[t][h][n] = *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + t) * 64 + 32 * h + 8 * lg);
+
+  float K[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, cnt = 0.f;
+  bool have_k = false;
+  const int s_begin = blockIdx.x * p.sps, s_end = min(p.strips, s_begin + p.sps);
+
+  for (int s = s_begin; s < s_end; ++s) {
+    const int n_img = fdiv(s, p.div_spi);
+    const int y0 = (s - n_img * p.spi) * p.R;
+    const int rows = min(p.R, H - y0), npix = rows * W;
+    __syncthreads();  // every wave is done with the previous strip's window
+    for (int qq = tid; qq < p.xq; qq += 256) {
+      const uint32_t P = qq >> 3;
+      const uint32_t rr = fdiv(P, p.div_wp), xx = P - rr * Wp;
+      const int yy = y0 - 1 + (int)rr, xi = (int)xx - 1;
+      const bool ok = yy >= 0 && yy < H && xi >= 0 && xi < W;
+      const uint32_t c = (qq & 7) ^ (P & 7u);
+      const bf16* g = ok ? p.x + ((size_t)(n_img * H + yy) * W + xi) * 64 + c * 8 : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, win + (qq - lane) * 16), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int nsub = (npix + 15) >> 4;
+    const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
+    for (int s0 = pg; s0 < nsub; s0 += 4) {
+      const int sub[2] = {s0, s0 + 2};
+      uint32_t base[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t pix = min(sub[u] * 16 + (int)lr, npix - 1);  // rows past the strip: clamped
+        const uint32_t r = fdiv(pix, p.div_w), xp = pix - r * W;
+        base[u] = r * Wp + xp;
+      }
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[u][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const uint32_t dt = (t / 3) * Wp + (t % 3);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 a[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            a[u] = *LDS_PTR(bf16x8, win + c3_addr(base[u] + dt, 4 * h + lg));
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw[t][h][n], acc[u][n], 0, 0, 0);
+        }
+      }
+      // epilogue: D[pixel 16 sub + 4 lg + i][co 32 ch + 16 n + lr]
+      if (!have_k) {  // per-wave statistics shift: the wave's first output (finite by construction)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) K[n] = __shfl(bf2f(f2bf(acc[0][n][0])), (int)lr, 64);
+        have_k = true;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pix = sub[u] * 16 + 4 * (int)lg + i;
+          const bool valid = pix < npix;
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const bf16 v = f2bf(acc[u][n][i]);
+            const float d = valid ? bf2f(v) - K[n] : 0.f;
+            s1[n] += d;
+            s2[n] = fmaf(d, d, s2[n]);
+            *LDS_PTR(bf16, stage + (u * 16 + 4 * lg + i) * 64 + (16 * n + lr) * 2) = v;
+          }
+          cnt += valid ? 1.f : 0.f;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging writes are done
+      __builtin_amdgcn_wave_barrier();
+      {
+        const int u = lane >> 5, pr = (lane >> 1) & 15, half = lane & 1;
+        const int pix = sub[u] * 16 + pr;
+        const bf16x8 v0 = *LDS_PTR(bf16x8, stage + (u * 16 + pr) * 64 + half * 32);
+        const bf16x8 v1 = *LDS_PTR(bf16x8, stage + (u * 16 + pr) * 64 + half * 32 + 16);
+        if (pix < npix) {
+          bf16* dst = p.y + ybase + (size_t)pix * 64 + 32 * ch + 16 * half;
+          *(bf16x8*)dst = v0;
+          *(bf16x8*)(dst + 8) = v1;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next writes
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (!p.part) return;
+
+  // per-wave channel sums: lanes lr share a channel across the 4 lane groups
+#pragma unroll
+  for (int off = 16; off < 64; off *= 2) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      s1[n] += __shfl_xor(s1[n], off, 64);
+      s2[n] += __shfl_xor(s2[n], off, 64);
+    }
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  __syncthreads();  // window / staging no longer read: reuse as scratch
+  float* sc = (float*)smem;  // [4 waves][2 n][16][4]: cnt, K, s1, s2
+  if (lg == 0)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      float* e = sc + ((wave * 2 + n) * 16 + lr) * 4;
+      e[0] = cnt;
+      e[1] = K[n];
+      e[2] = s1[n];
+      e[3] = s2[n];
+    }
+  __syncthreads();
+  if (tid < 64) {  // channel c = tid: waves (c >> 5) and (c >> 5) + 2 hold it, n = (c >> 4) & 1
+    const int c = tid, cw = c >> 5, n = (c >> 4) & 1, l = c & 15;
+    float nt = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float* e = sc + (((cw + 2 * q) * 2 + n) * 16 + l) * 4;
+      const float nb = e[0];
+      if (nb <= 0.f) continue;
+      const float mb = e[1] + e[2] / nb, m2b = fmaxf(e[3] - e[2] * e[2] / nb, 0.f);
+      const float ntot = nt + nb, delta = mb - mean;
+      mean += delta * nb / ntot;
+      m2 += m2b + delta * delta * nt * nb / ntot;
+      nt = ntot;
+    }
+    float* o = p.part + (size_t)blockIdx.x * 3 * 64;
+    o[c] = nt;
+    o[64 + c] = mean;
+    o[128 + c] = m2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+static int c3_rows(int H, int W) {
+  const int Wp = W + 2;
+  int R = kC3WinMax / (Wp * 128) - 2;
+  R = std::min(R, H);
+  if (R < 1) return 0;
+  const int spi = (H + R - 1) / R;  // equal strips per image
+  return (H + spi - 1) / spi;
+}
+
+bool conv3x3_c64_supported(int H, int W, int C, int Co) {
+  return g_tune[18] != 1 && C == 64 && Co == 64 && H >= 1 && W >= 1 && c3_rows(H, W) > 0;
+}
+
+int conv3x3_c64_blocks(int N, int H, int W, int num_cu) {
+  const int R = c3_rows(H, W);
+  const int strips = N * ((H + R - 1) / R);
+  const int target = std::max(1, 2 * num_cu);
+  const int sps = (strips + target - 1) / target;
+  return (strips + sps - 1) / sps;
+}
+
+void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
+                        int blocks, hipStream_t stream) {
+  C3Params p;
+  p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
+  p.H = H; p.W = W;
+  p.R = c3_rows(H, W);
+  p.spi = (H + p.R - 1) / p.R;
+  p.strips = N * p.spi;
+  p.sps = (p.strips + blocks - 1) / blocks;
+  p.Wp = W + 2;
+  p.xq = (p.R + 2) * p.Wp * 8;
+  p.div_wp = make_fastdiv(p.Wp);
+  p.div_w = make_fastdiv(W);
+  p.div_spi = make_fastdiv(p.spi);
+  const int lds = p.xq * 16 + kC3Stage;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kC3WinMax + kC3Stage);
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv3x3_c64_kernel, dim3(blocks), dim3(256), lds, stream, p);
+}
+
+}  // namespace dcp

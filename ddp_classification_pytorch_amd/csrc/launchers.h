@@ -190,6 +190,14 @@ void launch_cdr_threshold(const MTEntry* tab, const int2* chunks, int nchunks, u
 void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const uint32_t* state, float clip,
                      hipStream_t s);
 
+// direct 3x3 / s1 / p1 conv, 64 -> 64 channels (conv3x3.hip); part: [blocks][3][64] (n, mean, M2) or null
+bool conv3x3_c64_supported(int H, int W, int C, int Co);
+int conv3x3_c64_blocks(int N, int H, int W, int num_cu);
+void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
+                        int blocks, hipStream_t stream);
+
+// host int64 table -> device through kernel arguments (graph-capture safe, see misc.hip)
+void launch_table_fill(const int64_t* host, int64_t n, int64_t* out, hipStream_t s);
 void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16* wb, bf16* wt, hipStream_t s);
 // entries: packed {w, wb, wt, Co, T, Ci_src, Ci, Cp, tci, tco, pad} (56 B each); blocks: int2 (entry, tile)
 void launch_mt_weight_prep(const void* entries, const void* blocks, int nblocks, hipStream_t s);

@@ -9,6 +9,7 @@
 //   * nested_eval: best-K search of TestNested (NESTED/train.py:103-166, K19)
 //     as a prefix-cumulative classifier, with per-K top-1/top-3 counters and
 //     nothing materialised (the reference builds a [feat_dim, B, C] tensor).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -16,6 +17,29 @@
 #include "launchers.h"
 
 namespace dcp {
+
+// Small host table (kernel argument lists) -> device, carried in the KERNEL ARGUMENTS instead of a
+// host->device copy: a launch captured into a HIP graph replays with its arguments baked in, so
+// tables built while a step is being captured (optimizer / weight-prep pointer lists) need no
+// pinned staging buffer that outlives the capture.
+constexpr int kFillWords = 448;  // 3584 bytes of kernel arguments per launch
+struct FillArgs {
+  int64_t v[kFillWords];
+};
+
+__global__ void __launch_bounds__(kFillWords) table_fill_kernel(const FillArgs a, int64_t* __restrict__ out, int n) {
+  const int i = threadIdx.x;
+  if (i < n) out[i] = a.v[i];
+}
+
+void launch_table_fill(const int64_t* host, int64_t n, int64_t* out, hipStream_t s) {
+  for (int64_t o = 0; o < n; o += kFillWords) {
+    FillArgs a;
+    const int k = (int)std::min<int64_t>(kFillWords, n - o);
+    for (int i = 0; i < k; ++i) a.v[i] = host[o + i];
+    hipLaunchKernelGGL(table_fill_kernel, dim3(1), dim3(kFillWords), 0, s, a, out + o, k);
+  }
+}
 
 __global__ void __launch_bounds__(256) weight_prep_kernel(const float* __restrict__ w, int Co, int T, int Ci,
                                                           int Co_pad, bf16* __restrict__ wb, bf16* __restrict__ wt) {

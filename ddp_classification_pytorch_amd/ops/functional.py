@@ -41,20 +41,33 @@ def round_up(v: int, m: int) -> int:
 
 
 # ----------------------------------------------------------------------------- host tables
-_GRAPH_KEEPALIVE = []
+_DEV_ANCHOR = {}
 
 
 def table_to_device(rows, dtype, device) -> torch.Tensor:
-    """Small host table (kernel argument lists: pointers, shapes) -> device tensor, safe under
-    HIP-graph capture: the copy is issued from PINNED memory, and a table uploaded while a
-    stream is capturing keeps its host buffer alive for the graph's lifetime (the captured
-    memcpy node re-reads that buffer on every replay; a pageable temporary would be freed)."""
+    """Small host table (kernel argument lists: pointers, shapes) -> device tensor.  On the GPU
+    the values travel in the arguments of a fill kernel (``dcp::table_fill``), not a host->device
+    copy, so a table built while a step is being captured into a HIP graph replays correctly
+    (a captured memcpy would re-read a host buffer that is gone, and pinning memory is not
+    allowed during capture)."""
     host = torch.tensor(rows, dtype=dtype)
-    if torch.cuda.is_available():
-        host = host.pin_memory()
-        if torch.cuda.is_current_stream_capturing():
-            _GRAPH_KEEPALIVE.append(host)
-    return host.to(device, non_blocking=True)
+    device = torch.device(device)
+    if device.type != "cuda":
+        return host.to(device)
+    flat = host.reshape(-1)
+    if dtype == torch.int32:
+        if flat.numel() % 2:
+            flat = torch.cat([flat, flat.new_zeros(1)])
+        words = flat.view(torch.int64)
+    else:
+        words = flat.to(torch.int64) if dtype != torch.int64 else flat
+    anchor = _DEV_ANCHOR.get(device)
+    if anchor is None:
+        anchor = _DEV_ANCHOR[device] = torch.empty(1, device=device)
+    out = _ext.hip_ops().table_fill(words.contiguous(), anchor)
+    if dtype == torch.int32:
+        out = out.view(torch.int32)[:host.numel()]
+    return out.view(host.shape)
 
 
 # ----------------------------------------------------------------------------- weight cache

@@ -45,3 +45,14 @@ def test_graphed_step_matches_eager(name, size):
     assert all(abs(a - b) <= 1e-4 * max(1.0, abs(a)) for a, b in zip(ref, got)), (ref, got)
     for (n, p1), p2 in zip(m_eager.named_parameters(), m_graph.parameters()):
         assert torch.allclose(p1, p2, rtol=1e-4, atol=1e-5), n
+
+
+@pytest.mark.parametrize("n,dtype", [(1, torch.int64), (448, torch.int64), (1000, torch.int64), (7, torch.int32),
+                                     (2000, torch.int32)])
+def test_table_to_device_through_kernel_args(n, dtype):
+    rows = torch.randint(-2**30, 2**30, (n,), dtype=dtype).tolist()
+    out = Fn.table_to_device(rows, dtype, "cuda")
+    assert out.dtype == dtype and out.shape == (n,)
+    assert torch.equal(out.cpu(), torch.tensor(rows, dtype=dtype))
+    two = Fn.table_to_device([[1, 2], [3, 4], [5, 6]], dtype, "cuda")
+    assert two.shape == (3, 2) and two.cpu().tolist() == [[1, 2], [3, 4], [5, 6]]

@@ -845,3 +845,30 @@ def test_bn2_bwd_elemt_matches_two_passes(K):
     z = torch.zeros(C)
     dx1, _ = K.bn_bwd_elemt(d(g), d(x), None, d(pr[0]), d(z), d(pr[1]), d(pr[2]), d(pr[3]), count, 0, 0.0, False)
     assert relerr(dx, dx1) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 7, 9), (1, 13, 30), (2, 28, 28), (1, 1, 5), (1, 4, 126),
+                                   (2, 64, 64)])
+def test_conv3x3_direct_c64(K, N, H, W):
+    """The direct 64->64 3x3 kernel (conv3x3.hip) against the reference conv and against the
+    implicit GEMM it replaces (g_tune[18] = 1 forces the latter); BN partials vs bn_stats."""
+    torch.manual_seed(7)
+    x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
+    w = rnd(64, 3, 3, 64, scale=1.0 / 24)
+    y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
+    assert part.shape[1:] == (3, 64)  # (n, mean, M2) partials of the direct kernel
+    yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1, False)
+    assert relerr(y, yr) < 1e-2
+    K.set_tuning(18, 1)
+    try:
+        y2, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
+    finally:
+        K.set_tuning(18, 0)
+    assert relerr(y, y2) < 5e-3
+    st = K.bn_stats(y, part)
+    sr = _ref.bn_stats(y.float().cpu(), None)
+    assert torch.equal(st[0, 0].cpu(), sr[0, 0])
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4
+    assert relerr(st[0, 2], sr[0, 2]) < 1e-4
+    y3, none = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, False)
+    assert none.numel() == 0 and torch.equal(y3, y)

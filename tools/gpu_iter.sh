@@ -1,22 +1,14 @@
 #!/bin/bash
-# One build->measure iteration on the GPU box: kernel numerics tests (-k filter in $1),
-# the headline bench, optionally per-shape conv timings ($2 = "conv") and a rocprofv3
-# kernel trace ($3 = "prof").  Every GPU step has its own time limit; stops at the first failure.
+# iteration check: table transport + graph capture + direct 3x3 conv tests, then eager/graph bench
 set -e
-O=gpurun_out/iter; mkdir -p $O
-K="${1:-}"
-if [ -n "$K" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-  tail -2 $O/tests.log
-fi
-timeout -k 10 150 python -u bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1
-grep -o '"value": [0-9.]*' $O/bench.log
-if [ "$2" = "conv" ]; then
-  timeout -k 10 300 python -u tools/conv_bench.py --batch 512 --no-miopen > $O/conv_b512.txt 2>&1
-  tail -1 $O/conv_b512.txt
-fi
-if [ "$3" = "prof" ]; then
-  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 2 > $O/prof.log 2>&1
-fi
-echo iter done
+O=gpurun_out/${1:-iter}; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_graph_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "table or graphed or conv3x3_direct or conv_fwd" > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+tail -3 $O/test.log
+timeout -k 10 180 python -u bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+tail -1 $O/bench.log
+for b in 32 128; do
+  for g in "" "--graph"; do
+    timeout -k 10 180 python -u bench.py --batch $b --steps 30 --warmup 5 $g > $O/bench_b${b}${g}.log 2>&1 || { tail -20 $O/bench_b${b}${g}.log; exit 1; }
+    python -c "import json; d=json.loads(open('$O/bench_b${b}${g}.log').read().strip().splitlines()[-1]); print('b$b', '$g', d['value'], d['ms_per_step'])"
+  done
+done
