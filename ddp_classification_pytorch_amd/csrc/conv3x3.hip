@@ -17,7 +17,8 @@
 //    at a time (four independent accumulator chains);
 //  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
 //    (the numbers the BN normalises), and writes through a per-wave LDS staging tile as 32-byte
-//    row pieces; two workgroups per CU overlap one's window load with the other's MFMAs.
+//    row pieces; each workgroup double-buffers its windows (strip s+1 is fetched behind strip
+//    s's MFMAs) and two workgroups share a CU.
 #include <algorithm>
 
 #include "common.cuh"
@@ -26,7 +27,8 @@
 namespace dcp {
 
 namespace {
-constexpr int kC3WinMax = 48 * 1024;        // window bytes per workgroup (two workgroups per CU)
+constexpr int kC3WinMax = 48 * 1024;        // single window buffer: bytes per workgroup
+constexpr int kC3WinBuf2 = 35 * 1024;       // each of two window buffers (two workgroups per CU)
 constexpr int kC3Stage = 4 * 32 * 64;       // per-wave 32 px x 32 ch bf16 staging tiles
 
 struct C3Params {
@@ -39,6 +41,7 @@ struct C3Params {
   int R, spi;        // rows per strip, strips per image
   int strips, sps;   // strips in total, strips per workgroup
   int Wp, xq;        // window pitch (W + 2) and its 16-byte chunk count
+  int wbytes, nbuf;  // bytes per window buffer (1 KB aligned), window buffers (1 or 2)
   FastDiv div_wp, div_w, div_spi;
 };
 
@@ -49,11 +52,10 @@ __device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
 
 __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* win = smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ch = wave & 1, pg = wave >> 1;
-  char* stage = smem + p.xq * 16 + wave * (32 * 64);
+  char* stage = smem + p.nbuf * p.wbytes + wave * (32 * 64);
   const int H = p.H, W = p.W, Wp = p.Wp;
   const uint32_t lr = lane & 15, lg = lane >> 4;
 
@@ -71,11 +73,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
   bool have_k = false;
   const int s_begin = blockIdx.x * p.sps, s_end = min(p.strips, s_begin + p.sps);
 
-  for (int s = s_begin; s < s_end; ++s) {
+  // strip s's input window -> window buffer b (LDS-DMA; zero page outside the image)
+  auto load_strip = [&](int s, int b) {
+    char* wb = smem + b * p.wbytes;
     const int n_img = fdiv(s, p.div_spi);
     const int y0 = (s - n_img * p.spi) * p.R;
-    const int rows = min(p.R, H - y0), npix = rows * W;
-    __syncthreads();  // every wave is done with the previous strip's window
     for (int qq = tid; qq < p.xq; qq += 256) {
       const uint32_t P = qq >> 3;
       const uint32_t rr = fdiv(P, p.div_wp), xx = P - rr * Wp;
@@ -83,10 +85,25 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
       const bool ok = yy >= 0 && yy < H && xi >= 0 && xi < W;
       const uint32_t c = (qq & 7) ^ (P & 7u);
       const bf16* g = ok ? p.x + ((size_t)(n_img * H + yy) * W + xi) * 64 + c * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, win + (qq - lane) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, wb + (qq - lane) * 16), 16, 0, 0);
     }
+  };
+  if (p.nbuf == 2 && s_begin < s_end) load_strip(s_begin, 0);
+  for (int s = s_begin; s < s_end; ++s) {
+    const int n_img = fdiv(s, p.div_spi);
+    const int y0 = (s - n_img * p.spi) * p.R;
+    const int rows = min(p.R, H - y0), npix = rows * W;
+    const int b = p.nbuf == 2 ? (s - s_begin) & 1 : 0;
+    if (p.nbuf == 1) {
+      __syncthreads();  // every wave is done with the previous strip's window
+      load_strip(s, 0);
+    }
+    // strip s landed (own DMA drained, then the barrier); with two buffers every wave is also
+    // done with buffer b^1 (strip s-1), which now receives strip s+1 behind this strip's MFMAs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (p.nbuf == 2 && s + 1 < s_end) load_strip(s + 1, b ^ 1);
+    const char* win = smem + b * p.wbytes;
 
     const int nsub = (npix + 15) >> 4;
     const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
@@ -205,9 +222,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
 }
 
 // ---------------------------------------------------------------------------
+static int c3_nbuf() { return g_tune[19] == 1 ? 1 : 2; }
+
 static int c3_rows(int H, int W) {
   const int Wp = W + 2;
-  int R = kC3WinMax / (Wp * 128) - 2;
+  int R = (c3_nbuf() == 1 ? kC3WinMax : kC3WinBuf2) / (Wp * 128) - 2;
   R = std::min(R, H);
   if (R < 1) return 0;
   const int spi = (H + R - 1) / R;  // equal strips per image
@@ -237,14 +256,16 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.sps = (p.strips + blocks - 1) / blocks;
   p.Wp = W + 2;
   p.xq = (p.R + 2) * p.Wp * 8;
+  p.nbuf = c3_nbuf();
+  p.wbytes = (p.xq * 16 + 1023) / 1024 * 1024;
   p.div_wp = make_fastdiv(p.Wp);
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
-  const int lds = p.xq * 16 + kC3Stage;
+  const int lds = p.nbuf * p.wbytes + kC3Stage;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kC3WinMax + kC3Stage);
+                              2 * kC3WinBuf2 + 2048 + kC3Stage);
     attr = true;
   }
   hipLaunchKernelGGL(conv3x3_c64_kernel, dim3(blocks), dim3(256), lds, stream, p);
