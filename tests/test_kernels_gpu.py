@@ -856,7 +856,8 @@ def test_conv3x3_direct_c64(K, N, H, W):
     x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
     w = rnd(64, 3, 3, 64, scale=1.0 / 24)
     y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
-    assert part.shape[1:] == (3, 64)  # (n, mean, M2) partials of the direct kernel
+    if W <= 100:  # wider rows exceed the double-buffered window: the implicit GEMM (slabs) runs
+        assert part.shape[1:] == (3, 64)  # (n, mean, M2) partials of the direct kernel
     yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1, False)
     assert relerr(y, yr) < 1e-2
     K.set_tuning(18, 1)
