@@ -17,8 +17,8 @@
 //    at a time (four independent accumulator chains);
 //  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
 //    (the numbers the BN normalises), and writes through a per-wave LDS staging tile as 32-byte
-//    row pieces; each workgroup double-buffers its windows (strip s+1 is fetched behind strip
-//    s's MFMAs) and two workgroups share a CU.
+//    row pieces; two workgroups per CU overlap one's window load with the other's MFMAs
+//    (g_tune[19] = 2: double-buffered windows, measured slower: 366 vs 345 us at b1024).
 #include <algorithm>
 
 #include "common.cuh"
@@ -50,6 +50,88 @@ __device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
 }
 }  // namespace
 
+// NU (1 or 2) 16-pixel subtiles s0, s0 + 2 of the staged strip: 9 taps x 2 k-halves x NU
+// fragment reads, 36 NU MFMAs, then the bf16 epilogue (statistics, staged 32-byte row stores).
+// Staging rows (pixels) are 64 B = 4 chunks of 16 B, chunk XOR-swizzled by (row >> 2) & 3: the
+// ds_read_b128 lane groups of the read-back then hit 16 distinct slots (the 2-byte writes stay
+// at most 2-way, which costs nothing extra).
+template <int NU>
+__device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char* stage, const bf16x8 (&bw)[9][2][2],
+                                        int s0, int npix, size_t ybase, int ch, int lane, float (&K)[2],
+                                        float (&s1)[2], float (&s2)[2], float& cnt, bool& have_k) {
+  const uint32_t lr = lane & 15, lg = lane >> 4;
+  const int W = p.W, Wp = p.Wp;
+  uint32_t base[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const uint32_t pix = min((s0 + 2 * u) * 16 + (int)lr, npix - 1);  // past the strip: clamped
+    const uint32_t r = fdiv(pix, p.div_w), xp = pix - r * W;
+    base[u] = r * Wp + xp;
+  }
+  f32x4 acc[NU][2];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[u][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const uint32_t dt = (t / 3) * Wp + (t % 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 a[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) a[u] = *LDS_PTR(bf16x8, win + c3_addr(base[u] + dt, 4 * h + lg));
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw[t][h][n], acc[u][n], 0, 0, 0);
+    }
+  }
+  // epilogue: D[pixel 16 sub + 4 lg + i][co 32 ch + 16 n + lr]
+  if (!have_k) {  // per-wave statistics shift: the wave's first output (a valid pixel)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) K[n] = __shfl(bf2f(f2bf(acc[0][n][0])), (int)lr, 64);
+    have_k = true;
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = u * 16 + 4 * (int)lg + i;
+      const bool valid = (s0 + 2 * u) * 16 + 4 * (int)lg + i < npix;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const bf16 v = f2bf(acc[u][n][i]);
+        const float d = valid ? bf2f(v) - K[n] : 0.f;
+        s1[n] += d;
+        s2[n] = fmaf(d, d, s2[n]);
+        const uint32_t cc = (uint32_t)(2 * n + (lr >> 3)) ^ lg;  // (row >> 2) & 3 == lg
+        *LDS_PTR(bf16, stage + row * 64 + cc * 16 + (lr & 7) * 2) = v;
+      }
+      cnt += valid ? 1.f : 0.f;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging writes are done
+  __builtin_amdgcn_wave_barrier();
+  {
+    const int u = lane >> 5, pr = (lane >> 1) & 15, half = lane & 1;
+    const int row = u * 16 + pr, q = (pr >> 2) & 3;
+    const int pix = (s0 + 2 * u) * 16 + pr;
+    bf16x8 v0, v1;
+    if (u < NU) {
+      v0 = *LDS_PTR(bf16x8, stage + row * 64 + (((2 * half) ^ q) << 4));
+      v1 = *LDS_PTR(bf16x8, stage + row * 64 + (((2 * half + 1) ^ q) << 4));
+    }
+    if (u < NU && pix < npix) {
+      bf16* dst = p.y + ybase + (size_t)pix * 64 + 32 * ch + 16 * half;
+      *(bf16x8*)dst = v0;
+      *(bf16x8*)(dst + 8) = v1;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next writes
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -58,6 +140,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
   char* stage = smem + p.nbuf * p.wbytes + wave * (32 * 64);
   const int H = p.H, W = p.W, Wp = p.Wp;
   const uint32_t lr = lane & 15, lg = lane >> 4;
+  (void)Wp;
 
   // B fragments: lane holds co = 32 ch + 16 n + lr, ci = 32 h + 8 lg .. +7 of tap t
   bf16x8 bw[9][2][2];
@@ -108,72 +191,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
     const int nsub = (npix + 15) >> 4;
     const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
     for (int s0 = pg; s0 < nsub; s0 += 4) {
-      const int sub[2] = {s0, s0 + 2};
-      uint32_t base[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const uint32_t pix = min(sub[u] * 16 + (int)lr, npix - 1);  // rows past the strip: clamped
-        const uint32_t r = fdiv(pix, p.div_w), xp = pix - r * W;
-        base[u] = r * Wp + xp;
-      }
-      f32x4 acc[2][2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) acc[u][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const uint32_t dt = (t / 3) * Wp + (t % 3);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          bf16x8 a[2];
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            a[u] = *LDS_PTR(bf16x8, win + c3_addr(base[u] + dt, 4 * h + lg));
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int n = 0; n < 2; ++n)
-              acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw[t][h][n], acc[u][n], 0, 0, 0);
-        }
-      }
-      // epilogue: D[pixel 16 sub + 4 lg + i][co 32 ch + 16 n + lr]
-      if (!have_k) {  // per-wave statistics shift: the wave's first output (finite by construction)
-#pragma unroll
-        for (int n = 0; n < 2; ++n) K[n] = __shfl(bf2f(f2bf(acc[0][n][0])), (int)lr, 64);
-        have_k = true;
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int pix = sub[u] * 16 + 4 * (int)lg + i;
-          const bool valid = pix < npix;
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const bf16 v = f2bf(acc[u][n][i]);
-            const float d = valid ? bf2f(v) - K[n] : 0.f;
-            s1[n] += d;
-            s2[n] = fmaf(d, d, s2[n]);
-            *LDS_PTR(bf16, stage + (u * 16 + 4 * lg + i) * 64 + (16 * n + lr) * 2) = v;
-          }
-          cnt += valid ? 1.f : 0.f;
-        }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's staging writes are done
-      __builtin_amdgcn_wave_barrier();
-      {
-        const int u = lane >> 5, pr = (lane >> 1) & 15, half = lane & 1;
-        const int pix = sub[u] * 16 + pr;
-        const bf16x8 v0 = *LDS_PTR(bf16x8, stage + (u * 16 + pr) * 64 + half * 32);
-        const bf16x8 v1 = *LDS_PTR(bf16x8, stage + (u * 16 + pr) * 64 + half * 32 + 16);
-        if (pix < npix) {
-          bf16* dst = p.y + ybase + (size_t)pix * 64 + 32 * ch + 16 * half;
-          *(bf16x8*)dst = v0;
-          *(bf16x8*)(dst + 8) = v1;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging reads done before the next writes
-      __builtin_amdgcn_wave_barrier();
+      if (s0 + 2 < nsub)
+        c3_tile<2>(p, win, stage, bw, s0, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+      else  // odd tail: one subtile, no wasted MFMAs
+        c3_tile<1>(p, win, stage, bw, s0, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
     }
   }
   if (!p.part) return;
@@ -222,7 +243,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
 }
 
 // ---------------------------------------------------------------------------
-static int c3_nbuf() { return g_tune[19] == 1 ? 1 : 2; }
+static int c3_nbuf() { return g_tune[19] == 2 ? 2 : 1; }  // single buffer measured faster
 
 static int c3_rows(int H, int W) {
   const int Wp = W + 2;
