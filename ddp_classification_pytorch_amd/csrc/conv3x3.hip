@@ -8,7 +8,7 @@
 //  * the weights (9 taps x 64 x 64 bf16) live in VGPRs for the whole kernel: wave w holds the
 //    B fragments of output channels 32*(w&1) .. +31 for all taps (36 x 16 bytes per lane);
 //  * a workgroup walks a contiguous range of row strips (R output rows of one image); the
-//    strip's input window -- (R+2) x (W+2) pixels x 128 bytes, zero outside the image -- is
+//    strip's input window -- (R+2) x (W+8) pixels x 128 bytes, zero outside the image -- is
 //    staged ONCE in LDS by LDS-DMA, 16-byte chunks XOR-swizzled by the window pixel's low
 //    three bits so the ds_read_b128 fragment reads of 8 consecutive pixels hit 8 different
 //    bank groups; the nine taps are the same fragments at shifted window pixels;
@@ -40,7 +40,7 @@ struct C3Params {
   int H, W;
   int R, spi;        // rows per strip, strips per image
   int strips, sps;   // strips in total, strips per workgroup
-  int Wp, xq;        // window pitch (W + 2) and its 16-byte chunk count
+  int Wp, xq;        // window pitch (c3_pitch) and its 16-byte chunk count
   int wbytes, nbuf;  // bytes per window buffer (1 KB aligned), window buffers (1 or 2)
   FastDiv div_wp, div_w, div_spi;
 };
@@ -245,8 +245,12 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
 // ---------------------------------------------------------------------------
 static int c3_nbuf() { return g_tune[19] == 2 ? 2 : 1; }  // single buffer measured faster
 
+// window pitch: W + 8 pixels (>= the 2 halo columns, and Wp - W = 0 mod 8 keeps the 16-B chunk
+// swizzle residues consecutive across an output-row wrap inside a 16-pixel subtile)
+static int c3_pitch(int W) { return W + 8; }
+
 static int c3_rows(int H, int W) {
-  const int Wp = W + 2;
+  const int Wp = c3_pitch(W);
   int R = (c3_nbuf() == 1 ? kC3WinMax : kC3WinBuf2) / (Wp * 128) - 2;
   R = std::min(R, H);
   if (R < 1) return 0;
@@ -275,7 +279,7 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.spi = (H + p.R - 1) / p.R;
   p.strips = N * p.spi;
   p.sps = (p.strips + blocks - 1) / blocks;
-  p.Wp = W + 2;
+  p.Wp = c3_pitch(W);
   p.xq = (p.R + 2) * p.Wp * 8;
   p.nbuf = c3_nbuf();
   p.wbytes = (p.xq * 16 + 1023) / 1024 * 1024;
