@@ -46,6 +46,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--bucket-cap-mb", type=float, default=25.0)
     a("--first-bucket-mb", type=float, default=4.0)
     a("--device", default=None, help="cuda (default when available) or cpu")
+    a("--graph", action="store_true", help="1 GPU: replay the training step as a HIP graph (launch-bound small batches)")
     # data
     a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "shards"])
     a("--shard-train", dest="shard_train", default=None, help="--data shards: train shard (default <folder>/train.dcps)")

@@ -42,3 +42,50 @@ class GraphedStep:
     def __call__(self):
         self.graph.replay()
         return self.out
+
+
+class StepGrapher:
+    """Graph the training step of a data loop: ``grapher(*batch)`` runs the first ``warmup``
+    steps eagerly (side stream), captures the step on the next call and replays it (the capture
+    itself executes nothing, so that batch is trained by the first replay); later calls copy the
+    batch into the captured static inputs and replay.  A batch of a different shape (the short
+    last batch of an epoch) runs eagerly.  Call :meth:`reset` after changing anything baked into
+    the captured kernels' arguments (the learning rate at an epoch boundary): the next call
+    recaptures.  Every step -- eager, captured or replayed -- trains on exactly one batch."""
+
+    def __init__(self, step_fn, warmup: int = 2):
+        self.fn, self.warmup, self.calls = step_fn, max(1, warmup), 0
+        self.graph = self.static = self.out = None
+        self.captures = 0
+
+    def reset(self):
+        self.graph = self.static = self.out = None
+
+    def _eager(self, tensors):
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            out = self.fn(*tensors)
+        cur.wait_stream(side)
+        return out
+
+    def __call__(self, *tensors):
+        self.calls += 1
+        if self.calls <= self.warmup:
+            return self._eager(tensors)
+        if self.graph is not None and any(s.shape != t.shape or s.dtype != t.dtype
+                                          for s, t in zip(self.static, tensors)):
+            return self._eager(tensors)
+        if self.graph is None:
+            torch.cuda.synchronize()
+            self.static = [t.clone() for t in tensors]
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self.fn(*self.static)
+            self.captures += 1
+        else:
+            for s, t in zip(self.static, tensors):
+                s.copy_(t, non_blocking=True)
+        self.graph.replay()
+        return self.out

@@ -88,8 +88,31 @@ class ClassificationLoop:
             save_checkpoint(self._ckpt("best.pth"), self.models, {"opt": self.optimizer}, sched, **kw)
 
     # ------------------------------------------------------------------ epochs
+    def _train_step(self, *batch):
+        loss, rank = self.forward_train(batch)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.post_backward is not None:
+            self.post_backward()
+        self.optimizer.step()
+        return loss, rank
+
+    def _setup_graph(self):
+        """--graph: single-process GPU runs replay the whole step as a HIP graph (engine/graph.py),
+        recaptured at every epoch start (the learning rate is a captured kernel argument)."""
+        a = self.args
+        self._grapher = None
+        if getattr(a, "graph", False) and self.rt.device.type == "cuda" and self.rt.world == 1:
+            from .graph import StepGrapher
+
+            self._grapher = StepGrapher(self._train_step, warmup=2)
+
     def train_epoch(self, epoch):
         a, dev = self.args, self.rt.device
+        if not hasattr(self, "_grapher"):
+            self._setup_graph()
+        if self._grapher is not None:
+            self._grapher.reset()  # the epoch's learning rate is baked into the captured step
         for m in self.train_modules:
             m.train()
         sampler = getattr(self.train_data, "sampler", None)
@@ -106,12 +129,10 @@ class ClassificationLoop:
                 break
             if a.fail_at_step is not None and self.global_step == a.fail_at_step:
                 raise InjectedFailure(f"injected failure at global step {self.global_step}")
-            loss, rank = self.forward_train(batch)
-            self.optimizer.zero_grad(set_to_none=True)
-            loss.backward()
-            if self.post_backward is not None:
-                self.post_backward()
-            self.optimizer.step()
+            if self._grapher is not None:
+                loss, rank = self._grapher(*batch)
+            else:
+                loss, rank = self._train_step(*batch)
             B = rank.numel()
             step_stats = torch.stack([loss.detach().double() * B, (rank < 1).sum().double(),
                                       (rank < 3).sum().double(), torch.tensor(float(B), device=dev,

@@ -56,3 +56,23 @@ def test_table_to_device_through_kernel_args(n, dtype):
     assert torch.equal(out.cpu(), torch.tensor(rows, dtype=dtype))
     two = Fn.table_to_device([[1, 2], [3, 4], [5, 6]], dtype, "cuda")
     assert two.shape == (3, 2) and two.cpu().tolist() == [[1, 2], [3, 4], [5, 6]]
+
+
+def test_training_loop_graph_matches_eager(tmp_path):
+    """main.py --graph (StepGrapher: eager warm-up, capture, replays, recapture per epoch, eager
+    short last batch) trains to the same weights as the eager loop."""
+    import main as entry
+
+    common = ["--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+              "--batchsize", "16", "--synthetic-train-size", "120", "--synthetic-val-size", "32", "--epochs", "2",
+              "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "SGD",
+              "--lr", "0.05"]
+    outs = {}
+    for tag, extra in (("eager", []), ("graph", ["--graph"])):
+        torch.manual_seed(0)
+        entry.main(common + ["--out-dir", str(tmp_path / tag)] + extra)
+        outs[tag] = torch.load(tmp_path / tag / "last.pth", weights_only=True)
+    me, mg = outs["eager"]["models"]["model"], outs["graph"]["models"]["model"]
+    for k, v in me.items():
+        if v.dtype.is_floating_point:
+            assert torch.allclose(v, mg[k], rtol=2e-3, atol=2e-4), k
