@@ -157,7 +157,10 @@ class _MTWeightCache:
                 stale.append((k, e, w))
         if not stale:
             return
-        tkey = tuple(k for k, _, _ in stale) + tuple(w.data_ptr() for _, _, w in stale)
+        # keyed by every pointer the table holds: a model rebuilt in the same process can reuse
+        # the ids and master-weight addresses of a freed one while its bf16 copies moved
+        tkey = tuple((k, w.data_ptr(), e["wb"].data_ptr(), e["wt"].data_ptr() if e["transposed"] else 0)
+                     for k, e, w in stale)
         tab = self.tables.get(tkey)
         if tab is None:
             rows, blocks = [], []
