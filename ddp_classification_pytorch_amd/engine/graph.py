@@ -19,6 +19,16 @@ from __future__ import annotations
 import torch
 
 
+def _stale_weights():
+    """Mark every cached bf16 weight copy stale before a capture.  Which kernels the captured
+    step contains is decided by host-side state at capture time: a capture right after an
+    evaluation pass (weights fresh) would record no weight-prep launch, and every replay --
+    each ending in an optimizer step -- would then run on the pre-capture bf16 weights."""
+    from ..ops import functional as Fn
+
+    Fn.bump_weight_generation()
+
+
 class GraphedStep:
     """``GraphedStep(step_fn, warmup=3)``: runs ``step_fn`` ``warmup`` times on a side stream
     (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
@@ -35,6 +45,7 @@ class GraphedStep:
                 step_fn()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        _stale_weights()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn()
@@ -79,6 +90,7 @@ class StepGrapher:
             return self._eager(tensors)
         if self.graph is None:
             torch.cuda.synchronize()
+            _stale_weights()
             self.static = [t.clone() for t in tensors]
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
