@@ -46,8 +46,8 @@ class AvgPool2x2(nn.Module):
         super().__init__()
         self.register_buffer("filt", torch.full((2, 2), 0.25), persistent=False)
 
-    def forward(self, x):
-        return Fn.blur_pool(x, self.filt.to(x.device), k=2, s=2, p=0, reflect=False)
+    def forward(self, x, deposit=None):
+        return Fn.blur_pool(x, self.filt.to(x.device), k=2, s=2, p=0, reflect=False, deposit=deposit)
 
 
 class SEModule(nn.Module):
@@ -62,8 +62,8 @@ class SEModule(nn.Module):
         h = self.fc1(Fn.global_avg_pool(x), relu=True)
         return Fn.linear(h, self.fc2.weight, self.fc2.bias, act="sigmoid")
 
-    def forward(self, x, residual=None, relu=False):
-        return Fn.channel_scale(x, self.gate(x), residual, relu)
+    def forward(self, x, residual=None, relu=False, link=None):
+        return Fn.channel_scale(x, self.gate(x), residual, relu, link=link)
 
 
 class Downsample(nn.Module):
@@ -77,14 +77,27 @@ class Downsample(nn.Module):
             x = self.pool(x)
         return self.conv(x)
 
-    def raw(self, x):
+    def raw(self, x, deposit=None):
         """(conv output, BN statistics slabs, BN module): the shortcut before its BN, for a
-        consumer that normalises it on the fly (BatchNorm2d(residual_bn=...))."""
+        consumer that normalises it on the fly (BatchNorm2d(residual_bn=...)).  ``deposit``: the
+        block's GradJoin, which receives the shortcut's input gradient."""
         if self.pool is not None:
-            x = self.pool(x)
+            x = self.pool(x, deposit=deposit)
+            deposit = None
         bn = self.conv.bn
-        r, rs = self.conv.conv(x, stats=bn.training and not bn.frozen)
+        r, rs = self.conv.conv(x, stats=bn.training and not bn.frozen, deposit=deposit)
         return r, (bn, rs)
+
+    def normed(self, x, deposit=None):
+        r, (bn, rs) = self.raw(x, deposit)
+        return bn(r, rs, act="none")
+
+
+def _first_conv(cbn, x, join):
+    """A block's first ConvBN as the primary consumer of the block input: its dgrad epilogue adds
+    the shortcut's gradient (GradJoin) and fuses the producing BN's backward reduction."""
+    y, s = cbn.conv(x, stats=cbn.bn.training and not cbn.bn.frozen, link=join)
+    return cbn.bn(y, s, act=cbn.act, slope=cbn.slope)
 
 
 class TBasicBlock(nn.Module):
@@ -99,15 +112,22 @@ class TBasicBlock(nn.Module):
         self.downsample = Downsample(inplanes, planes, stride) if (stride != 1 or inplanes != planes) else None
 
     def forward(self, x):
-        shortcut = self.downsample(x) if self.downsample is not None else x
-        out = self.conv1(x)
+        # the block input's second consumer (identity residual / shortcut pool) hands its gradient
+        # to conv1 (GradJoin); the shortcut runs after the main path so its backward comes first
+        join = Fn.GradJoin(1)
+        out = _first_conv(self.conv1, x, join)
         if self.aa is not None:
             out = self.aa(out)
         if self.se is None:
             y, s = self.conv2.conv(out, stats=self.conv2.bn.training and not self.conv2.bn.frozen)
-            return self.conv2.bn(y, s, act="relu", residual=shortcut)
+            if self.downsample is not None:
+                r, rbn = self.downsample.raw(x, deposit=join)
+                return self.conv2.bn(y, s, act="relu", residual=r, residual_bn=rbn)
+            return self.conv2.bn(y, s, act="relu", residual=x, link=join)
         out = self.conv2(out)
-        return self.se(out, residual=shortcut, relu=True)
+        if self.downsample is not None:
+            return self.se(out, residual=self.downsample.normed(x, deposit=join), relu=True)
+        return self.se(out, residual=x, relu=True, link=join)
 
 
 class TBottleneck(nn.Module):
@@ -124,16 +144,20 @@ class TBottleneck(nn.Module):
                            if (stride != 1 or inplanes != planes * 4) else None)
 
     def forward(self, x):
-        # projection shortcut: its BN is applied inside conv3's BN pass (no shortcut activation)
-        shortcut, rbn = self.downsample.raw(x) if self.downsample is not None else (x, None)
-        out = self.conv1(x)
+        join = Fn.GradJoin(1)
+        out = _first_conv(self.conv1, x, join)
         out = self.conv2(out)
         if self.aa is not None:
             out = self.aa(out)
         if self.se is not None:
             out = self.se(out)
         y, s = self.conv3.conv(out, stats=self.conv3.bn.training and not self.conv3.bn.frozen)
-        return self.conv3.bn(y, s, act="relu", residual=shortcut, residual_bn=rbn)
+        if self.downsample is not None:
+            # projection shortcut (after the main path: its backward precedes conv1's); its BN is
+            # applied inside conv3's BN pass (no shortcut activation)
+            r, rbn = self.downsample.raw(x, deposit=join)
+            return self.conv3.bn(y, s, act="relu", residual=r, residual_bn=rbn)
+        return self.conv3.bn(y, s, act="relu", residual=x, link=join)
 
 
 class TResNet(nn.Module):

@@ -745,28 +745,34 @@ def space_to_depth(x, b=4):
 
 class _DWConv(Function):
     @staticmethod
-    def forward(ctx, x, filt, k, s, p, reflect):
+    def forward(ctx, x, filt, k, s, p, reflect, deposit):
         ctx.save_for_backward(filt)
         ctx.geo = (x.shape[1], x.shape[2], k, s, p, reflect)
+        ctx.deposit = deposit
         return K(x).dwconv_fwd(x, filt, k, s, p, reflect)
 
     @staticmethod
     def backward(ctx, dy):
         (filt,) = ctx.saved_tensors
         H, W, k, s, p, reflect = ctx.geo
-        return K(dy).dwconv_bwd(dy.contiguous(), filt, H, W, k, s, p, reflect), None, None, None, None, None
+        dx = K(dy).dwconv_bwd(dy.contiguous(), filt, H, W, k, s, p, reflect)
+        if ctx.deposit is not None:
+            dx = ctx.deposit.deposit(dx)  # summed by the block's first conv (GradJoin)
+        ctx.deposit = None
+        return dx, None, None, None, None, None, None
 
 
-def blur_pool(x, filt, k=3, s=2, p=1, reflect=True):
-    """Fixed depthwise low-pass filter + stride (anti-aliased downsampling)."""
-    return _DWConv.apply(x, filt, k, s, p, reflect)
+def blur_pool(x, filt, k=3, s=2, p=1, reflect=True, deposit: "GradJoin | None" = None):
+    """Fixed depthwise low-pass filter + stride (anti-aliased downsampling).  ``deposit``: hand the
+    input gradient to a GradJoin (a TResNet shortcut pool is the block input's second consumer)."""
+    return _DWConv.apply(x, filt, k, s, p, reflect, deposit)
 
 
 class _ChanScale(Function):
     @staticmethod
-    def forward(ctx, x, g, res, relu):
+    def forward(ctx, x, g, res, relu, link):
         ctx.save_for_backward(x, g, res)
-        ctx.relu = relu
+        ctx.relu, ctx.link = relu, link
         return K(x).chan_scale_fwd(x, g, res, relu)
 
     @staticmethod
@@ -774,13 +780,18 @@ class _ChanScale(Function):
         x, g, res = ctx.saved_tensors
         want_dres = res is not None and ctx.needs_input_grad[2]
         dx, dg, dres = K(dy).chan_scale_bwd(dy.contiguous(), x, g, res, ctx.relu, want_dres)
-        return dx, dg.to(g.dtype), (dres if want_dres else None), None
+        dres = dres if want_dres else None
+        if dres is not None and ctx.link is not None:
+            dres = ctx.link.deposit(dres)  # summed into the block input gradient by the first conv
+        ctx.link = None
+        return dx, dg.to(g.dtype), dres, None, None
 
 
-def channel_scale(x, g, residual=None, relu=False):
+def channel_scale(x, g, residual=None, relu=False, link: "GradJoin | None" = None):
     """act(x[n,h,w,c] * g[n,c] (+ residual)) — squeeze-and-excitation apply fused
-    with the block's residual add and ReLU."""
-    return _ChanScale.apply(x, g.contiguous(), residual, bool(relu))
+    with the block's residual add and ReLU.  ``link``: the identity residual's gradient goes to
+    the block's GradJoin instead of an autograd add."""
+    return _ChanScale.apply(x, g.contiguous(), residual, bool(relu), link)
 
 
 # ----------------------------------------------------------------------------- losses

@@ -162,3 +162,32 @@ def test_shortcut_bn_fusion_matches_unfused(name, size, cpad):
     for (n, b1), b2 in zip(m1.named_buffers(), m2.buffers()):
         if b1.dtype.is_floating_point:
             assert torch.allclose(b1, b2, rtol=1e-5, atol=1e-6), n
+
+
+@pytest.mark.parametrize("name,size,cpad", [("tresnet_m", 64, 3), ("resnet50", 64, 8)])
+def test_gradjoin_matches_autograd_sum(name, size, cpad, monkeypatch):
+    """The GradJoin hand-off (secondary consumers deposit, the block's first conv adds in its dgrad
+    epilogue) gives the same gradients as letting autograd sum the block-input gradients."""
+    import copy
+
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(4)
+    m1 = build_model(name, num_classes=10)
+    m2 = copy.deepcopy(m1)
+    imgs = torch.randn(2, 3, size, size)
+    labels = torch.randint(0, 10, (2,))
+
+    def run(m):
+        loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, cpad=cpad, nchw=True)), labels)
+        loss.backward()
+        return loss.detach()
+
+    l1 = run(m1)
+    with monkeypatch.context() as mp:  # every deposit refused: autograd adds the gradients
+        mp.setattr(Fn.GradJoin, "deposit", lambda self, g: g)
+        l2 = run(m2)
+    assert torch.allclose(l1, l2, rtol=1e-6, atol=1e-7)
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p1.grad, p2.grad, rtol=1e-3, atol=1e-5), n
