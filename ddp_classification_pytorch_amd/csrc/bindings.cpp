@@ -783,11 +783,17 @@ Tensor gap_fwd(const Tensor& x) {
   return y;
 }
 
-Tensor gap_bwd(const Tensor& dy, int64_t H, int64_t W) {
+Tensor gap_bwd(const Tensor& dy, int64_t H, int64_t W, const optional<Tensor>& add) {
   CHECK_ACT(dy);
   const int N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(C % 8 == 0, "gap_bwd channels");
+  if (add.has_value()) {
+    CHECK_ACT(*add);
+    TORCH_CHECK(add->dim() == 4 && add->size(0) == N && add->size(1) == H && add->size(2) == W && add->size(3) == C,
+                "gap_bwd add shape");
+  }
   auto dx = at::empty({N, H, W, C}, dy.options());
-  dcp::launch_gap_bwd(bp(dy), bpm(dx), N, H * W, C, cur_stream());
+  dcp::launch_gap_bwd(bp(dy), bpm(dx), N, H * W, C, cur_stream(), add.has_value() ? bp(*add) : nullptr);
   return dx;
 }
 
@@ -1199,7 +1205,7 @@ TORCH_LIBRARY(dcp, m) {
       "Tensor invstd, int act, Tensor sums, float count, int k, int s, int p) -> Tensor",
       &maxpool_bn_bwd_elemt);
   m.def("gap_fwd(Tensor x) -> Tensor", &gap_fwd);
-  m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &gap_bwd);
+  m.def("gap_bwd(Tensor dy, int H, int W, Tensor? add=None) -> Tensor", &gap_bwd);
   m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
   m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
   m.def("crop_resize(Tensor src, Tensor meta, int Ho, int Wo) -> Tensor", &crop_resize);

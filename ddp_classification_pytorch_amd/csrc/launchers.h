@@ -144,7 +144,7 @@ void launch_maxpool_bwd(const bf16* dy, const uint8_t* idx, bf16* dx, int N, int
 // part workspace holds S x N x C floats
 int hw_splits(int N, int HW, int C);
 void launch_gap_fwd(const bf16* x, bf16* y, float* part, int N, int HW, int C, hipStream_t st);
-void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st);
+void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st, const bf16* add = nullptr);
 void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int inverse, hipStream_t st);
 
 void launch_xent_fwd(const void* logits, bool is_bf16, int B, int ld, int C, const int64_t* labels, float* loss,

@@ -279,8 +279,10 @@ __global__ void __launch_bounds__(256) gap_final_kernel(const float* __restrict_
   y[i] = f2bf(t * inv);
 }
 
+// dx = broadcast(dy / HW) (+ add: the other consumers' gradient of the pooled tensor, e.g. a
+// squeeze-excitation block's channel-scale dgrad -- summed here instead of by an extra add pass)
 __global__ void __launch_bounds__(256) gap_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int N,
-                                                      int HW, int C) {
+                                                      int HW, int C, const bf16* __restrict__ add) {
   const int cpr = C >> 3;
   const size_t total = (size_t)N * HW * cpr;
   const float inv = 1.f / HW;
@@ -289,8 +291,14 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const bf16* __restrict__ d
     const size_t n = i / cpr / HW;
     const bf16x8 g = *(const bf16x8*)(dy + n * C + ch * 8);
     bf16x8 o;
+    if (add) {
+      const bf16x8 a = *(const bf16x8*)(add + i * 8);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = f2bf(bf2f(g[q]) * inv);
+      for (int q = 0; q < 8; ++q) o[q] = f2bf(fmaf(bf2f(g[q]), inv, bf2f(a[q])));
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = f2bf(bf2f(g[q]) * inv);
+    }
     *(bf16x8*)(dx + i * 8) = o;
   }
 }
@@ -406,9 +414,9 @@ void launch_gap_fwd(const bf16* x, bf16* y, float* part, int N, int HW, int C, h
   hipLaunchKernelGGL(gap_final_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, part, y, N * C, S, 1.f / HW);
 }
 
-void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st) {
+void launch_gap_bwd(const bf16* dy, bf16* dx, int N, int HW, int C, hipStream_t st, const bf16* add) {
   const size_t total = (size_t)N * HW * (C / 8);
-  hipLaunchKernelGGL(gap_bwd_kernel, dim3(ew_grid2(total)), dim3(256), 0, st, dy, dx, N, HW, C);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(ew_grid2(total)), dim3(256), 0, st, dy, dx, N, HW, C, add);
 }
 
 void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int inverse, hipStream_t st) {

@@ -58,12 +58,15 @@ class SEModule(nn.Module):
         self.fc1 = Linear(channels, reduction_channels)
         self.fc2 = Linear(reduction_channels, channels)
 
-    def gate(self, x):
-        h = self.fc1(Fn.global_avg_pool(x), relu=True)
+    def gate(self, x, join=None):
+        h = self.fc1(Fn.global_avg_pool(x, link=join), relu=True)
         return Fn.linear(h, self.fc2.weight, self.fc2.bias, act="sigmoid")
 
     def forward(self, x, residual=None, relu=False, link=None):
-        return Fn.channel_scale(x, self.gate(x), residual, relu, link=link)
+        # x feeds the pooling and the channel scale: the scale's backward (which runs first)
+        # deposits its x-gradient and the pooling's backward adds it while broadcasting
+        join = Fn.GradJoin(1)
+        return Fn.channel_scale(x, self.gate(x, join), residual, relu, link=link, deposit=join)
 
 
 class Downsample(nn.Module):

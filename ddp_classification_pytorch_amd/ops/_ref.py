@@ -329,9 +329,12 @@ def gap_fwd(x):
     return _f(x).reshape(N, -1, C).mean(1).to(x.dtype)
 
 
-def gap_bwd(dy, H, W):
+def gap_bwd(dy, H, W, add=None):
     N, C = dy.shape
-    return (_f(dy) / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).contiguous().to(dy.dtype)
+    g = (_f(dy) / (H * W)).view(N, 1, 1, C).expand(N, H, W, C)
+    if add is not None:
+        g = g + _f(add)
+    return g.contiguous().to(dy.dtype)
 
 
 def space_to_depth(x, b, inverse):

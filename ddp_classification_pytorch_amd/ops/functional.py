@@ -714,18 +714,27 @@ def max_pool2d(x, k=3, s=2, p=1):
 
 class _GAP(Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, link):
         ctx.hw = (x.shape[1], x.shape[2])
+        ctx.link = link
         return K(x).gap_fwd(x)
 
     @staticmethod
     def backward(ctx, dy):
-        return K(dy).gap_bwd(dy.contiguous(), *ctx.hw)
+        add = None
+        if ctx.link is not None:
+            add, _ = ctx.link.claim()  # the other consumers' gradient, summed in the same pass
+            ctx.link = None
+            if add is not None:
+                add = add.contiguous()
+        return K(dy).gap_bwd(dy.contiguous(), *ctx.hw, add), None
 
 
-def global_avg_pool(x):
-    """[N,H,W,C] -> [N,C] (torchvision AdaptiveAvgPool2d(1) + flatten)."""
-    return _GAP.apply(x)
+def global_avg_pool(x, link: "GradJoin | None" = None):
+    """[N,H,W,C] -> [N,C] (torchvision AdaptiveAvgPool2d(1) + flatten).  ``link``: a GradJoin
+    whose deposited gradient of ``x`` (e.g. a squeeze-excitation channel scale's) the backward
+    adds while broadcasting."""
+    return _GAP.apply(x, link)
 
 
 class _S2D(Function):
@@ -770,9 +779,9 @@ def blur_pool(x, filt, k=3, s=2, p=1, reflect=True, deposit: "GradJoin | None" =
 
 class _ChanScale(Function):
     @staticmethod
-    def forward(ctx, x, g, res, relu, link):
+    def forward(ctx, x, g, res, relu, link, deposit):
         ctx.save_for_backward(x, g, res)
-        ctx.relu, ctx.link = relu, link
+        ctx.relu, ctx.link, ctx.deposit = relu, link, deposit
         return K(x).chan_scale_fwd(x, g, res, relu)
 
     @staticmethod
@@ -783,15 +792,19 @@ class _ChanScale(Function):
         dres = dres if want_dres else None
         if dres is not None and ctx.link is not None:
             dres = ctx.link.deposit(dres)  # summed into the block input gradient by the first conv
-        ctx.link = None
-        return dx, dg.to(g.dtype), dres, None, None
+        if ctx.deposit is not None:
+            dx = ctx.deposit.deposit(dx)  # summed by the SE pooling's backward
+        ctx.link = ctx.deposit = None
+        return dx, dg.to(g.dtype), dres, None, None, None
 
 
-def channel_scale(x, g, residual=None, relu=False, link: "GradJoin | None" = None):
+def channel_scale(x, g, residual=None, relu=False, link: "GradJoin | None" = None,
+                  deposit: "GradJoin | None" = None):
     """act(x[n,h,w,c] * g[n,c] (+ residual)) — squeeze-and-excitation apply fused
     with the block's residual add and ReLU.  ``link``: the identity residual's gradient goes to
-    the block's GradJoin instead of an autograd add."""
-    return _ChanScale.apply(x, g.contiguous(), residual, bool(relu), link)
+    the block's GradJoin instead of an autograd add; ``deposit``: likewise for the gradient of
+    ``x`` (the SE block's pooling adds it)."""
+    return _ChanScale.apply(x, g.contiguous(), residual, bool(relu), link, deposit)
 
 
 # ----------------------------------------------------------------------------- losses

@@ -873,3 +873,12 @@ def test_conv3x3_direct_c64(K, N, H, W):
     assert relerr(st[0, 2], sr[0, 2]) < 1e-4
     y3, none = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, False)
     assert none.numel() == 0 and torch.equal(y3, y)
+
+
+def test_gap_bwd_with_add(K):
+    torch.manual_seed(9)
+    dy, add = rnd(3, 96), rnd(3, 5, 7, 96)
+    out = K.gap_bwd(dy.to(DEV), 5, 7, add.to(DEV))
+    ref = _ref.gap_bwd(dy, 5, 7, add)
+    assert relerr(out, ref) < 1e-2
+    assert relerr(K.gap_bwd(dy.to(DEV), 5, 7), _ref.gap_bwd(dy, 5, 7)) < 1e-2
