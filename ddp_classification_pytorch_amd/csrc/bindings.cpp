@@ -440,6 +440,25 @@ Tensor grouped_conv_fwd(const Tensor& x, const Tensor& w, int64_t groups, int64_
   return y;
 }
 
+// grouped conv forward + the output's BN partials [P][3][Co] (n, mean, M2) from the MFMA epilogue
+// (an empty tensor when the shape runs the direct fallback kernel)
+std::tuple<Tensor, Tensor> grouped_conv_fwd_stats(const Tensor& x, const Tensor& w, int64_t groups, int64_t stride,
+                                                  int64_t pad) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(C % groups == 0 && Co % groups == 0 && w.size(3) == C / groups, "grouped conv shapes");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "grouped conv channel multiples of 8");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
+  auto frag = at::empty({std::max(dcp::gconv_frag_elems(C, groups, KH, KW), 8)}, bf16_like(x));
+  auto part = at::empty({dcp::gconv_fwd_stat_blocks(N * Ho * Wo), 3, Co}, f32_like(x));
+  const bool ok = dcp::launch_grouped_conv_fwd(bp(x), bp(w), bpm(y), bpm(frag), N, H, W, C, Ho, Wo, Co, groups, KH, KW,
+                                               stride, pad, cur_stream(), part.data_ptr<float>());
+  return {y, ok ? part : at::empty({0}, f32_like(x))};
+}
+
 Tensor grouped_conv_dgrad(const Tensor& dy, const Tensor& w, int64_t H, int64_t W, int64_t groups, int64_t stride,
                           int64_t pad) {
   CHECK_ACT(dy);
@@ -1157,6 +1176,8 @@ TORCH_LIBRARY(dcp, m) {
   m.def("linear_wgrad(Tensor dy, Tensor x) -> Tensor", &linear_wgrad);
   m.def("weight_prep(Tensor w, int co_pad, bool transposed) -> (Tensor, Tensor)", &weight_prep);
   m.def("grouped_conv_fwd(Tensor x, Tensor w, int groups, int stride, int pad) -> Tensor", &grouped_conv_fwd);
+  m.def("grouped_conv_fwd_stats(Tensor x, Tensor w, int groups, int stride, int pad) -> (Tensor, Tensor)",
+        &grouped_conv_fwd_stats);
   m.def("grouped_conv_dgrad(Tensor dy, Tensor w, int H, int W, int groups, int stride, int pad) -> Tensor",
         &grouped_conv_dgrad);
   m.def("grouped_conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int groups, int stride, int pad) -> Tensor",

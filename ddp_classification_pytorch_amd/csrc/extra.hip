@@ -321,12 +321,14 @@ static inline int grid_of(size_t n) {
   return (int)g;
 }
 
-void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
-                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
-  if (launch_gconv_mfma_fwd(x, w, y, frag, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s)) return;
+bool launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s, float* stats) {
+  if (launch_gconv_mfma_fwd(x, w, y, frag, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s, stats))
+    return stats != nullptr;
   const size_t total = (size_t)N * Ho * Wo * (Co / 8);
   hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, s, x, w, y, N, H, W, C, Ho, Wo, Co, G, KH,
                      KW, stride, pad);
+  return false;
 }
 void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C,
                                int Ho, int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {

@@ -39,6 +39,7 @@ struct GconvParams {
   bf16* dst;        // fwd / dgrad output [N][Hd][Wd][C]
   const bf16* dy;   // wgrad: [N][Hd][Wd][C]
   float* part;      // wgrad: [splits][C][T][CG]
+  float* stats;     // fwd (optional): BN partials [pixel blocks][3][C] = (n, mean, M2) of the output
   const bf16* wfrag;  // fwd/dgrad: fragment-ordered block-diagonal weight (gconv_frag_kernel)
   const bf16* zero;   // >= 16 bytes of zeros (global)
   int nbuf;           // wgrad: 2 = double-buffered chunks
@@ -143,6 +144,80 @@ __device__ __forceinline__ bf16x8 w_frag(const GconvParams& p, int sg, int row, 
 // ---------------------------------------------------------------------------
 // fwd / dgrad: D[row = channel][col = pixel] = W_bd[row][k] * B[k][pixel]
 // ---------------------------------------------------------------------------
+// BN statistics of the forward tile (256 pixels x SG channels) from the bf16-rounded outputs:
+// per-wave shifted sums (shift = the wave's first output of each channel), lanes of one channel
+// group combined by shuffles, the four waves merged with Chan's formula -> (n, mean, M2) of the
+// tile's channels in partial row pb (the [P][3][C] layout bn_stats / bn_stats_finalize merge).
+template <int SG, int NRT, int CPT>
+__device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const f32x4 (&acc)[NRT][CPT], char* smem,
+                                                 int m0, int sg, int pb, int wave, int lane) {
+  float K[NRT][4], s1[NRT][4], s2[NRT][4], cnt = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      K[rt][r] = __shfl(bf2f(f2bf(acc[rt][0][r])), lane & 48, 64);
+      s1[rt][r] = s2[rt][r] = 0.f;
+    }
+#pragma unroll
+  for (int ct = 0; ct < CPT; ++ct) {
+    const bool valid = m0 + wave * 64 + ct * 16 + (lane & 15) < p.M;
+    cnt += valid ? 1.f : 0.f;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = valid ? bf2f(f2bf(acc[rt][ct][r])) - K[rt][r] : 0.f;
+        s1[rt][r] += d;
+        s2[rt][r] = fmaf(d, d, s2[rt][r]);
+      }
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off *= 2) {
+    cnt += __shfl_xor(cnt, off, 64);
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[rt][r] += __shfl_xor(s1[rt][r], off, 64);
+        s2[rt][r] += __shfl_xor(s2[rt][r], off, 64);
+      }
+  }
+  __syncthreads();  // every wave is done with the staged halo image: reuse it as scratch
+  float* sc = (float*)smem;  // [4 waves][SG channels][4]: cnt, K, s1, s2
+  if ((lane & 15) == 0)
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* e = sc + (wave * SG + rt * 16 + (lane >> 4) * 4 + r) * 4;
+        e[0] = cnt;
+        e[1] = K[rt][r];
+        e[2] = s1[rt][r];
+        e[3] = s2[rt][r];
+      }
+  __syncthreads();
+  if (threadIdx.x < SG) {
+    const int c = threadIdx.x;
+    float nt = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float* e = sc + (w * SG + c) * 4;
+      const float nb = e[0];
+      if (nb <= 0.f) continue;
+      const float mb = e[1] + e[2] / nb, m2b = fmaxf(e[3] - e[2] * e[2] / nb, 0.f);
+      const float ntot = nt + nb, delta = mb - mean;
+      mean += delta * nb / ntot;
+      m2 += m2b + delta * delta * nt * nb / ntot;
+      nt = ntot;
+    }
+    float* o = p.stats + (size_t)pb * 3 * p.C + sg * SG + c;
+    o[0] = nt;
+    o[p.C] = mean;
+    o[2 * p.C] = m2;
+  }
+}
+
 template <int SG, bool DGRAD>
 __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) {
   constexpr int NRT = SG / 16;                 // 16-row tiles of the output channels
@@ -223,6 +298,9 @@ __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) 
       for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[rt][ct][r]);
       *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = o;
     }
+  }
+  if constexpr (!DGRAD) {
+    if (p.stats) gconv_tile_stats<SG, NRT, CPT>(p, acc, smem, m0, sg, pb, wave, lane);
   }
 }
 
@@ -485,8 +563,11 @@ int gconv_frag_elems(int C, int G, int KH, int KW) {
   return (C / SG) * ((KH * KW + TPS - 1) / TPS) * (SG / 16) * 64 * 8;
 }
 
+int gconv_fwd_stat_blocks(int M) { return (M + GP - 1) / GP; }
+
 bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
-                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
+                           float* stats) {
   const int CG = C / G;
   const int SG = pick_sg(C, CG);
   if (SG == 0 || Co != C || KH * KW > GT || frag == nullptr) return false;
@@ -499,6 +580,7 @@ bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, in
   p.src = x;
   p.w = w;
   p.dst = y;
+  p.stats = stats;
   return SG == 16 ? launch_gather<16, false>(p, N, frag, s) : launch_gather<32, false>(p, N, frag, s);
 }
 

@@ -61,8 +61,12 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
                   const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream);
 // frag: gconv_frag_elems(...) bf16 workspace (MFMA path; may be null -> direct kernels)
-void launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
-                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+// stats (optional, [gconv_fwd_stat_blocks(M)][3][Co]): BN partials of y from the MFMA kernel's epilogue;
+// returns whether they were written (false: the direct fallback kernel ran)
+bool launch_grouped_conv_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
+                             float* stats = nullptr);
+int gconv_fwd_stat_blocks(int M);
 void launch_grouped_conv_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C,
                                int Ho, int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
 // dw is fully written; part = workspace of gconv_mfma_wgrad_splits(...) x Co*KH*KW*(C/G) floats
@@ -72,7 +76,8 @@ void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, float* 
 // MFMA super-group kernels (gconv.hip); return false for shapes they do not cover
 int gconv_frag_elems(int C, int G, int KH, int KW);
 bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
-                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+                           int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
+                           float* stats = nullptr);
 bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C, int Ho,
                              int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
 int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G);

@@ -40,8 +40,7 @@ class Conv2d(nn.Module):
         """Returns (y, bn_stat_slabs_or_None).  `link` / `deposit`: block-input gradient
         hand-off as primary / secondary consumer (ops.functional.GradJoin)."""
         if self.groups > 1:
-            y = Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding)
-            return y, None
+            return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding, stats=bool(stats))
         y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda, link, deposit)
         return y, (slabs if stats and x.is_cuda else None)
 

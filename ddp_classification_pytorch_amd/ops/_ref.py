@@ -151,6 +151,10 @@ def grouped_conv_fwd(x, w, groups, stride, pad):
     return _nhwc(y).to(x.dtype)
 
 
+def grouped_conv_fwd_stats(x, w, groups, stride, pad):
+    return grouped_conv_fwd(x, w, groups, stride, pad), x.new_empty(0, dtype=torch.float32)
+
+
 def grouped_conv_dgrad(dy, w, H, W, groups, stride, pad):
     N, Co = dy.shape[0], dy.shape[3]
     C = w.shape[3] * groups

@@ -326,28 +326,41 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0,
 
 class _GroupedConv2d(Function):
     @staticmethod
-    def forward(ctx, x, weight, wb, groups, stride, pad):
-        y = K(x).grouped_conv_fwd(x, wb, groups, stride, pad)
+    def forward(ctx, x, weight, wb, groups, stride, pad, stats):
+        if stats:  # BN partials of the output from the MFMA epilogue (empty: BN computes them)
+            y, part = K(x).grouped_conv_fwd_stats(x, wb, groups, stride, pad)
+        else:
+            y, part = K(x).grouped_conv_fwd(x, wb, groups, stride, pad), x.new_empty(0, dtype=torch.float32)
         ctx.save_for_backward(x, wb)
         ctx.geo = (weight.shape[1], weight.shape[2], groups, stride, pad)
-        return y
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpart):
+        if dy is None:
+            return (None,) * 7
         x, wb = ctx.saved_tensors
         KH, KW, groups, stride, pad = ctx.geo
         dy = dy.contiguous()
         k = K(dy)
         dx = k.grouped_conv_dgrad(dy, wb, x.shape[1], x.shape[2], groups, stride, pad) if ctx.needs_input_grad[0] else None
         dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
-def grouped_conv2d(x, weight, groups, stride=1, pad=0):
+def grouped_conv2d(x, weight, groups, stride=1, pad=0, stats=False):
+    """Grouped NHWC conv -> y, or (y, BN partials or None) with ``stats=True`` (GPU: the partials
+    come from the MFMA kernel's epilogue, so the following BN reads no extra pass over y)."""
     if groups == 1:
-        return conv2d(x, weight, stride, pad, False)[0]
+        y, slabs = conv2d(x, weight, stride, pad, stats and x.is_cuda)
+        return (y, slabs if stats and x.is_cuda else None) if stats else y
     wb, _ = prepared_weight(weight, 0, False)
-    return _GroupedConv2d.apply(x, weight, wb, groups, stride, pad)
+    y, part = _GroupedConv2d.apply(x, weight, wb, groups, stride, pad, bool(stats and x.is_cuda))
+    if not stats:
+        return y
+    return y, (part if part.numel() > 0 else None)
 
 
 # ----------------------------------------------------------------------------- linear

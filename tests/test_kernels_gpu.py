@@ -882,3 +882,21 @@ def test_gap_bwd_with_add(K):
     ref = _ref.gap_bwd(dy, 5, 7, add)
     assert relerr(out, ref) < 1e-2
     assert relerr(K.gap_bwd(dy.to(DEV), 5, 7), _ref.gap_bwd(dy, 5, 7)) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,s", [(2, 56, 128, 1), (3, 14, 512, 1), (2, 28, 256, 2), (1, 7, 1024, 1)])
+def test_grouped_conv_fwd_stats(K, N, H, C, s):
+    """ResNeXt 32x4d grouped 3x3 forward with the BN partials from the MFMA epilogue."""
+    torch.manual_seed(11)
+    G = 32
+    x = rnd(N, H, H, C, scale=2.0).abs()
+    w = rnd(C, 3, 3, C // G, scale=1.0 / math.sqrt(9 * C // G))
+    y0 = K.grouped_conv_fwd(x.to(DEV), w.to(DEV), G, s, 1)
+    y, part = K.grouped_conv_fwd_stats(x.to(DEV), w.to(DEV), G, s, 1)
+    assert torch.equal(y, y0)
+    assert part.dim() == 3 and part.shape[1:] == (3, C)
+    st = K.bn_stats(y, part)
+    sr = _ref.bn_stats(y.float().cpu(), None)
+    assert torch.equal(st[0, 0].cpu(), sr[0, 0])
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4
+    assert relerr(st[0, 2], sr[0, 2]) < 1e-4
