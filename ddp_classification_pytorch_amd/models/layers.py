@@ -40,7 +40,9 @@ class Conv2d(nn.Module):
         """Returns (y, bn_stat_slabs_or_None).  `link` / `deposit`: block-input gradient
         hand-off as primary / secondary consumer (ops.functional.GradJoin)."""
         if self.groups > 1:
-            return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding, stats=bool(stats))
+            if stats:
+                return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding, stats=True)
+            return Fn.grouped_conv2d(x, self.weight, self.groups, self.stride, self.padding), None
         y, slabs = Fn.conv2d(x, self.weight, self.stride, self.padding, stats and x.is_cuda, link, deposit)
         return y, (slabs if stats and x.is_cuda else None)
 

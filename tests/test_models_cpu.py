@@ -88,3 +88,18 @@ def test_arc_margin_reference_formula():
     loss, rank, out = arc(x, y, return_logits=True)
     assert torch.allclose(out, logits, atol=1e-4)
     assert abs(loss.item() - torch.nn.functional.cross_entropy(logits, y).item()) < 1e-4
+
+
+def test_resnext_train_and_eval_forward():
+    """grouped-conv blocks in both BN modes (training statistics / running statistics)."""
+    import torch
+
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    m = build_model("resnext50_32x4d", num_classes=5)
+    x = Fn.to_device_nhwc(torch.randn(2, 3, 64, 64), cpad=8, nchw=True)
+    assert m(x).shape == (2, 5)
+    m.eval()
+    with torch.no_grad():
+        assert m(x).shape == (2, 5)
