@@ -472,6 +472,40 @@ Tensor grouped_conv_dgrad(const Tensor& dy, const Tensor& w, int64_t H, int64_t 
   return dx;
 }
 
+// grouped dgrad fused with the backward reduction of the ReLU BN that produced the conv input z:
+// -> (g = dx * [z*scale + shift > 0], sums [2][C] = (sum g, sum g * (z - mean) * invstd)); an
+// empty `sums` means the shape runs the unfused kernels (the caller reduces separately)
+std::tuple<Tensor, Tensor> grouped_conv_dgrad_bn(const Tensor& dy, const Tensor& w, int64_t H, int64_t W,
+                                                 int64_t groups, int64_t stride, int64_t pad, const Tensor& z,
+                                                 const Tensor& scale, const Tensor& shift, const Tensor& mean,
+                                                 const Tensor& invstd) {
+  CHECK_ACT(dy);
+  CHECK_ACT(w);
+  CHECK_ACT(z);
+  const int N = dy.size(0), Ho = dy.size(1), Wo = dy.size(2), Co = dy.size(3);
+  const int KH = w.size(1), KW = w.size(2), C = w.size(3) * groups;
+  TORCH_CHECK(z.dim() == 4 && z.size(0) == N && z.size(1) == H && z.size(2) == W && z.size(3) == C,
+              "grouped_conv_dgrad_bn: z must be the conv input [N,H,W,C]");
+  for (const Tensor* t : {&scale, &shift, &mean, &invstd})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(),
+                "grouped_conv_dgrad_bn: per-channel fp32 [C] coefficients");
+  auto dx = at::empty({N, H, W, C}, bf16_like(dy));
+  auto frag = at::empty({std::max(dcp::gconv_frag_elems(C, groups, KH, KW), 8)}, bf16_like(dy));
+  const int npb = dcp::gconv_fwd_stat_blocks(N * H * W);
+  auto part = at::empty({(int64_t)npb * 2 * C + ((npb + 63) / 64) * 2 * C}, f32_like(dy));
+  dcp::GconvBnBwd bn{bp(z), scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), part.data_ptr<float>()};
+  if (!dcp::launch_gconv_mfma_dgrad(bp(dy), bp(w), bpm(dx), bpm(frag), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride,
+                                    pad, cur_stream(), &bn)) {
+    dcp::launch_grouped_conv_dgrad(bp(dy), bp(w), bpm(dx), bpm(frag), N, H, W, C, Ho, Wo, Co, groups, KH, KW, stride,
+                                   pad, cur_stream());
+    return {dx, at::empty({0}, f32_like(dy))};
+  }
+  auto sums = at::empty({2, C}, f32_like(dy));
+  dcp::launch_split_reduce(part.data_ptr<float>(), npb, 2 * C, sums.data_ptr<float>(), cur_stream());
+  return {dx, sums};
+}
+
 Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t groups, int64_t stride,
                           int64_t pad) {
   CHECK_ACT(dy);
@@ -1178,6 +1212,9 @@ TORCH_LIBRARY(dcp, m) {
   m.def("grouped_conv_fwd(Tensor x, Tensor w, int groups, int stride, int pad) -> Tensor", &grouped_conv_fwd);
   m.def("grouped_conv_fwd_stats(Tensor x, Tensor w, int groups, int stride, int pad) -> (Tensor, Tensor)",
         &grouped_conv_fwd_stats);
+  m.def("grouped_conv_dgrad_bn(Tensor dy, Tensor w, int H, int W, int groups, int stride, int pad, Tensor z, "
+        "Tensor scale, Tensor shift, Tensor mean, Tensor invstd) -> (Tensor, Tensor)",
+        &grouped_conv_dgrad_bn);
   m.def("grouped_conv_dgrad(Tensor dy, Tensor w, int H, int W, int groups, int stride, int pad) -> Tensor",
         &grouped_conv_dgrad);
   m.def("grouped_conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int groups, int stride, int pad) -> Tensor",

@@ -40,6 +40,12 @@ struct GconvParams {
   const bf16* dy;   // wgrad: [N][Hd][Wd][C]
   float* part;      // wgrad: [splits][C][T][CG]
   float* stats;     // fwd (optional): BN partials [pixel blocks][3][C] = (n, mean, M2) of the output
+  // dgrad (optional) fused backward of the ReLU BN that produced the conv input: dst receives the
+  // masked gradient g = dx * [z*scale + shift > 0] and bnsum[pixel block][2][C] its per-tile
+  // (sum g, sum g * (z - mean) * invstd)
+  const bf16* bnz;
+  const float *bn_scale, *bn_shift, *bn_mean, *bn_invstd;
+  float* bnsum;
   const bf16* wfrag;  // fwd/dgrad: fragment-ordered block-diagonal weight (gconv_frag_kernel)
   const bf16* zero;   // >= 16 bytes of zeros (global)
   int nbuf;           // wgrad: 2 = double-buffered chunks
@@ -218,6 +224,74 @@ __device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const f32
   }
 }
 
+// dgrad epilogue fused with the producing BN(+ReLU)'s backward reduction: store the masked
+// gradient and the tile's per-channel (sum g, sum g * xhat) -- the BN backward is then left with
+// its elementwise pass (no reduction pass re-reading g and z).
+template <int SG, int NRT, int CPT>
+__device__ __forceinline__ void gconv_dgrad_bn_epilogue(const GconvParams& p, const f32x4 (&acc)[NRT][CPT],
+                                                        char* smem, int m0, int sg, int pb, int wave, int lane) {
+  float sc[NRT][4], sh[NRT][4], mu[NRT][4], is[NRT][4], sg1[NRT][4], sg2[NRT][4];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = sg * SG + rt * 16 + (lane >> 4) * 4 + r;
+      sc[rt][r] = p.bn_scale[c];
+      sh[rt][r] = p.bn_shift[c];
+      mu[rt][r] = p.bn_mean[c];
+      is[rt][r] = p.bn_invstd[c];
+      sg1[rt][r] = sg2[rt][r] = 0.f;
+    }
+#pragma unroll
+  for (int ct = 0; ct < CPT; ++ct) {
+    const int m = m0 + wave * 64 + ct * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) {
+      const size_t off = (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4;
+      const bf16x4 z = *(const bf16x4*)(p.bnz + off);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float zf = bf2f(z[r]);
+        const bf16 gb = f2bf(zf * sc[rt][r] + sh[rt][r] > 0.f ? acc[rt][ct][r] : 0.f);
+        o[r] = gb;
+        const float g = bf2f(gb);
+        sg1[rt][r] += g;
+        sg2[rt][r] = fmaf(g, (zf - mu[rt][r]) * is[rt][r], sg2[rt][r]);
+      }
+      *(bf16x4*)(p.dst + off) = o;
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off *= 2)
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sg1[rt][r] += __shfl_xor(sg1[rt][r], off, 64);
+        sg2[rt][r] += __shfl_xor(sg2[rt][r], off, 64);
+      }
+  __syncthreads();  // every wave is done with the staged image: reuse it as scratch
+  float* xs = (float*)smem;  // [4 waves][2][SG]
+  if ((lane & 15) == 0)
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = rt * 16 + (lane >> 4) * 4 + r;
+        xs[(wave * 2 + 0) * SG + c] = sg1[rt][r];
+        xs[(wave * 2 + 1) * SG + c] = sg2[rt][r];
+      }
+  __syncthreads();
+  if (threadIdx.x < 2 * SG) {
+    const int k = threadIdx.x / SG, c = threadIdx.x % SG;
+    const float t = (xs[(0 * 2 + k) * SG + c] + xs[(1 * 2 + k) * SG + c]) +
+                    (xs[(2 * 2 + k) * SG + c] + xs[(3 * 2 + k) * SG + c]);
+    p.bnsum[((size_t)pb * 2 + k) * p.C + sg * SG + c] = t;
+  }
+}
+
 template <int SG, bool DGRAD>
 __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) {
   constexpr int NRT = SG / 16;                 // 16-row tiles of the output channels
@@ -286,6 +360,12 @@ __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) 
     }
   }
 
+  if constexpr (DGRAD) {
+    if (p.bnz) {
+      gconv_dgrad_bn_epilogue<SG, NRT, CPT>(p, acc, smem, m0, sg, pb, wave, lane);
+      return;
+    }
+  }
   // lane holds pixel column lane&15, channels (lane>>4)*4 .. +3 of each row tile
 #pragma unroll
   for (int ct = 0; ct < CPT; ++ct) {
@@ -585,7 +665,8 @@ bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, in
 }
 
 bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C, int Ho,
-                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s) {
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
+                             const GconvBnBwd* bn) {
   const int CG = C / G;
   const int SG = pick_sg(C, CG);
   if (SG == 0 || Co != C || KH * KW > GT || stride > 2 || frag == nullptr) return false;
@@ -598,6 +679,14 @@ bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag
   p.src = dy;
   p.w = w;
   p.dst = dx;
+  if (bn) {
+    p.bnz = bn->z;
+    p.bn_scale = bn->scale;
+    p.bn_shift = bn->shift;
+    p.bn_mean = bn->mean;
+    p.bn_invstd = bn->invstd;
+    p.bnsum = bn->part;
+  }
   return SG == 16 ? launch_gather<16, true>(p, N, frag, s) : launch_gather<32, true>(p, N, frag, s);
 }
 

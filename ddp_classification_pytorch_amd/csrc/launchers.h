@@ -78,8 +78,15 @@ int gconv_frag_elems(int C, int G, int KH, int KW);
 bool launch_gconv_mfma_fwd(const bf16* x, const bf16* w, bf16* y, bf16* frag, int N, int H, int W, int C, int Ho,
                            int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
                            float* stats = nullptr);
+// fused ReLU-BN backward reduction for the grouped dgrad (z: BN input; part: [gconv_fwd_stat_blocks(M)][2][C])
+struct GconvBnBwd {
+  const bf16* z;
+  const float *scale, *shift, *mean, *invstd;
+  float* part;
+};
 bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag, int N, int H, int W, int C, int Ho,
-                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s);
+                             int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
+                             const GconvBnBwd* bn = nullptr);
 int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G);
 bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
                              int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,

@@ -155,6 +155,15 @@ def grouped_conv_fwd_stats(x, w, groups, stride, pad):
     return grouped_conv_fwd(x, w, groups, stride, pad), x.new_empty(0, dtype=torch.float32)
 
 
+def grouped_conv_dgrad_bn(dy, w, H, W, groups, stride, pad, z, scale, shift, mean, invstd):
+    dx = _f(grouped_conv_dgrad(dy, w, H, W, groups, stride, pad))
+    zf = _f(z)
+    g = torch.where(zf * scale + shift > 0, dx, torch.zeros_like(dx)).to(dy.dtype)
+    gf = _rows(_f(g))
+    xh = (_rows(zf) - mean) * invstd
+    return g, torch.stack([gf.sum(0), (gf * xh).sum(0)])
+
+
 def grouped_conv_dgrad(dy, w, H, W, groups, stride, pad):
     N, Co = dy.shape[0], dy.shape[3]
     C = w.shape[3] * groups

@@ -326,13 +326,14 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0,
 
 class _GroupedConv2d(Function):
     @staticmethod
-    def forward(ctx, x, weight, wb, groups, stride, pad, stats):
+    def forward(ctx, x, weight, wb, groups, stride, pad, stats, bnsrc):
         if stats:  # BN partials of the output from the MFMA epilogue (empty: BN computes them)
             y, part = K(x).grouped_conv_fwd_stats(x, wb, groups, stride, pad)
         else:
             y, part = K(x).grouped_conv_fwd(x, wb, groups, stride, pad), x.new_empty(0, dtype=torch.float32)
         ctx.save_for_backward(x, wb)
         ctx.geo = (weight.shape[1], weight.shape[2], groups, stride, pad)
+        ctx.bnsrc = bnsrc
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -340,14 +341,26 @@ class _GroupedConv2d(Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return (None,) * 7
+            return (None,) * 8
         x, wb = ctx.saved_tensors
         KH, KW, groups, stride, pad = ctx.geo
         dy = dy.contiguous()
         k = K(dy)
-        dx = k.grouped_conv_dgrad(dy, wb, x.shape[1], x.shape[2], groups, stride, pad) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            src = ctx.bnsrc
+            if src is not None and src.act == 1 and src.tensors is not None and src.tensors[1] is None:
+                # the input came from a ReLU BN without residual: fuse its backward reduction
+                z, _, scale, shift, mean, invstd, _ = src.tensors
+                dx, sums = k.grouped_conv_dgrad_bn(dy, wb, x.shape[1], x.shape[2], groups, stride, pad, z, scale,
+                                                   shift, mean, invstd)
+                if sums.numel() > 0:
+                    src.fused = (dx, sums)
+            else:
+                dx = k.grouped_conv_dgrad(dy, wb, x.shape[1], x.shape[2], groups, stride, pad)
         dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None, None
+        ctx.bnsrc = None
+        return dx, dw, None, None, None, None, None, None
 
 
 def grouped_conv2d(x, weight, groups, stride=1, pad=0, stats=False):
@@ -357,7 +370,8 @@ def grouped_conv2d(x, weight, groups, stride=1, pad=0, stats=False):
         y, slabs = conv2d(x, weight, stride, pad, stats and x.is_cuda)
         return (y, slabs if stats and x.is_cuda else None) if stats else y
     wb, _ = prepared_weight(weight, 0, False)
-    y, part = _GroupedConv2d.apply(x, weight, wb, groups, stride, pad, bool(stats and x.is_cuda))
+    bnsrc = bn_source(x) if (stride == 1 and _FUSE_BN_BWD[0]) else None
+    y, part = _GroupedConv2d.apply(x, weight, wb, groups, stride, pad, bool(stats and x.is_cuda), bnsrc)
     if not stats:
         return y
     return y, (part if part.numel() > 0 else None)

@@ -191,3 +191,17 @@ def test_gradjoin_matches_autograd_sum(name, size, cpad, monkeypatch):
     assert torch.allclose(l1, l2, rtol=1e-6, atol=1e-7)
     for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
         assert torch.allclose(p1.grad, p2.grad, rtol=1e-3, atol=1e-5), n
+
+
+def test_resnext_grouped_dgrad_fuses_bn_backward(monkeypatch):
+    """ResNeXt's stride-1 grouped 3x3 convs fuse bn1's backward reduction into their dgrad
+    (grouped_conv_dgrad_bn) and the gradients equal the unfused path."""
+    calls = []
+    orig = _ref.grouped_conv_dgrad_bn
+    monkeypatch.setattr(_ref, "grouped_conv_dgrad_bn", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    l1, g1 = _grads("resnext50_32x4d", True)
+    assert len(calls) == 13  # the stride-1 grouped convs (16 blocks minus 3 stride-2 ones)
+    l0, g0 = _grads("resnext50_32x4d", False)
+    assert len(calls) == 13
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5

@@ -900,3 +900,24 @@ def test_grouped_conv_fwd_stats(K, N, H, C, s):
     assert torch.equal(st[0, 0].cpu(), sr[0, 0])
     assert relerr(st[0, 1], sr[0, 1]) < 1e-4
     assert relerr(st[0, 2], sr[0, 2]) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,C", [(2, 56, 128), (3, 14, 512), (1, 7, 1024)])
+def test_grouped_conv_dgrad_bn(K, N, H, C):
+    """Grouped dgrad with the ReLU-BN backward reduction in its epilogue vs the reference."""
+    torch.manual_seed(12)
+    G = 32
+    dy = rnd(N, H, H, C)
+    w = rnd(C, 3, 3, C // G, scale=1.0 / math.sqrt(9 * C // G))
+    z = rnd(N, H, H, C, scale=2.0)
+    scale, shift = torch.rand(C) + 0.5, torch.randn(C) * 0.3
+    mean, invstd = torch.randn(C) * 0.2, torch.rand(C) + 0.5
+    d = lambda t: t.to(DEV)
+    g, sums = K.grouped_conv_dgrad_bn(d(dy), d(w), H, H, G, 1, 1, d(z), d(scale), d(shift), d(mean), d(invstd))
+    gr, sr = _ref.grouped_conv_dgrad_bn(dy, w, H, H, G, 1, 1, z, scale, shift, mean, invstd)
+    assert relerr(g, gr) < 1e-2
+    assert sums.shape == (2, C)
+    assert relerr(sums, sr) < 2e-2
+    dx = K.grouped_conv_dgrad(d(dy), d(w), H, H, G, 1, 1)
+    zr = z.float() * scale + shift
+    assert torch.equal(g.cpu(), torch.where(zr > 0, dx.cpu(), torch.zeros_like(dx.cpu())))
