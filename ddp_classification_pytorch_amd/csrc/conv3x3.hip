@@ -140,7 +140,6 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
   char* stage = smem + p.nbuf * p.wbytes + wave * (32 * 64);
   const int H = p.H, W = p.W, Wp = p.Wp;
   const uint32_t lr = lane & 15, lg = lane >> 4;
-  (void)Wp;
 
   // B fragments: lane holds co = 32 ch + 16 n + lr, ci = 32 h + 8 lg .. +7 of tap t
   bf16x8 bw[9][2][2];
