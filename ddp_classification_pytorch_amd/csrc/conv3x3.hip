@@ -29,7 +29,7 @@ namespace dcp {
 namespace {
 constexpr int kC3WinMax = 48 * 1024;        // single window buffer: bytes per workgroup
 constexpr int kC3WinBuf2 = 35 * 1024;       // each of two window buffers (two workgroups per CU)
-constexpr int kC3Stage = 4 * 32 * 64;       // per-wave 32 px x 32 ch bf16 staging tiles
+constexpr int kC3Stage = 4 * 32 * 64;       // per-wave 32 px x 32 ch bf16 staging tiles (4 waves)
 
 struct C3Params {
   const bf16* x;     // [N][H][W][64]
@@ -57,14 +57,14 @@ __device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
 // at most 2-way, which costs nothing extra).
 template <int NU>
 __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char* stage, const bf16x8 (&bw)[9][2][2],
-                                        int s0, int npix, size_t ybase, int ch, int lane, float (&K)[2],
+                                        int s0, int du, int npix, size_t ybase, int ch, int lane, float (&K)[2],
                                         float (&s1)[2], float (&s2)[2], float& cnt, bool& have_k) {
   const uint32_t lr = lane & 15, lg = lane >> 4;
   const int W = p.W, Wp = p.Wp;
   uint32_t base[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const uint32_t pix = min((s0 + 2 * u) * 16 + (int)lr, npix - 1);  // past the strip: clamped
+    const uint32_t pix = min((s0 + du * u) * 16 + (int)lr, npix - 1);  // past the strip: clamped
     const uint32_t r = fdiv(pix, p.div_w), xp = pix - r * W;
     base[u] = r * Wp + xp;
   }
@@ -99,7 +99,7 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = u * 16 + 4 * (int)lg + i;
-      const bool valid = (s0 + 2 * u) * 16 + 4 * (int)lg + i < npix;
+      const bool valid = (s0 + du * u) * 16 + 4 * (int)lg + i < npix;
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         const bf16 v = f2bf(acc[u][n][i]);
@@ -116,7 +116,7 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
   {
     const int u = lane >> 5, pr = (lane >> 1) & 15, half = lane & 1;
     const int row = u * 16 + pr, q = (pr >> 2) & 3;
-    const int pix = (s0 + 2 * u) * 16 + pr;
+    const int pix = (s0 + du * u) * 16 + pr;
     bf16x8 v0, v1;
     if (u < NU) {
       v0 = *LDS_PTR(bf16x8, stage + row * 64 + (((2 * half) ^ q) << 4));
@@ -132,7 +132,11 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
   __builtin_amdgcn_wave_barrier();
 }
 
-__global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
+// NW waves per workgroup: wave w owns output-channel half w & 1 and pixel group w >> 1 (NW / 2
+// groups split a strip's 16-pixel subtiles); NW = 4 runs two workgroups per CU, NW = 8 one.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Params p) {
+  constexpr int NPG = NW / 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -160,7 +164,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
     char* wb = smem + b * p.wbytes;
     const int n_img = fdiv(s, p.div_spi);
     const int y0 = (s - n_img * p.spi) * p.R;
-    for (int qq = tid; qq < p.xq; qq += 256) {
+    for (int qq = tid; qq < p.xq; qq += 64 * NW) {
       const uint32_t P = qq >> 3;
       const uint32_t rr = fdiv(P, p.div_wp), xx = P - rr * Wp;
       const int yy = y0 - 1 + (int)rr, xi = (int)xx - 1;
@@ -189,11 +193,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
 
     const int nsub = (npix + 15) >> 4;
     const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
-    for (int s0 = pg; s0 < nsub; s0 += 4) {
-      if (s0 + 2 < nsub)
-        c3_tile<2>(p, win, stage, bw, s0, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+    for (int s0 = pg; s0 < nsub; s0 += 2 * NPG) {
+      if (s0 + NPG < nsub)
+        c3_tile<2>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
       else  // odd tail: one subtile, no wasted MFMAs
-        c3_tile<1>(p, win, stage, bw, s0, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+        c3_tile<1>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
     }
   }
   if (!p.part) return;
@@ -209,7 +213,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
     cnt += __shfl_xor(cnt, off, 64);
   }
   __syncthreads();  // window / staging no longer read: reuse as scratch
-  float* sc = (float*)smem;  // [4 waves][2 n][16][4]: cnt, K, s1, s2
+  float* sc = (float*)smem;  // [NW waves][2 n][16][4]: cnt, K, s1, s2
   if (lg == 0)
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -220,11 +224,11 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
       e[3] = s2[n];
     }
   __syncthreads();
-  if (tid < 64) {  // channel c = tid: waves (c >> 5) and (c >> 5) + 2 hold it, n = (c >> 4) & 1
+  if (tid < 64) {  // channel c = tid: waves (c >> 5) + 2 q hold it, n = (c >> 4) & 1
     const int c = tid, cw = c >> 5, n = (c >> 4) & 1, l = c & 15;
     float nt = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < NPG; ++q) {
       const float* e = sc + (((cw + 2 * q) * 2 + n) * 16 + l) * 4;
       const float nb = e[0];
       if (nb <= 0.f) continue;
@@ -242,7 +246,17 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c64_kernel(const C3Params p) {
 }
 
 // ---------------------------------------------------------------------------
-static int c3_nbuf() { return g_tune[19] == 2 ? 2 : 1; }  // single buffer measured faster
+// variants (g_tune[19]): 0 = 8 waves, one workgroup per CU, double-buffered windows (the next
+// strip streams in behind this strip's MFMAs); 1 = 4 waves, two workgroups per CU, one window
+// each; 2 = 4 waves, two double-buffered smaller windows
+struct C3Cfg {
+  int nw, nbuf, budget;  // waves, window buffers, bytes per window buffer
+};
+static C3Cfg c3_cfg() {
+  if (g_tune[19] == 1) return {4, 1, kC3WinMax};
+  if (g_tune[19] == 2) return {4, 2, kC3WinBuf2};
+  return {8, 2, kC3WinMax};
+}
 
 // window pitch: W + 8 pixels (>= the 2 halo columns, and Wp - W = 0 mod 8 keeps the 16-B chunk
 // swizzle residues consecutive across an output-row wrap inside a 16-pixel subtile)
@@ -250,7 +264,7 @@ static int c3_pitch(int W) { return W + 8; }
 
 static int c3_rows(int H, int W) {
   const int Wp = c3_pitch(W);
-  int R = (c3_nbuf() == 1 ? kC3WinMax : kC3WinBuf2) / (Wp * 128) - 2;
+  int R = c3_cfg().budget / (Wp * 128) - 2;
   R = std::min(R, H);
   if (R < 1) return 0;
   const int spi = (H + R - 1) / R;  // equal strips per image
@@ -264,13 +278,14 @@ bool conv3x3_c64_supported(int H, int W, int C, int Co) {
 int conv3x3_c64_blocks(int N, int H, int W, int num_cu) {
   const int R = c3_rows(H, W);
   const int strips = N * ((H + R - 1) / R);
-  const int target = std::max(1, 2 * num_cu);
+  const int target = std::max(1, num_cu * 8 / c3_cfg().nw);
   const int sps = (strips + target - 1) / target;
   return (strips + sps - 1) / sps;
 }
 
 void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
                         int blocks, hipStream_t stream) {
+  const C3Cfg cfg = c3_cfg();
   C3Params p;
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
   p.H = H; p.W = W;
@@ -280,19 +295,24 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.sps = (p.strips + blocks - 1) / blocks;
   p.Wp = c3_pitch(W);
   p.xq = (p.R + 2) * p.Wp * 8;
-  p.nbuf = c3_nbuf();
+  p.nbuf = cfg.nbuf;
   p.wbytes = (p.xq * 16 + 1023) / 1024 * 1024;
   p.div_wp = make_fastdiv(p.Wp);
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
-  const int lds = p.nbuf * p.wbytes + kC3Stage;
+  const int lds = p.nbuf * p.wbytes + cfg.nw * 32 * 64;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * kC3WinBuf2 + 2048 + kC3Stage);
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * kC3WinMax + 2048 + 2 * kC3Stage);
     attr = true;
   }
-  hipLaunchKernelGGL(conv3x3_c64_kernel, dim3(blocks), dim3(256), lds, stream, p);
+  if (cfg.nw == 8)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<8>, dim3(blocks), dim3(512), lds, stream, p);
+  else
+    hipLaunchKernelGGL(conv3x3_c64_kernel<4>, dim3(blocks), dim3(256), lds, stream, p);
 }
 
 }  // namespace dcp

@@ -20,7 +20,8 @@ def main():
     x = torch.randn(a.batch, a.hw, a.hw, 64, device="cuda").abs().bfloat16()
     w = (torch.randn(64, 3, 3, 64, device="cuda") / 24).bfloat16()
     flops = 2.0 * a.batch * a.hw * a.hw * 64 * 576
-    for name, tune in (("igemm", {18: 1}), ("direct", {}), ("direct-2buf", {19: 2})):
+    for name, tune in (("igemm", {18: 1}), ("direct-8w-2buf", {}), ("direct-4w-1buf", {19: 1}),
+                       ("direct-4w-2buf", {19: 2})):
         for k, v in tune.items():
             K.set_tuning(k, v)
         for _ in range(3):
