@@ -73,20 +73,25 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
   for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[u][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // 18 (tap, k-half) steps, software-pipelined: the fragments of step i+1 are read from LDS
+  // before the MFMAs of step i, so the LDS latency hides behind the previous step's MFMAs
+  auto frag = [&](int st, int u) {
+    const int t = st >> 1, h = st & 1;
+    return *LDS_PTR(bf16x8, win + c3_addr(base[u] + (t / 3) * Wp + (t % 3), 4 * h + lg));
+  };
+  bf16x8 a[2][NU];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const uint32_t dt = (t / 3) * Wp + (t % 3);
+  for (int u = 0; u < NU; ++u) a[0][u] = frag(0, u);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 a[NU];
+  for (int st = 0; st < 18; ++st) {
+    if (st + 1 < 18)
 #pragma unroll
-      for (int u = 0; u < NU; ++u) a[u] = *LDS_PTR(bf16x8, win + c3_addr(base[u] + dt, 4 * h + lg));
+      for (int u = 0; u < NU; ++u) a[(st + 1) & 1][u] = frag(st + 1, u);
 #pragma unroll
-      for (int u = 0; u < NU; ++u)
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bw[t][h][n], acc[u][n], 0, 0, 0);
-    }
+      for (int n = 0; n < 2; ++n)
+        acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st & 1][u], bw[st >> 1][st & 1][n], acc[u][n], 0, 0, 0);
   }
   // epilogue: D[pixel 16 sub + 4 lg + i][co 32 ch + 16 n + lr]
   if (!have_k) {  // per-wave statistics shift: the wave's first output (a valid pixel)
