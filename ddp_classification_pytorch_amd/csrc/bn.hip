@@ -685,8 +685,10 @@ void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t
   hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
 }
 
+// ~16 rows per workgroup (at most 128 partials): a linear layer's bias gradient over a 1024-row
+// batch with 1000 columns ran as 4 latency-bound workgroups (42 us) at 256 rows each
 int colsum_partials(int M) {
-  int g = (M + 255) / 256;
+  int g = (M + 15) / 16;
   return g > 128 ? 128 : (g < 1 ? 1 : g);
 }
 

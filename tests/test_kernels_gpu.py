@@ -927,3 +927,10 @@ def test_grouped_conv_dgrad_bn(K, N, H, C):
     zr = z.float() * scale + shift
     ref = torch.where(zr > 0, dx.cpu(), torch.zeros_like(dx.cpu()))
     assert (g.cpu() != ref).float().mean().item() < 1e-3  # masks may differ only where z*scale+shift ~ 0
+
+
+@pytest.mark.parametrize("M,C", [(1024, 1000), (7, 16), (3000, 2048), (1, 8), (513, 4096)])
+def test_colsum(K, M, C):
+    x = rnd(M, C)
+    out = K.colsum(x.to(DEV))
+    assert relerr(out, x.float().sum(0)) < 1e-5
