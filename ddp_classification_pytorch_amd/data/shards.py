@@ -359,19 +359,34 @@ class ShardLoader:
 
         fill()
         cur_stream = torch.cuda.current_stream(self.device) if self.cuda else None
-        while inflight:
-            s = inflight.popleft()
-            if self.cuda:
-                with torch.cuda.stream(self.stream):
+        try:
+            while inflight:
+                s = inflight.popleft()
+                if self.cuda:
+                    with torch.cuda.stream(self.stream):
+                        out = self._convert(s)
+                    cur_stream.wait_stream(self.stream)
+                    for t in out:
+                        t.record_stream(cur_stream)
+                else:
                     out = self._convert(s)
-                cur_stream.wait_stream(self.stream)
-                for t in out:
-                    t.record_stream(cur_stream)
-            else:
-                out = self._convert(s)
-            free.append(s)
-            fill()
-            yield out
+                free.append(s)
+                fill()
+                yield out
+        finally:
+            # an abandoned epoch (break / exception) must not leave host threads writing into
+            # slots that the next epoch, or the allocator, hands out again
+            for s in inflight:
+                try:
+                    self.gather.wait(s["ticket"])
+                except RuntimeError:
+                    pass
 
     def close(self):
         self.gather.close()
+
+    def __del__(self):
+        try:
+            self.close()  # joins the host threads while the pinned slots are still alive
+        except Exception:
+            pass

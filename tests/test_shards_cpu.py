@@ -175,3 +175,18 @@ def test_main_with_shards_end_to_end(tmp_path):
                 "--image-size", "32", "--num-classes", "3", "--batchsize", "4", "--epochs", "1", "--out-dir", out,
                 "--device", "cpu", "--log-interval", "100", "--loader-threads", "2"])
     assert os.path.exists(os.path.join(out, "last.pth"))
+
+
+def test_shard_loader_abandoned_epoch_then_new_epoch(shard):
+    """Breaking out of an epoch joins the in-flight gathers; the next epoch starts clean."""
+    p, imgs = shard
+    sampler = ShardSampler(list(range(37)), num_replicas=1, rank=0, shuffle=True, seed=1)
+    ld = ShardLoader(p, batch_size=4, sampler=sampler, aug=None, out_size=16, device="cpu", threads=4, prefetch=3,
+                     return_index=True)
+    for i, _ in enumerate(ld):
+        if i == 1:
+            break
+    ld.set_epoch(1)
+    seen = [j for _, _, idx in ld for j in idx.tolist()]
+    assert seen == list(sampler)
+    ld.close()
