@@ -241,6 +241,24 @@ __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict
     const int i = (int)(q % (uint32_t)Ho);
     const size_t n = q / (uint32_t)Ho;
     bf16 o[OC];
+    if (S == 2 && is_u8 && nchw && (W & 1) == 0) {
+      // uint8 NCHW (the benchmark / ToTensor layout): the two horizontal taps of a channel row
+      // are adjacent bytes -- one 2-byte load each instead of two byte loads
+#pragma unroll
+      for (int c = 0; c < CQ; ++c)
+#pragma unroll
+        for (int py = 0; py < S; ++py) {
+          float v0 = 0.f, v1 = 0.f;
+          if (c < C) {
+            const size_t si = ((n * C + c) * H + (size_t)i * S + py) * W + (size_t)j * S;
+            const uint16_t two = *(const uint16_t*)((const uint8_t*)src + si);
+            v0 = ((float)(two & 0xff) * in_scale - mu[c]) * is[c];
+            v1 = ((float)(two >> 8) * in_scale - mu[c]) * is[c];
+          }
+          o[(py * S + 0) * CQ + c] = f2bf(v0);
+          o[(py * S + 1) * CQ + c] = f2bf(v1);
+        }
+    } else
 #pragma unroll
     for (int py = 0; py < S; ++py)
 #pragma unroll
