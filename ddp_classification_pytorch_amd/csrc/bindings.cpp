@@ -259,7 +259,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
 std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int64_t pad, const optional<Tensor>& add,
                                          const Tensor& y, const optional<Tensor>& res, const Tensor& scale,
                                          const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act,
-                                         const optional<Tensor>& mask) {
+                                         const optional<Tensor>& mask, double slope) {
   CHECK_ACT(dy);
   CHECK_ACT(wt);
   CHECK_ACT(y);
@@ -270,7 +270,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(3) == C, "conv_dgrad_bn: BN input shape");
   const int H = y.size(1), W = y.size(2);
   TORCH_CHECK(H + 2 * pad - KH + 1 == Ho && W + 2 * pad - KW + 1 == Wo, "conv_dgrad_bn: stride-1 geometry");
-  TORCH_CHECK(act == 0 || act == 1, "conv_dgrad_bn: act must be none or ReLU");
+  TORCH_CHECK(act == 0 || act == 1 || act == 2, "conv_dgrad_bn: act must be none, ReLU or leaky ReLU");
+  TORCH_CHECK(act != 2 || (!mask.has_value() && !res.has_value()), "conv_dgrad_bn: leaky path has no mask / residual");
   for (const Tensor* t : {&scale, &shift, &mean, &invstd}) {
     CHECK_DEV(*t);
     CHECK_F32(*t);
@@ -314,7 +315,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
       t.widx[i] = i;
     }
   dcp::BnBwdEpi e{bp(y), resp, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
-                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act, maskp};
+                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act, maskp, (float)slope};
   auto st = cur_stream();
   dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr, nullptr,
                        0, zero_page(dy.get_device()), st, addp, &e);
@@ -1203,7 +1204,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("conv_dgrad(Tensor dy, Tensor wt, int H, int W, int stride, int pad, Tensor? add=None) -> Tensor", &conv_dgrad);
   m.def(
       "conv_dgrad_bn(Tensor dy, Tensor wt, int pad, Tensor? add, Tensor y, Tensor? res, Tensor scale, Tensor shift, "
-      "Tensor mean, Tensor invstd, int act, Tensor? mask=None) -> (Tensor, Tensor)",
+      "Tensor mean, Tensor invstd, int act, Tensor? mask=None, float slope=0.0) -> (Tensor, Tensor)",
       &conv_dgrad_bn);
   m.def("conv_wgrad(Tensor dy, Tensor x, int KH, int KW, int stride, int pad) -> Tensor", &conv_wgrad);
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, int act) -> Tensor", &linear_fwd);

@@ -549,15 +549,17 @@ tap_gemm_kernel(const TapGemmParams p) {
             float g = bf2f(v[e]);
             if (has_add) g = bf2f(f2bf(g + bf2f(av[q][e])));  // the rounding of the unfused add
             const float yf = bf2f(yv[q][e]);
+            float gd = 1.f;  // act'(z) for the leaky sums (the stored gradient stays raw)
             if (MASKED) {
               if (p.bnb.act == 1 && !((mk[q] >> e) & 1u)) g = 0.f;
             } else {
               float z = yf * sc[e] + sh[e];
               if (has_res) z += bf2f(rv[q][e]);
               if (p.bnb.act == 1 && !(z > 0.f)) g = 0.f;
+              if (p.bnb.act == 2 && !(z >= 0.f)) gd = p.bnb.slope;  // act_d's leaky convention (bn.hip)
             }
             o[e] = f2bf(g);
-            const float gr = bf2f(o[e]);
+            const float gr = bf2f(o[e]) * gd;
             s1[e] += gr;
             s2[e] += gr * (yf - mu[e]);
           }
@@ -1361,7 +1363,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb) {
   TapGemmParams p;
   p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
-  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0.f};
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
   p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;

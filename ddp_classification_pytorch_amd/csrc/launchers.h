@@ -38,8 +38,9 @@ struct BnBwdEpi {
   const float* mean;
   const float* invstd;
   float* part;          // [ceil(M/128)][2][C]
-  int act;              // 0 none, 1 ReLU
+  int act;              // 0 none, 1 ReLU (gradient stored masked), 2 leaky ReLU (stored RAW, summed masked)
   const uint8_t* mask;  // act'(z) > 0 as bits [M][C/8] (bn_act's mask output), or nullptr: recompute z
+  float slope;          // leaky slope (act 2)
 };
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,

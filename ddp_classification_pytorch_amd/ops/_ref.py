@@ -66,9 +66,11 @@ def unpack_mask(mask):
     return bits.reshape(*mask.shape[:-1], mask.shape[-1] * 8).float()
 
 
-def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act, mask=None):
+def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act, mask=None, slope=0.0):
     """Stride-1 dgrad + the backward reduction of the BN(+act)(+res) layer producing its input:
-    -> (activation-masked gradient g', [2, C] = (sum g', sum g' * xhat)).  ``mask``: the
+    -> (gradient, [2, C] = (sum g', sum g' * xhat)) with g' = act'(z) * dgrad.  ReLU / identity
+    return g' itself (masking is idempotent); leaky ReLU returns the RAW dgrad (its BN backward
+    re-applies act', so any other consumer's gradient can still be added).  ``mask``: the
     activation mask bits from :func:`bn_act_mask` (then ``res`` is not read)."""
     g = conv_dgrad(dy, wt, y.shape[1], y.shape[2], 1, pad, add)
     if mask is not None:
@@ -77,11 +79,16 @@ def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act, mas
         z = _f(y) * scale + shift
         if res is not None:
             z = z + _f(res)
-        d = _act_d(z, act, 0.0)
-    gm = (_f(g) * d).to(dy.dtype)
+        d = _act_d(z, act, slope)
+    if act == ACT_LEAKY:
+        gm = _f(g.to(dy.dtype)) * d
+        out = g.to(dy.dtype)
+    else:
+        out = (_f(g) * d).to(dy.dtype)
+        gm = _f(out)
     xh = (_rows(y) - mean) * invstd
     gr = _rows(gm)
-    return gm, torch.stack([gr.sum(0), (gr * xh).sum(0)])
+    return out, torch.stack([gr.sum(0), (gr * xh).sum(0)])
 
 
 def _pad_geo(xc, KH, KW, stride, pad, Ho, Wo):

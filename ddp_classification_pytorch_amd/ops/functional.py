@@ -229,10 +229,12 @@ class BNSource:
     from accumulating another consumer's gradient into that buffer in place; the BN
     backward uses the fused result only if it receives exactly that buffer."""
 
-    __slots__ = ("tensors", "act", "fused")
+    __slots__ = ("tensors", "act", "slope", "fused")
 
-    def __init__(self, act: int):
-        self.tensors, self.act, self.fused = None, act, None
+    def __init__(self, act: int, slope: float = 0.0):
+        # leaky ReLU (act 2): the conv returns the RAW gradient and only its sums are masked, so
+        # the BN backward re-applies act' and another consumer's gradient can still be added
+        self.tensors, self.act, self.slope, self.fused = None, act, float(slope), None
 
     def release(self):
         self.tensors = self.fused = None
@@ -293,7 +295,8 @@ class _Conv2d(Function):
                 y, res, scale, shift, mean, invstd, mask = src.tensors
                 if mask is not None:
                     res = None  # the activation mask bits replace the residual read
-                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act, mask)
+                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act, mask,
+                                           src.slope)
                 src.fused = (dx, sums)
             elif add is not None:
                 dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add)
@@ -496,8 +499,10 @@ class _BNAct(Function):
             if cfg.group is not None:
                 sums = local.clone()
                 dist.all_reduce(sums, group=cfg.group)
-            dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
-                                   False)
+            # ReLU / identity: g is already masked; leaky: g is raw and the elementwise pass applies act'
+            post_act = cfg.act if cfg.act == 2 else 0
+            dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), post_act,
+                                   cfg.slope, False)
             dres = g if want_dres else None
         else:
             need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
@@ -664,8 +669,9 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    if training_stats and cfg.act in (0, 1) and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
-        src = BNSource(cfg.act)
+    fusable = cfg.act in (0, 1) or (cfg.act == 2 and residual is None)
+    if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
+        src = BNSource(cfg.act, cfg.slope)
     out = _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link, src)
     if src is not None:
         out._dcp_bnsrc = src

@@ -205,3 +205,37 @@ def test_resnext_grouped_dgrad_fuses_bn_backward(monkeypatch):
     assert len(calls) == 13
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+
+
+def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
+    """TResNet's leaky-ReLU BNs (InplaceABN) fuse their backward reduction into the consuming
+    conv's dgrad (raw gradient returned, masked sums): gradients equal the unfused path."""
+    calls = []
+    orig = _ref.conv_dgrad_bn
+
+    def counting(*a, **k):
+        if a[10] == 2:
+            calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(_ref, "conv_dgrad_bn", counting)
+    out = []
+    for fuse in (True, False):
+        Fn.set_bn_backward_fusion(fuse)
+        try:
+            torch.manual_seed(5)
+            m = build_model("tresnet_m", num_classes=10)
+            g = torch.Generator().manual_seed(2)
+            imgs = torch.rand(2, 3, 64, 64, generator=g)
+            labels = torch.randint(0, 10, (2,), generator=g)
+            loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, cpad=3, nchw=True)), labels)
+            loss.backward()
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters()])))
+        finally:
+            Fn.set_bn_backward_fusion(True)
+        if fuse:
+            n_leaky = len(calls)
+    assert n_leaky > 10
+    (l1, g1), (l0, g0) = out
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5

@@ -934,3 +934,25 @@ def test_colsum(K, M, C):
     x = rnd(M, C)
     out = K.colsum(x.to(DEV))
     assert relerr(out, x.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("k,add", [(3, False), (1, True), (3, True)])
+def test_conv_dgrad_bn_leaky(K, k, add):
+    """Leaky-ReLU BN fused into the dgrad epilogue: raw gradient stored, masked sums."""
+    torch.manual_seed(13)
+    N, H, Ci, Co = 2, 14, 64, 128
+    pad = k // 2
+    dy = rnd(N, H, H, Co)
+    w = torch.randn(Co, k, k, Ci) / math.sqrt(k * k * Co)
+    _, wt = K.weight_prep(w.to(DEV), 0, True)
+    y = rnd(N, H, H, Ci, scale=2.0)
+    a = rnd(N, H, H, Ci) if add else None
+    scale, shift = torch.rand(Ci) + 0.5, torch.randn(Ci) * 0.3
+    mean, invstd = torch.randn(Ci) * 0.2, torch.rand(Ci) + 0.5
+    d = lambda t: t.to(DEV) if t is not None else None
+    g, s = K.conv_dgrad_bn(d(dy), wt, pad, d(a), d(y), None, d(scale), d(shift), d(mean), d(invstd), 2, None, 1e-3)
+    wtr = _ref.weight_prep(w.bfloat16().float(), 0, True)[1]
+    gr, sr = _ref.conv_dgrad_bn(dy.float(), wtr, pad, None if a is None else a.float(), y.float(), None, scale, shift,
+                                mean, invstd, 2, None, 1e-3)
+    assert relerr(g, gr) < 1e-2
+    assert relerr(s, sr) < 2e-2
