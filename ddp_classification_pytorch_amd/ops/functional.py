@@ -243,6 +243,16 @@ class BNSource:
 _FUSE_BN_BWD = [True]
 
 
+# Leaky-ReLU BNs through the fused dgrad epilogue: measured a net loss on TResNet-M at b1024
+# (the EPI-3 dgrads grew by 2.1 ms/step, the reduction passes they replace took 1.5 ms), so off
+# by default; kept selectable for A/B runs and tested.
+_FUSE_LEAKY = [False]
+
+
+def set_leaky_bn_backward_fusion(enabled: bool):
+    _FUSE_LEAKY[0] = bool(enabled)
+
+
 _FUSE_SHORTCUT_BN = [True]
 
 
@@ -669,7 +679,7 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    fusable = cfg.act in (0, 1) or (cfg.act == 2 and residual is None)
+    fusable = cfg.act in (0, 1) or (cfg.act == 2 and residual is None and _FUSE_LEAKY[0])
     if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
         src = BNSource(cfg.act, cfg.slope)
     out = _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link, src)

@@ -219,6 +219,7 @@ def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(_ref, "conv_dgrad_bn", counting)
+    Fn.set_leaky_bn_backward_fusion(True)  # opt-in (measured slower on the GPU)
     out = []
     for fuse in (True, False):
         Fn.set_bn_backward_fusion(fuse)
@@ -235,6 +236,7 @@ def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
             Fn.set_bn_backward_fusion(True)
         if fuse:
             n_leaky = len(calls)
+    Fn.set_leaky_bn_backward_fusion(False)
     assert n_leaky > 10
     (l1, g1), (l0, g0) = out
     assert abs(l1 - l0) < 1e-6
