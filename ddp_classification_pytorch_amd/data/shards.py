@@ -22,7 +22,7 @@ Shard file (little-endian)::
     Header (48 B)   magic "DCPSHRD1", u32 version=1, u32 channels=3, u64 count,
                     u64 index_off, u64 data_off, u64 max_bytes
     Index           count x {u64 offset (from data_off), u32 h, u32 w, i64 label}
-    Data            records, h*w*3 uint8 each (HWC, RGB)
+    Data            records, h*w*3 uint8 each (HWC, RGB), then zero padding to 8 bytes
 
 Differences from the PIL pipeline (documented, not hidden): the resample is plain bilinear on
 the stored (short_side-resized) image, without PIL's antialiasing filter on downscales, and
@@ -67,7 +67,9 @@ def write_shard(path: str, samples) -> int:
             off += a.nbytes
             max_bytes = max(max_bytes, a.nbytes)
         data_off = _HDR.size
-        index_off = data_off + off
+        pad = (-(data_off + off)) % 8  # 8-byte aligned index (the records themselves are byte data)
+        f.write(b"\0" * pad)
+        index_off = data_off + off + pad
         idx = np.array(index, dtype=_IDX) if index else np.zeros(0, dtype=_IDX)
         f.write(idx.tobytes())
         f.seek(0)
