@@ -12,6 +12,7 @@ version and cached on the parameter.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import weakref
@@ -247,6 +248,9 @@ _FUSE_BN_BWD = [True]
 # (the EPI-3 dgrads grew by 2.1 ms/step, the reduction passes they replace took 1.5 ms), so off
 # by default; kept selectable for A/B runs and tested.
 _FUSE_LEAKY = [False]
+# A/B: DCP_BN_FUSE=masked keeps the dgrad-epilogue fusion only for BN + residual + ReLU layers
+# (activation mask bits, EPI 4) and runs the plain BN + ReLU layers' reductions as separate passes
+_FUSE_PLAIN = [os.environ.get("DCP_BN_FUSE", "all") != "masked"]
 
 
 def set_leaky_bn_backward_fusion(enabled: bool):
@@ -679,7 +683,8 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    fusable = cfg.act in (0, 1) or (cfg.act == 2 and residual is None and _FUSE_LEAKY[0])
+    fusable = (cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0])) or \
+        (cfg.act == 2 and residual is None and _FUSE_LEAKY[0])
     if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
         src = BNSource(cfg.act, cfg.slope)
     out = _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link, src)
