@@ -248,9 +248,15 @@ _FUSE_BN_BWD = [True]
 # (the EPI-3 dgrads grew by 2.1 ms/step, the reduction passes they replace took 1.5 ms), so off
 # by default; kept selectable for A/B runs and tested.
 _FUSE_LEAKY = [False]
-# A/B: DCP_BN_FUSE=masked keeps the dgrad-epilogue fusion only for BN + residual + ReLU layers
-# (activation mask bits, EPI 4) and runs the plain BN + ReLU layers' reductions as separate passes
-_FUSE_PLAIN = [os.environ.get("DCP_BN_FUSE", "all") != "masked"]
+# The dgrad-epilogue BN fusion is used for BN + residual + ReLU layers (activation mask bits,
+# EPI 4).  For the plain BN + ReLU layers (mask recomputed from the BN input, EPI 3) the separate
+# reduction pass measured faster: ResNet-50 b1024 14,240 vs 14,170 img/s over two back-to-back
+# A/B pairs (`DCP_BN_FUSE=all` restores it; profiles/meas_r2c/bn_fuse_ab.txt).
+_FUSE_PLAIN = [os.environ.get("DCP_BN_FUSE", "masked") == "all"]
+
+
+def set_plain_bn_backward_fusion(enabled: bool):
+    _FUSE_PLAIN[0] = bool(enabled)
 
 
 def set_leaky_bn_backward_fusion(enabled: bool):

@@ -10,6 +10,14 @@ from ddp_classification_pytorch_amd.ops import _ref
 from ddp_classification_pytorch_amd.ops import functional as Fn
 
 
+@pytest.fixture(autouse=True)
+def _plain_fusion_on():
+    """Exercise the plain BN+ReLU epilogue fusion too (off by default: measured slower)."""
+    Fn.set_plain_bn_backward_fusion(True)
+    yield
+    Fn.set_plain_bn_backward_fusion(False)
+
+
 def _grads(name, fuse, size=32, seed=0):
     Fn.set_bn_backward_fusion(fuse)
     try:
@@ -239,5 +247,20 @@ def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
     Fn.set_leaky_bn_backward_fusion(False)
     assert n_leaky > 10
     (l1, g1), (l0, g0) = out
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+
+
+
+def test_default_fuses_only_masked_layers(monkeypatch):
+    """Default (plain fusion off): only the BN + residual + ReLU layers fuse (ResNet-50: conv1 of
+    the 15 blocks after the first), and gradients still equal the unfused path."""
+    Fn.set_plain_bn_backward_fusion(False)
+    calls = []
+    orig = _ref.conv_dgrad_bn
+    monkeypatch.setattr(_ref, "conv_dgrad_bn", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    l1, g1 = _grads("resnet50", True)
+    assert len(calls) == 15
+    l0, g0 = _grads("resnet50", False)
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
