@@ -241,7 +241,7 @@ class BNSource:
         self.tensors = self.fused = None
 
 
-_FUSE_BN_BWD = [True]
+_FUSE_BN_BWD = [os.environ.get("DCP_BN_FUSE", "masked") != "none"]
 
 
 # Leaky-ReLU BNs through the fused dgrad epilogue: measured a net loss on TResNet-M at b1024
