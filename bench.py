@@ -11,14 +11,23 @@ N > 1), fused SGD-momentum step.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+``--gpus N`` without a torchrun environment launches the N ranks itself (a
+``torch.distributed.run`` child process, started before anything touches the GPU);
+under torchrun ``--gpus`` must equal WORLD_SIZE.
+
 Rank 0 prints ONE JSON line; `value` = total images/s over all ranks, timed
-as the MAX over ranks of K steps bracketed by barrier + device sync.
+as the MAX over ranks of K steps bracketed by barrier + device sync.  With N > 1 a
+second timed phase of the same K steps runs the reference's cross-replica BN
+(SyncBN on its own RCCL communicator) and reports it as ``syncbn_value``; the
+headline ``value`` is local BN (per-GPU batch 1024).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,7 +49,8 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); launched here when no torchrun environment is set")
     ap.add_argument("--config", default="r50", choices=["r50", "arcface", "resnext", "r101", "tresnet"],
                     help="BASELINE.json config: r50 (headline), arcface (R50+ArcFace 10k cls @112), "
                          "resnext (ResNeXt-50 32x4d), r101 (ResNet-101 large batch), tresnet (BASELINE default)")
@@ -50,7 +60,10 @@ def parse(argv=None):
     ap.add_argument("--model", default=None)
     ap.add_argument("--image-size", type=int, default=None)
     ap.add_argument("--num-classes", type=int, default=None)
-    ap.add_argument("--syncbn", action="store_true", help="cross-replica BN (reference default); off = local BN")
+    ap.add_argument("--syncbn", action="store_true",
+                    help="headline phase with cross-replica BN (reference default); off = local BN")
+    ap.add_argument("--no-syncbn-phase", dest="syncbn_phase", action="store_false",
+                    help="N > 1: skip the second, SyncBN-timed phase")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="DDP gradient all-reduce precision (bf16 = bf16_compress_hook: half the xGMI bytes)")
@@ -93,14 +106,45 @@ def build_bench_model(a):
     return build_model(a.model, num_classes=a.num_classes)
 
 
+def rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n, argv):
+    """Run this script as N torchrun ranks in a child process and return its exit code.  Called
+    before any GPU work in this process (the parent never initialises HIP, and never execs)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(self_launch(a.gpus, argv))
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
     # one rank per GPU over RCCL ("nccl" on ROCm).  DCP_DIST_BACKEND=gloo lets tests run
     # several ranks on one GPU (RCCL refuses duplicate devices).
     backend = os.environ.get("DCP_DIST_BACKEND", "nccl")
@@ -125,6 +169,8 @@ def main(argv=None):
     model = build_bench_model(a).to(dev)
     if world > 1:
         model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb)
+        # created collectively now (every rank, same order) so the SyncBN phase can switch to it
+        bn_group = pddp.bn_process_group()
         if a.grad_comm == "bf16":
             from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
 
@@ -163,30 +209,51 @@ def main(argv=None):
     else:
         for _ in range(a.warmup):
             loss = step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+
+    def timed(n_steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            out = run()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, out
+
+    def gather_max(dt):
+        """(max over ranks, every rank's seconds)"""
+        if world == 1:
+            return dt, [dt]
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per = [float(v.item()) for v in allt]
+        return max(per), per
+
     prof = None
     if a.profile_dir and rank == 0:
         prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
                                                   torch.profiler.ProfilerActivity.CUDA])
         prof.__enter__()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss = run()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt, loss = timed(a.steps)
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(a.profile_dir, exist_ok=True)
         with open(os.path.join(a.profile_dir, "bench_profile.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt, per_rank = gather_max(dt)
+    sync = None
+    if world > 1 and not a.syncbn and a.syncbn_phase and not a.graph:
+        # second phase: the reference's SyncBN (BASELINE/main.py:148) on the dedicated BN communicator
+        pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group)
+        for _ in range(2):
+            run()
+        sdt, _ = timed(a.steps)
+        sdt, sper = gather_max(sdt)
+        sync = {"value": round(B * world * a.steps / sdt, 2), "ms_per_step": round(sdt / a.steps * 1000.0, 3),
+                "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in sper]}
     loss_v = float(loss.item())
     ms = dt / a.steps * 1000.0
     ips = B * world * a.steps / dt
@@ -204,6 +271,12 @@ def main(argv=None):
             "vs_baseline": None,  # the reference publishes no throughput
             "dtype": "bf16",
             "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
+            "dist_backend": (dist.get_backend() if world > 1 else None),
+            "world_size": (dist.get_world_size() if world > 1 else 1),
+            "rccl_version": rccl_version(),
+            "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
+            "syncbn_value": sync["value"] if sync else None,
+            "syncbn_ms_per_step": sync["ms_per_step"] if sync else None,
             "config": {
                 "model": a.model,
                 "global_batch": B * world,

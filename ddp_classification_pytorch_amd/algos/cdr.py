@@ -28,16 +28,30 @@ def _selected(params: Iterable[torch.Tensor]):
     return [p for p in params if p.grad is not None and p.dim() in (2, 4)]
 
 
+_TABLES = {}
+
+
 def _table(ps, device):
+    """Device (param, grad) pointer table + chunk list, cached per pointer set.  Built with
+    ``Fn.table_to_device`` (values in a fill kernel's arguments, no host->device copy), so a step
+    captured into a HIP graph (``--graph``) replays it correctly."""
+    from ..ops import functional as Fn
+
     entries, chunks = [], []
     for i, p in enumerate(ps):
         if not (p.is_contiguous() and p.grad.is_contiguous() and p.dtype == torch.float32):
             raise RuntimeError("CDR kernels need contiguous fp32 params/grads")
         entries.append((p.data_ptr(), p.grad.data_ptr(), 0, 0, 0, p.numel()))
-        chunks.extend((i, c) for c in range((p.numel() + CHUNK - 1) // CHUNK))
-    tab = torch.tensor(entries, dtype=torch.int64).view(-1, 6).to(device, non_blocking=True)
-    ch = torch.tensor(chunks, dtype=torch.int32).view(-1, 2).to(device, non_blocking=True)
-    return tab, ch
+    key = (str(device), tuple(entries))
+    hit = _TABLES.get(key)
+    if hit is None:
+        for i, p in enumerate(ps):
+            chunks.extend((i, c) for c in range((p.numel() + CHUNK - 1) // CHUNK))
+        if len(_TABLES) > 8:
+            _TABLES.clear()
+        hit = _TABLES[key] = (Fn.table_to_device(entries, torch.int64, device).view(-1, 6),
+                              Fn.table_to_device(chunks, torch.int32, device).view(-1, 2))
+    return hit
 
 
 @torch.no_grad()
@@ -55,8 +69,11 @@ def cdr_mask_gradients(params: Iterable[torch.Tensor], nonzero_ratio: float, cli
         return torch.tensor(float("inf"), device=dev)
     if ps[0].is_cuda:
         K = _ext.hip_ops()
+        from ..ops import functional as Fn
+
         tab, ch = _table(ps, dev)
-        state = torch.tensor([0, 0, nz, 0], dtype=torch.int32).to(dev, non_blocking=True)
+        # fresh every step (the select passes rewrite it): a fill kernel, so a graph replay resets it
+        state = Fn.table_to_device([0, 0, nz, 0], torch.int32, dev)
         thr = K.cdr_threshold(tab, ch, state)
         K.cdr_mask(tab, ch, state, float(clip))
         return thr.reshape(())

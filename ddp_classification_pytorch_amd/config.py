@@ -91,7 +91,11 @@ def build_parser() -> argparse.ArgumentParser:
     a("--max-steps-per-epoch", type=int, default=None, help="truncate epochs (smoke runs)")
     a("--eval-every", type=int, default=1)
     a("--fail-at-step", type=int, default=None, help="fault injection: raise at this global step")
-    a("--profile", action="store_true", help="torch.profiler trace of a few steps into out-dir")
+    a("--auto-resume", dest="auto_resume", action="store_true",
+      help="resume from <out-dir>/last.pth when it exists (restart after a failure)")
+    a("--heartbeat-every", dest="heartbeat_every", type=int, default=0,
+      help="every N steps append a line to <out-dir>/heartbeat_rank<r>.txt")
+    a("--profile", action="store_true", help="torch.profiler (roctracer) trace of 4 steps into <out-dir>/profile")
     # ARCFACE
     a("--s", "--arc-s", dest="arc_s", type=float, default=30.0)
     a("--m", "--arc-m", dest="arc_m", type=float, default=0.5)

@@ -1135,11 +1135,19 @@ void mt_sgd(const Tensor& table, const Tensor& chunks, double lr, double momentu
                      reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0), h, cur_stream());
 }
 
+// step_dev (optional int32[1] on the device): the step count the bias corrections use, read by
+// the kernel -- a HIP-graph replay then applies the current step's correction, not the captured one
 void mt_adam(const Tensor& table, const Tensor& chunks, double lr, double beta1, double beta2, double eps, double wd,
-             int64_t step, bool decoupled, double grad_scale) {
+             int64_t step, bool decoupled, double grad_scale, const c10::optional<Tensor>& step_dev) {
   CHECK_DEV(table);
   CHECK_DEV(chunks);
   dcp::AdamHyper h;
+  h.step_dev = nullptr;
+  if (step_dev.has_value() && step_dev->defined()) {
+    CHECK_DEV((*step_dev));
+    TORCH_CHECK(step_dev->scalar_type() == at::kInt && step_dev->numel() == 1, "mt_adam: step_dev int32[1]");
+    h.step_dev = step_dev->data_ptr<int>();
+  }
   h.lr = lr;
   h.beta1 = beta1;
   h.beta2 = beta2;
@@ -1311,7 +1319,7 @@ TORCH_LIBRARY(dcp, m) {
       &mt_sgd);
   m.def(
       "mt_adam(Tensor table, Tensor chunks, float lr, float beta1, float beta2, float eps, float wd, int step, bool "
-      "decoupled, float grad_scale) -> ()",
+      "decoupled, float grad_scale, Tensor? step_dev=None) -> ()",
       &mt_adam);
   m.def("cdr_threshold(Tensor table, Tensor chunks, Tensor state) -> Tensor", &cdr_threshold);
   m.def("cdr_mask(Tensor table, Tensor chunks, Tensor state, float clip) -> ()", &cdr_mask);

@@ -629,15 +629,15 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int m = m0 + pl;
         const bf16x8 v = vv[k];
         if (m < p.M && cok) {
-          uint32_t drow;
+          size_t drow;  // element offsets pass 2^32 at large batch (56x56x256 rows: N > 5,350)
           if (p.ds == 1) {
-            drow = (uint32_t)m * (uint32_t)p.Co;
+            drow = (size_t)m * (size_t)p.Co;
           } else {
             const uint32_t q = fdiv(m, p.div_wy);
             const uint32_t x = m - q * p.Wy;
             const uint32_t n = fdiv(q, p.div_hy);
             const uint32_t y = q - n * p.Hy;
-            drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+            drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
           }
           bf16x8 o = v;
           if (p.addsrc) {
@@ -659,13 +659,13 @@ tap_gemm_kernel(const TapGemmParams p) {
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     const bool mok = m < p.M;
-    uint32_t drow = 0;
+    size_t drow = 0;
     if (mok) {
       const uint32_t q = fdiv(m, p.div_wy);
       const uint32_t x = m - q * p.Wy;
       const uint32_t n = fdiv(q, p.div_hy);
       const uint32_t y = q - n * p.Hy;
-      drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+      drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -852,15 +852,15 @@ tap_gemm8_kernel(const TapGemmParams p) {
       const int m = m0 + pl;
       const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
       if (m < p.M && cok) {
-        uint32_t drow;
+        size_t drow;
         if (p.ds == 1) {
-          drow = (uint32_t)m * (uint32_t)p.Co;
+          drow = (size_t)m * (size_t)p.Co;
         } else {
           const uint32_t q = fdiv(m, p.div_wy);
           const uint32_t x = m - q * p.Wy;
           const uint32_t n = fdiv(q, p.div_hy);
           const uint32_t y = q - n * p.Hy;
-          drow = ((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (uint32_t)p.Co;
+          drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
         }
         bf16x8 o = v;
         if (p.addsrc) {

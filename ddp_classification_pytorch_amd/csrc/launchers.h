@@ -195,6 +195,7 @@ struct SgdHyper {
 struct AdamHyper {
   float lr, beta1, beta2, eps, wd, grad_scale, bc1, bc2;
   int decoupled;
+  const int* step_dev;  // optional device step count: bc1/bc2 computed in-kernel from it
 };
 void launch_mt_sgd(const MTEntry* tab, const int2* chunks, int nchunks, SgdHyper h, hipStream_t s);
 void launch_mt_adam(const MTEntry* tab, const int2* chunks, int nchunks, AdamHyper h, hipStream_t s);

@@ -55,7 +55,13 @@ __global__ void __launch_bounds__(256) mt_adam_kernel(const MTEntry* __restrict_
   const MTEntry e = tab[ck.x];
   const int64_t base = (int64_t)ck.y * kChunk;
   const int64_t end = min(e.n, base + kChunk);
-  const float rbc2 = 1.f / sqrtf(h.bc2);
+  float bc1 = h.bc1, bc2 = h.bc2;
+  if (h.step_dev) {  // 1 - beta^t without the cancellation of 1 - powf
+    const float t = (float)*h.step_dev;
+    bc1 = -expm1f(t * log1pf(-h.beta1));
+    bc2 = -expm1f(t * log1pf(-h.beta2));
+  }
+  const float rbc2 = 1.f / sqrtf(bc2);
   for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
     float g = e.g[i] * h.grad_scale;
     float p = e.p[i];
@@ -70,7 +76,7 @@ __global__ void __launch_bounds__(256) mt_adam_kernel(const MTEntry* __restrict_
     e.s1[i] = m;
     e.s2[i] = v;
     const float denom = sqrtf(v) * rbc2 + h.eps;
-    p -= (h.lr / h.bc1) * m / denom;
+    p -= (h.lr / bc1) * m / denom;
     e.p[i] = p;
     if (e.shadow) e.shadow[i] = f2bf(p);
   }

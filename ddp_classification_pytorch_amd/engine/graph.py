@@ -13,6 +13,12 @@ Constraints (checked or documented): inputs and labels must live in the static t
 step closes over (copy new batches into them); hyper-parameters baked into kernel arguments
 (the learning rate) are those at capture time -- recapture after changing them; single
 process (DDP's reducer hooks are not captured here).
+
+Host-side counters: a replay runs no Python, so counters the step advances on the host --
+BatchNorm2d's pending ``num_batches_tracked`` and FusedAdam's ``state["step"]`` -- would
+freeze at their capture-time values.  :class:`HostCounters` records what the captured call
+advanced and re-applies it after every replay (Adam's bias correction itself reads a device
+counter the captured step increments, optim/fused.py).
 """
 from __future__ import annotations
 
@@ -29,12 +35,34 @@ def _stale_weights():
     Fn.bump_weight_generation()
 
 
+class HostCounters:
+    """Per-replay host bookkeeping of a captured step: the BN ``_nbt_pending`` increments the
+    capture recorded (module by module) plus each optimizer's ``on_graph_replay`` hook."""
+
+    def __init__(self, modules=(), optimizers=()):
+        self.bns = [m for r in modules for m in r.modules() if hasattr(m, "_nbt_pending")]
+        self.opts = [o for o in optimizers if hasattr(o, "on_graph_replay")]
+        self.before = self.delta = None
+
+    def begin_capture(self):
+        self.before = [m._nbt_pending for m in self.bns]
+
+    def end_capture(self):
+        self.delta = [m._nbt_pending - b for m, b in zip(self.bns, self.before)]
+
+    def replayed(self):
+        for m, d in zip(self.bns, self.delta or ()):
+            m._nbt_pending += d
+        for o in self.opts:
+            o.on_graph_replay()
+
+
 class GraphedStep:
     """``GraphedStep(step_fn, warmup=3)``: runs ``step_fn`` ``warmup`` times on a side stream
     (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
     returns the captured step's output tensors (overwritten by every replay)."""
 
-    def __init__(self, step_fn, warmup: int = 3, device=None):
+    def __init__(self, step_fn, warmup: int = 3, device=None, counters: HostCounters = None):
         if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:
             raise RuntimeError("GraphedStep captures single-process steps (DDP reducer hooks are not graph-safe)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -46,12 +74,22 @@ class GraphedStep:
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
         _stale_weights()
+        self.counters = counters
+        if counters is not None:
+            counters.begin_capture()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn()
+        if counters is not None:
+            counters.end_capture()
+        self.replays = 0
 
     def __call__(self):
         self.graph.replay()
+        # the first replay executes the step whose host side effects the capture already made
+        if self.replays and self.counters is not None:
+            self.counters.replayed()
+        self.replays += 1
         return self.out
 
 
@@ -64,10 +102,11 @@ class StepGrapher:
     the captured kernels' arguments (the learning rate at an epoch boundary): the next call
     recaptures.  Every step -- eager, captured or replayed -- trains on exactly one batch."""
 
-    def __init__(self, step_fn, warmup: int = 2):
+    def __init__(self, step_fn, warmup: int = 2, counters: HostCounters = None):
         self.fn, self.warmup, self.calls = step_fn, max(1, warmup), 0
         self.graph = self.static = self.out = None
         self.captures = 0
+        self.counters = counters
 
     def reset(self):
         self.graph = self.static = self.out = None
@@ -92,12 +131,18 @@ class StepGrapher:
             torch.cuda.synchronize()
             _stale_weights()
             self.static = [t.clone() for t in tensors]
+            if self.counters is not None:
+                self.counters.begin_capture()
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self.out = self.fn(*self.static)
+            if self.counters is not None:
+                self.counters.end_capture()
             self.captures += 1
         else:
             for s, t in zip(self.static, tensors):
                 s.copy_(t, non_blocking=True)
+            if self.counters is not None:
+                self.counters.replayed()  # the capture call itself made the first replay's host effects
         self.graph.replay()
         return self.out

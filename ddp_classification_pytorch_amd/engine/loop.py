@@ -11,7 +11,16 @@ Differences from the reference, all deliberate:
 * ``set_epoch`` is always called (ARCFACE forgets it);
 * checkpoints are state_dicts written once by rank 0 (``last.pth`` /
   ``best.pth``) and ``--resume`` restores model/optimizer/scheduler/epoch/RNG;
-* ``--fail-at-step`` injects a failure for resume testing.
+* ``--fail-at-step`` injects a failure for resume testing; ``--auto-resume``
+  restarts from ``last.pth`` when it exists (a relaunch after a failure continues);
+* ``--warmup-iters`` ramps the learning rate linearly per iteration from 1e-6
+  (BASELINE ``WarmUp``, BASELINE/main.py:170-197; dead code in the reference,
+  wired here for every workload that goes through this loop);
+* GPU step time from HIP events (``gpu_ms_per_step`` in the JSONL log, no host
+  sync beyond the log interval's), a per-rank heartbeat file
+  (``heartbeat_rank<r>.txt``: wall time, step, loss every ``--heartbeat-every``
+  steps, so a hung or dead rank is visible), and ``--profile``: a torch.profiler
+  (roctracer) trace of a few steps of the first epoch into ``<out-dir>/profile``.
 """
 from __future__ import annotations
 
@@ -22,6 +31,7 @@ import time
 import torch
 import torch.distributed as dist
 
+from ..optim.schedulers import LinearWarmup
 from .checkpoint import load_checkpoint, save_checkpoint
 from .logger import MetricsLogger
 
@@ -59,6 +69,7 @@ class ClassificationLoop:
         self.scheduler_before_epoch = scheduler_before_epoch  # CDR steps its scheduler before training (:365-366)
         self.train_modules = train_modules or list(models.values())
         self.start_epoch, self.global_step, self.best = 0, 0, -1.0
+        self.warmup = None
 
     # ------------------------------------------------------------------ persistence
     def _ckpt(self, name):
@@ -70,9 +81,11 @@ class ClassificationLoop:
             path = self._ckpt("last.pth")
         if not path:
             return
+        # CPU map: the RNG ByteTensors must stay host tensors for set_rng_state; load_state_dict
+        # copies model / optimizer state onto the parameters' device
         extra = load_checkpoint(path, self.models, {"opt": self.optimizer},
                                 {"sched": self.scheduler} if self.scheduler is not None else None,
-                                map_location=self.rt.device)
+                                map_location="cpu")
         self.start_epoch = int(extra.get("epoch", -1)) + 1
         self.global_step = int(extra.get("global_step", 0))
         self.best = float(extra.get("best", -1.0))
@@ -99,13 +112,31 @@ class ClassificationLoop:
 
     def _setup_graph(self):
         """--graph: single-process GPU runs replay the whole step as a HIP graph (engine/graph.py),
-        recaptured at every epoch start (the learning rate is a captured kernel argument)."""
+        recaptured at every epoch start (the learning rate is a captured kernel argument) and
+        after the LR warm-up (its steps run eagerly: the LR changes every iteration)."""
         a = self.args
         self._grapher = None
         if getattr(a, "graph", False) and self.rt.device.type == "cuda" and self.rt.world == 1:
-            from .graph import StepGrapher
+            from .graph import HostCounters, StepGrapher
 
-            self._grapher = StepGrapher(self._train_step, warmup=2)
+            mods = list(self.models.values()) + list(self.train_modules)
+            self._grapher = StepGrapher(self._train_step, warmup=2, counters=HostCounters(mods, [self.optimizer]))
+
+    def _setup_warmup(self):
+        iters = int(getattr(self.args, "warmup_iters", 0) or 0)
+        if iters > 0 and self.global_step < iters and self.warmup is None:
+            target = self.optimizer.param_groups[0]["lr"]
+            self.warmup = LinearWarmup(self.optimizer, iters, target, start_lr=1e-6)
+            self.warmup.n = self.global_step  # resumed mid-warm-up: continue the ramp
+
+    def _heartbeat(self, epoch):
+        """Host-only (no device sync): wall time and step, so a stalled rank stops advancing."""
+        every = int(getattr(self.args, "heartbeat_every", 0) or 0)
+        if not every or self.global_step % every or not self.args.out_dir:
+            return
+        os.makedirs(self.args.out_dir, exist_ok=True)
+        with open(os.path.join(self.args.out_dir, f"heartbeat_rank{self.rt.rank}.txt"), "a") as f:
+            f.write(f"{time.time():.3f} rank {self.rt.rank} epoch {epoch} step {self.global_step}\n")
 
     def train_epoch(self, epoch):
         a, dev = self.args, self.rt.device
@@ -113,6 +144,18 @@ class ClassificationLoop:
             self._setup_graph()
         if self._grapher is not None:
             self._grapher.reset()  # the epoch's learning rate is baked into the captured step
+        self._setup_warmup()
+        prof = None
+        if getattr(a, "profile", False) and epoch == self.start_epoch and self.rt.is_main:
+            prof = torch.profiler.profile(
+                activities=[torch.profiler.ProfilerActivity.CPU] +
+                ([torch.profiler.ProfilerActivity.CUDA] if dev.type == "cuda" else []),
+                schedule=torch.profiler.schedule(wait=1, warmup=1, active=4, repeat=1))
+            prof.__enter__()
+        timing = dev.type == "cuda"
+        ev0 = torch.cuda.Event(enable_timing=True) if timing else None
+        ev1 = torch.cuda.Event(enable_timing=True) if timing else None
+        win_steps = 0
         for m in self.train_modules:
             m.train()
         sampler = getattr(self.train_data, "sampler", None)
@@ -129,10 +172,20 @@ class ClassificationLoop:
                 break
             if a.fail_at_step is not None and self.global_step == a.fail_at_step:
                 raise InjectedFailure(f"injected failure at global step {self.global_step}")
-            if self._grapher is not None:
+            if timing and win_steps == 0:
+                ev0.record()
+            in_warmup = self.warmup is not None and not self.warmup.done
+            if in_warmup:
+                self.warmup.step()
+            if self._grapher is not None and not in_warmup:
                 loss, rank = self._grapher(*batch)
             else:
                 loss, rank = self._train_step(*batch)
+                if in_warmup and self.warmup.done and self._grapher is not None:
+                    self._grapher.reset()  # capture at the final warm-up learning rate
+            win_steps += 1
+            if prof is not None:
+                prof.step()
             B = rank.numel()
             step_stats = torch.stack([loss.detach().double() * B, (rank < 1).sum().double(),
                                       (rank < 3).sum().double(), torch.tensor(float(B), device=dev,
@@ -140,8 +193,16 @@ class ClassificationLoop:
             acc += step_stats
             win += step_stats
             self.global_step += 1
+            self._heartbeat(epoch)
             if (i + 1) % a.log_interval == 0 or i + 1 == n_steps:
+                gpu_ms = None
+                if timing:
+                    ev1.record()
                 w = _allreduce(win.clone()).tolist()
+                if timing:
+                    ev1.synchronize()
+                    gpu_ms = ev0.elapsed_time(ev1) / max(win_steps, 1)
+                win_steps = 0
                 dt = time.time() - t0
                 eta = dt / (i + 1) * (n_steps - i - 1)
                 lr = self.optimizer.param_groups[0]["lr"]
@@ -151,8 +212,16 @@ class ClassificationLoop:
                     f"{(i + 1) * B * self.rt.world / max(dt, 1e-9):.0f} img/s "
                     f"eta {eta:.0f}s")
                 self.logger.log("train_iter", epoch=epoch, step=self.global_step, loss=w[0] / max(w[3], 1),
-                                top1=w[1] / max(w[3], 1), top3=w[2] / max(w[3], 1), lr=lr)
+                                top1=w[1] / max(w[3], 1), top3=w[2] / max(w[3], 1), lr=lr, gpu_ms_per_step=gpu_ms)
                 win.zero_()
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            pdir = os.path.join(a.out_dir, "profile")
+            os.makedirs(pdir, exist_ok=True)
+            with open(os.path.join(pdir, "steps.txt"), "w") as f:
+                f.write(prof.key_averages().table(sort_by="self_cuda_time_total" if timing else "self_cpu_time_total",
+                                                  row_limit=60))
+            prof.export_chrome_trace(os.path.join(pdir, "trace.json"))
         tot = _allreduce(acc).tolist()
         self.logger.progress("", end="\n")
         n = max(tot[3], 1)

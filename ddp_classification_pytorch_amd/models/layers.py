@@ -6,9 +6,10 @@
   and permutes them, so pretrained torchvision/timm checkpoints load.
 * :class:`BatchNorm2d` is called with the conv's statistics slabs, an
   activation and an optional residual: BN-apply + ReLU/leaky-ReLU + residual
-  add are one kernel, and SyncBN (``process_group``) all-reduces one packed
-  (sum, sumsq) vector per layer instead of torch's all_gather of
-  (mean, invstd, count) (reference: BASELINE/main.py:148).
+  add are one kernel.  SyncBN (``process_group``, reference BASELINE/main.py:148)
+  all-gathers each rank's per-channel (n, mean, M2) in forward -- Chan-merged by the
+  finalize kernel (torch gathers (mean, invstd, count)) -- and all-reduces (sum g, sum g*xhat) in backward; a projection
+  block's two BNs share one collective each way (ops/functional.py).
 * :class:`Linear` is an nn.Linear-compatible module over the MFMA GEMM.
 """
 from __future__ import annotations

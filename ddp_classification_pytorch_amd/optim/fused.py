@@ -10,6 +10,14 @@ reference uses at BASELINE/main.py:153 (SGD mom 0.9), ARCFACE/arc_main.py:249-25
 GPU: one kernel launch per parameter group updates every tensor; the device
 table of (param, grad, state) pointers is rebuilt only when a pointer changes.
 CPU: the same math with torch ops (tests / gloo plumbing).
+
+HIP-graph replay (engine/graph.py): a replayed step re-runs the captured kernels with
+their captured arguments.  Adam's bias corrections therefore come from a device step
+counter that the captured step itself increments (``mt_adam(step_dev=...)``), and
+:meth:`FusedAdam.on_graph_replay` advances the host ``state["step"]`` mirrors so
+``state_dict`` / resume see the true count.  SGD has no step-dependent argument; the
+learning rate of a captured step is the one at capture (the grapher recaptures when it
+changes).
 """
 from __future__ import annotations
 
@@ -117,6 +125,23 @@ class FusedAdam(torch.optim.Optimizer):
                         grad_scale=grad_scale)
         super().__init__(params, defaults)
         self._tables = {}
+        self._dsteps = {}        # launch key -> [device int32 step, host mirror, params]
+        self._captured = None    # launch keys of the step being / last captured into a HIP graph
+
+    def on_graph_replay(self):
+        """A captured step was replayed: its kernels advanced the device step counters; advance the
+        host mirrors and every stepped parameter's ``state["step"]`` to match."""
+        for key in self._captured or ():
+            ds = self._dsteps.get(key)
+            if ds is None:
+                continue
+            ds[1] += 1
+            for p in ds[2]:
+                self.state[p]["step"] += 1
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dsteps.clear()  # re-seeded from the loaded host step counts at the next step
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -124,6 +149,9 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if capturing:
+            self._captured = []
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
@@ -152,10 +180,20 @@ class FusedAdam(torch.optim.Optimizer):
                 st = self.state[p]
                 entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                                 st["exp_avg_sq"].data_ptr(), 0, p.numel()))
-            table, chunks = self._tables.setdefault((gi, len(params), params[0].data_ptr()),
-                                                    _TableCache()).get(entries, params[0].device)
+            key = (gi, len(params), params[0].data_ptr())
+            table, chunks = self._tables.setdefault(key, _TableCache()).get(entries, params[0].device)
+            ds = self._dsteps.get(key)
+            if ds is None or ds[1] != step - 1:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("FusedAdam: step counters must be seeded by an eager step before capture")
+                ds = self._dsteps[key] = [torch.full((1,), step - 1, dtype=torch.int32, device=params[0].device),
+                                          step - 1, params]
+            ds[0].add_(1)  # captured with the step: every replay advances the device count
+            ds[1], ds[2] = step, params
+            if self._captured is not None and torch.cuda.is_current_stream_capturing():
+                self._captured.append(key)
             _ext.hip_ops().mt_adam(table, chunks, group["lr"], b1, b2, group["eps"], group["weight_decay"], step,
-                                   group["decoupled"], group["grad_scale"])
+                                   group["decoupled"], group["grad_scale"], ds[0])
             return
         bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
         for p in params:

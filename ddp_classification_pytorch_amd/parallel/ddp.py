@@ -18,8 +18,14 @@ MI355X choices:
 * ``broadcast_buffers=False``: BN running stats are either identical by
   construction (SyncBN) or rank-local (local BN), so the per-forward buffer
   broadcast the reference pays (C3) is skipped;
-* SyncBN is our fused BN with a ``process_group``: one packed all_reduce of
-  (sum, sumsq) per layer forward, one of (sum dz, sum dz*xhat) backward.
+* SyncBN is our fused BN with a ``process_group``: forward all-gathers each rank's
+  per-channel (n, mean, M2) (Chan-merged, so unequal per-rank counts stay exact),
+  backward all-reduces (sum g, sum g*xhat); a projection block's two BNs share one
+  collective in each direction.  Those collectives run on a DEDICATED process group
+  (:func:`bn_process_group`: its own RCCL communicator and stream), so a 516 B..16 KB
+  statistics exchange that sits on the critical path never queues behind a 25 MiB
+  gradient bucket the Reducer has in flight on the default group.  Per ResNet-50
+  step: 49 forward gathers + 49 backward reduces (53 BNs, 4 projection pairs).
 """
 from __future__ import annotations
 
@@ -51,9 +57,25 @@ def init_distributed(backend: str = None, timeout_s: int = 1800):
     return rank, local, world
 
 
+_BN_GROUPS = {}
+
+
+def bn_process_group():
+    """The SyncBN communicator: one extra group over all ranks, created once per default group
+    (collectively: every rank calls this in the same order, from convert_sync_batchnorm)."""
+    if not dist.is_initialized():
+        return None
+    key = id(dist.group.WORLD)
+    g = _BN_GROUPS.get(key)
+    if g is None:
+        g = _BN_GROUPS[key] = dist.new_group(ranks=list(range(dist.get_world_size())))
+    return g
+
+
 def convert_sync_batchnorm(model: nn.Module, process_group=None) -> nn.Module:
-    """Attach a process group to every fused BatchNorm2d (in place)."""
-    group = process_group if process_group is not None else (dist.group.WORLD if dist.is_initialized() else None)
+    """Attach a process group to every fused BatchNorm2d (in place); by default the dedicated
+    SyncBN group (:func:`bn_process_group`), not the group the DDP Reducer all-reduces on."""
+    group = process_group if process_group is not None else bn_process_group()
     for m in model.modules():
         if isinstance(m, BatchNorm2d):
             m.process_group = group

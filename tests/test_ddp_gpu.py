@@ -2,7 +2,10 @@
 driver runs the real 1/2/4/8-GPU RCCL benchmark; RCCL refuses two ranks on one
 device, so these tests use gloo for the collectives while every op runs on cuda:0):
 
-* bench.py under torchrun with 2 ranks prints one JSON line with n_gpus == 2;
+* ``bench.py --gpus 2`` (self-launched ranks, no torchrun on the command line) prints one JSON
+  line with n_gpus == 2 and the SyncBN phase's number;
+* RCCL itself: a world_size-1 ``nccl`` process group (eager communicator init) under a forced
+  DDP wrapper, one ResNet-18 training step whose gradients pass through the RCCL Reducer;
 * DDP over 2 ranks x 4 images == one process over the same 8 images (loss and
   every gradient, within the bf16 noise floor), local BN and SyncBN."""
 import json
@@ -31,15 +34,88 @@ def _free_port():
 
 def test_bench_two_ranks_one_gpu():
     env = dict(os.environ, DCP_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "8", "--image-size", "64"]
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "8", "--image-size", "64"]
     out = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 16 and rec["value"] > 0
+    assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["config"]["global_batch"] == 16
+    assert rec["value"] > 0 and rec["syncbn_value"] > 0 and rec["dist_backend"] == "gloo"
+    assert len(rec["per_rank_ms"]) == 2
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--batch", "4", "--image-size", "64"]
+    out = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "--gpus 2" in out.stderr
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.optim import FusedSGD
+    from ddp_classification_pytorch_amd.parallel.ddp import bn_process_group, wrap_ddp
+
+    import datetime
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=120))
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=10).to(dev)
+    net = wrap_ddp(model, 0, syncbn=True, bucket_cap_mb=1, force=True)
+    assert isinstance(net, torch.nn.parallel.DistributedDataParallel)
+    bn_group = bn_process_group()
+    assert bn_group is not None and bn_group is not dist.group.WORLD
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(1)
+    imgs = torch.randint(0, 256, (8, 3, 64, 64), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (8,), generator=g)
+    x = Fn.to_device_nhwc(imgs.to(dev), (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), cpad=8, in_scale=1 / 255.0)
+    loss = Fn.cross_entropy(net(x), labels.to(dev))
+    loss.backward()
+    grads = {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()}
+    opt.step()
+    t = torch.ones(4, device=dev)
+    dist.all_reduce(t)  # the default (Reducer) communicator
+    dist.all_reduce(t, group=bn_group)  # the SyncBN communicator
+    torch.cuda.synchronize()
+    torch.save({"loss": loss.item(), "grads": grads, "t": t.cpu(), "backend": dist.get_backend(),
+                "rccl": str(torch.cuda.nccl.version())}, os.path.join(out_dir, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_ddp_step():
+    """RCCL executes: world-1 ``nccl`` group, forced DDP + SyncBN, gradients equal a plain step."""
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        got = torch.load(os.path.join(d, "rccl.pt"), weights_only=True)
+    assert got["backend"] == "nccl" and torch.equal(got["t"], torch.ones(4))
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=10).to(dev)
+    g = torch.Generator().manual_seed(1)
+    imgs = torch.randint(0, 256, (8, 3, 64, 64), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (8,), generator=g)
+    x = Fn.to_device_nhwc(imgs.to(dev), (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), cpad=8, in_scale=1 / 255.0)
+    loss = Fn.cross_entropy(model(x), labels.to(dev))
+    loss.backward()
+    assert abs(loss.item() - got["loss"]) < 1e-3 * max(1.0, abs(loss.item()))
+    for n, p in model.named_parameters():
+        ref = p.grad.detach().cpu().float()
+        err = (got["grads"][n].float() - ref).norm() / max(ref.norm().item(), 1e-12)
+        assert err < 2e-2, (n, float(err))
 
 
 def _worker(rank, world, port, syncbn, out_dir):

@@ -91,6 +91,62 @@ def test_ddp_syncbn_equals_single_process_full_batch():
     assert err <= 3 * floor + 1e-5, (err, floor)
 
 
+def _bn_group_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.models.layers import BatchNorm2d
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.parallel import ddp as pddp
+
+    torch.manual_seed(0)
+    model = build_model("cifar_resnet18", num_classes=10)
+    net = pddp.wrap_ddp(model, None, syncbn=True, bucket_cap_mb=1)
+    groups = {m.process_group for m in model.modules() if isinstance(m, BatchNorm2d)}
+    calls = []
+    real_ag, real_ar = dist.all_gather_into_tensor, dist.all_reduce
+
+    def ag(out, inp, group=None, **kw):
+        calls.append(("gather", group))
+        return real_ag(out, inp, group=group, **kw)
+
+    def ar(t, op=dist.ReduceOp.SUM, group=None, **kw):
+        calls.append(("reduce", group))
+        return real_ar(t, op=op, group=group, **kw)
+
+    dist.all_gather_into_tensor, dist.all_reduce = ag, ar
+    try:
+        x = Fn.to_device_nhwc(torch.randn(4, 3, 32, 32, generator=torch.Generator().manual_seed(rank)), cpad=8)
+        loss = Fn.cross_entropy(net(x), torch.randint(0, 10, (4,), generator=torch.Generator().manual_seed(3)))
+        n_fwd = len(calls)
+        loss.backward()
+    finally:
+        dist.all_gather_into_tensor, dist.all_reduce = real_ag, real_ar
+    bn = pddp.bn_process_group()
+    if rank == 0:
+        torch.save({"one_group": len(groups) == 1, "is_bn": groups == {bn}, "not_world": bn is not dist.group.WORLD,
+                    "all_on_bn": all(g is bn for _, g in calls), "n_fwd": n_fwd, "n_bwd": len(calls) - n_fwd,
+                    "kinds_fwd": sorted({k for k, _ in calls[:n_fwd]}),
+                    "n_bn": sum(isinstance(m, BatchNorm2d) for m in model.modules())},
+                   os.path.join(out_dir, "g.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_syncbn_uses_dedicated_group_and_coalesces():
+    """SyncBN collectives run on their own process group (never queued behind the Reducer's
+    buckets on the default group), one all-gather per BN forward and one all-reduce per BN
+    backward, a projection block's two BNs sharing one of each."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_bn_group_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        got = torch.load(os.path.join(d, "g.pt"), weights_only=True)
+    assert got["one_group"] and got["is_bn"] and got["not_world"] and got["all_on_bn"]
+    assert got["kinds_fwd"] == ["gather"]
+    n_bn, n_proj = got["n_bn"], 3  # CIFAR ResNet-18: 20 BNs, 3 projection shortcuts
+    assert n_bn == 20
+    assert got["n_fwd"] == n_bn - n_proj, got
+    assert got["n_bwd"] == n_bn - n_proj, got
+
+
 def _metrics_worker(rank, world, port, out_dir):
     _init(rank, world, port)
     from ddp_classification_pytorch_amd.parallel.ddp import all_reduce_metrics, reduce_loss

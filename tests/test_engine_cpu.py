@@ -67,3 +67,25 @@ def test_failure_and_resume_is_equivalent(tmp_path):
     assert "resumed from" in lines and "VAL Epoch 2" in lines
     recs = [json.loads(x) for x in open(tmp_path / "ref" / "metrics.jsonl")]
     assert {r["kind"] for r in recs} >= {"train_epoch", "val"}
+
+
+def test_warmup_heartbeat_profile_and_auto_resume(tmp_path):
+    """--warmup-iters ramps the LR per iteration from 1e-6 (BASELINE WarmUp, BASELINE/main.py:170-197),
+    --heartbeat-every writes a per-rank liveness file, --profile writes a torch.profiler table,
+    and --auto-resume continues from last.pth after a failure."""
+    out = tmp_path / "run"
+    base = ["--workload", "baseline", "--model", "cifar_resnet18", "--epochs", "2", "--optimizer", "SGD",
+            "--lr", "0.05"] + SYN
+    base = [a if a != "100" else "1" for a in base]  # log every step
+    with pytest.raises(InjectedFailure):
+        entry.main(base + ["--out-dir", str(out), "--warmup-iters", "3", "--heartbeat-every", "2", "--profile",
+                           "--fail-at-step", "6"])
+    recs = [json.loads(x) for x in open(out / "metrics.jsonl") if '"train_iter"' in x]
+    lrs = [r["lr"] for r in recs]
+    assert lrs[:4] == pytest.approx([1e-6 + (0.05 - 1e-6) * n / 3 for n in (1, 2, 3)] + [0.05])
+    hb = open(out / "heartbeat_rank0.txt").read().split("\n")
+    assert "step 2" in hb[0] and "step 4" in hb[1]
+    assert os.path.exists(out / "profile" / "steps.txt")
+    entry.main(base + ["--out-dir", str(out), "--auto-resume"])
+    text = open(out / "output.txt").read()
+    assert "resumed from" in text and "VAL Epoch 2" in text

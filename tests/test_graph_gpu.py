@@ -58,21 +58,58 @@ def test_table_to_device_through_kernel_args(n, dtype):
     assert two.shape == (3, 2) and two.cpu().tolist() == [[1, 2], [3, 4], [5, 6]]
 
 
-def test_training_loop_graph_matches_eager(tmp_path):
+@pytest.mark.parametrize("workload,extra", [
+    ("baseline", ["--optimizer", "SGD", "--lr", "0.05"]),
+    ("baseline", ["--optimizer", "SGD", "--lr", "0.05", "--warmup-iters", "4"]),  # eager ramp, then capture
+    ("arcface", ["--optimizer", "Adam", "--lr", "1e-3"]),  # device step counter (bias correction)
+    ("cdr", ["--lr", "0.05"]),                              # radix-select tables from fill kernels
+])
+def test_training_loop_graph_matches_eager(tmp_path, workload, extra):
     """main.py --graph (StepGrapher: eager warm-up, capture, replays, recapture per epoch, eager
-    short last batch) trains to the same weights as the eager loop."""
+    short last batch) trains to the same weights as the eager loop, and the host-side counters
+    (BN num_batches_tracked, Adam's per-parameter step) advance on every replay."""
     import main as entry
 
-    common = ["--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+    common = ["--workload", workload, "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
               "--batchsize", "16", "--synthetic-train-size", "120", "--synthetic-val-size", "32", "--epochs", "2",
-              "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "SGD",
-              "--lr", "0.05"]
+              "--workers", "0", "--log-interval", "100", "--num-classes", "10"] + extra
     outs = {}
-    for tag, extra in (("eager", []), ("graph", ["--graph"])):
+    for tag, flag in (("eager", []), ("graph", ["--graph"])):
         torch.manual_seed(0)
-        entry.main(common + ["--out-dir", str(tmp_path / tag)] + extra)
+        entry.main(common + ["--out-dir", str(tmp_path / tag)] + flag)
         outs[tag] = torch.load(tmp_path / tag / "last.pth", weights_only=True)
-    me, mg = outs["eager"]["models"]["model"], outs["graph"]["models"]["model"]
-    for k, v in me.items():
-        if v.dtype.is_floating_point:
-            assert torch.allclose(v, mg[k], rtol=2e-3, atol=2e-4), k
+    for name, me in outs["eager"]["models"].items():
+        mg = outs["graph"]["models"][name]
+        for k, v in me.items():
+            if v.dtype.is_floating_point:
+                assert torch.allclose(v, mg[k], rtol=2e-3, atol=2e-4), (name, k)
+            else:
+                assert torch.equal(v, mg[k]), (name, k)  # num_batches_tracked
+    oe, og = outs["eager"]["optimizers"]["opt"]["state"], outs["graph"]["optimizers"]["opt"]["state"]
+    for i, st in oe.items():
+        if "step" in st:
+            assert int(st["step"]) == int(og[i]["step"]) > 8, (i, st["step"], og[i]["step"])
+
+
+def test_gpu_failure_and_resume(tmp_path):
+    """Resume on the GPU (RNG ByteTensors must stay on the host): a run killed in epoch 2
+    and resumed from last.pth matches the uninterrupted run."""
+    import main as entry
+    from ddp_classification_pytorch_amd.engine.loop import InjectedFailure
+
+    base = ["--workload", "arcface", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+            "--batchsize", "16", "--synthetic-train-size", "64", "--synthetic-val-size", "16", "--epochs", "2",
+            "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "Adam"]
+    torch.manual_seed(0)
+    entry.main(base + ["--out-dir", str(tmp_path / "ref")])
+    with pytest.raises(InjectedFailure):
+        torch.manual_seed(0)
+        entry.main(base + ["--out-dir", str(tmp_path / "ft"), "--fail-at-step", "6"])
+    entry.main(base + ["--out-dir", str(tmp_path / "ft"), "--auto-resume"])
+    ref = torch.load(tmp_path / "ref" / "last.pth", weights_only=True)
+    got = torch.load(tmp_path / "ft" / "last.pth", weights_only=True)
+    assert got["epoch"] == ref["epoch"] == 1 and got["global_step"] == ref["global_step"]
+    for name, m in ref["models"].items():
+        for k, v in m.items():
+            if v.dtype.is_floating_point:
+                assert torch.allclose(v, got["models"][name][k], rtol=1e-3, atol=1e-4), (name, k)

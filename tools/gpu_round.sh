@@ -1,0 +1,63 @@
+#!/bin/bash
+# GPU-box measurement script (one gpurun call).  Steps run in the order given; each GPU step
+# has its own time limit and the chain stops at the first failure.
+#   /usr/local/graft/bin/gpurun --timeout 1100 -- bash tools/gpu_round.sh <tag> <step>...
+# steps:
+#   tests[=filter]  pytest -m gpu (optionally -k filter)      smoke   __graft_entry__.smoke()
+#   bench           headline bench.py (20 steps)              configs every BASELINE.json config
+#   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
+#   pmc             three PMC passes (SQ: MFMA busy / LDS conflicts / waits; FETCH_SIZE; WRITE_SIZE)
+#   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
+#   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
+#   sweep           headline batch sweep 128..2048
+set -e
+set -o pipefail
+T=${1:?tag}; shift
+O=gpurun_out/$T; mkdir -p $O
+prof_env() { cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; }
+for step in "$@"; do
+  case $step in
+    tests*)
+      k=${step#tests}; k=${k#=}
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${k:+-k "$k"} \
+        > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+      tail -2 $O/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1
+      tail -1 $O/bench.log ;;
+    configs)
+      for c in r50 arcface resnext r101 tresnet; do
+        timeout -k 10 240 python -u bench.py --config $c --steps 20 --warmup 5 > $O/bench_$c.log 2>&1
+        tail -1 $O/bench_$c.log
+      done ;;
+    gloo2)
+      DCP_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --batch 256 --steps 5 --warmup 2 \
+        > $O/bench_gloo2.log 2>&1
+      tail -1 $O/bench_gloo2.log ;;
+    prof)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 2 \
+        > $O/prof.log 2>&1
+      echo prof done ;;
+    pmc)
+      prof_env
+      PASS1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $PASS1 --output-format csv -d $O/pmc1 -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/pmc1.log 2>&1
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmc2 -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/pmc2.log 2>&1
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmc3 -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/pmc3.log 2>&1
+      echo pmc done ;;
+    stock)
+      timeout -k 10 600 python -u tools/bench_torch_reference.py --batch 256 --warmup 3 > $O/stock_r50_b256.log 2>&1
+      tail -1 $O/stock_r50_b256.log ;;
+    sweep)
+      for b in 128 256 512 1024 2048; do
+        timeout -k 10 240 python -u bench.py --batch $b --steps 10 --warmup 3 > $O/sweep_b$b.log 2>&1
+        tail -1 $O/sweep_b$b.log
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "gpu_round $T done"
