@@ -91,7 +91,9 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
   TORCH_CHECK(KH * KW <= dcp::kMaxTaps && pad <= 100 && KH <= 100, "unsupported conv geometry");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
-  TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)N * Ho * Wo * Co < (1ll << 32), "tensor too large");
+  // GEMM rows (pixels) index as int; element offsets are 64-bit (large per-GPU batches pass 2^32
+  // elements: tests/test_large_batch_gpu.py)
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31) && (int64_t)N * Ho * Wo < (1ll << 31), "conv_fwd: too many pixels");
   auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
   const int M = N * Ho * Wo;
   if (stride == 1 && pad == 1 && KH == 3 && KW == 3 && dcp::conv3x3_c64_supported(H, W, C, Co)) {
@@ -112,6 +114,61 @@ std::tuple<Tensor, Tensor> conv_fwd(const Tensor& x, const Tensor& w, int64_t st
                        stats ? slabs.data_ptr<float>() : nullptr, nullptr, 0, zero_page(x.get_device()),
                        cur_stream());
   return {y, slabs};
+}
+
+// forward conv with an eval-mode BN folded into the store: y = act(conv(x) * scale + shift [+ res])
+// (scale / shift per output channel, fp32; the BN of running statistics, AffineEpi in launchers.h)
+Tensor conv_fwd_affine(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad, const Tensor& scale,
+                       const Tensor& shift, int64_t act, double slope, const optional<Tensor>& res) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd_affine expects NHWC input and [Co,KH,KW,Ci] weight");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Co = w.size(0), KH = w.size(1), KW = w.size(2);
+  TORCH_CHECK(w.size(3) == C && C % 8 == 0 && Co % 8 == 0, "conv_fwd_affine channels");
+  TORCH_CHECK(KH * KW <= dcp::kMaxTaps && pad <= 100 && KH <= 100, "unsupported conv geometry");
+  TORCH_CHECK(act >= 0 && act <= 2, "conv_fwd_affine: act must be none, ReLU or leaky ReLU");
+  for (const Tensor* t : {&scale, &shift}) {
+    CHECK_DEV(*t);
+    CHECK_F32(*t);
+    CHECK_CONTIG(*t);
+    TORCH_CHECK(t->numel() == Co, "conv_fwd_affine: per-channel vector size");
+  }
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty conv output");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31) && (int64_t)N * Ho * Wo < (1ll << 31), "conv_fwd_affine: too many pixels");
+  auto y = at::empty({N, Ho, Wo, Co}, bf16_like(x));
+  const bf16* resp = nullptr;
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == y.sizes(), "conv_fwd_affine residual shape");
+    resp = bp(*res);
+  }
+  const auto taps = fwd_taps(KH, KW, pad);
+  dcp::AffineEpi aff{scale.data_ptr<float>(), shift.data_ptr<float>(), (int)act, (float)slope};
+  dcp::launch_tap_gemm(bp(x), N, H, W, C, bp(w), Co, KH * KW, bpm(y), Ho, Wo, Ho, Wo, stride, 1, 0, 0, taps, nullptr,
+                       nullptr, 0, zero_page(x.get_device()), cur_stream(), resp, nullptr, &aff);
+  return y;
+}
+
+// backward of act(c * scale + shift [+ r]) from its output y: (dc = g * scale, g = dy * act'(y) or empty)
+std::tuple<Tensor, Tensor> act_scale_bwd(const Tensor& dy, const Tensor& y, const Tensor& scale, int64_t act,
+                                         double slope, bool want_g) {
+  CHECK_ACT(dy);
+  CHECK_ACT(y);
+  TORCH_CHECK(dy.sizes() == y.sizes() && dy.dim() >= 2, "act_scale_bwd shapes");
+  const int C = y.size(-1);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "act_scale_bwd: C/8 must divide 256");
+  CHECK_DEV(scale);
+  CHECK_F32(scale);
+  TORCH_CHECK(scale.is_contiguous() && scale.numel() == C, "act_scale_bwd: scale [C]");
+  auto dc = at::empty_like(dy);
+  Tensor g = want_g ? at::empty_like(dy) : at::empty({0}, dy.options());
+  const int64_t M = dy.numel() / C;
+  TORCH_CHECK(M < (1ll << 31), "act_scale_bwd: too many rows");
+  dcp::launch_act_scale_bwd(bp(dy), bp(y), scale.data_ptr<float>(), M, C, (int)act, (float)slope, bpm(dc),
+                            want_g ? bpm(g) : nullptr, cur_stream());
+  return {dc, g};
 }
 
 // forward with an explicit output grid (asymmetric padding: output (oy, ox) reads input rows
@@ -206,6 +263,7 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
   TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_dgrad needs channel multiples of 8");
   TORCH_CHECK(stride == 1 || stride == 2, "conv_dgrad supports stride 1 and 2");
   TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "dgrad geometry");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31) && (int64_t)N * Ho * Wo < (1ll << 31), "conv_dgrad: too many pixels");
   auto dx = at::empty({N, H, W, C}, bf16_like(dy));
   const bf16* z = zero_page(dy.get_device());
   auto st = cur_stream();
@@ -270,6 +328,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(3) == C, "conv_dgrad_bn: BN input shape");
   const int H = y.size(1), W = y.size(2);
   TORCH_CHECK(H + 2 * pad - KH + 1 == Ho && W + 2 * pad - KW + 1 == Wo, "conv_dgrad_bn: stride-1 geometry");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "conv_dgrad_bn: too many pixels");
   TORCH_CHECK(act == 0 || act == 1 || act == 2, "conv_dgrad_bn: act must be none, ReLU or leaky ReLU");
   TORCH_CHECK(act != 2 || (!mask.has_value() && !res.has_value()), "conv_dgrad_bn: leaky path has no mask / residual");
   for (const Tensor* t : {&scale, &shift, &mean, &invstd}) {
@@ -332,6 +391,7 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   TORCH_CHECK(x.size(0) == N, "batch mismatch");
   TORCH_CHECK(C % 8 == 0 && Co % 8 == 0, "conv_wgrad needs channel multiples of 8");
   TORCH_CHECK((H + 2 * pad - KH) / stride + 1 == Ho && (W + 2 * pad - KW) / stride + 1 == Wo, "wgrad geometry");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31) && (int64_t)N * Ho * Wo < (1ll << 31), "conv_wgrad: too many pixels");
   auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
   const int ncu = num_cus(dy.get_device());
@@ -1322,5 +1382,11 @@ TORCH_LIBRARY(dcp, m) {
       "decoupled, float grad_scale, Tensor? step_dev=None) -> ()",
       &mt_adam);
   m.def("cdr_threshold(Tensor table, Tensor chunks, Tensor state) -> Tensor", &cdr_threshold);
+  m.def(
+      "conv_fwd_affine(Tensor x, Tensor w, int stride, int pad, Tensor scale, Tensor shift, int act, float slope, "
+      "Tensor? res) -> Tensor",
+      &conv_fwd_affine);
+  m.def("act_scale_bwd(Tensor dy, Tensor y, Tensor scale, int act, float slope, bool want_g) -> (Tensor, Tensor)",
+        &act_scale_bwd);
   m.def("cdr_mask(Tensor table, Tensor chunks, Tensor state, float clip) -> ()", &cdr_mask);
 }

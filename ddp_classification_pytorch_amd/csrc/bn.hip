@@ -789,4 +789,48 @@ void launch_bn2_bwd_elemt(const bf16* dy, const bf16* x, const bf16* r, const fl
                      rscale, rmean, rinvstd, rsums, inv_count, M, C, dx, dr);
 }
 
+// Backward of the folded eval-mode BN (launchers.h AffineEpi) from its bf16 output y:
+// g = dy * act'(y) (act' of the pre-activation: y keeps its sign), dc = g * scale per channel.
+// G: also store g (the gradient of the residual added before the activation).
+template <int ACT, bool G>
+__global__ void __launch_bounds__(256) act_scale_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                            const float* __restrict__ scale, int M, int C, float slope,
+                                                            bf16* __restrict__ dc, bf16* __restrict__ g) {
+  const RowTile t(C);
+  if (t.slot >= t.rpi) return;
+  float sc[8];
+  load8(scale + t.c0, sc);
+  const int step = gridDim.x * t.rpi;
+  for (int m = blockIdx.x * t.rpi + t.slot; m < M; m += step) {
+    const size_t off = (size_t)m * C + t.c0;
+    const bf16x8 d = *(const bf16x8*)(dy + off);
+    const bf16x8 v = ACT ? *(const bf16x8*)(y + off) : bf16x8{};
+    bf16x8 oc, og;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float gk = bf2f(d[k]);
+      if (ACT == 1 && !(bf2f(v[k]) > 0.f)) gk = 0.f;
+      if (ACT == 2 && !(bf2f(v[k]) >= 0.f)) gk *= slope;
+      og[k] = f2bf(gk);
+      oc[k] = f2bf(gk * sc[k]);
+    }
+    *(bf16x8*)(dc + off) = oc;
+    if (G) *(bf16x8*)(g + off) = og;
+  }
+}
+
+void launch_act_scale_bwd(const bf16* dy, const bf16* y, const float* scale, int64_t M, int C, int act, float slope,
+                          bf16* dc, bf16* g, hipStream_t s) {
+  const dim3 grid = ew_grid((int)M, C);
+#define DCP_ASB(A_)                                                                                          \
+  if (g) hipLaunchKernelGGL((act_scale_bwd_kernel<A_, true>), grid, dim3(256), 0, s, dy, y, scale, (int)M, C, \
+                            slope, dc, g);                                                                   \
+  else hipLaunchKernelGGL((act_scale_bwd_kernel<A_, false>), grid, dim3(256), 0, s, dy, y, scale, (int)M, C,  \
+                          slope, dc, g);
+  if (act == 1) { DCP_ASB(1) }
+  else if (act == 2) { DCP_ASB(2) }
+  else { DCP_ASB(0) }
+#undef DCP_ASB
+}
+
 }  // namespace dcp

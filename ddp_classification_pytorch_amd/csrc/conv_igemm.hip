@@ -63,6 +63,11 @@ struct TapGemmParams {
   // EPI 3 (stride-1 dgrad): backward of the BN(+ReLU)(+residual) layer that produced this
   // conv's input, fused into the epilogue (see launchers.h BnBwdEpi)
   BnBwdEpi bnb;
+  // EPI 0: eval-mode BN folded into the store (launchers.h AffineEpi); fscale == nullptr: off
+  const float* fscale;
+  const float* fshift;
+  int fact;
+  float fslope;
 };
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
@@ -620,6 +625,15 @@ tap_gemm_kernel(const TapGemmParams p) {
       constexpr int R = 256 / NCH;
       const int c = tid % NCH, pr0 = tid / NCH;
       const bool cok = n0 + c * 8 < p.Co;
+      float fsc[8], fsh[8];
+      const bool fold = EPI == 0 && p.fscale != nullptr;
+      if (fold) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          fsc[e] = cok ? p.fscale[n0 + c * 8 + e] : 0.f;
+          fsh[e] = cok ? p.fshift[n0 + c * 8 + e] : 0.f;
+        }
+      }
       bf16x8 vv[BM / R];
 #pragma unroll
       for (int k = 0; k < BM / R; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
@@ -640,7 +654,19 @@ tap_gemm_kernel(const TapGemmParams p) {
             drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
           }
           bf16x8 o = v;
-          if (p.addsrc) {
+          if (fold) {
+            // the bf16 conv output through the unfused BN-apply's fp32 math (bn_act_fwd_kernel)
+            bf16x8 a{};
+            if (p.addsrc) a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float t = bf2f(v[e]) * fsc[e] + fsh[e];
+              if (p.addsrc) t += bf2f(a[e]);
+              if (p.fact == 1) t = fmaxf(t, 0.f);
+              else if (p.fact == 2) t = t >= 0.f ? t : t * p.fslope;
+              o[e] = f2bf(t);
+            }
+          } else if (p.addsrc) {
             const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
@@ -1360,9 +1386,18 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                      const TapList& taps, float* stats, const float* bias, int relu,
-                     const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb) {
+                     const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb,
+                     const AffineEpi* aff) {
   TapGemmParams p;
   p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
+  p.fscale = aff ? aff->scale : nullptr;
+  p.fshift = aff ? aff->shift : nullptr;
+  p.fact = aff ? aff->act : 0;
+  p.fslope = aff ? aff->slope : 0.f;
+  if (aff != nullptr && (stats != nullptr || bias != nullptr || relu != 0 || bnb != nullptr)) {
+    fprintf(stderr, "launch_tap_gemm: the folded BN epilogue is a plain forward store\n");
+    abort();
+  }
   p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0.f};
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
@@ -1405,7 +1440,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // (K = 64, one 64-deep k-tile, measured faster with the 64-deep tile: 487 vs 511 us on the R50
   // stage-1 expansion at b1024, tools/fwd_epi_bench.py)
   if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
-  const bool use8 = g_tune[3] == 1;  // measured slower than the 4-wave kernel (tools/conv_bench.py --cfgs)
+  const bool use8 = g_tune[3] == 1 && aff == nullptr;  // measured slower than the 4-wave kernel (conv_bench --cfgs)
   if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
     constexpr size_t lds8 = 3 * (256 + 128) * 128;

@@ -43,10 +43,24 @@ struct BnBwdEpi {
   float slope;          // leaky slope (act 2)
 };
 
+// Eval-mode BN folded into the forward conv's store epilogue (running statistics: model.eval(),
+// NESTED's frozen BN): dst = act(acc_bf16 * scale + shift [+ addsrc]) per output channel, so the
+// conv output is never written un-normalised and no separate BN-apply pass runs.
+struct AffineEpi {
+  const float* scale;  // gamma * invstd(running var)
+  const float* shift;  // beta - running_mean * scale
+  int act;             // 0 none, 1 ReLU, 2 leaky ReLU
+  float slope;
+};
+
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,
-                     const BnBwdEpi* bnb = nullptr);
+                     const BnBwdEpi* bnb = nullptr, const AffineEpi* aff = nullptr);
+// backward of act(c * scale + shift [+ r]) from its output y: g = dy * act'(y) and dc = g * scale
+// (g only when want_g: the residual's gradient)
+void launch_act_scale_bwd(const bf16* dy, const bf16* y, const float* scale, int64_t M, int C, int act, float slope,
+                          bf16* dc, bf16* g, hipStream_t s);
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s);
 // partial-slab split-K weight gradient: dw is fully written when part != nullptr
 // (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw

@@ -58,8 +58,8 @@ __global__ void __launch_bounds__(256) mt_adam_kernel(const MTEntry* __restrict_
   float bc1 = h.bc1, bc2 = h.bc2;
   if (h.step_dev) {  // 1 - beta^t without the cancellation of 1 - powf
     const float t = (float)*h.step_dev;
-    bc1 = -expm1f(t * log1pf(-h.beta1));
-    bc2 = -expm1f(t * log1pf(-h.beta2));
+    bc1 = -expm1f(t * logf(h.beta1));
+    bc2 = -expm1f(t * logf(h.beta2));
   }
   const float rbc2 = 1.f / sqrtf(bc2);
   for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {

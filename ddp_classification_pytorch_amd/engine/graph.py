@@ -40,7 +40,12 @@ class HostCounters:
     capture recorded (module by module) plus each optimizer's ``on_graph_replay`` hook."""
 
     def __init__(self, modules=(), optimizers=()):
-        self.bns = [m for r in modules for m in r.modules() if hasattr(m, "_nbt_pending")]
+        seen, self.bns = set(), []
+        for r in modules:
+            for m in r.modules():
+                if hasattr(m, "_nbt_pending") and id(m) not in seen:  # a module reachable twice counts once
+                    seen.add(id(m))
+                    self.bns.append(m)
         self.opts = [o for o in optimizers if hasattr(o, "on_graph_replay")]
         self.before = self.delta = None
 
@@ -110,6 +115,11 @@ class StepGrapher:
 
     def reset(self):
         self.graph = self.static = self.out = None
+        self.calls = 0  # eager warm-up again before the next capture
+
+    def eager(self, *tensors):
+        """One eager step on a side stream (steps that must not be captured: LR warm-up)."""
+        return self._eager(tensors)
 
     def _eager(self, tensors):
         cur = torch.cuda.current_stream()

@@ -108,7 +108,10 @@ class ClassificationLoop:
         if self.post_backward is not None:
             self.post_backward()
         self.optimizer.step()
-        return loss, rank
+        # detached: a loss kept alive until the next step would keep this step's autograd graph --
+        # and with it the parameters' AccumulateGrad nodes, bound to this step's stream -- alive
+        # into a HIP-graph capture, whose gradient accumulation would then sync with that stream
+        return loss.detach(), rank
 
     def _setup_graph(self):
         """--graph: single-process GPU runs replay the whole step as a HIP graph (engine/graph.py),
@@ -179,10 +182,12 @@ class ClassificationLoop:
                 self.warmup.step()
             if self._grapher is not None and not in_warmup:
                 loss, rank = self._grapher(*batch)
+            elif self._grapher is not None:
+                loss, rank = self._grapher.eager(*batch)  # the grapher's side stream, as its own warm-up
+                if self.warmup.done:
+                    self._grapher.reset()  # capture at the final warm-up learning rate
             else:
                 loss, rank = self._train_step(*batch)
-                if in_warmup and self.warmup.done and self._grapher is not None:
-                    self._grapher.reset()  # capture at the final warm-up learning rate
             win_steps += 1
             if prof is not None:
                 prof.step()

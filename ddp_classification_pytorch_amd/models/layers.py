@@ -163,6 +163,18 @@ class Linear(nn.Module):
         return f"in={self.in_features}, out={self.out_features}, bias={self.bias is not None}"
 
 
+def conv_bn(conv: Conv2d, bn: BatchNorm2d, x, act="relu", residual=None, slope=0.01):
+    """act(BN(conv(x)) [+ residual]) for a BN that normalises with its running statistics
+    (``Fn.bn_foldable``: model.eval(), NESTED's frozen BN): the BN is folded
+    into the conv's store epilogue, so no un-normalised output is written and no BN pass runs.
+    Grouped convs (no folded kernel) run conv -> BN."""
+    if conv.groups == 1 and conv.weight.shape[3] == x.shape[3]:
+        return Fn.conv_bn_folded(x, conv.weight, conv.stride, conv.padding, bn, act=act, slope=slope,
+                                 residual=residual)
+    y, _ = conv(x)
+    return bn(y, None, act=act, residual=residual, slope=slope)
+
+
 class ConvBN(nn.Module):
     """conv -> BN (stats from the conv epilogue) -> act, optional residual."""
 
@@ -174,5 +186,7 @@ class ConvBN(nn.Module):
         self.act, self.slope = act, slope
 
     def forward(self, x, residual=None):
+        if Fn.bn_foldable(self.bn):
+            return conv_bn(self.conv, self.bn, x, act=self.act, residual=residual, slope=self.slope)
         y, slabs = self.conv(x, stats=self.bn.training and not self.bn.frozen)
         return self.bn(y, slabs, act=self.act, residual=residual, slope=self.slope)

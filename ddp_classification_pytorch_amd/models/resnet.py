@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as Fn
-from .layers import BatchNorm2d, Conv2d, Linear
+from .layers import BatchNorm2d, Conv2d, Linear, conv_bn
 
 
 # the one-op stem (conv + BN + ReLU + max pool, fused one-pass backward, stem.hip stem_bwd).
@@ -34,6 +34,12 @@ _FUSED_STEM = [os.environ.get("DCP_FUSED_STEM", "1") == "1"]
 
 def _train_stats(bn: BatchNorm2d) -> bool:
     return bn.training and not bn.frozen
+
+
+def _folded(*bns) -> bool:
+    """Every BN of the block normalises with running statistics and needs no affine gradient:
+    run the block as conv launches with the BNs folded into their epilogues (layers.conv_bn)."""
+    return all(b is not None and Fn.bn_foldable(b) for b in bns)
 
 
 class BasicBlock(nn.Module):
@@ -48,6 +54,10 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        if _folded(self.bn1, self.bn2, self.downsample[1] if self.downsample is not None else self.bn2):
+            y = conv_bn(self.conv1, self.bn1, x)
+            r = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x, act="none")
+            return conv_bn(self.conv2, self.bn2, y, residual=r)
         t = _train_stats(self.bn1)
         # the block input's second consumer (residual add / downsample conv) hands its
         # gradient to conv1, which sums it in its dgrad epilogue (strided conv1: no join)
@@ -76,6 +86,11 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        if _folded(self.bn1, self.bn2, self.bn3, self.downsample[1] if self.downsample is not None else self.bn3):
+            y = conv_bn(self.conv1, self.bn1, x)
+            y = conv_bn(self.conv2, self.bn2, y)
+            r = x if self.downsample is None else conv_bn(self.downsample[0], self.downsample[1], x, act="none")
+            return conv_bn(self.conv3, self.bn3, y, residual=r)
         t = _train_stats(self.bn1)
         # the block input's second consumer (the residual add of an identity block, the
         # downsample conv of a projection block) hands its gradient to conv1, which sums it
@@ -143,9 +158,13 @@ class ResNet(nn.Module):
     def forward_features(self, x):
         """x: NHWC [N,H,W,8] (or the s2d stem's [N,H/2,W/2,16]) -> pooled features [N, feat_dim]."""
         t = _train_stats(self.bn1)
+        fold = _folded(self.bn1)
         if self.stem_s2d and (x.shape[-1] == 16 or (x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0)):
             if x.shape[-1] != 16:
                 x = Fn.nhwc_to_s2d(x)
+            if fold:  # eval-mode / frozen stem BN: conv, then BN + ReLU + max pool in one pass
+                y, _ = Fn.stem_conv_s2d(x, self.conv1.weight, self._stem_w16, stats=False)
+                return self._forward_stages(Fn.bn_eval_act_maxpool(y, self.bn1, act="relu"))
             if (t and self.variant == "imagenet" and _FUSED_STEM[0] and self.bn1.weight is not None
                     and Fn.stem_bn_pool_fusable(x)):
                 # conv + BN + ReLU + max pool as one op with the one-pass fused backward
@@ -156,6 +175,8 @@ class ResNet(nn.Module):
                 return self._forward_stages(y)
             y, s = Fn.stem_conv_s2d(x, self.conv1.weight, self._stem_w16, stats=t)
             s = s if (t and x.is_cuda) else None
+        elif fold and self.variant == "cifar":
+            return self._forward_stages(conv_bn(self.conv1, self.bn1, x))
         else:
             y, s = self.conv1(x, stats=t)
         if self.variant == "imagenet":

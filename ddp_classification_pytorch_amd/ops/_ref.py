@@ -259,6 +259,20 @@ def bn_act(x, res, scale, shift, act, slope):
     return _act(z, act, slope).to(x.dtype)
 
 
+def conv_fwd_affine(x, w, stride, pad, scale, shift, act, slope, res):
+    """conv -> eval-mode BN (per-channel scale / shift) [+ res] -> act, through the bf16-rounded
+    conv output like the unfused chain."""
+    c, _ = conv_fwd(x, w, stride, pad, False)
+    return bn_act(c, res, scale, shift, act, slope)
+
+
+def act_scale_bwd(dy, y, scale, act, slope, want_g):
+    g = _f(dy) * _act_d(_f(y), act, slope)
+    gd = g.to(dy.dtype)
+    dc = (_f(gd) * scale.float()).to(dy.dtype)
+    return dc, (gd if want_g else torch.empty(0, dtype=dy.dtype))
+
+
 def bn_act_mask(x, res, scale, shift, act, slope):
     z = _f(x) * scale + shift
     if res is not None:

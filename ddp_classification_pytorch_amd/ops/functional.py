@@ -699,6 +699,99 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     return out
 
 
+# ----------------------------------------------------------------------------- eval-mode BN folded into the conv
+_EVAL_COEFF = weakref.WeakKeyDictionary()
+
+
+def bn_eval_coefficients(bn):
+    """(mean, invstd, scale, shift) of a BatchNorm2d's running statistics, cached until any of the
+    four source tensors changes (frozen BN recomputes nothing per step; a HIP-graph replay reads the
+    same cached tensors)."""
+    g, b, rm, rv = bn.weight, bn.bias, bn.running_mean, bn.running_var
+    key = tuple((t._version, t.data_ptr()) if t is not None else None for t in (g, b, rm, rv)) + (bn.eps,)
+    hit = _EVAL_COEFF.get(bn)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        coeff = K(rm).bn_eval_coeff(g.detach() if g is not None else None, b.detach() if b is not None else None,
+                                    rm, rv, bn.eps)
+    _EVAL_COEFF[bn] = (key, coeff)
+    return coeff
+
+
+def bn_foldable(bn) -> bool:
+    """A BN that normalises with its running statistics (model.eval(), NESTED's frozen BN) and whose
+    affine parameters need no gradient can be folded into the producing conv's epilogue."""
+    if bn.training and not bn.frozen:
+        return False
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (bn.weight, bn.bias)):
+        return False
+    return True
+
+
+class _ConvAffine(Function):
+    """y = act(conv(x) * scale + shift [+ res]) with the affine (an eval-mode BN) applied in the
+    conv's store epilogue (``conv_fwd_affine``).  Backward from the stored output: one pass
+    g = dy * act'(y), dc = g * scale (``act_scale_bwd``), then the conv's dgrad / wgrad of dc."""
+
+    @staticmethod
+    def forward(ctx, x, weight, wb, wt, stride, pad, scale, shift, act, slope, res):
+        y = K(x).conv_fwd_affine(x, wb, stride, pad, scale, shift, act, slope, res)
+        ctx.save_for_backward(x, wt, y, scale)
+        ctx.geo = (weight.shape[1], weight.shape[2], stride, pad, act, slope, res is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt, y, scale = ctx.saved_tensors
+        KH, KW, stride, pad, act, slope, has_res = ctx.geo
+        k = K(dy)
+        want_g = has_res and ctx.needs_input_grad[10]
+        dc, g = k.act_scale_bwd(dy.contiguous(), y, scale, act, slope, want_g)
+        dx = k.conv_dgrad(dc, wt, x.shape[1], x.shape[2], stride, pad) if ctx.needs_input_grad[0] else None
+        dw = k.conv_wgrad(dc, x, KH, KW, stride, pad) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None, None, None, None, None, (g if want_g else None)
+
+
+def conv_bn_folded(x, weight, stride, pad, bn, act="relu", slope=0.01, residual=None):
+    """conv -> eval-mode BN -> (+ residual) -> act as ONE conv launch (see :class:`_ConvAffine`)."""
+    _, _, scale, shift = bn_eval_coefficients(bn)
+    wb, wt = prepared_weight(weight, 0, True)
+    res = residual.contiguous() if residual is not None else None
+    return _ConvAffine.apply(x, weight, wb, wt, stride, pad, scale, shift, ACT[act], float(slope), res)
+
+
+class _BNActPoolEval(Function):
+    """Eval-mode BN + ReLU/identity + max pool (the stem tail of a frozen-BN / eval network) in one
+    pass (``bn_act_maxpool`` with running-statistics coefficients); backward: the pooled gradient
+    scattered, masked and scaled in one pass (``maxpool_bn_bwd_elemt`` with zero batch sums)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, shift, mean, invstd, act, pool):
+        y, idx = K(x).bn_act_maxpool(x, scale, shift, act, *pool)
+        ctx.save_for_backward(x, idx, scale, shift, mean, invstd)
+        ctx.act, ctx.pool = act, pool
+        ctx.mark_non_differentiable(idx)
+        ctx.set_materialize_grads(False)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, dy, _didx):
+        if dy is None or not ctx.needs_input_grad[0]:
+            return (None,) * 7
+        x, idx, scale, shift, mean, invstd = ctx.saved_tensors
+        zeros = torch.zeros(2, x.shape[-1], dtype=torch.float32, device=x.device)
+        dx = K(dy).maxpool_bn_bwd_elemt(dy.contiguous(), idx, x, scale, shift, mean, invstd, ctx.act, zeros, 1.0,
+                                        *ctx.pool)
+        return dx, None, None, None, None, None, None
+
+
+def bn_eval_act_maxpool(x, bn, act="relu", k=3, s=2, p=1):
+    mean, invstd, scale, shift = bn_eval_coefficients(bn)
+    y, _ = _BNActPoolEval.apply(x, scale, shift, mean, invstd, ACT[act], (k, s, p))
+    return y
+
+
 class _BNActPool(Function):
     """Training-mode BN + ReLU/identity + k x k max pool (the ResNet stem tail) without the
     full-resolution activation: forward pools act(bn(x)) on the fly; backward gathers the

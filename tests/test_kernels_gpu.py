@@ -956,3 +956,36 @@ def test_conv_dgrad_bn_leaky(K, k, add):
                                 mean, invstd, 2, None, 1e-3)
     assert relerr(g, gr) < 1e-2
     assert relerr(s, sr) < 2e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 56, 56, 64, 256, 1, 1, 0), (2, 28, 28, 128, 128, 3, 1, 1),
+                                   (2, 56, 56, 128, 128, 3, 2, 1), (2, 28, 28, 256, 512, 1, 2, 0),
+                                   (3, 9, 11, 64, 72, 3, 1, 1), (2, 7, 7, 512, 2048, 1, 1, 0)])
+@pytest.mark.parametrize("act,res", [(1, False), (1, True), (0, False), (2, False)])
+def test_conv_fwd_affine_folded_bn(K, shape, act, res):
+    """Eval-mode BN folded into the conv store epilogue == conv -> bf16 -> BN apply (+res) -> act."""
+    N, H, W, Ci, Co, k, s, p = shape
+    x = rnd(N, H, W, Ci)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
+    scale = torch.rand(Co) + 0.5
+    shift = torch.randn(Co) * 0.2
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    r = rnd(N, Ho, Wo, Co) if res else None
+    y = K.conv_fwd_affine(x.to(DEV), w.to(DEV), s, p, scale.to(DEV), shift.to(DEV), act, 0.1,
+                          r.to(DEV) if res else None)
+    c, _ = K.conv_fwd(x.to(DEV), w.to(DEV), s, p, False)  # the unfused chain's bf16 conv output
+    yr = _ref.bn_act(c.cpu().float(), r.float() if res else None, scale, shift, act, 0.1)
+    assert y.shape == yr.shape
+    assert relerr(y, yr) < 5e-3
+
+
+@pytest.mark.parametrize("act,want_g", [(1, True), (1, False), (0, False), (2, True)])
+def test_act_scale_bwd(K, act, want_g):
+    M, C = 3000, 256
+    dy, y = rnd(M, C), rnd(M, C)
+    scale = torch.rand(C) + 0.5
+    dc, g = K.act_scale_bwd(dy.to(DEV), y.to(DEV), scale.to(DEV), act, 0.1, want_g)
+    dcr, gr = _ref.act_scale_bwd(dy.float(), y.float(), scale, act, 0.1, want_g)
+    assert relerr(dc, dcr) < 5e-3
+    if want_g:
+        assert relerr(g, gr) < 5e-3

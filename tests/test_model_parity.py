@@ -104,3 +104,77 @@ def test_gpu_training_reduces_loss_like_mirror():
         o2.step()
     assert h1[-1] < 0.5 * h1[0], h1
     assert abs(h1[-1] - h2[-1]) < 0.25 * max(h2[-1], 0.2), (h1, h2)
+
+
+def _frozen_copy(m, seed=3):
+    """Non-trivial running statistics / affine, BN frozen (NESTED freeze_bn: eval + no affine grad)."""
+    from ddp_classification_pytorch_amd.models.layers import BatchNorm2d
+
+    g = torch.Generator().manual_seed(seed)
+    for mod in m.modules():
+        if isinstance(mod, BatchNorm2d):
+            C = mod.num_features
+            with torch.no_grad():
+                mod.running_mean.copy_(torch.randn(C, generator=g) * 0.1)
+                mod.running_var.copy_(torch.rand(C, generator=g) * 0.5 + 0.75)
+                mod.weight.copy_(torch.rand(C, generator=g) * 0.5 + 0.5)
+                mod.bias.copy_(torch.randn(C, generator=g) * 0.1)
+            mod.eval()
+            mod.weight.requires_grad_(False)
+            mod.bias.requires_grad_(False)
+    return m
+
+
+def _run_frozen(model, imgs, labels, ours):
+    if ours:
+        logits = model(Fn.to_device_nhwc(imgs, cpad=8, nchw=True))
+        loss = Fn.cross_entropy(logits, labels)
+    else:
+        logits = mirror_forward(model, imgs, training=False)
+        loss = torch.nn.functional.cross_entropy(logits.float(), labels)
+    loss.backward()
+    return loss.detach(), logits.detach()
+
+
+def _conv_grads(m):
+    return torch.cat([p.grad.detach().double().flatten().cpu() for p in m.parameters() if p.grad is not None])
+
+
+@pytest.mark.parametrize("name,size", [("cifar_resnet18", 32), ("resnet50", 64), ("resnet18", 64)])
+def test_cpu_frozen_bn_folded_matches_mirror(name, size):
+    """Frozen BN folded into the conv epilogues (layers.conv_bn, eval-mode stem pool): the CPU
+    reference-math path equals an fp64 eval-BN mirror (NESTED/model/model.py:44-55)."""
+    torch.manual_seed(0)
+    m1 = _frozen_copy(build_model(name, num_classes=10))
+    m2 = copy.deepcopy(m1)
+    m3 = copy.deepcopy(m1).double()
+    imgs = torch.randn(4, 3, size, size)
+    labels = torch.randint(0, 10, (4,))
+    l1, o1 = _run_frozen(m1, imgs, labels, True)
+    _run_frozen(m2, imgs, labels, False)
+    l3, o3 = _run_frozen(m3, imgs.double(), labels, False)
+    assert relerr(o1, o3) < 1e-4 and abs(l1.item() - l3.item()) < 1e-4
+    e_ours, e_mirror = relerr(_conv_grads(m1), _conv_grads(m3)), relerr(_conv_grads(m2), _conv_grads(m3))
+    assert e_ours < max(3 * e_mirror, 1e-4), (e_ours, e_mirror)  # fp32 noise floor of this net
+    assert all(b.grad is None for n, b in m1.named_parameters() if "bn" in n or "downsample.1" in n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,size,batch", [("resnet50", 112, 16), ("resnet18", 64, 8)])
+def test_gpu_frozen_bn_folded_as_accurate_as_torch_bf16(name, size, batch):
+    """GPU folded path (conv_fwd_affine + act_scale_bwd, no BN pass) vs the fp64 frozen-BN mirror,
+    at least as close as stock PyTorch bf16 autocast of the same net."""
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    m1 = _frozen_copy(build_model(name, num_classes=100)).to(dev)
+    m_ref = copy.deepcopy(m1).double()
+    m_bf = copy.deepcopy(m1)
+    imgs = torch.randn(batch, 3, size, size, device=dev)
+    labels = torch.randint(0, 100, (batch,), device=dev)
+    _, o1 = _run_frozen(m1, imgs, labels, True)
+    _, o3 = _run_frozen(m_ref, imgs.double(), labels, False)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, ob = _run_frozen(m_bf, imgs, labels, False)
+    assert relerr(o1, o3) <= 1.25 * relerr(ob, o3) + 1e-2, (relerr(o1, o3), relerr(ob, o3))
+    g1, gb, g3 = _conv_grads(m1), _conv_grads(m_bf), _conv_grads(m_ref)
+    assert relerr(g1, g3) <= 1.25 * relerr(gb, g3) + 1e-3, (relerr(g1, g3), relerr(gb, g3))

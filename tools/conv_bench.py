@@ -68,7 +68,11 @@ def main():
     tot = {"ours": [0, 0, 0], "miopen": [0, 0, 0]}
     rows = []
     print(f"{'shape':34s} {'fwd us':>8s} {'TF':>6s} {'dgrad':>8s} {'TF':>6s} {'wgrad':>8s} {'TF':>6s} | "
-          f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s}")
+          f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s} | roofline us f/d/w (eff %)")
+    # roofline: minimum HBM bytes (each operand once; a strided 1x1 reads 1/s^2 of its input) at
+    # 5.5 TB/s against the MFMA at 2.0 PF/s (bf16 dense at the clock the chip holds under load)
+    HBM, MFMA = 5.5e12, 2.0e15
+    ideal_tot = [0.0, 0.0, 0.0]
     only = {int(i) for i in a.only.split(",")} if a.only else None
     for idx, (Ci, Co, k, s, H, cnt) in enumerate(R50):
         if only is not None and idx not in only:
@@ -96,8 +100,16 @@ def main():
                 dyc, xc, wc, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [False, True, False]), a.iters)
         tf = lambda t: flop / t / 1e6 if t > 0 else 0.0  # noqa: E731
         name = f"{Ci}->{Co} k{k} s{s} {H}->{Ho} x{cnt}"
+        xin = N * H * H * Ci * 2 / (s * s if k == 1 else 1)
+        yout = N * Ho * Ho * Co * 2
+        ideal = [max((xin + yout) / HBM, flop / MFMA) * 1e6 for _ in range(3)]
+        ideal[1] = max((N * H * H * Ci * 2 + yout) / HBM, flop / MFMA) * 1e6 if Ci > 8 else 0.0
+        eff = [100.0 * i / t if t > 0 else 0.0 for i, t in zip(ideal, (t_f, t_d, t_w))]
+        for j in range(3):
+            ideal_tot[j] += cnt * ideal[j]
         print(f"{name:34s} {t_f:8.1f} {tf(t_f):6.0f} {t_d:8.1f} {tf(t_d):6.0f} {t_w:8.1f} {tf(t_w):6.0f} | "
-              f"{mi[0]:8.1f} {mi[1]:8.1f} {mi[2]:8.1f}", flush=True)
+              f"{mi[0]:8.1f} {mi[1]:8.1f} {mi[2]:8.1f} | {ideal[0]:6.0f} {ideal[1]:6.0f} {ideal[2]:6.0f} "
+              f"({eff[0]:3.0f} {eff[1]:3.0f} {eff[2]:3.0f})", flush=True)
         for i, t in enumerate((t_f, t_d, t_w)):
             tot["ours"][i] += cnt * t
         for i, t in enumerate(mi):
@@ -105,6 +117,8 @@ def main():
         rows.append(dict(shape=name, flop=flop, ours=[t_f, t_d, t_w], miopen=mi, count=cnt))
     print("per-step totals (ms): ours fwd/dgrad/wgrad = " + "/".join(f"{v / 1e3:.2f}" for v in tot["ours"]) +
           f" sum {sum(tot['ours']) / 1e3:.2f}")
+    print("                      roofline          = " + "/".join(f"{v / 1e3:.2f}" for v in ideal_tot) +
+          f" sum {sum(ideal_tot) / 1e3:.2f}")
     if not a.no_miopen:
         print("                      miopen            = " + "/".join(f"{v / 1e3:.2f}" for v in tot["miopen"]) +
               f" sum {sum(tot['miopen']) / 1e3:.2f}")

@@ -10,6 +10,7 @@
 #   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
 #   sweep           headline batch sweep 128..2048
+#   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
 set -e
 set -o pipefail
 T=${1:?tag}; shift
@@ -57,6 +58,9 @@ for step in "$@"; do
         timeout -k 10 240 python -u bench.py --batch $b --steps 10 --warmup 3 > $O/sweep_b$b.log 2>&1
         tail -1 $O/sweep_b$b.log
       done ;;
+    convbench)
+      timeout -k 10 400 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen > $O/conv_bench_b1024.txt 2>&1
+      tail -3 $O/conv_bench_b1024.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
