@@ -25,7 +25,6 @@ import time
 import numpy as np
 import torch
 import torch.distributed as dist
-import torch.nn.functional as F
 
 from ..engine.checkpoint import is_rank0, load_checkpoint
 from ..engine.logger import MetricsLogger
@@ -53,7 +52,7 @@ def _step(net_feat, net_cls, opts, x, y, dist_k, dropout, nb_cls, rng):
         k = int(rng.choice(len(dist_k), p=dist_k))
         feature = Fn.nested_mask(feature, k)
     elif dropout > 0:
-        feature = F.dropout(feature.float(), p=dropout, training=True).to(feature.dtype)
+        feature = Fn.dropout(feature, p=dropout, training=True)
     out = net_cls(feature)
     loss, rank = Fn.cross_entropy(out, y, nb_cls, return_rank=True)
     loss.backward()

@@ -171,6 +171,52 @@ std::tuple<Tensor, Tensor> act_scale_bwd(const Tensor& dy, const Tensor& y, cons
   return {dc, g};
 }
 
+// Philox dropout: (y, used) -- `offset` int64[1] device call counter (bumped here after the launch,
+// graph-capturable), `used` int64[1] receives the counter value the mask was drawn with
+std::tuple<Tensor, Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, const Tensor& offset) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "dropout: bf16 or fp32");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: p in [0, 1)");
+  CHECK_DEV(offset);
+  TORCH_CHECK(offset.scalar_type() == at::kLong && offset.numel() == 1, "dropout: offset int64[1]");
+  auto y = at::empty_like(x);
+  auto used = at::empty({1}, offset.options());
+  dcp::launch_dropout(x.data_ptr(), y.data_ptr(), x.numel(), x.scalar_type() == at::kBFloat16, (float)p,
+                      (uint64_t)seed, offset.data_ptr<int64_t>(), used.data_ptr<int64_t>(), cur_stream());
+  offset.add_(1);
+  return {y, used};
+}
+
+// the same mask (same seed and the forward's `used` offset) applied to the gradient
+Tensor dropout_bwd(const Tensor& dy, double p, int64_t seed, const Tensor& used) {
+  CHECK_DEV(dy);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat, "dropout: bf16 or fp32");
+  TORCH_CHECK(used.scalar_type() == at::kLong && used.numel() == 1 && used.is_cuda(), "dropout: used int64[1]");
+  auto g = dy.contiguous();
+  auto dx = at::empty_like(g);
+  dcp::launch_dropout(g.data_ptr(), dx.data_ptr(), g.numel(), g.scalar_type() == at::kBFloat16, (float)p,
+                      (uint64_t)seed, used.data_ptr<int64_t>(), nullptr, cur_stream());
+  return dx;
+}
+
+// adaptive average pool NHWC x [N,H,W,C] -> [N,OH,OW,C]
+Tensor adaptive_avg_pool(const Tensor& x, int64_t OH, int64_t OW) {
+  CHECK_ACT(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0 && OH > 0 && OW > 0, "adaptive_avg_pool shapes");
+  auto y = at::empty({x.size(0), OH, OW, x.size(3)}, x.options());
+  dcp::launch_adaptive_avg(bp(x), bpm(y), x.size(0), x.size(1), x.size(2), x.size(3), OH, OW, false, cur_stream());
+  return y;
+}
+
+Tensor adaptive_avg_pool_bwd(const Tensor& dy, int64_t H, int64_t W) {
+  CHECK_ACT(dy);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(3) % 8 == 0 && H > 0 && W > 0, "adaptive_avg_pool_bwd shapes");
+  auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  dcp::launch_adaptive_avg(bp(dy), bpm(dx), dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2), true, cur_stream());
+  return dx;
+}
+
 // forward with an explicit output grid (asymmetric padding: output (oy, ox) reads input rows
 // oy*stride + kh - pad, columns ox*stride + kw - pad; out-of-range taps read zeros)
 std::tuple<Tensor, Tensor> conv_fwd_geo(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad, int64_t Ho,
@@ -742,10 +788,12 @@ std::tuple<Tensor, Tensor> bn2_act_mask(const Tensor& x, const Tensor& res, cons
 }
 
 Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& res, const Tensor& scale,
-                     const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act, double slope) {
+                     const Tensor& shift, const Tensor& mean, const Tensor& invstd, int64_t act, double slope,
+                     bool inv) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
+  TORCH_CHECK(!inv || ((act == 0 || act == 2) && !res.has_value()), "bn_bwd_reduce: inv needs an invertible act");
   TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_reduce shapes");
   if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "residual shape");
   const int M = x.numel() / C;
@@ -753,24 +801,25 @@ Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& 
   auto out = at::empty({2, C}, f32_like(x));
   dcp::launch_bn_bwd_reduce(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
                             shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, C, act,
-                            (float)slope, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+                            (float)slope, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream(), inv ? 1 : 0);
   return out;
 }
 
 std::tuple<Tensor, Tensor> bn_bwd_elemt(const Tensor& dy, const Tensor& x, const optional<Tensor>& res,
                                         const Tensor& scale, const Tensor& shift, const Tensor& mean,
                                         const Tensor& invstd, const optional<Tensor>& sums, double count, int64_t act,
-                                        double slope, bool want_dres) {
+                                        double slope, bool want_dres, bool inv) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
+  TORCH_CHECK(!inv || ((act == 0 || act == 2) && !res.has_value()), "bn_bwd_elemt: inv needs an invertible act");
   TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_elemt shapes");
   auto dx = at::empty_like(x);
   Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
   dcp::launch_bn_bwd_elemt(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
                            shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), fp(sums),
                            (float)(1.0 / count), x.numel(), C, act, (float)slope, bpm(dx),
-                           want_dres ? bpm(dres) : nullptr, cur_stream());
+                           want_dres ? bpm(dres) : nullptr, cur_stream(), inv ? 1 : 0);
   return {dx, dres};
 }
 
@@ -1313,11 +1362,11 @@ TORCH_LIBRARY(dcp, m) {
         &bn_act_mask);
   m.def(
       "bn_bwd_reduce(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, int "
-      "act, float slope) -> Tensor",
+      "act, float slope, bool inv=False) -> Tensor",
       &bn_bwd_reduce);
   m.def(
       "bn_bwd_elemt(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, "
-      "Tensor? sums, float count, int act, float slope, bool want_dres) -> (Tensor, Tensor)",
+      "Tensor? sums, float count, int act, float slope, bool want_dres, bool inv=False) -> (Tensor, Tensor)",
       &bn_bwd_elemt);
   m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)", &maxpool_fwd);
   m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int p) -> Tensor", &maxpool_bwd);
@@ -1388,5 +1437,9 @@ TORCH_LIBRARY(dcp, m) {
       &conv_fwd_affine);
   m.def("act_scale_bwd(Tensor dy, Tensor y, Tensor scale, int act, float slope, bool want_g) -> (Tensor, Tensor)",
         &act_scale_bwd);
+  m.def("dropout_fwd(Tensor x, float p, int seed, Tensor(a!) offset) -> (Tensor, Tensor)", &dropout_fwd);
+  m.def("dropout_bwd(Tensor dy, float p, int seed, Tensor used) -> Tensor", &dropout_bwd);
+  m.def("adaptive_avg_pool(Tensor x, int OH, int OW) -> Tensor", &adaptive_avg_pool);
+  m.def("adaptive_avg_pool_bwd(Tensor dy, int H, int W) -> Tensor", &adaptive_avg_pool_bwd);
   m.def("cdr_mask(Tensor table, Tensor chunks, Tensor state, float clip) -> ()", &cdr_mask);
 }

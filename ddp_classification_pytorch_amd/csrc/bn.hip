@@ -40,6 +40,11 @@ __device__ __forceinline__ float act_d(float z, int act, float slope) {
   return 1.f;
 }
 
+// pre-activation from the activation output (invertible activations only: identity, leaky ReLU)
+__device__ __forceinline__ float act_inv(float y, int act, float slope) {
+  return (act == 2 && y < 0.f) ? y / slope : y;
+}
+
 // Chan et al. pairwise merge of (n, mean, M2) accumulators
 struct Welford {
   float n, mean, m2;
@@ -412,7 +417,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restri
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, int M, int C,
-                                                            float slope, float* __restrict__ out) {
+                                                            float slope, float* __restrict__ out, int inv) {
+  // inv (InplaceABN backward, X3/K21): x holds the layer's OUTPUT y = act(z); z = act^-1(y) is
+  // recovered in registers and mean / invstd carry beta / 1/gamma, so xhat = (z - beta) / gamma --
+  // the BN input itself is never stored
   const RowTile t(C);
   float s1[8], s2[8], sc[8], sh[8], mu[8], is[8];
 #pragma unroll
@@ -438,9 +446,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restri
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float xv = bf2f(v[u][k]);
+          float xv = bf2f(v[u][k]);
           float z = xv * sc[k] + sh[k];
           if (RES) z += bf2f(r[u][k]);
+          if (inv) xv = z = act_inv(bf2f(v[u][k]), ACT, slope);
           const float dz = bf2f(g[u][k]) * act_d(z, ACT, slope);
           s1[k] += dz;
           s2[k] += dz * (xv - mu[k]);
@@ -454,9 +463,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16* __restri
       if (RES) r = *(const bf16x8*)(res + off);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float xv = bf2f(v[k]);
+        float xv = bf2f(v[k]);
         float z = xv * sc[k] + sh[k];
         if (RES) z += bf2f(r[k]);
+        if (inv) xv = z = act_inv(bf2f(v[k]), ACT, slope);
         const float dz = bf2f(g[k]) * act_d(z, ACT, slope);
         s1[k] += dz;
         s2[k] += dz * (xv - mu[k]);
@@ -497,7 +507,9 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ sums, float inv_count, int M,
                                                            int C, float slope, bf16* __restrict__ dx,
-                                                           bf16* __restrict__ dres) {
+                                                           bf16* __restrict__ dres, int inv) {
+  // inv: InplaceABN backward from the output y (see bn_bwd_reduce_kernel); mean / invstd = beta /
+  // 1/gamma, scale = the true gamma * invstd
   const RowTile t(C);
   if (t.slot >= t.rpi) return;
   float sc[8], sh[8], ca[8], cb[8], cc[8];
@@ -531,9 +543,10 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
     bf16x8 o, od;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float xv = bf2f(v[k]);
+      float xv = bf2f(v[k]);
       float z = xv * sc[k] + sh[k];
       if (RES) z += bf2f(r[k]);
+      if (inv) xv = z = act_inv(bf2f(v[k]), ACT, slope);
       const float dz = bf2f(g[k]) * act_d(z, ACT, slope);
       od[k] = f2bf(dz);
       o[k] = f2bf(ca[k] * dz + cb[k] * xv + cc[k]);
@@ -763,20 +776,20 @@ int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }
 // partials must hold bn_bwd_reduce_blocks(M, C) x 2 x C floats; out [2][C]
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,
-                          float* out, hipStream_t s) {
+                          float* out, hipStream_t s, int inv) {
   const int g = bn_bwd_reduce_blocks(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, dim3(g), 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean,
-                       invstd, M, C, slope, partials);
+                       invstd, M, C, slope, partials, inv);
   hipLaunchKernelGGL(partial_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, partials, g, 2 * C, out);
 }
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
-                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s) {
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv) {
   const int M = (int)(numel / C);
   const dim3 grid = ew_grid(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_elemt_kernel, grid, 0, s, res, act, dy, x, res, scale, shift, mean, invstd, sums,
-                       inv_count, M, C, slope, dx, dres);
+                       inv_count, M, C, slope, dx, dres, inv);
 }
 
 

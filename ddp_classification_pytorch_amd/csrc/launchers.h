@@ -150,10 +150,12 @@ void launch_bn2_bwd_elemt(const bf16* dy, const bf16* x, const bf16* r, const fl
 int bn_bwd_reduce_blocks(int M, int C);
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                           const float* mean, const float* invstd, int M, int C, int act, float slope, float* partials,
-                          float* out, hipStream_t s);
+                          float* out, hipStream_t s, int inv = 0);
+// inv = 1: InplaceABN backward -- x is the layer OUTPUT y (act invertible: none / leaky), mean /
+// invstd are beta / 1/gamma, and the pre-activation is recovered in registers
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
-                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s);
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv = 0);
 
 void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
                         int s, int p, hipStream_t st, const float* scale = nullptr, const float* shift = nullptr,
@@ -238,6 +240,13 @@ void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int 
 void launch_crop_resize(const uint8_t* src, const int64_t* meta, int B, int Ho, int Wo, uint8_t* out, hipStream_t s);
 void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
+// Philox dropout (misc.hip): y = x * keep / (1 - p); keep from (seed, *offset_ptr, element index);
+// `used` (optional) receives the offset the launch drew with (for the mask-regenerating backward)
+void launch_dropout(const void* x, void* y, size_t n, int is_bf16, float p, uint64_t seed, const int64_t* offset_ptr,
+                    int64_t* used, hipStream_t s);
+// adaptive average pool NHWC [N,H,W,C] -> [N,OH,OW,C]; backward = true: dy [N,OH,OW,C] -> dx [N,H,W,C]
+void launch_adaptive_avg(const bf16* src, bf16* dst, int N, int H, int W, int C, int OH, int OW, bool backward,
+                         hipStream_t s);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
                         hipStream_t s);
 

@@ -340,4 +340,74 @@ void launch_nested_eval(const float* feat, const float* W, const int64_t* labels
   hipLaunchKernelGGL(nested_eval_kernel, dim3(B), dim3(256), 0, s, feat, W, labels, D, C, counts);
 }
 
+
+// ---------------------------------------------------------------------------
+// Dropout (NESTED --dropout, NESTED/train.py:252; VGG classifier) with a
+// counter-based Philox-4x32-10 mask: element i of call `offset` keeps iff the uniform drawn from
+// counter (i / 4, 0, offset) under key `seed` is >= p.  The backward regenerates the same mask
+// from (seed, offset) -- nothing is stored.  The call offset lives in a device counter the
+// launcher bumps after the kernel (so a HIP-graph replay draws a fresh mask every replay); the
+// kernel copies the value it used to `used` for the backward.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
+    const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_f(const T* p, size_t i) {
+  if constexpr (sizeof(T) == 2) return bf2f(((const bf16*)p)[i]);
+  else return ((const float*)p)[i];
+}
+template <typename T>
+__device__ __forceinline__ void st_f(T* p, size_t i, float v) {
+  if constexpr (sizeof(T) == 2) ((bf16*)p)[i] = f2bf(v);
+  else ((float*)p)[i] = v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_kernel(const T* __restrict__ x, T* __restrict__ y, size_t n, float p,
+                                                      uint64_t seed, const int64_t* __restrict__ offset_ptr,
+                                                      int64_t* __restrict__ used) {
+  const uint64_t off = (uint64_t)*offset_ptr;
+  if (used && blockIdx.x == 0 && threadIdx.x == 0) *used = (int64_t)off;
+  const float scale = 1.f / (1.f - p);
+  const size_t n4 = (n + 3) / 4;
+  for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (size_t)gridDim.x * 256) {
+    uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)off, (uint32_t)(off >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t i = q * 4 + e;
+      if (i < n) {
+        const float u = (float)(c[e] >> 8) * (1.f / 16777216.f);
+        st_f(y, i, u >= p ? ld_f(x, i) * scale : 0.f);
+      }
+    }
+  }
+}
+
+void launch_dropout(const void* x, void* y, size_t n, int is_bf16, float p, uint64_t seed, const int64_t* offset_ptr,
+                    int64_t* used, hipStream_t s) {
+  size_t g = ((n + 3) / 4 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  if (is_bf16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, dim3((int)g), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n, p, seed,
+                       offset_ptr, used);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, dim3((int)g), dim3(256), 0, s, (const float*)x, (float*)y, n, p, seed,
+                       offset_ptr, used);
+}
+
 }  // namespace dcp

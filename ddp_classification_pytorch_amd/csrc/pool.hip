@@ -424,4 +424,86 @@ void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int i
   hipLaunchKernelGGL(s2d_kernel, dim3(ew_grid2(total)), dim3(256), 0, st, x, y, N, H, W, C, b, inverse);
 }
 
+
+// ---------------------------------------------------------------------------
+// Adaptive average pool NHWC -> [N, OH, OW, C] (torchvision VGG's AdaptiveAvgPool2d((7, 7)),
+// NESTED/model/vgg.py:48): output cell (oh, ow) averages rows [floor(oh H / OH), ceil((oh+1) H / OH))
+// and the same for columns.  Backward: each input pixel gathers the cells whose window holds it.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int ad_start(int o, int I, int O) { return (o * I) / O; }
+__device__ __forceinline__ int ad_end(int o, int I, int O) { return ((o + 1) * I + O - 1) / O; }
+
+__global__ void __launch_bounds__(256) adaptive_avg_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
+                                                               int H, int W, int C, int OH, int OW) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * OH * OW * cpr;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int ow = (int)(t % OW);
+    t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    const int h0 = ad_start(oh, H, OH), h1 = ad_end(oh, H, OH), w0 = ad_start(ow, W, OW), w1 = ad_end(ow, W, OW);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) {
+        const bf16x8 v = *(const bf16x8*)(x + (((size_t)n * H + h) * W + w) * C + ch * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+      }
+    const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e] * inv);
+    *(bf16x8*)(y + (((size_t)n * OH + oh) * OW + ow) * C + ch * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) adaptive_avg_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                               int N, int H, int W, int C, int OH, int OW) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * H * W * cpr;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // cells whose window holds row h: oh in [floor(h OH / H) - 1, ...] -- scan the (few) candidates
+    const int oh_lo = max(0, (h * OH) / H - 1), oh_hi = min(OH - 1, ((h + 1) * OH) / H + 1);
+    const int ow_lo = max(0, (w * OW) / W - 1), ow_hi = min(OW - 1, ((w + 1) * OW) / W + 1);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int h0 = ad_start(oh, H, OH), h1 = ad_end(oh, H, OH);
+      if (h < h0 || h >= h1) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int w0 = ad_start(ow, W, OW), w1 = ad_end(ow, W, OW);
+        if (w < w0 || w >= w1) continue;
+        const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+        const bf16x8 g = *(const bf16x8*)(dy + (((size_t)n * OH + oh) * OW + ow) * C + ch * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(g[e]) * inv;
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+void launch_adaptive_avg(const bf16* src, bf16* dst, int N, int H, int W, int C, int OH, int OW, bool backward,
+                         hipStream_t s) {
+  const size_t total = (size_t)N * (backward ? H * W : OH * OW) * (C / 8);
+  size_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  if (backward)
+    hipLaunchKernelGGL(adaptive_avg_bwd_kernel, dim3((int)g), dim3(256), 0, s, src, dst, N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(adaptive_avg_fwd_kernel, dim3((int)g), dim3(256), 0, s, src, dst, N, H, W, C, OH, OW);
+}
+
 }  // namespace dcp

@@ -84,6 +84,15 @@ class BatchNorm2d(nn.Module):
         self.process_group = None  # set by parallel.convert_sync_batchnorm
         self.frozen = False
         self._nbt_pending = 0
+        # InplaceABN semantics (mapillary inplace_abn, used by timm's TResNet): the
+        # effective weight is |gamma| + eps and only the activation output is kept for backward
+        self.inplace_abn = False
+        self.iabn_eps = 1e-5
+
+    def _gamma(self):
+        if self.inplace_abn and self.weight is not None:
+            return self.weight.abs() + self.iabn_eps
+        return self.weight
 
     def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None, residual_bn=None):
         """``residual_bn=(bn, rslabs)``: ``residual`` is the raw input of BatchNorm2d ``bn`` (a
@@ -106,9 +115,11 @@ class BatchNorm2d(nn.Module):
                                                 group=self.process_group if stats else None)
         if stats:
             self._nbt_pending += 1  # folded into num_batches_tracked lazily (no per-step device add)
-        return Fn.batch_norm_act(x, slabs, self.weight, self.bias, self.running_mean, self.running_var, stats,
-                                 self.momentum, self.eps, act=act, slope=slope, residual=residual,
-                                 group=self.process_group if stats else None, link=link)
+        iabn = self.inplace_abn and residual is None and act in ("none", "leaky", "leaky_relu")
+        return Fn.batch_norm_act(x, slabs, self._gamma() if iabn else self.weight, self.bias, self.running_mean,
+                                 self.running_var, stats, self.momentum, self.eps, act=act, slope=slope,
+                                 residual=residual, group=self.process_group if stats else None, link=link,
+                                 iabn=iabn)
 
     def forward_pool(self, x, slabs=None, act="relu", k=3, s=2, p=1):
         """BN + act + k x k / s max pool.  Training-mode statistics with a ReLU/identity
@@ -178,11 +189,12 @@ def conv_bn(conv: Conv2d, bn: BatchNorm2d, x, act="relu", residual=None, slope=0
 class ConvBN(nn.Module):
     """conv -> BN (stats from the conv epilogue) -> act, optional residual."""
 
-    def __init__(self, cin, cout, k, stride=1, padding=None, groups=1, act="relu", slope=0.01):
+    def __init__(self, cin, cout, k, stride=1, padding=None, groups=1, act="relu", slope=0.01, inplace_abn=False):
         super().__init__()
         padding = k // 2 if padding is None else padding
         self.conv = Conv2d(cin, cout, k, stride, padding, groups)
         self.bn = BatchNorm2d(cout)
+        self.bn.inplace_abn = bool(inplace_abn)
         self.act, self.slope = act, slope
 
     def forward(self, x, residual=None):

@@ -9,9 +9,11 @@ Architecture (timm TResNet; not vendored in the reference):
   SE in layers 1-3; stride-2 blocks downsample with a stride-1 conv followed
   by an anti-aliased 3x3 blur (reflect pad; ``dwconv`` kernel); the residual
   path downsamples with AvgPool2d(2) + 1x1 conv-BN;
-* InplaceABN = BN + leaky-ReLU (slope 1e-3 inside blocks) fused in one
-  kernel with its backward recomputing the activation from the BN input
-  (no extra activation tensor kept);
+* InplaceABN = BN + leaky-ReLU (slope 1e-3 inside blocks, 1e-2 in the stem) in
+  one kernel, with inplace_abn's semantics: effective weight |gamma| + eps, and
+  only the activation OUTPUT kept -- the backward inverts the leaky ReLU and the
+  affine transform in registers (``bn_bwd_* inv``), so the BN input is freed
+  after the forward (one activation per layer less than BN + activation);
 * global average pool -> fc.
 Input: NHWC activations with 3 channels (``cpad=3``).
 """
@@ -108,7 +110,7 @@ class TBasicBlock(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, use_se=True):
         super().__init__()
-        self.conv1 = ConvBN(inplanes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK)
+        self.conv1 = ConvBN(inplanes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK, inplace_abn=True)
         self.aa = AntiAliasDownsample() if stride == 2 else None
         self.conv2 = ConvBN(planes, planes, 3, 1, act="none")
         self.se = SEModule(planes, max(planes // 4, 64)) if use_se else None
@@ -138,8 +140,8 @@ class TBottleneck(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, use_se=True):
         super().__init__()
-        self.conv1 = ConvBN(inplanes, planes, 1, 1, 0, act="leaky", slope=LEAKY_BLOCK)
-        self.conv2 = ConvBN(planes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK)
+        self.conv1 = ConvBN(inplanes, planes, 1, 1, 0, act="leaky", slope=LEAKY_BLOCK, inplace_abn=True)
+        self.conv2 = ConvBN(planes, planes, 3, 1, act="leaky", slope=LEAKY_BLOCK, inplace_abn=True)
         self.aa = AntiAliasDownsample() if stride == 2 else None
         self.se = SEModule(planes, max(planes * 4 // 8, 64)) if use_se else None
         self.conv3 = ConvBN(planes, planes * 4, 1, 1, 0, act="none")
@@ -167,7 +169,7 @@ class TResNet(nn.Module):
     def __init__(self, layers=(3, 4, 11, 3), num_classes=1000, width_factor=1.0, in_chans=3):
         super().__init__()
         self.inplanes = self.planes = int(64 * width_factor)
-        self.stem = ConvBN(in_chans * 16, self.planes, 3, 1, act="leaky", slope=LEAKY_STEM)
+        self.stem = ConvBN(in_chans * 16, self.planes, 3, 1, act="leaky", slope=LEAKY_STEM, inplace_abn=True)
         self.layer1 = self._make(TBasicBlock, self.planes, layers[0], 1, True)
         self.layer2 = self._make(TBasicBlock, self.planes * 2, layers[1], 2, True)
         self.layer3 = self._make(TBottleneck, self.planes * 4, layers[2], 2, True)

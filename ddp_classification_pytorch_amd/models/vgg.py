@@ -1,16 +1,18 @@
 """VGG19-bn and its NESTED feature net (NESTED/model/vgg.py:10-75; dead code in
 the reference, provided for capability parity).
 
-Convolutions/BN/ReLU/max-pool run on the gfx950 kernels (NHWC); the
-classifier flattens in NHWC (H, W, C) order, so torchvision classifier
-weights would need a column permutation.  ``VGGNetFeat`` exposes the split
-classifier of the reference: features -> fc1 -> ReLU -> [mask / dropout
-point] -> fc2 -> ReLU, feature dim 4096.
+Convolutions/BN/ReLU/max-pool run on the gfx950 kernels (NHWC); an adaptive
+7x7 average pool (torchvision's ``AdaptiveAvgPool2d((7, 7))``, identity at 224 px)
+precedes the classifier, which flattens in NHWC (H, W, C) order, so torchvision
+classifier weights would need a column permutation.  Dropout is the Philox HIP
+kernel (``Fn.dropout``).  ``VGGNetFeat`` is the reference's split classifier:
+features -> avgpool -> fc1 -> ReLU -> [x * mask1] -> [dropout1] -> fc2 -> ReLU ->
+[dropout2], feature dim 4096; its dropouts exist only when ``vgg_dropout > 0``
+(the reference skips torchvision's p = 0.5 dropouts otherwise, NESTED/model/vgg.py:20-30).
 """
 from __future__ import annotations
 
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops import functional as Fn
 from .layers import ConvBN, Linear
@@ -44,16 +46,21 @@ class VGG(nn.Module):
             else:
                 x = self.convs[k](x)
                 k += 1
-        if x.shape[1] != 7 or x.shape[2] != 7:
-            raise ValueError("VGG classifier expects a 7x7 feature map (224px input)")
+        x = Fn.adaptive_avg_pool2d(x, 7, 7)
         return x.reshape(x.shape[0], -1)
 
-    def _drop(self, h):
-        return F.dropout(h, self.dropout, self.training) if self.dropout > 0 else h
+    def _drop(self, h, p=None):
+        p = self.dropout if p is None else p
+        return Fn.dropout(h, p, self.training) if p > 0 else h
 
-    def forward_features(self, x):
-        h = self._drop(self.fc1(self.forward_conv(x), relu=True))
-        return self._drop(self.fc2(h, relu=True))
+    def forward_features(self, x, mask1=None, dropout=None):
+        """``mask1``: multiplied into the fc1 activations (NESTED's mask point); ``dropout``:
+        overrides the classifier dropout probability (the reference NetFeat's ``vgg_dropout``)."""
+        h = self.fc1(self.forward_conv(x), relu=True)
+        if mask1 is not None:
+            h = h * mask1.to(h.dtype)
+        h = self._drop(h, dropout)
+        return self._drop(self.fc2(h, relu=True), dropout)
 
     def forward(self, x):
         f = self.forward_features(x)
@@ -65,12 +72,32 @@ def vgg19_bn(num_classes=1000, **kw):
 
 
 class VGGNetFeat(nn.Module):
-    """NESTED/model/vgg.py NetFeat: features + first classifier layers (dim 4096)."""
+    """NESTED/model/vgg.py NetFeat: features + first classifier layers (dim 4096), ``forward(x,
+    mask1=None)``, dropout only when ``vgg_dropout > 0``, ``train(mode, freeze_bn)``."""
 
-    def __init__(self, pretrained=None):
+    def __init__(self, pretrained=None, vgg_dropout=0.0):
         super().__init__()
         self.net = vgg19_bn(num_classes=0)
+        self.vgg_dropout = float(vgg_dropout)
         self.feat_dim = 4096
+        self.freeze_bn = False
+        if pretrained:
+            from .pretrained import load_pretrained
 
-    def forward(self, x):
-        return self.net.forward_features(x)
+            load_pretrained(self.net, pretrained)
+
+    def train(self, mode=True, freeze_bn=False):
+        from .layers import BatchNorm2d
+
+        super().train(mode)
+        self.freeze_bn = freeze_bn
+        if freeze_bn:
+            for m in self.modules():
+                if isinstance(m, BatchNorm2d):
+                    m.eval()
+                    m.weight.requires_grad_(False)
+                    m.bias.requires_grad_(False)
+        return self
+
+    def forward(self, x, mask1=None):
+        return self.net.forward_features(x, mask1=mask1, dropout=self.vgg_dropout)

@@ -286,8 +286,17 @@ def bn2_act_mask(x, res, scale, shift, rscale, rshift, act, slope):
     return bn_act_mask(x, _f(res) * rscale + rshift, scale, shift, act, slope)
 
 
-def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope):
-    z = _f(x) * scale + shift
+def _act_inv(y, act, slope):
+    y = _f(y)
+    return torch.where(y < 0, y / slope, y) if act == ACT_LEAKY else y
+
+
+def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope, inv=False):
+    if inv:  # InplaceABN: x is the output y; mean / invstd carry beta / 1/gamma
+        x = _act_inv(x, act, slope)
+        z = x
+    else:
+        z = _f(x) * scale + shift
     if res is not None:
         z = z + _f(res)
     dz = _rows(dy * 1.0) * _act_d(z, act, slope).reshape(-1, x.shape[-1])
@@ -295,7 +304,14 @@ def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope):
     return torch.stack([dz.sum(0), (dz * xh).sum(0)])
 
 
-def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope, want_dres):
+def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope, want_dres, inv=False):
+    if inv:  # InplaceABN: x is the output y; mean / invstd carry beta / 1/gamma
+        x = _act_inv(x, act, slope)
+        z = x
+        dz = _f(dy) * _act_d(z, act, slope)
+        xh = (x - mean) * invstd
+        dx = scale * (dz - sums[0] / count - xh * sums[1] / count) if sums is not None else scale * dz
+        return dx.to(dy.dtype), (dz.to(dy.dtype) if want_dres else dy.new_empty(0))
     z = _f(x) * scale + shift
     if res is not None:
         z = z + _f(res)
@@ -592,3 +608,33 @@ def arcface_bwd(cosv, labels, C, s, m, easy, dphi, grad_out, scale):
 
 def transpose2d(x):
     return x.t().contiguous()
+
+
+# ----------------------------------------------------------------------------- dropout / adaptive pool
+def _drop_mask(shape, p, seed, offset, device):
+    g = torch.Generator().manual_seed((int(seed) * 1000003 + int(offset)) & ((1 << 63) - 1))
+    return (torch.rand(shape, generator=g) >= p).to(device)
+
+
+def dropout_fwd(x, p, seed, offset):
+    used = offset.clone()
+    y = (_f(x) * _drop_mask(x.shape, p, seed, int(used.item()), x.device) / (1.0 - p)).to(x.dtype)
+    offset.add_(1)
+    return y, used
+
+
+def dropout_bwd(dy, p, seed, used):
+    return (_f(dy) * _drop_mask(dy.shape, p, seed, int(used.item()), dy.device) / (1.0 - p)).to(dy.dtype)
+
+
+def adaptive_avg_pool(x, oh, ow):
+    return _nhwc(F.adaptive_avg_pool2d(_nchw(_f(x)), (oh, ow))).to(x.dtype)
+
+
+def adaptive_avg_pool_bwd(dy, H, W):
+    N, OH, OW, C = dy.shape
+    xin = torch.zeros(N, C, H, W, dtype=torch.float64, requires_grad=True)
+    with torch.enable_grad():  # called from an autograd backward, where grad mode is off
+        y = F.adaptive_avg_pool2d(xin, (OH, OW))
+        y.backward(_nchw(dy.double()))
+    return _nhwc(xin.grad).to(dy.dtype)

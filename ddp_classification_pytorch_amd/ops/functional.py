@@ -448,9 +448,9 @@ def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
 
 # ----------------------------------------------------------------------------- batch norm (+act, +residual)
 class BNConfig:
-    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world")
+    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world", "iabn")
 
-    def __init__(self, training_stats, momentum, eps, act, slope, group, world):
+    def __init__(self, training_stats, momentum, eps, act, slope, group, world, iabn=False):
         self.training_stats = training_stats
         self.momentum = momentum
         self.eps = eps
@@ -458,6 +458,7 @@ class BNConfig:
         self.slope = slope
         self.group = group
         self.world = world
+        self.iabn = iabn  # InplaceABN: backward from the output (see _BNAct)
 
 
 def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
@@ -491,7 +492,13 @@ class _BNAct(Function):
             y, mask = k.bn_act_mask(x, res, scale, shift, cfg.act, cfg.slope)
         else:
             y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
-        ctx.save_for_backward(x, res, gamma, scale, shift, mean, invstd)
+        if cfg.iabn:
+            # InplaceABN (mapillary inplace_abn, X3/K21): keep only the output.  The BN input x is
+            # not saved (the consumer conv saves y anyway), so one activation per layer is freed;
+            # backward recovers z = act^-1(y) and xhat = (z - beta) / gamma in registers.
+            ctx.save_for_backward(y, None, gamma, scale, shift, beta, invstd)
+        else:
+            ctx.save_for_backward(x, res, gamma, scale, shift, mean, invstd)
         ctx.cfg = cfg
         ctx.count = count
         ctx.has_res = res is not None
@@ -512,6 +519,24 @@ class _BNAct(Function):
         if src is not None:
             src.release()
         want_dres = ctx.has_res and ctx.needs_input_grad[4]
+        if cfg.iabn:
+            y, beta = x, mean  # saved (y, beta) in place of (x, mean)
+            rgamma = torch.reciprocal(gamma.detach().float())
+            need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+            local = sums = None
+            if cfg.training_stats or need_affine:
+                local = k.bn_bwd_reduce(dy, y, None, scale, shift, beta.detach().float(), rgamma, cfg.act, cfg.slope,
+                                        True)
+                sums = local
+                if cfg.training_stats and cfg.group is not None:
+                    sums = local.clone()
+                    dist.all_reduce(sums, group=cfg.group)
+            dx, _ = k.bn_bwd_elemt(dy, y, None, scale, shift, beta.detach().float(), rgamma,
+                                   sums if cfg.training_stats else None, float(ctx.count), cfg.act, cfg.slope, False,
+                                   True)
+            dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
+            dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
+            return dx, None, dgamma, dbeta, None, None, None, None, None, None
         if fused is not None and fused[0].data_ptr() == dy.data_ptr() and fused[0].shape == dy.shape:
             # the consuming conv's dgrad epilogue already masked the gradient and reduced it
             g, local = fused
@@ -681,16 +706,19 @@ def batch_norm_add_bn_act(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, r
 
 
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
-                   slope=0.01, residual=None, group=None, link=None):
+                   slope=0.01, residual=None, group=None, link=None, iabn=False):
+    """``iabn``: InplaceABN storage (invertible act: identity / leaky, no residual, a gamma bounded
+    away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention)."""
     world = dist.get_world_size(group) if group is not None else 1
-    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
+    iabn = bool(iabn) and residual is None and ACT[act] in (0, 2) and gamma is not None and beta is not None
+    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn)
     if slabs is None or (slabs.numel() == 0):
         slabs = None
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    fusable = (cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0])) or \
-        (cfg.act == 2 and residual is None and _FUSE_LEAKY[0])
+    fusable = not iabn and ((cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0])) or
+                            (cfg.act == 2 and residual is None and _FUSE_LEAKY[0]))
     if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
         src = BNSource(cfg.act, cfg.slope)
     out = _BNAct.apply(x, slabs, gamma, beta, residual, run_mean, run_var, cfg, link, src)
@@ -713,8 +741,10 @@ def bn_eval_coefficients(bn):
     if hit is not None and hit[0] == key:
         return hit[1]
     with torch.no_grad():
-        coeff = K(rm).bn_eval_coeff(g.detach() if g is not None else None, b.detach() if b is not None else None,
-                                    rm, rv, bn.eps)
+        gd = g.detach() if g is not None else None
+        if gd is not None and getattr(bn, "inplace_abn", False):
+            gd = gd.abs() + bn.iabn_eps  # InplaceABN's effective weight
+        coeff = K(rm).bn_eval_coeff(gd, b.detach() if b is not None else None, rm, rv, bn.eps)
     _EVAL_COEFF[bn] = (key, coeff)
     return coeff
 
@@ -837,6 +867,66 @@ def batch_norm_act_maxpool(x, slabs, gamma, beta, run_mean, run_var, momentum, e
         slabs = None
     y, _ = _BNActPool.apply(x, slabs, gamma, beta, run_mean, run_var, cfg, (k, s, p))
     return y
+
+
+# ----------------------------------------------------------------------------- dropout
+_DROPOUT_STATE = {}
+
+
+def _dropout_state(device):
+    """(seed, device call counter) per device: the counter is advanced by every dropout launch
+    on the device itself, so a replayed HIP graph draws a new mask each replay."""
+    key = str(device)
+    st = _DROPOUT_STATE.get(key)
+    if st is None:
+        if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dropout: first use inside a HIP-graph capture (run an eager step first)")
+        st = _DROPOUT_STATE[key] = (int(torch.initial_seed()) & ((1 << 63) - 1),
+                                    torch.zeros(1, dtype=torch.int64, device=device))
+    return st
+
+
+class _Dropout(Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        seed, offset = _dropout_state(x.device)
+        y, used = K(x).dropout_fwd(x.contiguous(), float(p), seed, offset)
+        ctx.save_for_backward(used)
+        ctx.p, ctx.seed = float(p), seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (used,) = ctx.saved_tensors
+        return K(dy).dropout_bwd(dy, ctx.p, ctx.seed, used), None
+
+
+def dropout(x, p=0.5, training=True):
+    """Inverted dropout on the Philox HIP kernel (the mask is regenerated in backward, not stored);
+    SURVEY.md §2.5 K24 (NESTED --dropout, NESTED/train.py:252; VGG classifier)."""
+    if not training or p <= 0:
+        return x
+    return _Dropout.apply(x, p)
+
+
+# ----------------------------------------------------------------------------- adaptive average pool
+class _AdaptiveAvg(Function):
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return K(x).adaptive_avg_pool(x.contiguous(), oh, ow)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K(dy).adaptive_avg_pool_bwd(dy.contiguous(), *ctx.hw), None, None
+
+
+def adaptive_avg_pool2d(x, oh, ow):
+    """NHWC adaptive average pool (torchvision VGG's AdaptiveAvgPool2d((7, 7))); identity when the
+    map already has the target size."""
+    if x.shape[1] == oh and x.shape[2] == ow:
+        return x
+    return _AdaptiveAvg.apply(x, oh, ow)
 
 
 # ----------------------------------------------------------------------------- pooling

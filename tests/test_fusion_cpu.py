@@ -234,6 +234,9 @@ def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
         try:
             torch.manual_seed(5)
             m = build_model("tresnet_m", num_classes=10)
+            for mod in m.modules():  # the leaky fusion covers the non-InplaceABN storage mode
+                if hasattr(mod, "inplace_abn"):
+                    mod.inplace_abn = False
             g = torch.Generator().manual_seed(2)
             imgs = torch.rand(2, 3, 64, 64, generator=g)
             labels = torch.randint(0, 10, (2,), generator=g)
@@ -264,3 +267,36 @@ def test_default_fuses_only_masked_layers(monkeypatch):
     l0, g0 = _grads("resnet50", False)
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_tresnet_inplace_abn_matches_stored_input_backward(train):
+    """InplaceABN (only the activation output saved; backward inverts leaky ReLU and the affine
+    in place of reading the BN input) == the same net with the BN input saved: loss and every
+    gradient (|gamma| + eps effective weight in both), training and frozen-statistics modes."""
+    out = []
+    for iabn in (True, False):
+        torch.manual_seed(5)
+        m = build_model("tresnet_m", num_classes=10)
+        n = 0
+        for mod in m.modules():
+            if getattr(mod, "inplace_abn", False):
+                n += 1
+                if not iabn:  # same effective weight, BN-input storage
+                    mod.inplace_abn = False
+                    with torch.no_grad():
+                        mod.weight.copy_(mod.weight.abs() + mod.iabn_eps)
+        assert n == 1 + 3 + 4 + 2 * 11 + 2 * 3  # stem, basic conv1, bottleneck conv1 + conv2
+        if not train:
+            for mod in m.modules():
+                if hasattr(mod, "inplace_abn"):
+                    mod.frozen = True
+        g = torch.Generator().manual_seed(2)
+        imgs = torch.rand(2, 3, 64, 64, generator=g)
+        labels = torch.randint(0, 10, (2,), generator=g)
+        loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, cpad=3, nchw=True)), labels)
+        loss.backward()
+        out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None])))
+    (l1, g1), (l0, g0) = out
+    assert abs(l1 - l0) < 1e-5
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-4

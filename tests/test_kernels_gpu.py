@@ -989,3 +989,58 @@ def test_act_scale_bwd(K, act, want_g):
     assert relerr(dc, dcr) < 5e-3
     if want_g:
         assert relerr(g, gr) < 5e-3
+
+
+@pytest.mark.parametrize("act", [2, 0])
+def test_bn_backward_inplace_abn_from_output(K, act):
+    """InplaceABN backward kernels (inv): reading only the output y = act(x*scale + shift) with
+    beta / 1/gamma in the mean / invstd slots == the standard backward reading the input x."""
+    M, C = 4096, 128
+    x = rnd(M, C)
+    gamma = torch.rand(C) + 0.5
+    beta = torch.randn(C) * 0.3
+    mean = torch.randn(C) * 0.1
+    invstd = torch.rand(C) + 0.5
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    slope = 0.01
+    y = _ref.bn_act(x.float(), None, scale, shift, act, slope).bfloat16()
+    dy = rnd(M, C)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    got = K.bn_bwd_reduce(d(dy), d(y), None, d(scale), d(shift), d(beta), d(1.0 / gamma), act, slope, True)
+    ref = _ref.bn_bwd_reduce(dy.float(), x.float(), None, scale, shift, mean, invstd, act, slope)
+    assert relerr(got, ref) < 2e-2  # y is bf16: the recovered xhat carries its rounding
+    dx, _ = K.bn_bwd_elemt(d(dy), d(y), None, d(scale), d(shift), d(beta), d(1.0 / gamma), d(ref), float(M), act,
+                           slope, False, True)
+    dxr, _ = _ref.bn_bwd_elemt(dy.float(), x.float(), None, scale, shift, mean, invstd, ref, float(M), act, slope,
+                               False)
+    assert relerr(dx, dxr) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_philox_dropout(K, dtype):
+    """Philox dropout: keep fraction ~ 1 - p, kept values scaled by 1/(1-p), backward regenerates the
+    forward's mask, and every call (the device counter advances) draws a new mask."""
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    x = torch.ones(257, 1031, device=DEV, dtype=dtype, requires_grad=True)
+    y = Fn.dropout(x, 0.3)
+    keep = (y != 0)
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.7) < 0.01, frac
+    assert torch.allclose(y[keep].float(), torch.full_like(y[keep].float(), 1 / 0.7), rtol=1e-2)
+    y.backward(torch.ones_like(y))
+    assert torch.equal(x.grad != 0, keep)
+    y2 = Fn.dropout(x, 0.3)
+    assert not torch.equal(y2 != 0, keep)
+
+
+def test_adaptive_avg_pool_kernels(K):
+    x = rnd(2, 10, 13, 64)
+    y = K.adaptive_avg_pool(x.to(DEV), 7, 7)
+    yr = _ref.adaptive_avg_pool(x.float(), 7, 7)
+    assert relerr(y, yr) < 5e-3
+    dy = rnd(2, 7, 7, 64)
+    dx = K.adaptive_avg_pool_bwd(dy.to(DEV), 10, 13)
+    dxr = _ref.adaptive_avg_pool_bwd(dy.float(), 10, 13)
+    assert relerr(dx, dxr) < 5e-3

@@ -103,3 +103,53 @@ def test_resnext_train_and_eval_forward():
     m.eval()
     with torch.no_grad():
         assert m(x).shape == (2, 5)
+
+
+def test_vgg_netfeat_mask_dropout_and_adaptive_pool():
+    """NESTED/model/vgg.py NetFeat semantics: any input size (adaptive 7x7 pool), mask1 applied to the
+    fc1 activations, no dropout unless vgg_dropout > 0, frozen BN via train(mode, freeze_bn)."""
+    import torch.nn.functional as F
+
+    from ddp_classification_pytorch_amd.models.vgg import VGGNetFeat
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    net = VGGNetFeat()
+    net.train(True, freeze_bn=True)
+    x = Fn.to_device_nhwc(torch.randn(2, 3, 64, 64), cpad=8, nchw=True)
+    f1 = net(x)
+    assert f1.shape == (2, 4096)
+    assert torch.equal(net(x), f1)  # no dropout at vgg_dropout = 0 (deterministic in train mode)
+    mask = torch.zeros(1, 4096)
+    mask[:, :100] = 1
+    f2 = net(x, mask1=mask)
+    # reference: relu(fc2(relu(fc1(h)) * mask1))
+    h = net.net.forward_conv(x)
+    a = F.relu(F.linear(h, net.net.fc1.weight, net.net.fc1.bias)) * mask
+    ref = F.relu(F.linear(a, net.net.fc2.weight, net.net.fc2.bias))
+    assert torch.allclose(f2, ref, rtol=1e-4, atol=1e-5)
+    net_d = VGGNetFeat(vgg_dropout=0.5)
+    net_d.load_state_dict(net.state_dict())
+    net_d.train(True, freeze_bn=True)
+    assert not torch.equal(net_d(x), net_d(x))  # fresh dropout masks per call
+    net_d.eval()
+    assert torch.allclose(net_d(x), net(x))
+
+
+def test_adaptive_avg_pool_and_dropout_cpu():
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    x = torch.randn(2, 5, 6, 16, requires_grad=True)
+    y = Fn.adaptive_avg_pool2d(x, 7, 7)
+    ref = torch.nn.functional.adaptive_avg_pool2d(x.detach().permute(0, 3, 1, 2), (7, 7)).permute(0, 2, 3, 1)
+    assert torch.allclose(y, ref, atol=1e-6)
+    y.sum().backward()
+    xr = x.detach().clone().requires_grad_(True)
+    torch.nn.functional.adaptive_avg_pool2d(xr.permute(0, 3, 1, 2), (7, 7)).sum().backward()
+    assert torch.allclose(x.grad, xr.grad, atol=1e-6)
+    z = torch.ones(1000, 64, requires_grad=True)
+    d = Fn.dropout(z, 0.25)
+    kept = (d != 0).float().mean().item()
+    assert 0.72 < kept < 0.78 and torch.allclose(d[d != 0], torch.full_like(d[d != 0], 1 / 0.75))
+    d.sum().backward()
+    assert torch.equal((z.grad != 0), (d != 0))  # backward regenerates the same mask
