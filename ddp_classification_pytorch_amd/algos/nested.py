@@ -118,7 +118,7 @@ def run(args):
     net_cls = NetClassifier(net_feat.feat_dim, args.num_classes).to(rt.device)
     feat_dim, nb_cls = net_feat.feat_dim, args.num_classes
     if args.resume:
-        load_checkpoint(args.resume, {"feat": net_feat, "cls": net_cls}, map_location=rt.device)
+        load_checkpoint(args.resume, {"feat": net_feat, "cls": net_cls}, map_location="cpu")
     dist_k = gaussian_dist(args.mu, args.nested, feat_dim) if args.nested > 0 else None
     # torch semantics: a params list that requires no grad is skipped by the fused kernel
     opt_feat = FusedSGD([p for p in net_feat.parameters()], lr=1e-4, momentum=args.momentum,

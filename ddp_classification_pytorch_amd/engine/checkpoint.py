@@ -93,7 +93,14 @@ def load_checkpoint(path, models: dict, optimizers: dict = None, schedulers: dic
     if state.get("format") != "dcp-ckpt-v1":
         # plain state_dict (e.g. NESTED netBest.pth {'feat','cls'} or a bare model state_dict)
         if "feat" in state and "cls" in state and "feat" in models:
-            _unwrap(models["feat"]).load_state_dict(state["feat"], strict=strict)
+            feat = _unwrap(models["feat"])
+            sd = state["feat"]
+            if hasattr(feat, "net") and not any(k.startswith("net.") for k in sd):
+                # a reference-trained NetFeat (feat_net.* / conv2_x names): onto our NetFeat.net
+                from ..models.pretrained import remap_reference_keys
+
+                sd = {"net." + k: v for k, v in remap_reference_keys(sd).items()}
+            feat.load_state_dict(sd, strict=strict)
             _unwrap(models["cls"]).load_state_dict(state["cls"], strict=strict)
         else:
             next(iter(models.values())).load_state_dict(state, strict=strict)

@@ -94,7 +94,8 @@ class BatchNorm2d(nn.Module):
             return self.weight.abs() + self.iabn_eps
         return self.weight
 
-    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None, residual_bn=None):
+    def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None, residual_bn=None,
+                fuse_bwd=False):
         """``residual_bn=(bn, rslabs)``: ``residual`` is the raw input of BatchNorm2d ``bn`` (a
         projection shortcut), normalised inside this layer's apply pass (Fn.batch_norm_add_bn_act)."""
         stats = self.training and not self.frozen
@@ -119,7 +120,7 @@ class BatchNorm2d(nn.Module):
         return Fn.batch_norm_act(x, slabs, self._gamma() if iabn else self.weight, self.bias, self.running_mean,
                                  self.running_var, stats, self.momentum, self.eps, act=act, slope=slope,
                                  residual=residual, group=self.process_group if stats else None, link=link,
-                                 iabn=iabn)
+                                 iabn=iabn, fuse_bwd=fuse_bwd)
 
     def forward_pool(self, x, slabs=None, act="relu", k=3, s=2, p=1):
         """BN + act + k x k / s max pool.  Training-mode statistics with a ReLU/identity

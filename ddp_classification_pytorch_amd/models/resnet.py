@@ -98,7 +98,8 @@ class Bottleneck(nn.Module):
         # The downsample branch runs after conv3 so its backward precedes conv1's.
         join = Fn.GradJoin(1)
         y, s = self.conv1(x, stats=t, link=join)
-        y = self.bn1(y, s, act="relu")
+        # a grouped conv2 (ResNeXt) fuses bn1's backward reduction into its dgrad
+        y = self.bn1(y, s, act="relu", fuse_bwd=self.conv2.groups > 1)
         y, s = self.conv2(y, stats=t)
         y = self.bn2(y, s, act="relu")
         y, s = self.conv3(y, stats=t)

@@ -706,9 +706,11 @@ def batch_norm_add_bn_act(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, r
 
 
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
-                   slope=0.01, residual=None, group=None, link=None, iabn=False):
+                   slope=0.01, residual=None, group=None, link=None, iabn=False, fuse_bwd=False):
     """``iabn``: InplaceABN storage (invertible act: identity / leaky, no residual, a gamma bounded
-    away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention)."""
+    away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention).  ``fuse_bwd``:
+    offer this plain BN + ReLU's backward reduction to its consumer even under the masked-only
+    default (the consumer is a grouped conv, whose dgrad fusion measured a win: ResNeXt)."""
     world = dist.get_world_size(group) if group is not None else 1
     iabn = bool(iabn) and residual is None and ACT[act] in (0, 2) and gamma is not None and beta is not None
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn)
@@ -717,7 +719,7 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    fusable = not iabn and ((cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0])) or
+    fusable = not iabn and ((cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0] or fuse_bwd)) or
                             (cfg.act == 2 and residual is None and _FUSE_LEAKY[0]))
     if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
         src = BNSource(cfg.act, cfg.slope)

@@ -153,3 +153,90 @@ def test_adaptive_avg_pool_and_dropout_cpu():
     assert 0.72 < kept < 0.78 and torch.allclose(d[d != 0], torch.full_like(d[d != 0], 1 / 0.75))
     d.sum().backward()
     assert torch.equal((z.grad != 0), (d != 0))  # backward regenerates the same mask
+
+
+def _reference_format_cifar_feat_sd(ours):
+    """The NESTED NetFeat state_dict a reference run would save for the CIFAR ResNet-18, written
+    from our module's tensors under the reference's names (NESTED/model/model.py:17-25: feat_net =
+    Sequential(conv1, conv2_x..conv5_x); NESTED/model/cifar_resnet.py:24-42,84-95: conv1 =
+    Sequential(conv, bn, relu), residual_function = (conv, bn, relu, conv, bn), shortcut = (conv,
+    bn)) in the torch conv layout [Co, Ci, KH, KW]."""
+    sd = {}
+
+    def put(prefix, conv=None, bn=None):
+        if conv is not None:
+            sd[prefix + "weight"] = conv.weight.detach().permute(0, 3, 1, 2).clone()
+        if bn is not None:
+            for n in ("weight", "bias", "running_mean", "running_var", "num_batches_tracked"):
+                sd[prefix + n] = getattr(bn, n).detach().clone()
+
+    net = ours.net
+    put("feat_net.0.0.", conv=net.conv1)
+    put("feat_net.0.1.", bn=net.bn1)
+    for li, layer in enumerate((net.layer1, net.layer2, net.layer3, net.layer4)):
+        for bi, blk in enumerate(layer):
+            p = f"feat_net.{li + 1}.{bi}."
+            put(p + "residual_function.0.", conv=blk.conv1)
+            put(p + "residual_function.1.", bn=blk.bn1)
+            put(p + "residual_function.3.", conv=blk.conv2)
+            put(p + "residual_function.4.", bn=blk.bn2)
+            if blk.downsample is not None:
+                put(p + "shortcut.0.", conv=blk.downsample[0])
+                put(p + "shortcut.1.", bn=blk.downsample[1])
+    return sd
+
+
+def test_reference_cifar_netfeat_checkpoint_loads():
+    """A NESTED-reference checkpoint {'feat': NetFeat (feat_net.*), 'cls': ...} of the CIFAR ResNet-18
+    (reference names conv1.0/1, convK_x.i.residual_function.j, shortcut; torch conv layout, including
+    the ambiguous 3x3x3 stem) resumes into a fresh NetFeat and computes the same features."""
+    import os
+    import tempfile
+
+    from ddp_classification_pytorch_amd.engine.checkpoint import load_checkpoint
+    from ddp_classification_pytorch_amd.models.heads import NetClassifier
+    from ddp_classification_pytorch_amd.models.nested import NetFeat
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(0)
+    src = NetFeat("resnet18", "CIFAR100")
+    g = torch.Generator().manual_seed(1)
+    for m in src.modules():
+        if hasattr(m, "running_mean"):
+            m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
+    src.eval()
+    sd = _reference_format_cifar_feat_sd(src)
+    assert "feat_net.1.0.residual_function.0.weight" in sd and sd["feat_net.0.0.weight"].shape == (64, 3, 3, 3)
+    cls_w = torch.randn(512, 100)
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "netBest.pth")
+        torch.save({"feat": sd, "cls": {"weight": cls_w}}, f)
+        torch.manual_seed(7)
+        ours, cls = NetFeat("resnet18", "CIFAR100"), NetClassifier(512, 100)
+        load_checkpoint(f, {"feat": ours, "cls": cls}, restore_rng=False)
+    ours.eval()
+    x = Fn.to_device_nhwc(torch.randn(2, 3, 32, 32), cpad=8, nchw=True)
+    with torch.no_grad():
+        want, got = src(x), ours(x)
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-6), (got - want).abs().max()
+    assert torch.equal(cls.weight.detach(), cls_w)
+
+
+def test_torchvision_format_weights_load(tmp_path):
+    """load_pretrained: a torchvision-layout ResNet state_dict file ([Co,Ci,KH,KW] convs, 'module.'
+    prefix, different fc width skipped) lands on our NHWC modules."""
+    from ddp_classification_pytorch_amd.models.pretrained import load_pretrained
+
+    torch.manual_seed(0)
+    src = build_model("resnet18", num_classes=0)
+    sd = {"module." + k: (v.permute(0, 3, 1, 2).contiguous() if v.dim() == 4 else v)
+          for k, v in src.state_dict().items()}
+    sd["module.fc.weight"] = torch.randn(1000, 512)
+    f = tmp_path / "tv.pth"
+    torch.save(sd, f)
+    torch.manual_seed(3)
+    dst = build_model("resnet18", num_classes=0)
+    missing, unexpected = load_pretrained(dst, str(f))
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v), k
