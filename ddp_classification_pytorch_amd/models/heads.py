@@ -67,6 +67,41 @@ class ArcMarginProduct(nn.Module):
         return (one_hot * phi + (1.0 - one_hot) * cos) * self.s
 
 
+class NewFC(nn.Module):
+    """ARCFACE/arc_main.py:106-113 ``NewFC``: a plain Linear returning the features (unused in the
+    reference's training path; provided for API parity) -- on the MFMA GEMM."""
+
+    def __init__(self, in_features, out_features):
+        super().__init__()
+        self.fc = Linear(in_features, out_features)
+
+    def forward(self, features):
+        return self.fc(features)
+
+
+class ArcFaceNet(nn.Module):
+    """ARCFACE/arc_main.py:115-129 ``ArcFaceNet`` (dead code in the reference, kept for API parity):
+    log(exp(s cos(theta_y + m)) / (sum_j exp(s cos theta_j) - exp(s cos theta_y) + exp(s cos(theta_y + m))))
+    for EVERY column y (the reference's un-labelled formulation), with theta = acos(cos / 10) -- the
+    reference divides the cosine by 10 before acos ("prevents underflow"); kept as written.  The
+    cosine GEMM runs on the MFMA kernel; the transcendental tail is plain torch (no training path
+    uses this head)."""
+
+    def __init__(self, cls_num=10, feature_dim=2):
+        super().__init__()
+        self.w = nn.Parameter(torch.randn(feature_dim, cls_num))
+
+    def forward(self, features, m=1.0, s=10.0):
+        f = torch.nn.functional.normalize(features.float(), dim=1)
+        w = torch.nn.functional.normalize(self.w.float(), dim=0)
+        cos = Fn.linear(f.to(features.dtype), w.t().contiguous()).float()
+        theta = torch.acos(cos / 10)
+        num = torch.exp(s * torch.cos(theta + m))
+        e = torch.exp(s * torch.cos(theta))
+        den = e.sum(dim=1, keepdim=True) - e + num
+        return torch.log(num / den)
+
+
 class NetClassifier(nn.Module):
     def __init__(self, feat_dim, nb_cls):
         super().__init__()

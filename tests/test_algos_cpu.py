@@ -182,3 +182,22 @@ def test_lr_schedules():
     assert np.allclose(got, [0.01, 0.01, 0.001, 0.001, 0.0001])
     w = LinearWarmup([o2], 10, 0.1)  # NESTED/train.py:292-295: lr * n / warmUpIter
     assert abs(w.step() - 0.01) < 1e-12 and abs(w.lr_at(5) - 0.05) < 1e-12 and abs(w.lr_at(10) - 0.1) < 1e-12
+
+
+def test_arcfacenet_and_newfc_heads():
+    """ARCFACE/arc_main.py:106-129 (dead in the reference): closed form on CPU."""
+    import torch.nn.functional as F
+
+    from ddp_classification_pytorch_amd.models.heads import ArcFaceNet, NewFC
+
+    torch.manual_seed(0)
+    head = ArcFaceNet(cls_num=7, feature_dim=5)
+    x = torch.randn(4, 5)
+    out = head(x, m=1, s=10)
+    cos = F.normalize(x, dim=1) @ F.normalize(head.w, dim=0)
+    th = torch.acos(cos / 10)
+    num = torch.exp(10 * torch.cos(th + 1))
+    den = torch.exp(10 * torch.cos(th)).sum(1, keepdim=True) - torch.exp(10 * torch.cos(th)) + num
+    assert torch.allclose(out, torch.log(num / den), atol=1e-5)
+    fc = NewFC(5, 3)
+    assert torch.allclose(fc(x), F.linear(x, fc.fc.weight, fc.fc.bias), atol=1e-6)
