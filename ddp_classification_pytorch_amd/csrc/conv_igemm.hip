@@ -714,6 +714,252 @@ tap_gemm_kernel(const TapGemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent tap GEMM (FAST shapes, EPI 0 / 1, no residual add): each workgroup walks a
+// contiguous run of output tiles (column tiles of one row block back to back, so the A rows
+// they share come from this XCD's L2), and its NS-stage LDS-DMA ring runs ACROSS tile
+// boundaries -- the first k-tiles of tile i+1 are in flight while tile i's epilogue writes its
+// image, stores the output and reduces the BN statistics.  In the one-tile-per-workgroup kernel
+// that epilogue (and the k-loop's load latency) is hidden only by the other workgroups on the CU;
+// the 1x1 "expansion" convs (the output 4x the input) and the deep-K shapes stall on it.
+// Synchronisation: LDS-only raw barriers (lgkmcnt(0) + s_barrier) everywhere -- a
+// __syncthreads() would drain vmcnt, i.e. the prefetched stages AND the epilogue's stores.  The
+// counted vmcnt before each k-step counts the stages issued after the needed one plus, for the
+// first k-steps of a tile, the previous epilogue's stores when they were issued after it
+// (counted only for full tiles, where every wave issues every store; otherwise 0 = wait longer).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// tile_stats128 with LDS-only barriers (the persistent kernel keeps loads / stores in flight)
+template <int BN>
+__device__ __forceinline__ void tile_stats128_nb(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
+  constexpr int NCH = BN / 8, G = 256 / NCH, RPT = 128 / G, RB = BN * 2;
+  const int c = tid % NCH, g = tid / NCH, lane = tid & 63, wave = tid >> 6;
+  const int nvalid = min(128, p.M - m0);
+  float K[8], s1[8], s2[8];
+  {
+    const bf16x8 v = eimg_chunk<NCH>(E, 0, c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      K[e] = bf2f(v[e]);
+      s1[e] = s2[e] = 0.f;
+    }
+  }
+  bf16x8 vv[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) vv[k] = eimg_chunk<NCH>(E, g + G * k, c);
+#pragma unroll
+  for (int k = 0; k < RPT; ++k)
+    if (g + G * k < nvalid)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = bf2f(vv[k][e]) - K[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+#pragma unroll
+  for (int off = NCH; off < 64; off *= 2)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += __shfl_xor(s1[e], off, 64);
+      s2[e] += __shfl_xor(s2[e], off, 64);
+    }
+  lds_barrier();  // every image read done: rows 8.. become scratch
+  float* xch = (float*)(E + 8 * RB);
+  if (lane < NCH)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xch[(wave * 2 + 0) * BN + c * 8 + e] = s1[e];
+      xch[(wave * 2 + 1) * BN + c * 8 + e] = s2[e];
+    }
+  lds_barrier();
+  if (tid < BN && n0 + tid < p.Co) {
+    float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      S1 += xch[(w * 2 + 0) * BN + tid];
+      S2 += xch[(w * 2 + 1) * BN + tid];
+    }
+    const float k0 = bf2f(eimg_chunk<NCH>(E, 0, tid >> 3)[tid & 7]);
+    const float n = (float)nvalid;
+    const size_t rb = (size_t)(m0 / 128);
+    p.stats[(rb * 2 + 0) * p.Co + n0 + tid] = k0 + S1 / n;
+    p.stats[(rb * 2 + 1) * p.Co + n0 + tid] = fmaxf(S2 - S1 * S1 / n, 0.f);
+  }
+}
+
+template <int BN, int EPI, int NS, int BK>
+__global__ void __launch_bounds__(256, 2)
+tap_gemm_ps_kernel(const TapGemmParams p) {
+  static_assert(EPI == 0 || EPI == 1, "persistent tap GEMM: plain / statistics epilogue");
+  static_assert(NS >= 3, "the ring keeps NS-2 stages in flight across each barrier");
+  constexpr int BM = 128;
+  constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;
+  constexpr int AI = BM / (4 * RPI), BI = BN / (4 * RPI), LPT = AI + BI;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int TN = BN / 32, NCH = BN / 8, RB = BN * 2, R = 256 / NCH, SPT = BM / R;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* E = smem + NS * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const uint32_t T = ntm * ntn;
+  const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * T) / gridDim.x);
+  const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * T) / gridDim.x);
+  if (t0 >= t1) return;
+  const int nkt = p.nkt, tiles_per_tap = p.cpt / CH;
+  const int G = (int)(t1 - t0) * nkt;  // k-steps of this workgroup
+
+  // ---- issue side: the tile whose k-tiles are being staged ----
+  const bf16* fa_ptr[AI];
+  uint32_t fa_vm[AI];
+  const bf16* fb_ptr[BI];
+  auto setup_issue = [&](uint32_t tile) {
+    const int m0 = (int)(tile / ntn) * BM, n0 = (int)(tile % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int r = (wave * AI + i) * RPI + lane / CH;
+      const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+      const uint32_t q = fdiv(mm, p.div_wy);
+      const uint32_t x = mm - q * p.Wy;
+      const uint32_t n = fdiv(q, p.div_hy);
+      const uint32_t y = q - n * p.Hy;
+      const int ys = y * p.ss, xs = x * p.ss;
+      fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs +
+                  ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+      uint32_t vm = 0;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int tv = p.tap[t];
+        const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+        vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+      }
+      fa_vm[i] = vm;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int r = (wave * BI + i) * RPI + lane / CH;
+      fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+    }
+  };
+  uint32_t iss_tile = t0;
+  int iss_kt = 0;
+  setup_issue(iss_tile);
+  auto issue = [&](int slot) {
+    char* As = smem + slot * STAGE;
+    char* Bs = As + A_BYTES;
+    const int t = iss_kt / tiles_per_tap;
+    const int cbase = (iss_kt - t * tiles_per_tap) * BK;
+    const int tv = p.tap[t];
+    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;
+    const long boff = (long)tap_w(tv) * p.Cs + cbase;
+    const uint32_t tbit = 1u << t;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024),
+                                       16, 0, 0);
+    if (++iss_kt == nkt) {
+      iss_kt = 0;
+      if (++iss_tile < t1) setup_issue(iss_tile);
+    }
+  };
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int issued = 0;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (issued < G) issue(issued++ % NS);
+  int store_mark = 0, store_cnt = 0;  // the last epilogue's stores precede stage `store_mark`
+  uint32_t tile = t0;
+  int kt = 0;
+  for (int g = 0; g < G; ++g) {
+    wait_vmcnt(LPT * (issued - g - 1) + (g < store_mark ? store_cnt : 0));
+    lds_barrier();  // stage g landed for every wave; stage g-1's slot is free
+    if (issued < G) issue(issued++ % NS);
+    {
+      const char* As = smem + (g % NS) * STAGE;
+      const char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        const uint32_t c = s * 4 + (lane >> 4);
+        bf16x8 wf[TN], af[4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (BN / 2) + j * 16 + (lane & 15), c));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 64 + i * 16 + (lane & 15), c));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+      }
+    }
+    if (++kt < nkt) continue;
+    // ---- epilogue of `tile` (its own LDS image: the ring keeps streaming) ----
+    kt = 0;
+    const int m0 = (int)(tile / ntn) * BM, n0 = (int)(tile % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        *LDS_PTR(bf16x4, E + eimg_off8<NCH>(pl, cl)) = o;
+        acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    lds_barrier();
+    const int c = tid % NCH, pr0 = tid / NCH;
+    const bool cok = n0 + c * 8 < p.Co;
+    bf16x8 vv[SPT];
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
+#pragma unroll
+    for (int k = 0; k < SPT; ++k) {
+      const int m = m0 + pr0 + k * R;
+      if (m < p.M && cok) {
+        size_t drow;
+        if (p.ds == 1) {
+          drow = (size_t)m * (size_t)p.Co;
+        } else {
+          const uint32_t q = fdiv(m, p.div_wy);
+          const uint32_t x = m - q * p.Wy;
+          const uint32_t n = fdiv(q, p.div_hy);
+          const uint32_t y = q - n * p.Hy;
+          drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
+        }
+        *(bf16x8*)(p.dst + drow + n0 + c * 8) = vv[k];
+      }
+    }
+    const bool full = m0 + BM <= p.M && n0 + BN <= p.Co;
+    store_cnt = full ? SPT : 0;
+    if constexpr (EPI == 1) {
+      tile_stats128_nb<BN>(p, E, m0, n0, tid);
+      if (full && wave * 64 < BN) store_cnt += 2;
+    }
+    store_mark = issued;
+    ++tile;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 8-wave variant for the common one-tap-per-k-tile shapes with Co >= 128:
 // 256 pixel rows x 128 output channels per workgroup (the weight tile is shared
 // by twice the rows: 6 instead of 8 LDS-DMA instructions per thread per 64-deep
@@ -1441,6 +1687,45 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // stage-1 expansion at b1024, tools/fwd_epi_bench.py)
   if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
   const bool use8 = g_tune[3] == 1 && aff == nullptr;  // measured slower than the 4-wave kernel (conv_bench --cfgs)
+  // persistent cross-tile-prefetch kernel (tap_gemm_ps_kernel): FAST shapes, plain / statistics
+  // epilogue, no residual add / fold; g_tune[20] = 1 on, 2 off (A/B), 0 = heuristic
+  const int ps_mode = g_tune[20];
+  // (a parity class with no taps -- stride-2 1x1 dgrad -- only writes zeros: the plain kernel)
+  const bool ps_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && addsrc == nullptr && aff == nullptr &&
+                     bnb == nullptr;
+  if (ps_ok && ps_mode == 1) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (ncu <= 0) ncu = 256;
+    }
+    const int ps_bk = g_tune[21] == 64 ? 64 : 32;
+    const int tiles = ntm * ((Co + bn - 1) / bn);
+    const int grid = std::min(tiles, 2 * ncu);
+#define DCP_PS(BN_, EPI_, BK_)                                                                          \
+  {                                                                                                     \
+    p.nkt = (p.ntaps * p.cpt + BK_ / 8 - 1) / (BK_ / 8);                                                \
+    constexpr size_t lds = 3 * (size_t)(128 + BN_) * BK_ * 2 + (size_t)128 * 2 * BN_;                   \
+    static bool attr = false;                                                                           \
+    if (!attr) {                                                                                        \
+      hipFuncSetAttribute((const void*)tap_gemm_ps_kernel<BN_, EPI_, 3, BK_>,                            \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                        \
+      attr = true;                                                                                      \
+    }                                                                                                   \
+    hipLaunchKernelGGL((tap_gemm_ps_kernel<BN_, EPI_, 3, BK_>), dim3(grid), dim3(256), lds, stream, p); \
+  }
+    if (bn == 64) {
+      if (epi == 1) { if (ps_bk == 64) DCP_PS(64, 1, 64) else DCP_PS(64, 1, 32) }
+      else { if (ps_bk == 64) DCP_PS(64, 0, 64) else DCP_PS(64, 0, 32) }
+    } else {
+      if (epi == 1) { if (ps_bk == 64) DCP_PS(128, 1, 64) else DCP_PS(128, 1, 32) }
+      else { if (ps_bk == 64) DCP_PS(128, 0, 64) else DCP_PS(128, 0, 32) }
+    }
+#undef DCP_PS
+    return;
+  }
   if (fast && Co >= 128 && epi < 2 && use8) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
     constexpr size_t lds8 = 3 * (256 + 128) * 128;

@@ -1044,3 +1044,38 @@ def test_adaptive_avg_pool_kernels(K):
     dx = K.adaptive_avg_pool_bwd(dy.to(DEV), 10, 13)
     dxr = _ref.adaptive_avg_pool_bwd(dy.float(), 10, 13)
     assert relerr(dx, dxr) < 5e-3
+
+
+@pytest.mark.parametrize("shape", [(4, 56, 56, 64, 256, 1, 1, 0), (3, 28, 28, 128, 512, 1, 1, 0),
+                                   (2, 14, 14, 256, 256, 3, 1, 1), (2, 28, 28, 256, 512, 1, 2, 0),
+                                   (3, 9, 11, 64, 128, 3, 1, 1), (2, 7, 7, 512, 2048, 1, 1, 0),
+                                   (1, 13, 13, 128, 64, 3, 1, 1)])
+@pytest.mark.parametrize("bk", [32, 64])
+def test_persistent_tap_gemm_matches(K, shape, bk):
+    """The persistent cross-tile-prefetch tap GEMM (g_tune[20] = 1) == the one-tile-per-workgroup
+    kernel: forward with BN statistics and the data gradient (stride 1 and the stride-2 parity
+    classes), ragged M included."""
+    N, H, W, Ci, Co, k, s, p = shape
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co).to(DEV)
+    wb, wt = K.weight_prep(w.float(), 0, True)
+    outs = []
+    try:
+        for mode in (2, 1):
+            K.set_tuning(20, mode)
+            K.set_tuning(21, bk)
+            y, slabs = K.conv_fwd(x, wb, s, p, True)
+            st = K.bn_stats(y, slabs)
+            dx = K.conv_dgrad(dy, wt, H, W, s, p)
+            torch.cuda.synchronize()
+            outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
+    finally:
+        K.set_tuning(20, 0)
+        K.set_tuning(21, 0)
+    (y0, s0, d0), (y1, s1, d1) = outs
+    assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
+    assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
+    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
+    assert relerr(y1, yr) < 1e-2

@@ -128,7 +128,7 @@ def main():
 
 
 def _apply(K, cfg):
-    for i in range(16):
+    for i in range(32):
         K.set_tuning(i, 0)
     for kv in filter(None, cfg.split(";")):
         i, v = kv.split("=")
