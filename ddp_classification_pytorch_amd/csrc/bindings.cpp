@@ -249,7 +249,7 @@ std::tuple<Tensor, Tensor> stem_fwd(const Tensor& x, const Tensor& w, bool stats
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   if (!dcp::stem_fwd_supported(H, W, C, w.size(0), w.size(1), w.size(2)))
     return conv_fwd_geo(x, w, 1, 2, H, W, stats);
-  TORCH_CHECK((int64_t)N * H * W * 64 < (1ll << 32), "tensor too large");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "stem_fwd: too many pixels");  // 64-bit row offsets
   auto y = at::empty({N, H, W, 64}, bf16_like(x));
   Tensor part = stats ? at::empty({dcp::stem_fwd_blocks(N, H), 3, 64}, f32_like(x)) : at::empty({0}, f32_like(x));
   dcp::launch_stem_fwd(bp(x), bp(w), bpm(y), stats ? part.data_ptr<float>() : nullptr, zero_page(x.get_device()), N,
@@ -276,7 +276,9 @@ std::tuple<Tensor, Tensor> stem_bn_pool_bwd(const Tensor& dy, const Tensor& idx,
                   x16.size(3) == 16 && dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) == 64 &&
                   idx.numel() == dy.numel() && idx.scalar_type() == at::kByte,
               "stem_bn_pool_bwd shapes");
-  TORCH_CHECK((int64_t)N * H * W * 64 < (1ll << 31), "tensor too large");
+  // full-resolution rows are addressed with 64-bit offsets, the pooled tensors with 32-bit ones
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31) && (int64_t)N * (H / 2) * (W / 2) * 64 < (1ll << 32),
+              "stem_bn_pool_bwd: tensor too large");
   const int nb = dcp::stem_bwd_blocks(N, H, num_cus(z.get_device()));
   const int pf = dcp::stem_bwd_part_floats();
   auto part = at::empty({(int64_t)(nb + (nb + 63) / 64) * pf}, f32_like(z));

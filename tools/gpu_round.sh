@@ -11,6 +11,8 @@
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
 #   sweep           headline batch sweep 128..2048
 #   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
+#   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
+#   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
 set -e
 set -o pipefail
 T=${1:?tag}; shift
@@ -57,6 +59,18 @@ for step in "$@"; do
       for b in 128 256 512 1024 2048; do
         timeout -k 10 240 python -u bench.py --batch $b --steps 10 --warmup 3 > $O/sweep_b$b.log 2>&1
         tail -1 $O/sweep_b$b.log
+      done ;;
+    small)
+      for b in 32 128; do
+        timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 > $O/small_b$b.log 2>&1
+        tail -1 $O/small_b$b.log | grep -o '"value": [0-9.]*'
+        timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 --graph > $O/small_b${b}_graph.log 2>&1
+        tail -1 $O/small_b${b}_graph.log | grep -o '"value": [0-9.]*'
+      done ;;
+    large)
+      for b in 2048 3072; do
+        timeout -k 10 400 python -u bench.py --config r101 --batch $b --steps 5 --warmup 2 > $O/r101_b$b.log 2>&1
+        tail -1 $O/r101_b$b.log
       done ;;
     convbench)
       timeout -k 10 400 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen > $O/conv_bench_b1024.txt 2>&1
