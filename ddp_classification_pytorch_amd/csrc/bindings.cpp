@@ -623,7 +623,8 @@ Tensor grouped_conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t
   const int H = x.size(1), W = x.size(2), C = x.size(3);
   auto dw = at::empty({Co, KH, KW, C / groups}, f32_like(dy));
   const int splits = Co == C ? dcp::gconv_mfma_wgrad_splits(N, Ho, Wo, C, groups) : 0;
-  auto part = at::empty({std::max(splits, 1) * (int64_t)dw.numel()}, f32_like(dy));
+  const int fsplits = dcp::gconv_fallback_wgrad_splits(N * Ho * Wo, (int)dw.numel());
+  auto part = at::empty({std::max({splits, fsplits, 1}) * (int64_t)dw.numel()}, f32_like(dy));
   dcp::launch_grouped_conv_wgrad(bp(dy), bp(x), dw.data_ptr<float>(), part.data_ptr<float>(), splits,
                                  zero_page(dy.get_device()), N, H, W, C, Ho,
                                  Wo, Co, groups, KH, KW, stride, pad, cur_stream());

@@ -4,6 +4,8 @@
 //   * depthwise k x k filter with reflect padding (TResNet anti-aliased
 //     downsampling "blur pool", timm tresnet);
 //   * per-(sample, channel) scaling for squeeze-and-excitation (K22).
+#include <algorithm>
+
 #include "common.cuh"
 #include "launchers.h"
 
@@ -101,9 +103,10 @@ __global__ void __launch_bounds__(256) gconv_dgrad_kernel(const bf16* __restrict
   }
 }
 
-// dW[co][kh][kw][cig]: one thread per weight element, workgroup-split over rows + atomics
+// dW[co][kh][kw][cig]: one thread per weight element, workgroup-split over rows; split y writes
+// its partial to out + y * nw (reduced by split_reduce -- deterministic, no float atomics)
 __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                          float* __restrict__ dw, int N, int H, int W, int C, int Ho,
+                                                          float* __restrict__ out, int N, int H, int W, int C, int Ho,
                                                           int Wo, int Co, int G, int KH, int KW, int s, int p,
                                                           int rows_per_split) {
   const int Cg = C / G, Cog = Co / G;
@@ -128,7 +131,7 @@ __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const bf16* __restrict
     if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) continue;
     acc += bf2f(dy[(size_t)m * Co + co]) * bf2f(x[(((size_t)n * H + hi) * W + wi) * C + ci]);
   }
-  atomicAdd(dw + e, acc);
+  out[(size_t)blockIdx.y * nw + e] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -341,15 +344,21 @@ void launch_grouped_conv_wgrad(const bf16* dy, const bf16* x, float* dw, float* 
                                int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
                                int pad, hipStream_t s) {
   if (launch_gconv_mfma_wgrad(dy, x, dw, part, splits, zero, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, s)) return;
-  hipMemsetAsync(dw, 0, sizeof(float) * (size_t)Co * KH * KW * (C / G), s);
   const int M = N * Ho * Wo;
   const int nw = Co * KH * KW * (C / G);
-  int nsplit = 2048 / ((nw + 255) / 256);
-  if (nsplit < 1) nsplit = 1;
-  if (nsplit > (M + 63) / 64) nsplit = (M + 63) / 64;
+  const int nsplit = gconv_fallback_wgrad_splits(M, nw);
   const int rps = (M + nsplit - 1) / nsplit;
-  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((nw + 255) / 256, nsplit), dim3(256), 0, s, dy, x, dw, N, H, W, C, Ho,
-                     Wo, Co, G, KH, KW, stride, pad, rps);
+  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((nw + 255) / 256, nsplit), dim3(256), 0, s, dy, x,
+                     nsplit == 1 ? dw : part, N, H, W, C, Ho, Wo, Co, G, KH, KW, stride, pad, rps);
+  if (nsplit > 1) launch_split_reduce(part, nsplit, nw, dw, s);
+}
+// row splits of the direct fallback: ~2048 workgroups, at most 64 (one split_reduce pass), one
+// when the weight count is not a multiple of 4 (the float4 reduction)
+int gconv_fallback_wgrad_splits(int M, int nw) {
+  if (nw % 4) return 1;
+  int nsplit = 2048 / ((nw + 255) / 256);
+  nsplit = std::min(std::max(nsplit, 1), 64);
+  return std::max(1, std::min(nsplit, (M + 63) / 64));
 }
 void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
                        int s, int p, int reflect, hipStream_t st) {

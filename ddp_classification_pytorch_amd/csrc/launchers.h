@@ -103,6 +103,7 @@ bool launch_gconv_mfma_dgrad(const bf16* dy, const bf16* w, bf16* dx, bf16* frag
                              int Wo, int Co, int G, int KH, int KW, int stride, int pad, hipStream_t s,
                              const GconvBnBwd* bn = nullptr);
 int gconv_mfma_wgrad_splits(int N, int Ho, int Wo, int C, int G);
+int gconv_fallback_wgrad_splits(int M, int nw);  // part rows the direct fallback needs
 bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* part, int splits, const bf16* zero,
                              int N, int H, int W, int C, int Ho, int Wo, int Co, int G, int KH, int KW, int stride,
                              int pad, hipStream_t s);

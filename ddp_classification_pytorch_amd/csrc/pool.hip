@@ -15,7 +15,8 @@ namespace dcp {
 
 // 32-bit decode of a flat (pixel, 8-channel chunk) index i = ((n*H + y)*W + x)*cpr + ch with
 // magic-number divisions (64-bit integer division is emulated on the GPU and dominated these
-// memory-bound kernels); flat indices < 2^31 are checked on the host
+// memory-bound kernels); chunk indices < 2^31 are checked on the host, element offsets are
+// 64-bit (the R101 b3072 stem pool output is 2.47e9 elements)
 struct PixDiv {
   FastDiv cpr, w, h;
   __device__ __forceinline__ void decode(uint32_t i, int& ch, int& x, int& y, int& n) const {
@@ -73,7 +74,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
           const int hi = ho * SS - PP + kh, wi = wo * SS - PP + kw;
           ok[kh * KK + kw] = ((unsigned)hi < (unsigned)H) & ((unsigned)wi < (unsigned)W);
           const int hc = min(max(hi, 0), H - 1), wc = min(max(wi, 0), W - 1);
-          v[kh * KK + kw] = *(const bf16x8*)(x + ((uint32_t)(n * H + hc) * W + wc) * C + ch * 8);
+          v[kh * KK + kw] = *(const bf16x8*)(x + (size_t)((uint32_t)(n * H + hc) * W + wc) * C + ch * 8);
         }
 #pragma unroll
       for (int t = 0; t < KK * KK; ++t)
@@ -96,7 +97,7 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
         for (int kw = 0; kw < k; ++kw) {
           const int wi = wo * s - p + kw;
           if ((unsigned)wi >= (unsigned)W) continue;
-          const bf16x8 v = *(const bf16x8*)(x + ((uint32_t)(n * H + hi) * W + wi) * C + ch * 8);
+          const bf16x8 v = *(const bf16x8*)(x + (size_t)((uint32_t)(n * H + hi) * W + wi) * C + ch * 8);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             float f = bf2f(v[q]);
@@ -116,12 +117,12 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16* __restrict
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = f2bf(best[q]);
-    *(bf16x8*)(y + i * 8) = o;
+    *(bf16x8*)(y + (size_t)i * 8) = o;
     if (idx) {
       uint64_t packed = 0;
 #pragma unroll
       for (int q = 0; q < 8; ++q) packed |= (uint64_t)bi[q] << (8 * q);
-      *(uint64_t*)(idx + i * 8) = packed;
+      *(uint64_t*)(idx + (size_t)i * 8) = packed;
     }
   }
 }
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16* __restrict
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
-    *(bf16x8*)(dx + i * 8) = o;
+    *(bf16x8*)(dx + (size_t)i * 8) = o;
   }
 }
 
@@ -190,7 +191,7 @@ __global__ void __launch_bounds__(256) maxpool_bn_bwd_kernel(const bf16* __restr
     int chd, wi, hi, n;
     dv.decode(i, chd, wi, hi, n);
     float g[8];
-    const bf16x8 xv = *(const bf16x8*)(x + i * 8);
+    const bf16x8 xv = *(const bf16x8*)(x + (size_t)i * 8);
     gather_pool_grad<KK, SS, PP>(dy, idx, n, hi, wi, Ho, Wo, C, ch, k, s, p, g);
     bf16x8 o;
 #pragma unroll
@@ -205,7 +206,7 @@ __global__ void __launch_bounds__(256) maxpool_bn_bwd_kernel(const bf16* __restr
         o[q] = f2bf(ca[q] * gq + cb[q] * xf + cc[q]);
       }
     }
-    if (PASS == 1) *(bf16x8*)(dx + i * 8) = o;
+    if (PASS == 1) *(bf16x8*)(dx + (size_t)i * 8) = o;
   }
   if (PASS == 0) {
     __shared__ float red[2][256][8];
@@ -334,8 +335,8 @@ static inline int ew_grid2(size_t n) {
 }
 
 static void check_flat(size_t elems) {
-  if (elems >= (1ull << 31)) {
-    fprintf(stderr, "pool kernels: tensor of %zu elements exceeds the 32-bit index range\n", elems);
+  if (elems / 8 >= (1ull << 31)) {
+    fprintf(stderr, "pool kernels: tensor of %zu elements exceeds the 2^31 8-channel-chunk index range\n", elems);
     abort();
   }
 }

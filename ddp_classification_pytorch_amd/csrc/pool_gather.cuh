@@ -27,7 +27,7 @@ __device__ __forceinline__ void gather_pool_grad(const bf16* __restrict__ dy, co
       const int ho = (c >> 1) ? h1 : h0, wo = (c & 1) ? w1 : w0;
       ok[c] = ho < Ho && wo < Wo && ((c >> 1) == 0 || h1 != h0) && ((c & 1) == 0 || w1 != w0);
       want[c] = (uint8_t)((hi - (ho * 2 - 1)) * 3 + (wi - (wo * 2 - 1)));
-      const uint32_t o = ((uint32_t)(n * Ho + min(ho, Ho - 1)) * Wo + min(wo, Wo - 1)) * C + ch * 8;
+      const size_t o = (size_t)((uint32_t)(n * Ho + min(ho, Ho - 1)) * Wo + min(wo, Wo - 1)) * C + ch * 8;
       pk[c] = *(const uint64_t*)(idx + o);
       gv[c] = *(const bf16x8*)(dy + o);
     }
@@ -47,7 +47,7 @@ __device__ __forceinline__ void gather_pool_grad(const bf16* __restrict__ dy, co
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
         const int kw = wi - (wo * s - p);
         if (kw < 0 || kw >= k) continue;
-        const uint32_t o = ((uint32_t)(n * Ho + ho) * Wo + wo) * C + ch * 8;
+        const size_t o = (size_t)((uint32_t)(n * Ho + ho) * Wo + wo) * C + ch * 8;
         const uint64_t packed = *(const uint64_t*)(idx + o);
         const bf16x8 gw = *(const bf16x8*)(dy + o);
         const uint8_t w = (uint8_t)(kh * k + kw);

@@ -395,6 +395,9 @@ def test_grouped_conv_shapes(K, N, H, W, C, G, KH, stride, pad):
     assert relerr(dx, _ref.grouped_conv_dgrad(dy.float(), w.float(), H, W, G, stride, pad)) < 1e-2
     dw = K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), KH, KH, G, stride, pad)
     assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), KH, KH, G, stride, pad)) < 5e-3
+    # split partials + a fixed-order reduce on every path (the direct fallback included): bitwise
+    # reproducible
+    assert torch.equal(dw, K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), KH, KH, G, stride, pad))
 
 
 @pytest.mark.parametrize("sg", [16, 32])

@@ -34,3 +34,30 @@ def test_conv_output_past_2pow32_elements():
     assert int(st[0, 0, 0].item()) == N * H * W
     del x, y, slabs
     torch.cuda.empty_cache()
+
+
+def test_stem_maxpool_past_2pow31_elements():
+    """The stem's 3x3/2 max pool at R101 b3072 (BASELINE.json config 5 swept to 3072): the input
+    holds 2.47e9 elements, past the old 2^31 flat-index guard; element offsets are 64-bit now."""
+    import torch.nn.functional as F
+
+    K = _ext.hip_ops()
+    N, H, W, C = 3072, 112, 112, 64
+    assert N * H * W * C > 2**31
+    dev = torch.device("cuda")
+    x = torch.empty(N, H, W, C, device=dev, dtype=torch.bfloat16)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for i in range(0, N, 512):  # fill in chunks: an fp32 temporary of the whole would be 9.9 GB
+        x[i:i + 512] = torch.randn(min(512, N - i), H, W, C, device=dev, generator=g).bfloat16()
+    y, idx = K.maxpool_fwd(x, 3, 2, 1)
+    dy = torch.ones_like(y)
+    dx = K.maxpool_bwd(dy, idx, H, W, 3, 2, 1)
+    torch.cuda.synchronize()
+    for n in (0, 2**31 // (H * W * C), N - 1):
+        xn = x[n:n + 1].permute(0, 3, 1, 2).float()
+        ref = F.max_pool2d(xn, 3, 2, 1).permute(0, 2, 3, 1)
+        assert torch.equal(y[n:n + 1].float(), ref), n
+        # every window's argmax receives its 1.0: the gradient mass equals the window count
+        assert dx[n].float().sum().item() == float(y[n].numel()), n
+    del x, y, idx, dy, dx
+    torch.cuda.empty_cache()
