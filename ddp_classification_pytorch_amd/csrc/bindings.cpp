@@ -151,6 +151,57 @@ Tensor conv_fwd_affine(const Tensor& x, const Tensor& w, int64_t stride, int64_t
   return y;
 }
 
+void check_pro_vec(const Tensor& t, int C, const char* what) {
+  CHECK_DEV(t);
+  CHECK_F32(t);
+  CHECK_CONTIG(t);
+  TORCH_CHECK(t.numel() == C, what, ": per-input-channel vector size");
+}
+
+// 1x1 stride-1 conv of relu(x * scale + shift) with that BN + ReLU applied to the A operand in
+// registers (K5 prologue; x is the BN's input, the normalised activation is never written).
+// -> (y, BN statistics slabs of y or empty), as conv_fwd
+std::tuple<Tensor, Tensor> conv_fwd_pro(const Tensor& x, const Tensor& w, const Tensor& scale, const Tensor& shift,
+                                        bool stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == 1 && w.size(2) == 1, "conv_fwd_pro: 1x1 NHWC conv");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Co = w.size(0);
+  TORCH_CHECK(w.size(3) == C && C % 64 == 0 && Co % 8 == 0, "conv_fwd_pro: C % 64 == 0, Co % 8 == 0");
+  check_pro_vec(scale, C, "conv_fwd_pro scale");
+  check_pro_vec(shift, C, "conv_fwd_pro shift");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "conv_fwd_pro: too many pixels");
+  auto y = at::empty({N, H, W, Co}, bf16_like(x));
+  const int M = N * H * W;
+  Tensor slabs = stats ? at::empty({(M + 127) / 128, 2, Co}, f32_like(x)) : at::empty({0}, f32_like(x));
+  const auto taps = fwd_taps(1, 1, 0);
+  dcp::launch_tap_gemm(bp(x), N, H, W, C, bp(w), Co, 1, bpm(y), H, W, H, W, 1, 1, 0, 0, taps,
+                       stats ? slabs.data_ptr<float>() : nullptr, nullptr, 0, zero_page(x.get_device()), cur_stream(),
+                       nullptr, nullptr, nullptr, scale.data_ptr<float>(), shift.data_ptr<float>());
+  return {y, slabs};
+}
+
+// weight gradient of conv_fwd_pro: dW = dY^T relu(x * scale + shift), the input recomputed in the
+// B-fragment registers
+Tensor conv_wgrad_pro(const Tensor& dy, const Tensor& x, const Tensor& scale, const Tensor& shift) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = dy.size(0), H = dy.size(1), W = dy.size(2), Co = dy.size(3), C = x.size(3);
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == H && x.size(2) == W, "conv_wgrad_pro: 1x1 geometry");
+  TORCH_CHECK(C % 8 == 0 && Co % 8 == 0 && C <= 2048 && !(Co <= 64 && C >= 128), "conv_wgrad_pro: channel layout");
+  check_pro_vec(scale, C, "conv_wgrad_pro scale");
+  check_pro_vec(shift, C, "conv_wgrad_pro shift");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "conv_wgrad_pro: too many pixels");
+  auto dw = at::empty({Co, 1, 1, C}, f32_like(dy));
+  const auto taps = fwd_taps(1, 1, 0);
+  const int ncu = num_cus(dy.get_device());
+  const int splits = dcp::wgrad_plan_splits(N, H, W, Co, H, W, C, 1, taps, ncu);
+  auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
+  dcp::launch_wgrad(bp(dy), N, H, W, Co, bp(x), H, W, C, 1, taps, dw.data_ptr<float>(), part.data_ptr<float>(),
+                    zero_page(dy.get_device()), ncu, cur_stream(), scale.data_ptr<float>(), shift.data_ptr<float>());
+  return dw;
+}
+
 // backward of act(c * scale + shift [+ r]) from its output y: (dc = g * scale, g = dy * act'(y) or empty)
 std::tuple<Tensor, Tensor> act_scale_bwd(const Tensor& dy, const Tensor& y, const Tensor& scale, int64_t act,
                                          double slope, bool want_g) {
@@ -1372,6 +1423,8 @@ TORCH_LIBRARY(dcp, m) {
       "Tensor? sums, float count, int act, float slope, bool want_dres, bool inv=False) -> (Tensor, Tensor)",
       &bn_bwd_elemt);
   m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)", &maxpool_fwd);
+  m.def("conv_fwd_pro(Tensor x, Tensor w, Tensor scale, Tensor shift, bool stats) -> (Tensor, Tensor)", &conv_fwd_pro);
+  m.def("conv_wgrad_pro(Tensor dy, Tensor x, Tensor scale, Tensor shift) -> Tensor", &conv_wgrad_pro);
   m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int p) -> Tensor", &maxpool_bwd);
   m.def("bn_act_maxpool(Tensor x, Tensor scale, Tensor shift, int act, int k, int s, int p) -> (Tensor, Tensor)",
         &bn_act_maxpool);

@@ -68,6 +68,11 @@ struct TapGemmParams {
   const float* fshift;
   int fact;
   float fslope;
+  // PRO (1x1 / stride-1 FAST shapes): the A operand is a training-mode BN's INPUT, normalised
+  // and ReLU'd in registers between the LDS fragment read and the MFMA,
+  // a = bf16(relu(x * pscale[c] + pshift[c])) -- the BN + ReLU output is never written (K5)
+  const float* pscale;
+  const float* pshift;
 };
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
@@ -273,10 +278,11 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // the raw s_barrier, drained by a counted vmcnt -- for deep-K shapes at one block per CU.
 // three waves per SIMD: the fused BN-backward epilogue otherwise lands one register past the
 // 168-register step and halves to two workgroups per CU
-template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64>
+template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64, bool PRO = false>
 __global__ void __launch_bounds__(256, 3)
 tap_gemm_kernel(const TapGemmParams p) {
   static_assert(NS == 2 || FAST, "the LDS ring needs the one-tap-per-k-tile path");
+  static_assert(!PRO || (FAST && NS == 2 && EPI < 2), "the BN prologue: FAST double-buffered forward only");
   static_assert(BK == 64 || BK == 32, "k-tile depth");
   constexpr int BM = 128;                 // pixel rows per block
   constexpr int ROWB = BK * 2;            // bytes per image row (BK bf16)
@@ -379,6 +385,15 @@ tap_gemm_kernel(const TapGemmParams p) {
     if (tid < p.ntaps) *LDS_PTR(int, smem + NS * STAGE + tid * 4) = p.tap[tid];
     __syncthreads();
   }
+  // PRO: the per-channel (scale, shift) table behind the stages the k-loop uses, fp32 [2][Cs]
+  // (one tap: k-tile kt covers channels kt*BK ..); made visible by the barrier after stage 0
+  float* pro_tbl = (float*)(smem + min(NS, max(p.nkt, 1)) * STAGE);
+  if constexpr (PRO) {
+    for (int i = tid; i < p.Cs; i += 256) {
+      pro_tbl[i] = p.pscale[i];
+      pro_tbl[p.Cs + i] = p.pshift[i];
+    }
+  }
 
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STAGE;
@@ -435,7 +450,7 @@ tap_gemm_kernel(const TapGemmParams p) {
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = p.nkt;
-  auto compute = [&](const char* As, const char* Bs) {
+  auto compute = [&](const char* As, const char* Bs, int kt) {
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
       const uint32_t c = s * 4 + (lane >> 4);
@@ -449,6 +464,18 @@ tap_gemm_kernel(const TapGemmParams p) {
       for (int i = 0; i < 4; ++i) {
         const uint32_t r = wm * 64 + i * 16 + (lane & 15);
         af[i] = *(const bf16x8*)(As + swzk<BK>(r, c));
+      }
+      if constexpr (PRO) {
+        // the lane's 8 channels of this k-step: kt*BK + 8c .. +7 (fragment elements in order)
+        const float* t = pro_tbl + kt * BK + c * 8;
+        const f32x4 s0 = *LDS_PTR(const f32x4, t), s1 = *LDS_PTR(const f32x4, t + 4);
+        const f32x4 h0 = *LDS_PTR(const f32x4, t + p.Cs), h1 = *LDS_PTR(const f32x4, t + p.Cs + 4);
+        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[i][e] = f2bf(fmaxf(bf2f(af[i][e]) * sc[e] + sh[e], 0.f));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -467,7 +494,7 @@ tap_gemm_kernel(const TapGemmParams p) {
       const int buf = kt & 1;
       if (kt + 1 < nkt && !(p.ablate & 1)) stage(kt + 1, buf ^ 1);
       const char* As = smem + buf * STAGE;
-      if (!(p.ablate & 2)) compute(As, As + A_BYTES);
+      if (!(p.ablate & 2)) compute(As, As + A_BYTES, kt);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -483,7 +510,7 @@ tap_gemm_kernel(const TapGemmParams p) {
       asm volatile("" ::: "memory");
       if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
       const char* As = smem + (kt % NS) * STAGE;
-      compute(As, As + A_BYTES);
+      compute(As, As + A_BYTES, kt);
     }
     __syncthreads();
   }
@@ -1161,6 +1188,9 @@ struct WgradParams {
   int cpt, kc_total, rows_per_split;
   int ablate;  // tuning experiments only: 8 = skip the atomic flush
   int direct;  // 1x1 stride-1 (no padding): the input pixel of GEMM row m is m
+  // PRO (direct only): the input is a BN's input x, used as relu(x * pscale[c] + pshift[c]) (K5)
+  const float* pscale;
+  const float* pshift;
   FastDiv div_wo, div_ho, div_cpt;
   int8_t dy_t[kMaxTaps], dx_t[kMaxTaps];
 };
@@ -1184,7 +1214,15 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, uint32_t row0, uint32
 }
 
 // BK = pixel rows per k-tile (64, or 32: half the LDS, twice the workgroups per CU)
-template <int BK>
+// PRO: the B (input) fragments hold one channel per lane (column lane & 15 of the 16-wide
+// subtile), so the BN prologue is one (scale, shift) register pair per subtile for the whole
+// kernel.  Zero-page rows turn into relu(shift) but meet zero dY rows.
+__device__ __forceinline__ void pro_frag(bf16x8& f, float sc, float sh) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = f2bf(fmaxf(bf2f(f[e]) * sc + sh, 0.f));
+}
+
+template <int BK, bool PRO = false>
 __global__ void __launch_bounds__(256, 3)
 wgrad_kernel(const WgradParams p) {
   constexpr int IMG = BK * 256;   // BK rows x 128 bf16
@@ -1259,6 +1297,15 @@ wgrad_kernel(const WgradParams p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float psc[4], psh[4];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = min(kcol0 + wn * 64 + j * 16 + (lane & 15), p.Cs - 1);
+      psc[j] = p.pscale[c];
+      psh[j] = p.pshift[c];
+    }
+  }
 
   if (nkt > 0) {
     stage(0, 0);
@@ -1278,6 +1325,9 @@ wgrad_kernel(const WgradParams p) {
       for (int i = 0; i < 4; ++i) af[i] = tr_frag(Ai, row0, wm * 64 + i * 16, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bi, row0, wn * 64 + j * 16, lane);
+      if constexpr (PRO)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pro_frag(bfr[j], psc[j], psh[j]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1325,6 +1375,7 @@ __device__ __forceinline__ bf16x8 tr_frag512(const char* img, uint32_t row0, uin
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+template <bool PRO = false>
 __global__ void __launch_bounds__(512)
 wgrad256_kernel(const WgradParams p) {
   constexpr int BK = 64;
@@ -1396,6 +1447,15 @@ wgrad256_kernel(const WgradParams p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // PRO: (scale, shift) pairs in LDS behind the two stages -- 16 more registers per lane would
+  // spill this 254-register kernel; read back per k-step (visible after the first barrier)
+  float* pro_tbl = (float*)(smem + 2 * STAGE);
+  if constexpr (PRO) {
+    for (int i = tid; i < p.Cs; i += 512) {
+      pro_tbl[2 * i] = p.pscale[i];
+      pro_tbl[2 * i + 1] = p.pshift[i];
+    }
+  }
 
   if (nkt > 0) {
     stage(0, 0);
@@ -1410,16 +1470,38 @@ wgrad256_kernel(const WgradParams p) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint32_t row0 = s * 32 + 8 * (lane >> 4);
-      bf16x8 af[4], bfr[8];
+      bf16x8 af[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = tr_frag512(Ai, row0, wm * 64 + i * 16, lane);
+      if constexpr (PRO) {
+        // input fragments in two halves of 4 (the transform's temporaries fit beside them)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bfr[j] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 bh[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * h + jj;
+            bh[jj] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
+            const int c = min(kcol0 + wn * 128 + j * 16 + (lane & 15), p.Cs - 1);
+            const f32x2 t = *LDS_PTR(const f32x2, pro_tbl + 2 * c);
+            pro_frag(bh[jj], t[0], t[1]);
+          }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              acc[i][4 * h + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bh[jj], acc[i][4 * h + jj], 0, 0, 0);
+        }
+      } else {
+        bf16x8 bfr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bfr[j] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1603,7 +1685,7 @@ wgrad64_kernel(const WgradParams p) {
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-template <int BN, int EPI, bool FAST, int NS, int BK = 64>
+template <int BN, int EPI, bool FAST, int NS, int BK = 64, bool PRO = false>
 static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   p.nkt = (p.ntaps * p.cpt + BK / 8 - 1) / (BK / 8);
   // LDS: the stages the k-loop actually uses (short-K shapes -- 1x1 convs with 64 input
@@ -1617,15 +1699,17 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   if (EPI == 3 || EPI == 4) epi = std::max((size_t)128 * 2 * BN, (size_t)2 * 8 * 260 * 4);
   size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
   if (!FAST) lds = std::max(lds, full + kMaxTaps * sizeof(int));  // LDS tap table behind the stages
+  // BN-prologue (scale, shift) table behind the stages in use
+  if (PRO) lds = std::max(lds, (size_t)std::min(NS, std::max(p.nkt, 1)) * stage + (size_t)p.Cs * 2 * sizeof(float));
   if (full > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK>,
+      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
       attr = true;
     }
   }
-  hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK>), dim3(grid), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>), dim3(grid), dim3(256), lds, stream, p);
 }
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
@@ -1633,8 +1717,10 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                      const TapList& taps, float* stats, const float* bias, int relu,
                      const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb,
-                     const AffineEpi* aff) {
+                     const AffineEpi* aff, const float* pscale, const float* pshift) {
   TapGemmParams p;
+  p.pscale = pscale;
+  p.pshift = pshift;
   p.src = src; p.wt = wt; p.dst = dst; p.stats = stats; p.zero = zero; p.addsrc = addsrc;
   p.fscale = aff ? aff->scale : nullptr;
   p.fshift = aff ? aff->shift : nullptr;
@@ -1692,7 +1778,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   const int ps_mode = g_tune[20];
   // (a parity class with no taps -- stride-2 1x1 dgrad -- only writes zeros: the plain kernel)
   const bool ps_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && addsrc == nullptr && aff == nullptr &&
-                     bnb == nullptr;
+                     bnb == nullptr && pscale == nullptr;
   if (ps_ok && ps_mode == 1) {
     static int ncu = 0;
     if (!ncu) {
@@ -1726,7 +1812,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
 #undef DCP_PS
     return;
   }
-  if (fast && Co >= 128 && epi < 2 && use8) {
+  if (fast && Co >= 128 && epi < 2 && use8 && pscale == nullptr) {
     const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
     constexpr size_t lds8 = 3 * (256 + 128) * 128;
     static bool attr8 = false;
@@ -1740,6 +1826,26 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     return;
   }
   const int grid = ntm * ((Co + bn - 1) / bn);
+  if (pscale != nullptr) {
+    // BN prologue on the A operand: 1x1 / stride-1 / FAST, plain or statistics epilogue,
+    // double-buffered (the per-channel table is indexed by k-tile)
+    if (!(fast && taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && ds == 1 && (epi == 0 || epi == 1) &&
+          addsrc == nullptr && aff == nullptr && bnb == nullptr)) {
+      fprintf(stderr, "launch_tap_gemm: the BN prologue needs a plain 1x1 stride-1 forward with C %% 64 == 0\n");
+      abort();
+    }
+#define DCP_TG_PRO(BN_)                                                                      \
+  if (epi == 1) {                                                                            \
+    if (bk32) launch_tg<BN_, 1, true, 2, 32, true>(p, grid, stream);                        \
+    else launch_tg<BN_, 1, true, 2, 64, true>(p, grid, stream);                             \
+  } else {                                                                                   \
+    if (bk32) launch_tg<BN_, 0, true, 2, 32, true>(p, grid, stream);                        \
+    else launch_tg<BN_, 0, true, 2, 64, true>(p, grid, stream);                             \
+  }
+    if (bn == 64) { DCP_TG_PRO(64) } else { DCP_TG_PRO(128) }
+#undef DCP_TG_PRO
+    return;
+  }
 #define DCP_TG_NS(BN_, EPI_, FAST_)                                                    \
   if (bk32 && ns == 2) launch_tg<BN_, EPI_, FAST_, 2, 32>(p, grid, stream);             \
   else if (bk32 && ns == 3) launch_tg<BN_, EPI_, (FAST_ || true), 3, 32>(p, grid, stream);  \
@@ -1864,9 +1970,12 @@ int wgrad_plan_splits(int N, int Ho, int Wo, int Co, int Hs, int Ws, int Cs, int
 
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
                   const bf16* src, int Hs, int Ws, int Cs, int ss,
-                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream) {
+                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream,
+                  const float* pscale, const float* pshift) {
   WgradParams p;
   p.dy = dy; p.src = src; p.dw = dw; p.zero = zero;
+  p.pscale = pscale; p.pshift = pshift;
+  const bool pro = pscale != nullptr;
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs; p.Ho = Ho; p.Wo = Wo; p.ss = ss;
   p.Co = Co; p.M = N * Ho * Wo; p.ldw = taps.n * Cs;
   p.cpt = Cs / 8; p.kc_total = taps.n * p.cpt;
@@ -1875,7 +1984,7 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
-  if (is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
+  if (!pro && is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
     const int s3 = wgrad3x3_splits(N, Ho, Wo, Cs, Co, num_cu);
     if (s3 > 0) {
       // part holds wgrad_plan_splits(...) = s3 partial slices (the caller sized it by that plan)
@@ -1887,6 +1996,10 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   p.direct = (taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && Hs == Ho && Ws == Wo) ? 1 : 0;
   const bool big = wgrad_big(Co, p.ldw);
   const bool narrow = wgrad_narrow(Co, p.ldw);
+  if (pro && (!p.direct || narrow)) {  // (the 64-row kernel has no prologue)
+    fprintf(stderr, "launch_wgrad: the BN prologue needs a 1x1 stride-1 conv with Co > 64 or Cs < 128\n");
+    abort();
+  }
   const int tiles = wgrad_tiles(Co, p.ldw);
   p.ablate = g_tune[2];
   if (g_tune[6] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
@@ -1915,10 +2028,21 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     constexpr int lds = 4 * 64 * 512;
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)wgrad256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipFuncSetAttribute((const void*)wgrad256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr = true;
     }
-    hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * splits), dim3(512), lds, stream, p);
+    static bool attr_pro = false;
+    if (pro && !attr_pro) {  // + the (scale, shift) table of up to 2048 channels
+      hipFuncSetAttribute((const void*)wgrad256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          lds + 8 * 2048);
+      attr_pro = true;
+    }
+    if (pro)
+      hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(tiles * splits), dim3(512), lds + 8 * Cs, stream, p);
+    else hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(tiles * splits), dim3(512), lds, stream, p);
+  } else if (pro) {
+    if (wbk32) hipLaunchKernelGGL((wgrad_kernel<32, true>), dim3(tiles * splits), dim3(256), 4 * 32 * 256, stream, p);
+    else hipLaunchKernelGGL((wgrad_kernel<64, true>), dim3(tiles * splits), dim3(256), 4 * 64 * 256, stream, p);
   } else {
     if (wbk32) hipLaunchKernelGGL(wgrad_kernel<32>, dim3(tiles * splits), dim3(256), 4 * 32 * 256, stream, p);
     else hipLaunchKernelGGL(wgrad_kernel<64>, dim3(tiles * splits), dim3(256), 4 * 64 * 256, stream, p);

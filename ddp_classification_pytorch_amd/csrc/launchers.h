@@ -56,7 +56,10 @@ struct AffineEpi {
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,
-                     const BnBwdEpi* bnb = nullptr, const AffineEpi* aff = nullptr);
+                     const BnBwdEpi* bnb = nullptr, const AffineEpi* aff = nullptr,
+                     const float* pscale = nullptr, const float* pshift = nullptr);
+// (pscale, pshift: BN + ReLU prologue on the input of a 1x1 stride-1 forward, K5 -- the input is
+// the BN's input x and the conv sees bf16(relu(x * pscale[c] + pshift[c])))
 // backward of act(c * scale + shift [+ r]) from its output y: g = dy * act'(y) and dc = g * scale
 // (g only when want_g: the residual's gradient)
 void launch_act_scale_bwd(const bf16* dy, const bf16* y, const float* scale, int64_t M, int C, int act, float slope,
@@ -74,7 +77,8 @@ void launch_wgrad3x3(const bf16* dy, const bf16* x, int N, int H, int W, int C, 
                      const bf16* zero, hipStream_t stream);
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream);
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
-                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream);
+                  const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream,
+                  const float* pscale = nullptr, const float* pshift = nullptr);
 // frag: gconv_frag_elems(...) bf16 workspace (MFMA path; may be null -> direct kernels)
 // stats (optional, [gconv_fwd_stat_blocks(M)][3][Co]): BN partials of y from the MFMA kernel's epilogue;
 // returns whether they were written (false: the direct fallback kernel ran)

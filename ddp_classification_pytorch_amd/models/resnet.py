@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as Fn
-from .layers import BatchNorm2d, Conv2d, Linear, conv_bn
+from .layers import BatchNorm2d, Conv2d, Linear, bn_relu_conv, conv_bn
 
 
 # the one-op stem (conv + BN + ReLU + max pool, fused one-pass backward, stem.hip stem_bwd).
@@ -101,8 +101,8 @@ class Bottleneck(nn.Module):
         # a grouped conv2 (ResNeXt) fuses bn1's backward reduction into its dgrad
         y = self.bn1(y, s, act="relu", fuse_bwd=self.conv2.groups > 1)
         y, s = self.conv2(y, stats=t)
-        y = self.bn2(y, s, act="relu")
-        y, s = self.conv3(y, stats=t)
+        # bn2 + ReLU run inside conv3's GEMMs (layers.bn_relu_conv): no activation pass
+        y, s = bn_relu_conv(self.bn2, self.conv3, y, s, stats=t)
         if self.downsample is not None:
             r, rs = self.downsample[0](x, stats=t, deposit=join)
             return self.bn3(y, s, act="relu", residual=r, residual_bn=(self.downsample[1], rs))

@@ -266,6 +266,16 @@ def conv_fwd_affine(x, w, stride, pad, scale, shift, act, slope, res):
     return bn_act(c, res, scale, shift, act, slope)
 
 
+def conv_fwd_pro(x, w, scale, shift, stats):
+    """1x1 conv of the bf16 activation bf16(relu(x * scale + shift)) (the BN + ReLU the kernel
+    applies to its A operand, K5)."""
+    return conv_fwd(bn_act(x, None, scale, shift, 1, 0.0), w, 1, 0, stats)
+
+
+def conv_wgrad_pro(dy, x, scale, shift):
+    return conv_wgrad(dy, bn_act(x, None, scale, shift, 1, 0.0), 1, 1, 1, 0)
+
+
 def act_scale_bwd(dy, y, scale, act, slope, want_g):
     g = _f(dy) * _act_d(_f(y), act, slope)
     gd = g.to(dy.dtype)

@@ -571,6 +571,100 @@ class _BNAct(Function):
         return dx, None, dgamma, dbeta, dres, None, None, None, None, None
 
 
+# ----------------------------------------------------------------------------- BN + ReLU as a conv prologue
+# A training-mode BN + ReLU whose only consumer is a 1x1 stride-1 conv (a bottleneck's bn2 ->
+# conv3) can be applied inside that conv: the forward tap GEMM normalises its A fragments in
+# registers, the weight-gradient GEMM its B fragments.  The activation
+# relu(bn(x)) is then never written nor kept for backward (ResNet-50 b1024: 2.8 GB less
+# activation memory).  Off by default because it measured slower on MI355X: every column tile of
+# the GEMM (Co / 128 of them, up to 16) and every wave sharing a fragment re-applies the
+# transform, which costs more VALU time than the 0.9 ms/step BN-apply pass it removes
+# (profiles/r3/bn_prologue_ab_b1024.txt: conv3 fwd + wgrad 7.61 -> 9.34 ms/step against
+# 0.92 ms of BN-apply saved; headline 14,222 -> 14,090 img/s).  DCP_BN_PROLOGUE=1 /
+# set_bn_prologue(True) turns it on (memory-bound runs, A/B).
+_BN_PROLOGUE = [os.environ.get("DCP_BN_PROLOGUE", "0") == "1"]
+
+
+def set_bn_prologue(enabled: bool):
+    _BN_PROLOGUE[0] = bool(enabled)
+
+
+def bn_prologue_enabled() -> bool:
+    return _BN_PROLOGUE[0]
+
+
+def bn_prologue_fits(C: int, Co: int) -> bool:
+    """Channel layouts the prologue kernels take: C % 64 == 0 (one tap per 64-deep k-tile),
+    C <= 2048 (the LDS table), and not the narrow Co <= 64 / C >= 128 weight-gradient tile."""
+    return C % 64 == 0 and Co % 8 == 0 and C <= 2048 and not (Co <= 64 and C >= 128)
+
+
+class _BNReluConv1x1(Function):
+    """y = conv1x1(relu(BN(x))) with the BN + ReLU applied to the conv's operands in registers.
+
+    Forward: the BN coefficients from x's producer statistics (SyncBN: the all-gather), then
+    ``conv_fwd_pro`` (and the statistics of y for the next BN).  Backward: the conv's dgrad gives
+    the gradient of relu(BN(x)); ``conv_wgrad_pro`` recomputes relu(BN(x)) from x in the
+    weight-gradient GEMM; the BN + ReLU backward runs from x as in :class:`_BNAct`."""
+
+    @staticmethod
+    def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig, weight, wb, wt, stats):
+        k = K(x)
+        if cfg.training_stats:
+            mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
+        else:
+            mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
+            count = x.numel() // x.shape[-1]
+        y, yslabs = k.conv_fwd_pro(x, wb, scale, shift, stats)
+        ctx.save_for_backward(x, scale, shift, mean, invstd, wt)
+        ctx.cfg, ctx.count = cfg, count
+        ctx.mark_non_differentiable(yslabs)
+        ctx.set_materialize_grads(False)
+        return y, yslabs
+
+    @staticmethod
+    def backward(ctx, dy, _dslabs):
+        if dy is None:
+            return (None,) * 11
+        x, scale, shift, mean, invstd, wt = ctx.saved_tensors
+        cfg = ctx.cfg
+        dy = dy.contiguous()
+        k = K(dy)
+        dx = dgamma = dbeta = dw = None
+        need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        g = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], 1, 0) if need_x else None
+        if ctx.needs_input_grad[7]:
+            dw = k.conv_wgrad_pro(dy, x, scale, shift)
+        if g is not None:
+            need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+            local = sums = None
+            if cfg.training_stats or need_affine:
+                local = k.bn_bwd_reduce(g, x, None, scale, shift, mean, invstd, 1, 0.0)
+                sums = local
+                if cfg.training_stats and cfg.group is not None:
+                    sums = local.clone()
+                    dist.all_reduce(sums, group=cfg.group)
+            dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums if cfg.training_stats else None,
+                                   float(ctx.count), 1, 0.0, False)
+            dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
+            dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
+        return dx, None, dgamma, dbeta, None, None, None, dw, None, None, None
+
+
+def bn_relu_conv1x1(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats=False,
+                    group=None):
+    """conv1x1(relu(BN(x))) through :class:`_BNReluConv1x1` -> (y, statistics slabs of y or None).
+    weight: fp32 [Co, 1, 1, C]."""
+    world = dist.get_world_size(group) if group is not None else 1
+    cfg = BNConfig(training_stats, momentum, eps, 1, 0.0, group, world)
+    if slabs is not None and slabs.numel() == 0:
+        slabs = None
+    wb, wt = prepared_weight(weight, 0, True)
+    want = bool(stats and x.is_cuda)
+    y, yslabs = _BNReluConv1x1.apply(x, slabs, gamma, beta, run_mean, run_var, cfg, weight, wb, wt, want)
+    return y, (yslabs if want else None)
+
+
 def _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
     if cfg.training_stats:
         return _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)

@@ -53,13 +53,40 @@ def test_fused_bn_backward_matches_unfused(name, monkeypatch):
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
 
 
-def test_resnet50_fuses_expected_layers(monkeypatch):
+@pytest.mark.parametrize("prologue", [True, False])
+def test_resnet50_fuses_expected_layers(monkeypatch, prologue):
     calls = []
     orig = _ref.conv_dgrad_bn
     monkeypatch.setattr(_ref, "conv_dgrad_bn", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    _grads("resnet50", True)
-    # conv2 of the 13 stride-1 blocks, conv3 of all 16, conv1 of the 15 blocks after the first
-    assert len(calls) == 13 + 16 + 15
+    Fn.set_bn_prologue(prologue)
+    try:
+        _grads("resnet50", True)
+    finally:
+        Fn.set_bn_prologue(False)
+    # conv2 of the 13 stride-1 blocks, conv1 of the 15 blocks after the first, and conv3 of all 16
+    # unless bn2 runs as conv3's prologue (its backward is then the prologue op's own)
+    assert len(calls) == 13 + 15 + (0 if prologue else 16)
+
+
+@pytest.mark.parametrize("name", ["resnet50", "resnext50_32x4d"])
+def test_bn_prologue_matches_separate_bn(name, monkeypatch):
+    """bn2 + ReLU inside conv3's GEMMs (K5 prologue) == BN-apply pass then conv: same loss and
+    gradients, and the prologue ops run for every bottleneck."""
+    calls = []
+    orig = _ref.conv_fwd_pro
+    monkeypatch.setattr(_ref, "conv_fwd_pro", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    Fn.set_plain_bn_backward_fusion(False)
+    try:
+        Fn.set_bn_prologue(True)
+        l1, g1 = _grads(name, True)
+        assert len(calls) == 16
+        Fn.set_bn_prologue(False)
+        l0, g0 = _grads(name, True)
+        assert len(calls) == 16
+    finally:
+        Fn.set_bn_prologue(False)
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
 
 
 class _Probe(torch.autograd.Function):

@@ -1082,3 +1082,35 @@ def test_persistent_tap_gemm_matches(K, shape, bk):
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
     yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
     assert relerr(y1, yr) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 56, 56, 64, 256),    # stage-1 conv3: one 64-deep k-tile, 128-wide tiles
+    (3, 28, 28, 128, 512),   # stage 2: 32-deep k-tiles
+    (2, 14, 14, 256, 1024),  # stage 3 (weight gradient: the 256x256 tile kernel)
+    (4, 7, 7, 512, 2048),    # stage 4
+    (3, 13, 11, 128, 256),   # M not a multiple of 128
+    (2, 9, 9, 64, 64),       # 64-wide tiles
+])
+def test_conv_bn_prologue(K, shape):
+    """K5: BN + ReLU applied to the 1x1 conv's operands in registers == the fp32 reference of
+    conv(bf16(relu(x * scale + shift))) -- forward output, its BN statistics slabs and the weight
+    gradient (the input recomputed in the B fragments)."""
+    N, H, W, C, Co = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, C)
+    w = rnd(Co, 1, 1, C, scale=1.0 / math.sqrt(C))
+    scale = torch.rand(C) + 0.5
+    shift = torch.randn(C) * 0.5
+    y, slabs = K.conv_fwd_pro(x.to(DEV), w.to(DEV), scale.to(DEV), shift.to(DEV), True)
+    yr, _ = _ref.conv_fwd_pro(x.float(), w.float(), scale, shift, False)
+    assert y.shape == (N, H, W, Co)
+    assert relerr(y, yr) < 5e-3
+    st = K.bn_stats(y, slabs)
+    rst = _ref.bn_stats(y.cpu().float(), None)
+    assert relerr(st[0, 1], rst[0, 1]) < 1e-3 and relerr(st[0, 2], rst[0, 2]) < 1e-3
+    dy = rnd(N, H, W, Co)
+    dw = K.conv_wgrad_pro(dy.to(DEV), x.to(DEV), scale.to(DEV), shift.to(DEV))
+    dwr = _ref.conv_wgrad_pro(dy.float(), x.float(), scale, shift)
+    assert dw.shape == (Co, 1, 1, C)
+    assert relerr(dw, dwr) < 5e-3

@@ -79,3 +79,39 @@ def test_tresnet_inplace_abn_saves_activation_memory():
         del m, loss, x
         torch.cuda.empty_cache()
     assert peaks[True] < 0.9 * peaks[False], peaks
+
+
+def test_bn_prologue_step_matches_separate_bn():
+    """ResNet-50 training step with bn2 + ReLU inside conv3's GEMMs (DCP_BN_PROLOGUE, K5) against
+    the separate BN-apply pass: same loss and gradients up to bf16 accumulation order, and less
+    peak memory (the normalised activations are not kept for backward)."""
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    dev = torch.device("cuda", 0)
+    res = {}
+    try:
+        for pro in (False, True):
+            Fn.set_bn_prologue(pro)
+            torch.manual_seed(0)
+            m = build_model("resnet50", num_classes=100).to(dev)
+            imgs = torch.randint(0, 256, (32, 3, 112, 112), dtype=torch.uint8, device=dev,
+                                 generator=torch.Generator(device=dev).manual_seed(1))
+            labels = torch.arange(32, device=dev) % 100
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), cpad=3, nchw=True, in_scale=1 / 255.0)
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats(dev)
+            base = torch.cuda.memory_allocated(dev)
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            peak = torch.cuda.max_memory_allocated(dev) - base
+            res[pro] = (loss.item(), torch.cat([p.grad.flatten().float() for p in m.parameters()]), peak)
+            del m, loss, x
+            torch.cuda.empty_cache()
+    finally:
+        Fn.set_bn_prologue(False)
+    (l0, g0, p0), (l1, g1, p1) = res[False], res[True]
+    assert abs(l1 - l0) < 1e-2 * abs(l0), (l0, l1)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 2e-2
+    assert p1 < p0, (p0, p1)
