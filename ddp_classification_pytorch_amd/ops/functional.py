@@ -249,14 +249,24 @@ _FUSE_BN_BWD = [os.environ.get("DCP_BN_FUSE", "masked") != "none"]
 # by default; kept selectable for A/B runs and tested.
 _FUSE_LEAKY = [False]
 # The dgrad-epilogue BN fusion is used for BN + residual + ReLU layers (activation mask bits,
-# EPI 4).  For the plain BN + ReLU layers (mask recomputed from the BN input, EPI 3) the separate
-# reduction pass measured faster: ResNet-50 b1024 14,240 vs 14,170 img/s over two back-to-back
-# A/B pairs (`DCP_BN_FUSE=all` restores it; profiles/meas_r2c/bn_fuse_ab.txt).
-_FUSE_PLAIN = [os.environ.get("DCP_BN_FUSE", "masked") == "all"]
+# EPI 4).  For the plain BN + ReLU layers (mask recomputed from the BN input, EPI 3) it depends on
+# the layer size: on large activations the separate reduction pass measured as fast or faster
+# (ResNet-50 b1024: 14,240 vs 14,170 img/s in round 2, 14,099 vs 14,079 in round 3), on small ones
+# the fusion saves a launch-bound reduction + partial-sum pair per layer (b32 graph 4,392 -> 4,592,
+# b128 9,742 -> 9,933 img/s; profiles/r3/bn_fuse_ab_batch.txt).  Default ("auto"): fuse plain
+# layers whose activation has at most _PLAIN_FUSE_MAX elements (every layer at batch <= 128, stage 4
+# at 1024); DCP_BN_FUSE=all fuses every plain layer, =masked none of them.
+_BN_FUSE_MODE = os.environ.get("DCP_BN_FUSE", "auto")
+_FUSE_PLAIN = [_BN_FUSE_MODE == "all"]
+_PLAIN_FUSE_MAX = [0 if _BN_FUSE_MODE == "masked" else int(os.environ.get("DCP_BN_FUSE_PLAIN_MAX", str(1 << 25)))]
 
 
-def set_plain_bn_backward_fusion(enabled: bool):
+def set_plain_bn_backward_fusion(enabled: bool, max_elems: "int | None" = None):
+    """Fuse every plain BN + ReLU backward reduction (True) or apply the size rule (False) with
+    threshold ``max_elems`` (unchanged when None; 0 = never)."""
     _FUSE_PLAIN[0] = bool(enabled)
+    if max_elems is not None:
+        _PLAIN_FUSE_MAX[0] = int(max_elems)
 
 
 def set_leaky_bn_backward_fusion(enabled: bool):
@@ -813,7 +823,8 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the
     # gradient early composes with any unfused fallback
     src = None
-    fusable = not iabn and ((cfg.act in (0, 1) and (residual is not None or _FUSE_PLAIN[0] or fuse_bwd)) or
+    plain = _FUSE_PLAIN[0] or fuse_bwd or x.numel() <= _PLAIN_FUSE_MAX[0]
+    fusable = not iabn and ((cfg.act in (0, 1) and (residual is not None or plain)) or
                             (cfg.act == 2 and residual is None and _FUSE_LEAKY[0]))
     if training_stats and fusable and _FUSE_BN_BWD[0] and torch.is_grad_enabled():
         src = BNSource(cfg.act, cfg.slope)

@@ -12,10 +12,11 @@ from ddp_classification_pytorch_amd.ops import functional as Fn
 
 @pytest.fixture(autouse=True)
 def _plain_fusion_on():
-    """Exercise the plain BN+ReLU epilogue fusion too (off by default: measured slower)."""
+    """Exercise the plain BN+ReLU epilogue fusion on every layer (by default only on small ones)."""
+    saved = Fn._PLAIN_FUSE_MAX[0]
     Fn.set_plain_bn_backward_fusion(True)
     yield
-    Fn.set_plain_bn_backward_fusion(False)
+    Fn.set_plain_bn_backward_fusion(False, saved)
 
 
 def _grads(name, fuse, size=32, seed=0):
@@ -75,7 +76,8 @@ def test_bn_prologue_matches_separate_bn(name, monkeypatch):
     calls = []
     orig = _ref.conv_fwd_pro
     monkeypatch.setattr(_ref, "conv_fwd_pro", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    Fn.set_plain_bn_backward_fusion(False)
+    saved = Fn._PLAIN_FUSE_MAX[0]
+    Fn.set_plain_bn_backward_fusion(False, 0)
     try:
         Fn.set_bn_prologue(True)
         l1, g1 = _grads(name, True)
@@ -85,6 +87,7 @@ def test_bn_prologue_matches_separate_bn(name, monkeypatch):
         assert len(calls) == 16
     finally:
         Fn.set_bn_prologue(False)
+        Fn.set_plain_bn_backward_fusion(False, saved)
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
 
@@ -282,16 +285,25 @@ def test_tresnet_leaky_bn_backward_fusion(monkeypatch):
 
 
 
-def test_default_fuses_only_masked_layers(monkeypatch):
-    """Default (plain fusion off): only the BN + residual + ReLU layers fuse (ResNet-50: conv1 of
-    the 15 blocks after the first), and gradients still equal the unfused path."""
-    Fn.set_plain_bn_backward_fusion(False)
+@pytest.mark.parametrize("max_elems,expect", [(0, 15), (8192, 15 + 10 + 13), (1 << 25, 15 + 13 + 16)])
+def test_plain_fusion_size_rule(monkeypatch, max_elems, expect):
+    """Plain BN + ReLU layers fuse their backward reduction into the consuming stride-1 conv's dgrad
+    only up to ``max_elems`` activation elements.  Threshold 0: only the BN + residual + ReLU layers
+    (ResNet-50: conv1 of the 15 blocks after the first).  32px ResNet-50 at batch 4, threshold 8192:
+    stage 1's plain BN outputs (16,384 elements) stay unfused; in stages 2-4 conv2 of the 3 + 5 + 2
+    stride-1 blocks and conv3 of all 4 + 6 + 3 blocks fuse.  Gradients equal the unfused path."""
+    saved = Fn._PLAIN_FUSE_MAX[0]
+    Fn.set_plain_bn_backward_fusion(False, max_elems)
     calls = []
     orig = _ref.conv_dgrad_bn
     monkeypatch.setattr(_ref, "conv_dgrad_bn", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    l1, g1 = _grads("resnet50", True)
-    assert len(calls) == 15
-    l0, g0 = _grads("resnet50", False)
+    try:
+        l1, g1 = _grads("resnet50", True)
+        n = len(calls)
+        l0, g0 = _grads("resnet50", False)
+    finally:
+        Fn.set_plain_bn_backward_fusion(False, saved)
+    assert n == expect
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-5
 
