@@ -184,6 +184,52 @@ __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part
   return a;
 }
 
+// conv slabs [R][2][C] (per-128-row (mean, M2), slab r holds min(128, M - 128 r) rows) merged
+// straight into (n, mean, M2) of channel blockIdx.x*64 + lane, complete in wave 0 -- the one-level
+// path for R <= kDirectSlabs (small activations: no bn_slab_partial launch, whose per-launch cost
+// dominated the statistics of every layer at batch 32-128)
+constexpr int kDirectSlabs = 1024;
+__device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, int R, int M, int C) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  Welford a{0.f, 0.f, 0.f};
+  if (c < C) {
+    int r = w;
+    for (; r + 3 * kMergeWaves < R; r += 4 * kMergeWaves) {
+      float mb[4], m2b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mb[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a.merge((float)min(128, M - 128 * (r + u * kMergeWaves)), mb[u], m2b[u]);
+    }
+    for (; r < R; r += kMergeWaves)
+      a.merge((float)min(128, M - 128 * r), slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
+  }
+  __shared__ float red[3][kMergeWaves][64];
+  red[0][w][lane] = a.n;
+  red[1][w][lane] = a.mean;
+  red[2][w][lane] = a.m2;
+  __syncthreads();
+  if (w == 0)
+    for (int k = 1; k < kMergeWaves; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+  return a;
+}
+
+// slabs [R][2][C] -> out [3][C] (R <= kDirectSlabs)
+__global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_merge_kernel(const float* __restrict__ slabs, int R, int M,
+                                                                         int C, float* __restrict__ out) {
+  const Welford a = merge_slabs(slabs, R, M, C);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) == 0 && c < C) {
+    out[c] = a.n;
+    out[C + c] = a.mean;
+    out[2 * C + c] = a.m2;
+  }
+}
+
 // partials [P][3][C] -> out [3][C]
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_kernel(const float* __restrict__ part, int P, int C,
                                                        float* __restrict__ out) {
@@ -224,6 +270,20 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_finalize_kernel(
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
     float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
   const Welford m = merge_partials(part, P, C);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  Welford a{0.f, 0.f, 0.f};
+  a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
+}
+
+// local BN from the conv slabs in one launch (R <= kDirectSlabs): merge + finalize; the same
+// merge order as bn_slab_merge_kernel, so SyncBN at world size 1 stays bit-identical
+__global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
+    const float* __restrict__ slabs, int R, int M, int C, float eps, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
+    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+  const Welford m = merge_slabs(slabs, R, M, C);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) != 0 || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
@@ -671,6 +731,11 @@ static int launch_stat_partials(const bf16* x, const float* slabs, int M, int C,
 
 // part: bn_stats_partials(...) x 3 x C scratch; out [3][C]
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
+  const int R = (M + 127) / 128;
+  if (slabs && R <= kDirectSlabs) {
+    hipLaunchKernelGGL(bn_slab_merge_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C, out);
+    return;
+  }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
   hipLaunchKernelGGL(bn_merge_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, out);
 }
@@ -678,6 +743,12 @@ void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* par
 void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                               float* shift, float* rm, float* rv, float momentum, hipStream_t s) {
+  const int R = (M + 127) / 128;
+  if (slabs && R <= kDirectSlabs) {
+    hipLaunchKernelGGL(bn_slab_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C,
+                       eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
+    return;
+  }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
   hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps, gamma, beta,
                      mean, invstd, scale, shift, rm, rv, momentum);

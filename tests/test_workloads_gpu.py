@@ -98,7 +98,7 @@ def test_bn_prologue_step_matches_separate_bn():
             imgs = torch.randint(0, 256, (32, 3, 112, 112), dtype=torch.uint8, device=dev,
                                  generator=torch.Generator(device=dev).manual_seed(1))
             labels = torch.arange(32, device=dev) % 100
-            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), cpad=3, nchw=True, in_scale=1 / 255.0)
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), nchw=True, in_scale=1 / 255.0)
             torch.cuda.synchronize()
             torch.cuda.reset_peak_memory_stats(dev)
             base = torch.cuda.memory_allocated(dev)
