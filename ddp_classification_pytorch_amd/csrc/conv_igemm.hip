@@ -271,6 +271,91 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+// Store epilogue of the 4-wave 128-row tap GEMMs (EPI 0: bf16 store, optionally folding an
+// eval-mode BN and adding addsrc; EPI 1: + the per-128-row BN statistics).  Entered after a
+// barrier with no loads in flight; the accumulators go through the LDS image E.
+template <int BN, int EPI>
+__device__ __forceinline__ void tg_store_epilogue(const TapGemmParams& p, const f32x4 (&acc)[BN / 32][4], char* smem,
+                                                  int m0, int n0, int tid, int lane, int wm, int wn) {
+  constexpr int BM = 128, TN = BN / 32;
+  // ---- epilogue through LDS: the k-loop ended with a barrier and no loads in flight ----
+  // tile image E[BM pixels][BN channels] bf16, 16-byte chunks XOR-swizzled by (pixel>>1)
+  constexpr int RB = BN * 2, NCH = BN / 8;
+  char* E = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+      const uint32_t off = eimg_off8<NCH>(pl, cl);
+      *LDS_PTR(bf16x4, E + off) = o;
+    }
+  }
+  __syncthreads();
+  // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels.  All the
+  // thread's image chunks are read first, so its stores issue back to back instead of each
+  // waiting for its own LDS read.
+  {
+    constexpr int R = 256 / NCH;
+    const int c = tid % NCH, pr0 = tid / NCH;
+    const bool cok = n0 + c * 8 < p.Co;
+    float fsc[8], fsh[8];
+    const bool fold = EPI == 0 && p.fscale != nullptr;
+    if (fold) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        fsc[e] = cok ? p.fscale[n0 + c * 8 + e] : 0.f;
+        fsh[e] = cok ? p.fshift[n0 + c * 8 + e] : 0.f;
+      }
+    }
+    bf16x8 vv[BM / R];
+#pragma unroll
+    for (int k = 0; k < BM / R; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
+#pragma unroll
+    for (int k = 0; k < BM / R; ++k) {
+      const int pl = pr0 + k * R;
+      const int m = m0 + pl;
+      const bf16x8 v = vv[k];
+      if (m < p.M && cok) {
+        size_t drow;  // element offsets pass 2^32 at large batch (56x56x256 rows: N > 5,350)
+        if (p.ds == 1) {
+          drow = (size_t)m * (size_t)p.Co;
+        } else {
+          const uint32_t q = fdiv(m, p.div_wy);
+          const uint32_t x = m - q * p.Wy;
+          const uint32_t n = fdiv(q, p.div_hy);
+          const uint32_t y = q - n * p.Hy;
+          drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
+        }
+        bf16x8 o = v;
+        if (fold) {
+          // the bf16 conv output through the unfused BN-apply's fp32 math (bn_act_fwd_kernel)
+          bf16x8 a{};
+          if (p.addsrc) a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float t = bf2f(v[e]) * fsc[e] + fsh[e];
+            if (p.addsrc) t += bf2f(a[e]);
+            if (p.fact == 1) t = fmaxf(t, 0.f);
+            else if (p.fact == 2) t = t >= 0.f ? t : t * p.fslope;
+            o[e] = f2bf(t);
+          }
+        } else if (p.addsrc) {
+          const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
+        }
+        *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
+      }
+    }
+  }
+  if constexpr (EPI == 1) tile_stats128<BN>(p, E, m0, n0, tid);
+}
+
 // EPI: 0 = bf16 store, 1 = store + per-64-row BN statistics, 2 = bias / activation (linear heads)
 // FAST: Cs % 64 == 0, one tap per 64-deep k-tile
 // NS: LDS stages.  NS = 2: double buffer, vmcnt(0) + barrier per k-tile (several blocks per
@@ -627,82 +712,7 @@ tap_gemm_kernel(const TapGemmParams p) {
   }
 
   if constexpr (EPI != 2) {
-    // ---- epilogue through LDS: the k-loop ended with a barrier and no loads in flight ----
-    // tile image E[BM pixels][BN channels] bf16, 16-byte chunks XOR-swizzled by (pixel>>1)
-    constexpr int RB = BN * 2, NCH = BN / 8;
-    char* E = smem;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        const uint32_t off = eimg_off8<NCH>(pl, cl);
-        *LDS_PTR(bf16x4, E + off) = o;
-      }
-    }
-    __syncthreads();
-    // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels.  All the
-    // thread's image chunks are read first, so its stores issue back to back instead of each
-    // waiting for its own LDS read.
-    {
-      constexpr int R = 256 / NCH;
-      const int c = tid % NCH, pr0 = tid / NCH;
-      const bool cok = n0 + c * 8 < p.Co;
-      float fsc[8], fsh[8];
-      const bool fold = EPI == 0 && p.fscale != nullptr;
-      if (fold) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          fsc[e] = cok ? p.fscale[n0 + c * 8 + e] : 0.f;
-          fsh[e] = cok ? p.fshift[n0 + c * 8 + e] : 0.f;
-        }
-      }
-      bf16x8 vv[BM / R];
-#pragma unroll
-      for (int k = 0; k < BM / R; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
-#pragma unroll
-      for (int k = 0; k < BM / R; ++k) {
-        const int pl = pr0 + k * R;
-        const int m = m0 + pl;
-        const bf16x8 v = vv[k];
-        if (m < p.M && cok) {
-          size_t drow;  // element offsets pass 2^32 at large batch (56x56x256 rows: N > 5,350)
-          if (p.ds == 1) {
-            drow = (size_t)m * (size_t)p.Co;
-          } else {
-            const uint32_t q = fdiv(m, p.div_wy);
-            const uint32_t x = m - q * p.Wy;
-            const uint32_t n = fdiv(q, p.div_hy);
-            const uint32_t y = q - n * p.Hy;
-            drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
-          }
-          bf16x8 o = v;
-          if (fold) {
-            // the bf16 conv output through the unfused BN-apply's fp32 math (bn_act_fwd_kernel)
-            bf16x8 a{};
-            if (p.addsrc) a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              float t = bf2f(v[e]) * fsc[e] + fsh[e];
-              if (p.addsrc) t += bf2f(a[e]);
-              if (p.fact == 1) t = fmaxf(t, 0.f);
-              else if (p.fact == 2) t = t >= 0.f ? t : t * p.fslope;
-              o[e] = f2bf(t);
-            }
-          } else if (p.addsrc) {
-            const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
-          }
-          *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
-        }
-      }
-    }
-    if constexpr (EPI == 1) tile_stats128<BN>(p, E, m0, n0, tid);
+    tg_store_epilogue<BN, EPI>(p, acc, smem, m0, n0, tid, lane, wm, wn);
     return;
   }
 
@@ -738,6 +748,147 @@ tap_gemm_kernel(const TapGemmParams p) {
       if (mok && co < p.Co) *(bf16x4*)(p.dst + drow + co) = o;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Window tap GEMM: 3x3-neighbourhood taps (|dy|, |dx| <= 1, stride 1, output grid == input grid:
+// the 3x3 / pad-1 forward conv and its data gradient), C % 64 == 0.
+//
+// tap_gemm_kernel gathers a fresh 128-row A tile for every (tap, 64-channel chunk) k-step, so
+// every input pixel crosses L2 -> LDS nine times.  Here a workgroup's 128 GEMM rows are 128
+// consecutive output pixels (NHWC order), and the input pixels any of their taps can touch form
+// ONE contiguous range, [m0 - W - 1, m0 + 128 + W + 1): that "window" is staged once per
+// 64-channel chunk (one LDS-DMA per 16-byte piece, pieces XOR-swizzled by the window pixel's low
+// three bits so a fragment read of 16 consecutive pixels is conflict free), and tap t reads it
+// shifted by dy * W + dx.  A tap whose source pixel lies outside the image (image edges, other
+// images of the batch) is masked to zero per fragment from a 9-bit validity mask computed once.
+// The k-steps run chunk-major (9 taps of one chunk, then the next): the next chunk's window
+// streams in one instruction per step over the first steps, the next step's weight tile
+// (128 channels x 64) is double-buffered; vmcnt(0) + barrier per step as in tap_gemm_kernel.
+// LDS: 2 windows of (128 + 2W + 2) x 128 B (rounded to 4 KB) + 2 x 16 KB weights: two workgroups
+// per CU up to W = 28.
+// Measured (profiles/r3/conv3x3_window_ab_b1024.txt): no faster than the gather kernel on the
+// ResNet-50 3x3 shapes (128 ch 28x28: 301.6 vs 299.8 us forward; 256 ch 14x14: 257.8 vs 249.2;
+// headline 14,236 -> 14,186 img/s) -- cutting the A staging to a ninth does not move a k-loop
+// bound by its per-step barrier and load latency.  Kept behind g_tune[22] = 1 (off by default).
+// ---------------------------------------------------------------------------
+constexpr int kWinMaxW = 64;  // widest image row (the next window streams in over <= 9 steps)
+
+__host__ __device__ constexpr int win_instrs(int W) { return ((128 + 2 * W + 2) * 8 + 255) / 256; }
+
+__device__ __forceinline__ uint32_t win_off(uint32_t w, uint32_t k) { return w * 128u + ((k ^ (w & 7u)) << 4); }
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) tap_win_kernel(const TapGemmParams p) {
+  constexpr int BN = 128, BM = 128, BK = 64, TN = BN / 32;
+  constexpr int B_BYTES = BN * BK * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int W = p.Ws, H = p.Hs;
+  const int WP = BM + 2 * W + 2;
+  const int nwi = win_instrs(W);
+  const int wbytes = nwi * 4096;
+  char* const win0 = smem;
+  char* const bst0 = smem + 2 * wbytes;
+  const int wbase = m0 - W - 1;  // input pixel at window index 0
+  const int ntaps = p.ntaps;
+  const int nkt = (p.Cs / BK) * ntaps;
+
+  // per A fragment: which taps read a pixel inside the image (bit t)
+  uint32_t vm[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t mm = (uint32_t)min(m0 + wm * 64 + i * 16 + (int)(lane & 15), p.M - 1);
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const int x = (int)(mm - q * p.Wy);
+    const int y = (int)(q - fdiv(q, p.div_hy) * p.Hy);
+    uint32_t v = 0;
+    for (int t = 0; t < ntaps; ++t) {
+      const int tv = p.tap[t];
+      v |= ((unsigned)(y + tap_dy(tv)) < (unsigned)H && (unsigned)(x + tap_dx(tv)) < (unsigned)W) ? (1u << t) : 0u;
+    }
+    vm[i] = v;
+  }
+  // weight tile rows (tap_gemm_kernel's FAST B staging, 64-deep)
+  const bf16* fb_ptr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (wave * 4 + i) * 8 + lane / 8;
+    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % 8) ^ swz_chunk<BK>(r)) * 8;
+  }
+
+  auto stage_win = [&](int ch, int b, int j) {
+    const int L = j * 256 + tid;  // physical 16-byte slot of the window buffer
+    const int w = L >> 3;
+    if (w < WP) {
+      const int k = (L & 7) ^ (w & 7);
+      const int q = wbase + w;
+      const bf16* g = (q >= 0 && q < p.M) ? p.src + (size_t)q * p.Cs + ch * BK + k * 8 : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, win0 + b * wbytes + (j * 256 + wave * 64) * 16),
+                                       16, 0, 0);
+    }
+  };
+  auto stage_b = [&](int kt, int b) {
+    const int ch = kt / ntaps, t = kt - ch * ntaps;
+    const long boff = (long)tap_w(p.tap[t]) * p.Cs + ch * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff),
+                                       LDS_PTR(void, bst0 + b * B_BYTES + (wave * 4 + i) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int j = 0; j < nwi; ++j) stage_win(0, 0, j);
+  stage_b(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int ch = kt / ntaps, t = kt - ch * ntaps;
+    // the next chunk's window: one instruction per step over this chunk's first nwi steps (its
+    // buffer was last read by the previous chunk, which ended behind a barrier)
+    if (t < nwi && (ch + 1) * ntaps < nkt) stage_win(ch + 1, (ch + 1) & 1, t);
+    if (kt + 1 < nkt) stage_b(kt + 1, (kt + 1) & 1);
+    const char* Wn = win0 + (ch & 1) * wbytes;
+    const char* Bs = bst0 + (kt & 1) * B_BYTES;
+    const int tv = p.tap[t];
+    const int shift = W + 1 + tap_dy(tv) * W + tap_dx(tv);
+    const uint32_t tbit = 1u << t;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      const uint32_t c = s * 4 + (lane >> 4);
+      bf16x8 wf[TN], af[4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint32_t r = wn * (BN / 2) + j * 16 + (lane & 15);
+        wf[j] = *(const bf16x8*)(Bs + swzk<BK>(r, c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t w = wm * 64 + i * 16 + (lane & 15) + shift;
+        const bf16x8 a = *(const bf16x8*)(Wn + win_off(w, c));
+        af[i] = (vm[i] & tbit) ? a : bf16x8{};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  tg_store_epilogue<BN, EPI>(p, acc, smem, m0, n0, tid, lane, wm, wn);
 }
 
 // ---------------------------------------------------------------------------
@@ -1773,6 +1924,27 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // stage-1 expansion at b1024, tools/fwd_epi_bench.py)
   if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
   const bool use8 = g_tune[3] == 1 && aff == nullptr;  // measured slower than the 4-wave kernel (conv_bench --cfgs)
+  // window kernel (tap_win_kernel): 3x3-neighbourhood taps on a same-size stride-1 grid, C % 64 == 0,
+  // plain / statistics epilogue; g_tune[22] = 1 turns it on (measured no faster, A/B only)
+  bool win_ok = fast && (Cs % 64) == 0 && ss == 1 && ds == 1 && Hy == Hs && Wy == Ws && Hd == Hy && Wd == Wy &&
+                Ws <= kWinMaxW && taps.n > 1 && (epi == 0 || epi == 1) && addsrc == nullptr && aff == nullptr &&
+                bnb == nullptr && pscale == nullptr && g_tune[22] != 2;
+  for (int i = 0; i < taps.n && win_ok; ++i)
+    win_ok = taps.dy[i] >= -1 && taps.dy[i] <= 1 && taps.dx[i] >= -1 && taps.dx[i] <= 1;
+  if (win_ok && g_tune[22] == 1) {
+    const int grid = ntm * ((Co + 127) / 128);
+    const size_t lds = 2 * (size_t)win_instrs(Ws) * 4096 + 2 * 128 * 64 * 2;
+    static bool attr = false;
+    if (!attr) {
+      const int mx = 2 * win_instrs(kWinMaxW) * 4096 + 2 * 128 * 64 * 2;
+      hipFuncSetAttribute((const void*)tap_win_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      hipFuncSetAttribute((const void*)tap_win_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      attr = true;
+    }
+    if (epi == 1) hipLaunchKernelGGL(tap_win_kernel<1>, dim3(grid), dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL(tap_win_kernel<0>, dim3(grid), dim3(256), lds, stream, p);
+    return;
+  }
   // persistent cross-tile-prefetch kernel (tap_gemm_ps_kernel): FAST shapes, plain / statistics
   // epilogue, no residual add / fold; g_tune[20] = 1 on, 2 off (A/B), 0 = heuristic
   const int ps_mode = g_tune[20];

@@ -1122,3 +1122,35 @@ def test_conv_bn_prologue(K, shape):
     dwr = _ref.conv_wgrad_pro(dy.float(), x.float(), scale, shift)
     assert dw.shape == (Co, 1, 1, C)
     assert relerr(dw, dwr) < 5e-3
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (4, 7, 7, 512, 512), (2, 9, 11, 64, 72),
+    (5, 13, 13, 128, 64), (8, 2, 2, 512, 512), (1, 56, 56, 64, 128)])
+def test_conv3x3_window_kernel(K, shape):
+    """tap_win_kernel (g_tune[22] = 1): 3x3 / pad-1 / stride-1 forward (+ BN statistics) and data
+    gradient from one staged pixel window per 64-channel chunk == the fp32 reference, and == the
+    gather kernel to bf16 rounding."""
+    N, H, W, Ci, Co = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, 3, 3, Ci, scale=1.0 / math.sqrt(9 * Ci))
+    dy = rnd(N, H, W, Co).to(DEV)
+    _, wt = K.weight_prep(w.float().to(DEV), 0, True)
+    try:
+        K.set_tuning(22, 1)
+        y, slabs = K.conv_fwd(x, w.to(DEV), 1, 1, True)
+        dx = K.conv_dgrad(dy, wt, H, W, 1, 1) if Co % 64 == 0 else None
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(22, 0)
+    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float(), 1, 1, False)
+    assert relerr(y, yr) < 1e-2
+    st, sr = K.bn_stats(y, slabs), _ref.bn_stats(y.float().cpu(), None)
+    assert torch.equal(st[0, 0].cpu(), sr[0, 0])
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4 and relerr(st[0, 2], sr[0, 2]) < 1e-4
+    y2, _ = K.conv_fwd(x, w.to(DEV), 1, 1, True)
+    assert relerr(y, y2) < 5e-3
+    if dx is not None:
+        dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().permute(3, 1, 2, 0), H, W, 1, 1)
+        assert relerr(dx, dxr) < 1e-2
