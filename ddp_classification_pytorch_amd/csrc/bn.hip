@@ -153,34 +153,35 @@ __global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* _
 }
 
 // partials [P][3][C] -> (n, mean, M2) of channel blockIdx.x*64 + lane, complete in wave 0;
-// one workgroup (kMergeWaves waves splitting P) per 64 channels
+// one workgroup (NW waves splitting P) per 64 channels
 constexpr int kMergeWaves = 16;
+template <int NW = kMergeWaves>
 __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part, int P, int C) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int p = w;
-    for (; p + 3 * kMergeWaves < P; p += 4 * kMergeWaves) {
+    for (; p + 3 * NW < P; p += 4 * NW) {
       float v[4][3];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) v[u][q] = part[((size_t)(p + u * kMergeWaves) * 3 + q) * C + c];
+        for (int q = 0; q < 3; ++q) v[u][q] = part[((size_t)(p + u * NW) * 3 + q) * C + c];
 #pragma unroll
       for (int u = 0; u < 4; ++u) a.merge(v[u][0], v[u][1], v[u][2]);
     }
-    for (; p < P; p += kMergeWaves)
+    for (; p < P; p += NW)
       a.merge(part[((size_t)p * 3 + 0) * C + c], part[((size_t)p * 3 + 1) * C + c],
               part[((size_t)p * 3 + 2) * C + c]);
   }
-  __shared__ float red[3][kMergeWaves][64];
+  __shared__ float red[3][NW][64];
   red[0][w][lane] = a.n;
   red[1][w][lane] = a.mean;
   red[2][w][lane] = a.m2;
   __syncthreads();
   if (w == 0)
-    for (int k = 1; k < kMergeWaves; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+    for (int k = 1; k < NW; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
   return a;
 }
 
@@ -289,6 +290,56 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
   Welford a{0.f, 0.f, 0.f};
   a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
   finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
+}
+
+// Local BN from the conv slabs in ONE launch for any slab count: bn_slab_partial's workgroups
+// (grid (C/64, P)) store their split partials, and the last to arrive for each 64-channel group
+// (last_arrival) merges the P partials in split order and finalizes -- the bn_slab_partial +
+// bn_merge_finalize pair without the second launch.
+__global__ void __launch_bounds__(256) bn_slab_partial_finalize_kernel(
+    const float* __restrict__ slabs, int R, int M, int C, int tiles_per_split, float* __restrict__ part,
+    unsigned* __restrict__ ctr, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * tiles_per_split;
+  const int r1 = min(R, r0 + tiles_per_split);
+  Welford a{0.f, 0.f, 0.f};
+  if (c < C) {
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      float mb[4], m2b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
+    }
+    for (; r < r1; r += 4) {
+      const float nb = (float)min(128, M - 128 * r);
+      a.merge(nb, slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
+    }
+  }
+  __shared__ float red[3][4][64];
+  red[0][w][lane] = a.n;
+  red[1][w][lane] = a.mean;
+  red[2][w][lane] = a.m2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+    part[((size_t)blockIdx.y * 3 + 0) * C + c] = a.n;
+    part[((size_t)blockIdx.y * 3 + 1) * C + c] = a.mean;
+    part[((size_t)blockIdx.y * 3 + 2) * C + c] = a.m2;
+  }
+  if (!last_arrival(ctr + blockIdx.x, gridDim.y)) return;
+  const Welford m = merge_partials<4>(part, gridDim.y, C);
+  if (w != 0 || c >= C) return;
+  Welford f{0.f, 0.f, 0.f};
+  f.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
+  finalize_channel(f, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
 }
 
 // [P][K] -> [K] column sums; one workgroup per 64 columns, 4 waves x 4-deep unroll over P
@@ -747,6 +798,16 @@ void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, f
   if (slabs && R <= kDirectSlabs) {
     hipLaunchKernelGGL(bn_slab_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C,
                        eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
+    return;
+  }
+  // one launch (merge + finalize in each channel group's last workgroup): g_tune[23] = 1 only, measured
+  // slower -- see launch_split_reduce
+  unsigned* ctr = (slabs && g_tune[23] == 1) ? ticket_counters((C + 63) / 64) : nullptr;
+  if (ctr) {
+    const int P = bn_stats_partials(M, C, true);
+    const int tps = (R + P - 1) / P;
+    hipLaunchKernelGGL(bn_slab_partial_finalize_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps,
+                       part, ctr, eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
     return;
   }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);

@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.cuh"
 #include "launchers.h"
@@ -2069,6 +2070,75 @@ __global__ void __launch_bounds__(256) split_reduce1_kernel(const float4* __rest
   }
 }
 
+// split_reduce1 whose second level runs in the last-arriving workgroup of each 64-column group:
+// chunk sums -> tmp[chunk], then that workgroup adds the column group's chunk rows in chunk
+// order (4 waves over the rows, fixed LDS combine: deterministic whichever workgroup is last)
+__global__ void __launch_bounds__(256) split_reduce2_kernel(const float4* __restrict__ part, int splits, int n4,
+                                                            float4* __restrict__ tmp, float4* __restrict__ out,
+                                                            unsigned* __restrict__ ctr) {
+  __shared__ float4 red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int k0 = blockIdx.y * 64;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+#pragma unroll 4
+    for (int k = k0 + sub; k < min(splits, k0 + 64); k += 4) {
+      const float4 v = part[(size_t)k * n4 + col];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && col < n4) {
+    float4 t = red[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float4 v = red[q][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    tmp[(size_t)blockIdx.y * n4 + col] = t;
+  }
+  if (!last_arrival(ctr + blockIdx.x, gridDim.y)) return;
+  const int chunks = gridDim.y;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+#pragma unroll 4
+    for (int k = sub; k < chunks; k += 4) {
+      const float4 v = tmp[(size_t)k * n4 + col];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  __syncthreads();  // red reused
+  red[sub][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (sub == 0 && col < n4) {
+    float4 t = red[0][threadIdx.x];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float4 v = red[q][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    out[col] = t;
+  }
+}
+
+unsigned* ticket_counters(int n) {
+  static std::mutex mu;
+  static unsigned* pool[64] = {nullptr};
+  if (n > kTicketCounters) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!pool[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(unsigned) * kTicketCounters) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(unsigned) * kTicketCounters) != hipSuccess) return nullptr;
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    pool[dev] = (unsigned*)p;
+  }
+  return pool[dev];
+}
+
 // out[i] = sum_k part[k][i]; n % 4 == 0.  part must hold splits*n + ceil(splits/64)*n floats
 // when splits > 64 (the chunk sums are written behind the partials).
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream) {
@@ -2080,6 +2150,16 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
     return;
   }
   float* tmp = const_cast<float*>(part) + (size_t)splits * n;
+  // one launch with the second level in each column group's last workgroup: g_tune[23] = 1 only.
+  // Measured much slower (R50 b1024 14,181 -> 13,538, b32 graph 4,618 -> 3,693 img/s,
+  // profiles/r3/ticket_reduce_ab.txt): the device-scope release fence every workgroup needs before
+  // its ticket writes back its XCD's whole L2, which costs far more than the launch it saves.
+  unsigned* ctr = g_tune[23] == 1 ? ticket_counters((n4 + 63) / 64) : nullptr;
+  if (ctr) {
+    hipLaunchKernelGGL(split_reduce2_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
+                       splits, n4, (float4*)tmp, (float4*)out, ctr);
+    return;
+  }
   hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
                      splits, n4, (float4*)tmp);
   // second level: 4 waves per 64 columns split the chunk rows (a thread-per-column loop over

@@ -1154,3 +1154,26 @@ def test_conv3x3_window_kernel(K, shape):
     if dx is not None:
         dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().permute(3, 1, 2, 0), H, W, 1, 1)
         assert relerr(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_split_reduce_single_launch_ticket(K, mode):
+    """Weight gradient with > 64 split-K partials: the second reduction level as its own launch
+    (default) or in the last workgroup of each column group (last-arrival ticket, g_tune[23] = 1,
+    measured slower); both equal the fp32 reference and are bitwise reproducible run to run."""
+    torch.manual_seed(0)
+    N, H, C, Co = 48, 56, 128, 128  # 150,528 rows: 512 splits -> 8 chunks of 64
+    x = rnd(N, H, H, C).to(DEV)
+    dy = rnd(N, H, H, Co).to(DEV)
+    try:
+        K.set_tuning(23, mode)
+        dw1 = K.conv_wgrad(dy, x, 1, 1, 1, 0)
+        dw2 = K.conv_wgrad(dy, x, 1, 1, 1, 0)
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(23, 0)
+    assert torch.equal(dw1, dw2)
+    dwr = _ref.conv_wgrad(dy[:4].float().cpu(), x[:4].float().cpu(), 1, 1, 1, 0)  # scale check on a slice
+    full = (dy.float().reshape(-1, Co).t() @ x.float().reshape(-1, C)).cpu()
+    assert relerr(dw1.reshape(Co, C), full) < 1e-3
+    assert dwr.shape == dw1.shape
