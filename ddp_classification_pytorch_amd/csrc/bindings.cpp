@@ -224,6 +224,28 @@ std::tuple<Tensor, Tensor> act_scale_bwd(const Tensor& dy, const Tensor& y, cons
 
 // Philox dropout: (y, used) -- `offset` int64[1] device call counter (bumped here after the launch,
 // graph-capturable), `used` int64[1] receives the counter value the mask was drawn with
+// InplaceABN effective weight and its reciprocal: (|g| + eps, 1 / (|g| + eps))
+std::tuple<Tensor, Tensor> iabn_gamma(const Tensor& g, double eps) {
+  CHECK_DEV(g);
+  CHECK_F32(g);
+  CHECK_CONTIG(g);
+  auto geff = at::empty_like(g), rg = at::empty_like(g);
+  dcp::launch_iabn_gamma(g.data_ptr<float>(), (float)eps, geff.data_ptr<float>(), rg.data_ptr<float>(), g.numel(),
+                         cur_stream());
+  return {geff, rg};
+}
+
+// d * sign(g) (the gradient of |g| + eps)
+Tensor sign_mul(const Tensor& d, const Tensor& g) {
+  CHECK_DEV(d);
+  CHECK_F32(d);
+  CHECK_F32(g);
+  TORCH_CHECK(d.is_contiguous() && g.is_contiguous() && d.numel() == g.numel(), "sign_mul shapes");
+  auto out = at::empty_like(d);
+  dcp::launch_sign_mul(d.data_ptr<float>(), g.data_ptr<float>(), out.data_ptr<float>(), d.numel(), cur_stream());
+  return out;
+}
+
 std::tuple<Tensor, Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, const Tensor& offset) {
   CHECK_DEV(x);
   CHECK_CONTIG(x);
@@ -1503,6 +1525,8 @@ TORCH_LIBRARY(dcp, m) {
   m.def("act_scale_bwd(Tensor dy, Tensor y, Tensor scale, int act, float slope, bool want_g) -> (Tensor, Tensor)",
         &act_scale_bwd);
   m.def("dropout_fwd(Tensor x, float p, int seed, Tensor(a!) offset) -> (Tensor, Tensor)", &dropout_fwd);
+  m.def("iabn_gamma(Tensor g, float eps) -> (Tensor, Tensor)", &iabn_gamma);
+  m.def("sign_mul(Tensor d, Tensor g) -> Tensor", &sign_mul);
   m.def("dropout_bwd(Tensor dy, float p, int seed, Tensor used) -> Tensor", &dropout_bwd);
   m.def("adaptive_avg_pool(Tensor x, int OH, int OW) -> Tensor", &adaptive_avg_pool);
   m.def("adaptive_avg_pool_bwd(Tensor dy, int H, int W) -> Tensor", &adaptive_avg_pool_bwd);

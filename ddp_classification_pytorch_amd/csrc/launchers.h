@@ -247,6 +247,9 @@ void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int a
 void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, hipStream_t s);
 // Philox dropout (misc.hip): y = x * keep / (1 - p); keep from (seed, *offset_ptr, element index);
 // `used` (optional) receives the offset the launch drew with (for the mask-regenerating backward)
+// InplaceABN effective weight: geff = |g| + eps, rg = 1 / geff; backward out = d * sign(g)
+void launch_iabn_gamma(const float* g, float eps, float* geff, float* rg, int C, hipStream_t s);
+void launch_sign_mul(const float* d, const float* g, float* out, int C, hipStream_t s);
 void launch_dropout(const void* x, void* y, size_t n, int is_bf16, float p, uint64_t seed, const int64_t* offset_ptr,
                     int64_t* used, hipStream_t s);
 // adaptive average pool NHWC [N,H,W,C] -> [N,OH,OW,C]; backward = true: dy [N,OH,OW,C] -> dx [N,H,W,C]

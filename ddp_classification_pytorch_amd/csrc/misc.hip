@@ -410,4 +410,34 @@ void launch_dropout(const void* x, void* y, size_t n, int is_bf16, float p, uint
                        offset_ptr, used);
 }
 
+// ---------------------------------------------------------------------------
+// InplaceABN effective weight (mapillary inplace_abn, X3/K21): g_eff = |g| + eps and its
+// reciprocal in one launch; backward dg = dg_eff * sign(g) (one launch) -- instead of the abs / add
+// / reciprocal / sgn / mul ATen chain per layer
+// ---------------------------------------------------------------------------
+__global__ void iabn_gamma_kernel(const float* __restrict__ g, float eps, float* __restrict__ geff,
+                                  float* __restrict__ rg, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float e = fabsf(g[c]) + eps;
+  geff[c] = e;
+  rg[c] = 1.f / e;
+}
+
+__global__ void sign_mul_kernel(const float* __restrict__ d, const float* __restrict__ g, float* __restrict__ out,
+                                int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float v = g[c];
+  out[c] = v > 0.f ? d[c] : (v < 0.f ? -d[c] : 0.f);
+}
+
+void launch_iabn_gamma(const float* g, float eps, float* geff, float* rg, int C, hipStream_t s) {
+  hipLaunchKernelGGL(iabn_gamma_kernel, dim3((C + 255) / 256), dim3(256), 0, s, g, eps, geff, rg, C);
+}
+
+void launch_sign_mul(const float* d, const float* g, float* out, int C, hipStream_t s) {
+  hipLaunchKernelGGL(sign_mul_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d, g, out, C);
+}
+
 }  // namespace dcp

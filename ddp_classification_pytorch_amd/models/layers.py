@@ -89,11 +89,6 @@ class BatchNorm2d(nn.Module):
         self.inplace_abn = False
         self.iabn_eps = 1e-5
 
-    def _gamma(self):
-        if self.inplace_abn and self.weight is not None:
-            return self.weight.abs() + self.iabn_eps
-        return self.weight
-
     def forward(self, x, slabs=None, act="relu", residual=None, slope=0.01, link=None, residual_bn=None,
                 fuse_bwd=False):
         """``residual_bn=(bn, rslabs)``: ``residual`` is the raw input of BatchNorm2d ``bn`` (a
@@ -117,10 +112,13 @@ class BatchNorm2d(nn.Module):
         if stats:
             self._nbt_pending += 1  # folded into num_batches_tracked lazily (no per-step device add)
         iabn = self.inplace_abn and residual is None and act in ("none", "leaky", "leaky_relu")
-        return Fn.batch_norm_act(x, slabs, self._gamma() if iabn else self.weight, self.bias, self.running_mean,
-                                 self.running_var, stats, self.momentum, self.eps, act=act, slope=slope,
-                                 residual=residual, group=self.process_group if stats else None, link=link,
-                                 iabn=iabn, fuse_bwd=fuse_bwd)
+        gamma, rgamma = self.weight, None
+        if iabn and self.weight is not None:
+            gamma, rgamma = Fn.iabn_gamma(self.weight, self.iabn_eps)
+        return Fn.batch_norm_act(x, slabs, gamma, self.bias, self.running_mean, self.running_var, stats, self.momentum,
+                                 self.eps, act=act, slope=slope, residual=residual,
+                                 group=self.process_group if stats else None, link=link, iabn=iabn,
+                                 fuse_bwd=fuse_bwd, rgamma=rgamma)
 
     def forward_pool(self, x, slabs=None, act="relu", k=3, s=2, p=1):
         """BN + act + k x k / s max pool.  Training-mode statistics with a ReLU/identity

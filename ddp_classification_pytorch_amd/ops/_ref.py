@@ -648,3 +648,12 @@ def adaptive_avg_pool_bwd(dy, H, W):
         y = F.adaptive_avg_pool2d(xin, (OH, OW))
         y.backward(_nchw(dy.double()))
     return _nhwc(xin.grad).to(dy.dtype)
+
+
+def iabn_gamma(g, eps):
+    e = g.abs() + eps
+    return e, 1.0 / e
+
+
+def sign_mul(d, g):
+    return d * torch.sign(g)

@@ -458,9 +458,9 @@ def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
 
 # ----------------------------------------------------------------------------- batch norm (+act, +residual)
 class BNConfig:
-    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world", "iabn")
+    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world", "iabn", "rgamma")
 
-    def __init__(self, training_stats, momentum, eps, act, slope, group, world, iabn=False):
+    def __init__(self, training_stats, momentum, eps, act, slope, group, world, iabn=False, rgamma=None):
         self.training_stats = training_stats
         self.momentum = momentum
         self.eps = eps
@@ -469,6 +469,7 @@ class BNConfig:
         self.group = group
         self.world = world
         self.iabn = iabn  # InplaceABN: backward from the output (see _BNAct)
+        self.rgamma = rgamma  # InplaceABN: 1 / gamma, when the caller has it (iabn_gamma)
 
 
 def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
@@ -531,7 +532,7 @@ class _BNAct(Function):
         want_dres = ctx.has_res and ctx.needs_input_grad[4]
         if cfg.iabn:
             y, beta = x, mean  # saved (y, beta) in place of (x, mean)
-            rgamma = torch.reciprocal(gamma.detach().float())
+            rgamma = cfg.rgamma if cfg.rgamma is not None else torch.reciprocal(gamma.detach().float())
             need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
             local = sums = None
             if cfg.training_stats or need_affine:
@@ -809,15 +810,37 @@ def batch_norm_add_bn_act(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, r
     return out
 
 
+class _IABNGamma(Function):
+    """InplaceABN's effective weight |gamma| + eps (and its reciprocal for the backward from the
+    output) in one launch; gradient d * sign(gamma) in one launch."""
+
+    @staticmethod
+    def forward(ctx, g, eps):
+        geff, rg = K(g).iabn_gamma(g, eps)
+        ctx.save_for_backward(g)
+        ctx.mark_non_differentiable(rg)
+        return geff, rg
+
+    @staticmethod
+    def backward(ctx, dgeff, _drg):
+        (g,) = ctx.saved_tensors
+        return (K(g).sign_mul(dgeff.contiguous(), g) if dgeff is not None else None), None
+
+
+def iabn_gamma(g, eps):
+    """(|g| + eps, 1 / (|g| + eps)) -- differentiable in g through the first output."""
+    return _IABNGamma.apply(g, float(eps))
+
+
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
-                   slope=0.01, residual=None, group=None, link=None, iabn=False, fuse_bwd=False):
+                   slope=0.01, residual=None, group=None, link=None, iabn=False, fuse_bwd=False, rgamma=None):
     """``iabn``: InplaceABN storage (invertible act: identity / leaky, no residual, a gamma bounded
     away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention).  ``fuse_bwd``:
     offer this plain BN + ReLU's backward reduction to its consumer even under the masked-only
     default (the consumer is a grouped conv, whose dgrad fusion measured a win: ResNeXt)."""
     world = dist.get_world_size(group) if group is not None else 1
     iabn = bool(iabn) and residual is None and ACT[act] in (0, 2) and gamma is not None and beta is not None
-    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn)
+    cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn, rgamma if iabn else None)
     if slabs is None or (slabs.numel() == 0):
         slabs = None
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the

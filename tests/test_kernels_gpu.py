@@ -1177,3 +1177,14 @@ def test_split_reduce_single_launch_ticket(K, mode):
     full = (dy.float().reshape(-1, Co).t() @ x.float().reshape(-1, C)).cpu()
     assert relerr(dw1.reshape(Co, C), full) < 1e-3
     assert dwr.shape == dw1.shape
+
+
+def test_iabn_gamma_and_sign_mul(K):
+    """InplaceABN effective weight |g| + eps with its reciprocal, and the gradient d * sign(g)."""
+    g = torch.randn(1000)
+    g[::7] = 0.0
+    d = torch.randn(1000)
+    ge, rg = K.iabn_gamma(g.to(DEV), 1e-5)
+    rge, rrg = _ref.iabn_gamma(g, 1e-5)
+    assert torch.allclose(ge.cpu(), rge) and torch.allclose(rg.cpu(), rrg, rtol=1e-6)
+    assert torch.equal(K.sign_mul(d.to(DEV), g.to(DEV)).cpu(), _ref.sign_mul(d, g))
