@@ -218,7 +218,8 @@ __device__ __forceinline__ void tile_stats128(const TapGemmParams& p, char* E, i
       xch[(wave * 2 + 1) * BN + c * 8 + e] = s2[e];
     }
   __syncthreads();
-  if (tid < BN && n0 + tid < p.Co) {
+  // (nvalid <= 0: a 128-row quadrant of a 256-row tile past M -- no slab to write)
+  if (tid < BN && n0 + tid < p.Co && nvalid > 0) {
     float S1 = 0.f, S2 = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -272,6 +273,9 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+template <int BN, int EPI>
+__device__ __forceinline__ void tg_image_store(const TapGemmParams& p, char* E, int m0, int n0, int tid);
+
 // Store epilogue of the 4-wave 128-row tap GEMMs (EPI 0: bf16 store, optionally folding an
 // eval-mode BN and adding addsrc; EPI 1: + the per-128-row BN statistics).  Entered after a
 // barrier with no loads in flight; the accumulators go through the LDS image E.
@@ -281,7 +285,7 @@ __device__ __forceinline__ void tg_store_epilogue(const TapGemmParams& p, const 
   constexpr int BM = 128, TN = BN / 32;
   // ---- epilogue through LDS: the k-loop ended with a barrier and no loads in flight ----
   // tile image E[BM pixels][BN channels] bf16, 16-byte chunks XOR-swizzled by (pixel>>1)
-  constexpr int RB = BN * 2, NCH = BN / 8;
+  constexpr int NCH = BN / 8;
   char* E = smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -297,6 +301,15 @@ __device__ __forceinline__ void tg_store_epilogue(const TapGemmParams& p, const 
     }
   }
   __syncthreads();
+  tg_image_store<BN, EPI>(p, E, m0, n0, tid);
+}
+
+// The image -> global half of the store epilogue, for 256 threads over one [128][BN] image E
+// (tg_store_epilogue, and per 128 x 128 quadrant in tap_gemm_big_kernel): coalesced 16-byte
+// stores, the optional eval-BN fold / add source, then (EPI 1) the slab's BN statistics.
+template <int BN, int EPI>
+__device__ __forceinline__ void tg_image_store(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
+  constexpr int BM = 128, NCH = BN / 8;
   // coalesced 16-byte stores: a pass covers 256/NCH pixel rows x all BN channels.  All the
   // thread's image chunks are read first, so its stores issue back to back instead of each
   // waiting for its own LDS read.
@@ -1327,6 +1340,193 @@ tap_gemm8_kernel(const TapGemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Big-tile tap GEMM: WM x WN waves, each owning 128 pixel rows x 64 output channels (8 x 4
+// accumulator fragments: 12 fragment reads feed 32 MFMAs per 32-deep k-step, against 8 for 16
+// in the 4-wave kernel); workgroup tile BM = 128 WM x BN = 64 WN, e.g. 256 x 256 at 8 waves,
+// one workgroup per CU.  The 128-row kernels above run at the ceiling of their structure (two
+// barriers' worth of exposed load latency per k-step, 2-3 workgroups per CU: ~900 TF/s on the
+// deep-K shapes, cdna_hip_programming.md §5 ladder) and move 32 KB of LDS-DMA per 2 MFLOP; this
+// one moves 32 KB per 4.2 MFLOP (256 x 256 x 32) and keeps NS-2 k-tiles of LDS-DMA in flight
+// across every raw s_barrier (NS-slot ring of 32-deep k-tiles, counted vmcnt, never 0 in the
+// loop; the slot re-staged after barrier kt is the one every wave finished reading before it).
+// FAST shapes (Cs % 64 == 0, one tap per k-tile), plain / statistics epilogue (+ eval-BN fold /
+// add source): the accumulators go to a whole-tile LDS image cut into 128 x 128 quadrants, which
+// the 256-thread groups store through tg_image_store (the 4-wave kernel's epilogue).
+// ---------------------------------------------------------------------------
+template <int WM, int WN, int NS, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN, 2)
+tap_gemm_big_kernel(const TapGemmParams p) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int BM = 128 * WM, BN = 64 * WN, BK = 32;
+  constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;  // 64-byte rows, 16 rows per LDS-DMA
+  constexpr int AI = BM / (NW * RPI), BI = BN / (NW * RPI), LPT = AI + BI;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int QN = BN / 128, NQ = WM * QN, NG = NT / 256, QPG = NQ / NG;  // epilogue quadrants
+  static_assert(AI >= 1 && BI >= 1 && AI * NW * RPI == BM && BI * NW * RPI == BN, "LDS-DMA split");
+  static_assert(BN % 128 == 0 && NT % 256 == 0 && NQ % NG == 0 && NS >= 3, "tile geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-slot source pointers + tap-validity masks (as tap_gemm_kernel's FAST path); rows past M
+  // and channels past Co read a clamped valid row and are never stored or counted
+  const bf16* fa_ptr[AI];
+  uint32_t fa_vm[AI];
+  const bf16* fb_ptr[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * RPI + lane / CH;
+    const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const uint32_t x = mm - q * p.Wy;
+    const uint32_t n = fdiv(q, p.div_hy);
+    const uint32_t y = q - n * p.Hy;
+    const int ys = y * p.ss, xs = x * p.ss;
+    fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+    uint32_t vm = 0;
+    for (int t = 0; t < p.ntaps; ++t) {
+      const int tv = p.tap[t];
+      const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+      vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+    }
+    fa_vm[i] = vm;
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int r = (wave * BI + i) * RPI + lane / CH;
+    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+  }
+  const int tiles_per_tap = p.cpt / CH;
+  auto stage = [&](int kt, int slot) {
+    char* As = smem + slot * STAGE;
+    char* Bs = As + A_BYTES;
+    const int t = kt / tiles_per_tap;
+    const int cbase = (kt - t * tiles_per_tap) * BK;
+    const int tv = p.tap[t];
+    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
+    const long boff = (long)tap_w(tv) * p.Cs + cbase;
+    const uint32_t tbit = 1u << t;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16,
+                                       0, 0);
+  };
+
+  f32x4 acc[4][8];  // [16-channel fragment][16-pixel fragment]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = p.nkt;
+  const uint32_t c = lane >> 4;
+  bf16x8 wf[4], af[8];
+  auto frag_w = [&](int slot) {
+    const char* Bs = smem + slot * STAGE + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * 64 + j * 16 + (lane & 15), c));
+  };
+  auto frag_a = [&](int slot, int i0) {
+    const char* As = smem + slot * STAGE;
+#pragma unroll
+    for (int i = i0; i < i0 + 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 128 + i * 16 + (lane & 15), c));
+  };
+  auto mfma_half = [&](int i0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+  };
+  // raw barrier: this wave's fragment reads retired first (WAR on the slot re-staged after it);
+  // the counted vmcnt before it is the RAW wait -- no vmcnt(0), the ring stays in flight
+  auto ring_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nkt) stage(i, i);
+  if (p.cvar != 1) {
+    for (int kt = 0; kt < nkt; ++kt) {
+      wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
+      ring_barrier();  // ... for every wave; slot kt-1 is free
+      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      frag_w(kt % NS);
+      frag_a(kt % NS, 0);
+      frag_a(kt % NS, 4);
+      mfma_half(0);
+      mfma_half(4);
+    }
+  } else if (nkt > 0) {
+    // g_tune[4] = 1: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of
+    // k-tile kt -- pixel fragments 0..3 after its first half, the rest after its second half
+    wait_vmcnt(LPT * min(NS - 2, nkt - 1));
+    ring_barrier();
+    if (NS - 1 < nkt) stage(NS - 1, NS - 1);
+    frag_w(0);
+    frag_a(0, 0);
+    frag_a(0, 4);
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int nx = (kt + 1) % NS;
+      mfma_half(0);
+      if (kt + 1 < nkt) {
+        wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));  // k-tile kt+1 landed (this wave's share)
+        ring_barrier();  // ... for every wave; every read of slot kt retired: re-stage it
+        if (kt + NS < nkt) stage(kt + NS, kt % NS);
+        frag_a(nx, 0);
+      }
+      mfma_half(4);
+      if (kt + 1 < nkt) {
+        frag_w(nx);
+        frag_a(nx, 4);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
+  {
+    char* Q = smem + (wm * QN + (wn * 64) / 128) * 32768;
+    const uint32_t cb = (wn * 64) % 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t pl = i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+      }
+    }
+  }
+  __syncthreads();
+  // group g (threads 256g ..) stores quadrants g*QPG ..; every group passes the same barriers
+  // (tile_stats128's), so the quadrant loop stays uniform
+  const int g = tid >> 8, gtid = tid & 255;
+#pragma unroll
+  for (int k = 0; k < QPG; ++k) {
+    const int q = g * QPG + k;
+    tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
 struct WgradParams {
@@ -1864,6 +2064,33 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>), dim3(grid), dim3(256), lds, stream, p);
 }
 
+template <int WM, int WN, int NS>
+static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
+  constexpr int BM = 128 * WM, BN = 64 * WN;
+  constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 64, (size_t)WM * (BN / 128) * 32768);
+  const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr = true;
+  }
+  if (epi == 1) hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 1>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
+  else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
+}
+
+// 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[24].
+static int big_tile_pick(int mode, int M, int Co, int K) {
+  if (mode == 2) return 0;
+  if (mode == 1) return Co >= 256 ? 1 : 2;
+  if (mode == 3) return 2;
+  (void)M;
+  (void)K;
+  return 0;  // heuristic: off until measured (tools/conv_bench.py --cfgs "24=1")
+}
+
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
@@ -1983,6 +2210,18 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
       else { if (ps_bk == 64) DCP_PS(128, 0, 64) else DCP_PS(128, 0, 32) }
     }
 #undef DCP_PS
+    return;
+  }
+  // big-tile kernel (tap_gemm_big_kernel): FAST, plain / statistics epilogue, >= 128 output
+  // channels.  g_tune[24]: 1 = on wherever it applies (256 x 256 for Co >= 256, else 256 x 128),
+  // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
+  const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
+                      Co >= 128;
+  const int big = big_ok ? big_tile_pick(g_tune[24], p.M, Co, taps.n * Cs) : 0;
+  if (big != 0) {
+    p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)
+    if (big == 1) launch_big<2, 4, 4>(p, epi, stream);
+    else launch_big<2, 2, 3>(p, epi, stream);
     return;
   }
   if (fast && Co >= 128 && epi < 2 && use8 && pscale == nullptr) {

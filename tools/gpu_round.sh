@@ -11,6 +11,7 @@
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
 #   sweep           headline batch sweep 128..2048
 #   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
+#   blas            torch.mm (hipBLASLt) on the R50 1x1 stride-1 GEMM shapes, b1024 (library yardstick)
 #   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
 set -e
@@ -75,6 +76,15 @@ for step in "$@"; do
     convbench)
       timeout -k 10 400 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen > $O/conv_bench_b1024.txt 2>&1
       tail -3 $O/conv_bench_b1024.txt ;;
+    ab=*)
+      # per-shape in-process A/B of g_tune configs, e.g. ab=24=2,24=1,24=3
+      c=${step#ab=}
+      timeout -k 10 600 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen --cfgs "$c" \
+        > $O/conv_ab_$(echo "$c" | tr ',;=' '_._').txt 2>&1
+      tail -2 $O/conv_ab_*.txt ;;
+    blas)
+      timeout -k 10 300 python -u tools/blas_ref_bench.py --batch 1024 --iters 10 > $O/blas_ref_b1024.txt 2>&1
+      tail -2 $O/blas_ref_b1024.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
