@@ -1459,7 +1459,8 @@ tap_gemm_big_kernel(const TapGemmParams p) {
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nkt) stage(i, i);
-  if (p.cvar != 1) {
+  if (p.cvar == 2) {
+    // g_tune[4] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
     for (int kt = 0; kt < nkt; ++kt) {
       wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
       ring_barrier();  // ... for every wave; slot kt-1 is free
@@ -1471,8 +1472,9 @@ tap_gemm_big_kernel(const TapGemmParams p) {
       mfma_half(4);
     }
   } else if (nkt > 0) {
-    // g_tune[4] = 1: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of
-    // k-tile kt -- pixel fragments 0..3 after its first half, the rest after its second half
+    // default: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of k-tile
+    // kt -- pixel fragments 0..3 after its first half, the rest after its second half (measured
+    // 2-4 % faster than reading them after the barrier: profiles/r3/big_tile_ab_b1024_pipelined.txt)
     wait_vmcnt(LPT * min(NS - 2, nkt - 1));
     ring_barrier();
     if (NS - 1 < nkt) stage(NS - 1, NS - 1);
@@ -2081,14 +2083,27 @@ static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
   else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
 }
 
-// 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[24].
-static int big_tile_pick(int mode, int M, int Co, int K) {
+// 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[24]
+// (0 = this heuristic).  Per-shape A/B at b1024 (profiles/r3/big_tile_ab_b1024_pipelined.txt): the
+// big tiles win where the 128-row kernels' grid is short or their k-loop is exposed, and lose on
+// the 1x1 stride-1 shapes and the 256-channel 3x3s (784 256 x 256 tiles = 3.06 rounds of 256 CUs):
+//   * stride-2 data-gradient parity classes (ds = 2), 256 x 128: 128 ch 3x3 581 -> 497 us,
+//     256 ch 3x3 374 -> 348, 1x1 1024 -> 2048 377 -> 323;
+//   * 3x3 with 128 output channels, 256 x 128: 28x28 fwd 307 -> 285, dgrad 288 -> 274, the
+//     stride-2 fwd 369 -> 349;
+//   * 3x3 with >= 512 output channels (the 7x7 outputs), 256 x 256: 257 -> 247 fwd, 253 -> 244 dgrad.
+// Only where the big-tile grid still fills the chip (>= 256 tiles): at batch 32 the 7x7 3x3
+// convs are 14 256 x 256 tiles (122 us against the 128-row kernel's 52-workgroup grid).
+static int big_tile_pick(int mode, int M, int Co, int ntaps, int ds) {
   if (mode == 2) return 0;
   if (mode == 1) return Co >= 256 ? 1 : 2;
   if (mode == 3) return 2;
-  (void)M;
-  (void)K;
-  return 0;  // heuristic: off until measured (tools/conv_bench.py --cfgs "24=1")
+  int pick = 0;
+  if (ds == 2) pick = 2;
+  else if (ntaps == 9 && Co == 128) pick = 2;
+  else if (ntaps == 9 && Co >= 512) pick = 1;
+  const long tiles = (long)((M + 255) / 256) * ((Co + (pick == 1 ? 255 : 127)) / (pick == 1 ? 256 : 128));
+  return pick != 0 && tiles >= 256 ? pick : 0;
 }
 
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
@@ -2217,7 +2232,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
-  const int big = big_ok ? big_tile_pick(g_tune[24], p.M, Co, taps.n * Cs) : 0;
+  const int big = big_ok ? big_tile_pick(g_tune[24], p.M, Co, taps.n, ds) : 0;
   if (big != 0) {
     p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)
     if (big == 1) launch_big<2, 4, 4>(p, epi, stream);

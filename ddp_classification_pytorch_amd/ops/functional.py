@@ -294,6 +294,56 @@ def bn_source(x):
     return getattr(x, "_dcp_bnsrc", None)
 
 
+# ----------------------------------------------------------------------------- wgrad stream
+# A conv's weight gradient does not feed the rest of the backward pass, only the optimizer (and
+# the DDP buckets): with DCP_WGRAD_STREAM=1 it runs on a second HIP stream beside the data
+# gradient, so the two kernels fill each other's tail waves (a 128-row conv grid is 3-7 rounds
+# of 256 CUs; the last round runs part-empty).  The main stream joins the side stream before the
+# backward function returns (the gradient is complete when autograd / the DDP hook sees it).
+_WGRAD_STREAM = [os.environ.get("DCP_WGRAD_STREAM", "0") == "1"]
+_SIDE = {}
+
+
+def set_wgrad_stream(enabled: bool):
+    _WGRAD_STREAM[0] = bool(enabled)
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _WgradOnSide:
+    """``with _WgradOnSide(t) as side: dw = ...`` runs the body on the side stream (forked from
+    the current stream); ``side.join()`` makes the current stream wait for it.  A no-op on the
+    CPU or when the option is off."""
+
+    def __init__(self, t: torch.Tensor):
+        self.on = _WGRAD_STREAM[0] and t.is_cuda
+        self.main = torch.cuda.current_stream(t.device) if self.on else None
+        self.side = _side_stream(t.device) if self.on else None
+        self._ctx = None
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            self._ctx.__exit__(*exc)
+            self._ctx = None
+        return False
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
 class _Conv2d(Function):
     @staticmethod
     def forward(ctx, x, weight, wb, wt, stride, pad, stats, link, bnsrc, deposit):
@@ -319,6 +369,10 @@ class _Conv2d(Function):
             if add is not None:
                 add = add.contiguous()
         dx = dw = None
+        side = _WgradOnSide(dy)
+        if ctx.needs_input_grad[1] and side.on:
+            with side:
+                dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
         if ctx.needs_input_grad[0]:
             src = ctx.bnsrc
             if src is not None and complete and stride == 1 and src.tensors is not None:
@@ -334,8 +388,9 @@ class _Conv2d(Function):
                 dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
             if ctx.deposit is not None:
                 dx = ctx.deposit.deposit(dx)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not side.on:
             dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
+        side.join()
         ctx.link = ctx.bnsrc = ctx.deposit = None
         return dx, dw, None, None, None, None, None, None, None, None
 
@@ -379,7 +434,11 @@ class _GroupedConv2d(Function):
         KH, KW, groups, stride, pad = ctx.geo
         dy = dy.contiguous()
         k = K(dy)
-        dx = None
+        dx = dw = None
+        side = _WgradOnSide(dy)
+        if ctx.needs_input_grad[1] and side.on:
+            with side:
+                dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad)
         if ctx.needs_input_grad[0]:
             src = ctx.bnsrc
             if src is not None and src.act == 1 and src.tensors is not None and src.tensors[1] is None:
@@ -391,7 +450,9 @@ class _GroupedConv2d(Function):
                     src.fused = (dx, sums)
             else:
                 dx = k.grouped_conv_dgrad(dy, wb, x.shape[1], x.shape[2], groups, stride, pad)
-        dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad) if ctx.needs_input_grad[1] else None
+        if ctx.needs_input_grad[1] and not side.on:
+            dw = k.grouped_conv_wgrad(dy, x, KH, KW, groups, stride, pad)
+        side.join()
         ctx.bnsrc = None
         return dx, dw, None, None, None, None, None, None
 

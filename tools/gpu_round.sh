@@ -11,8 +11,12 @@
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
 #   sweep           headline batch sweep 128..2048
 #   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
+#   convbench32     the same at batch 32 (the reference's per-process batch)
+#   benchab=CFG     headline bench default vs DCP_TUNE=CFG, interleaved twice
+#   benchenv=V=X    headline bench default vs with environment V=X, interleaved twice
 #   blas            torch.mm (hipBLASLt) on the R50 1x1 stride-1 GEMM shapes, b1024 (library yardstick)
 #   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
+#   smallenv=V=X    b32 graph / b128 eager, default vs with environment V=X
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
 set -e
 set -o pipefail
@@ -68,6 +72,16 @@ for step in "$@"; do
         timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 --graph > $O/small_b${b}_graph.log 2>&1
         tail -1 $O/small_b${b}_graph.log | grep -o '"value": [0-9.]*'
       done ;;
+    smallenv=*)
+      # b32 HIP-graph and b128 eager, default vs with an environment assignment
+      c=${step#smallenv=}
+      for args in "--batch 32 --graph" "--batch 128"; do
+        tag=$(echo "$args" | tr -d ' -')
+        timeout -k 10 240 python -u bench.py $args --steps 30 --warmup 5 > $O/smallenv_${tag}_default.log 2>&1
+        echo "$args default: $(grep -o '"value": [0-9.]*' $O/smallenv_${tag}_default.log)"
+        env "$c" timeout -k 10 240 python -u bench.py $args --steps 30 --warmup 5 > $O/smallenv_${tag}_set.log 2>&1
+        echo "$args $c: $(grep -o '"value": [0-9.]*' $O/smallenv_${tag}_set.log)"
+      done ;;
     large)
       for b in 2048 3072; do
         timeout -k 10 400 python -u bench.py --config r101 --batch $b --steps 5 --warmup 2 > $O/r101_b$b.log 2>&1
@@ -76,12 +90,33 @@ for step in "$@"; do
     convbench)
       timeout -k 10 400 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen > $O/conv_bench_b1024.txt 2>&1
       tail -3 $O/conv_bench_b1024.txt ;;
+    convbench32)
+      timeout -k 10 400 python -u tools/conv_bench.py --batch 32 --iters 50 --no-miopen > $O/conv_bench_b32.txt 2>&1
+      tail -3 $O/conv_bench_b32.txt ;;
     ab=*)
       # per-shape in-process A/B of g_tune configs, e.g. ab=24=2,24=1,24=3
       c=${step#ab=}
       timeout -k 10 600 python -u tools/conv_bench.py --batch 1024 --iters 10 --no-miopen --cfgs "$c" \
         > $O/conv_ab_$(echo "$c" | tr ',;=' '_._').txt 2>&1
       tail -2 $O/conv_ab_*.txt ;;
+    benchab=*)
+      # headline bench, default vs DCP_TUNE=<cfg>, interleaved twice (same box, back to back)
+      c=${step#benchab=}
+      for r in 1 2; do
+        timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/benchab_default_$r.log 2>&1
+        echo "default: $(grep -o '"value": [0-9.]*' $O/benchab_default_$r.log)"
+        DCP_TUNE="$c" timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/benchab_tuned_$r.log 2>&1
+        echo "DCP_TUNE=$c: $(grep -o '"value": [0-9.]*' $O/benchab_tuned_$r.log)"
+      done ;;
+    benchenv=*)
+      # headline bench, default vs with an environment assignment (e.g. DCP_WGRAD_STREAM=1), twice
+      c=${step#benchenv=}
+      for r in 1 2; do
+        timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/benchenv_default_$r.log 2>&1
+        echo "default: $(grep -o '"value": [0-9.]*' $O/benchenv_default_$r.log)"
+        env "$c" timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/benchenv_set_$r.log 2>&1
+        echo "$c: $(grep -o '"value": [0-9.]*' $O/benchenv_set_$r.log)"
+      done ;;
     blas)
       timeout -k 10 300 python -u tools/blas_ref_bench.py --batch 1024 --iters 10 > $O/blas_ref_b1024.txt 2>&1
       tail -2 $O/blas_ref_b1024.txt ;;
