@@ -6,6 +6,7 @@
 #   tests[=filter]  pytest -m gpu (optionally -k filter)      smoke   __graft_entry__.smoke()
 #   bench           headline bench.py (20 steps)              configs every BASELINE.json config
 #   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
+#   profcfg=CFG     the same for another bench config (e.g. arcface)
 #   pmc             three PMC passes (SQ: MFMA busy / LDS conflicts / waits; FETCH_SIZE; WRITE_SIZE)
 #   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
@@ -50,6 +51,13 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 2 \
         > $O/prof.log 2>&1
       echo prof done ;;
+    profcfg=*)
+      # rocprofv3 kernel stats of another BASELINE config, e.g. profcfg=arcface
+      c=${step#profcfg=}
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run -- python3 -u bench.py --config $c --steps 8 --warmup 2 \
+        > $O/prof_$c.log 2>&1
+      echo prof $c done ;;
     pmc)
       prof_env
       PASS1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
