@@ -1107,7 +1107,7 @@ Tensor crop_resize(const Tensor& src, const Tensor& meta, int64_t Ho, int64_t Wo
 }
 
 Tensor to_nhwc_s2d(const Tensor& src, bool nchw, double in_scale, const optional<Tensor>& mean,
-                   const optional<Tensor>& stdv) {
+                   const optional<Tensor>& stdv, int64_t block) {
   CHECK_DEV(src);
   CHECK_CONTIG(src);
   TORCH_CHECK(src.scalar_type() == at::kByte || src.scalar_type() == at::kFloat, "to_nhwc_s2d input u8 or fp32");
@@ -1115,10 +1115,12 @@ Tensor to_nhwc_s2d(const Tensor& src, bool nchw, double in_scale, const optional
   const int C = nchw ? src.size(1) : src.size(3);
   const int H = nchw ? src.size(2) : src.size(1);
   const int W = nchw ? src.size(3) : src.size(2);
-  TORCH_CHECK(C <= 4 && H % 2 == 0 && W % 2 == 0, "to_nhwc_s2d needs <= 4 channels and even H, W");
-  auto y = at::empty({N, H / 2, W / 2, 16}, src.options().dtype(at::kBFloat16));
+  TORCH_CHECK(block == 2 || block == 4, "to_nhwc_s2d block is 2 or 4");
+  const int b = (int)block, cq = b == 2 ? 4 : 3;
+  TORCH_CHECK(C <= cq && H % b == 0 && W % b == 0, "to_nhwc_s2d needs <= ", cq, " channels and H, W divisible by ", b);
+  auto y = at::empty({N, H / b, W / b, b * b * cq}, src.options().dtype(at::kBFloat16));
   dcp::launch_to_nhwc_s2d(src.data_ptr(), src.scalar_type() == at::kByte, nchw, N, C, H, W, (float)in_scale, fp(mean),
-                          fp(stdv), bpm(y), cur_stream());
+                          fp(stdv), bpm(y), cur_stream(), b);
   return y;
 }
 
@@ -1472,7 +1474,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("space_to_depth(Tensor x, int b, bool inverse) -> Tensor", &space_to_depth);
   m.def("to_nhwc(Tensor src, bool nchw, int cpad, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc);
   m.def("crop_resize(Tensor src, Tensor meta, int Ho, int Wo) -> Tensor", &crop_resize);
-  m.def("to_nhwc_s2d(Tensor src, bool nchw, float in_scale, Tensor? mean, Tensor? std) -> Tensor", &to_nhwc_s2d);
+  m.def("to_nhwc_s2d(Tensor src, bool nchw, float in_scale, Tensor? mean, Tensor? std, int block=2) -> Tensor", &to_nhwc_s2d);
   m.def("conv_fwd_geo(Tensor x, Tensor w, int stride, int pad, int Ho, int Wo, bool stats) -> (Tensor, Tensor)",
         &conv_fwd_geo);
   m.def("stem_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)", &stem_fwd);

@@ -238,9 +238,10 @@ void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16*
 void launch_mt_weight_prep(const void* entries, const void* blocks, int nblocks, hipStream_t s);
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,
                     const float* mean, const float* stdv, bf16* dst, hipStream_t s);
-// space-to-depth 2x2 input of the s2d stem: dst [N][H/2][W/2][16], channel (py*2+px)*4 + c (c < 3 real)
+// space-to-depth input: block 2 (ResNet s2d stem) dst [N][H/2][W/2][16], channel (py*2+px)*4 + c (c < 3
+// real); block 4 (TResNet SpaceToDepth(4)) dst [N][H/4][W/4][48], channel (py*4+px)*3 + c
 void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
-                        const float* mean, const float* stdv, bf16* dst, hipStream_t s);
+                        const float* mean, const float* stdv, bf16* dst, hipStream_t s, int block = 2);
 // shard-loader augmentation: meta [B][8] = {byte offset, H, W, y0, x0, h, w, flip} -> out [B][Ho][Wo][3]
 void launch_crop_resize(const uint8_t* src, const int64_t* meta, int B, int Ho, int Wo, uint8_t* out, hipStream_t s);
 void launch_act_bwd(const bf16* dy, const bf16* y, bf16* dx, size_t numel, int act, hipStream_t s);

@@ -219,7 +219,8 @@ void launch_weight_prep(const float* w, int Co, int T, int Ci, int Co_pad, bf16*
 
 // One thread per OUTPUT pixel, 16-byte stores: dst [N][H/S][W/S][S*S*Cq] with channel
 // (py*S + px)*Cq + c = normalised src[n][c][i*S+py][j*S+px] (c < C, else 0).  S = 2 is the
-// space-to-depth input of the 4x4 stride-1 form of the 7x7/2 stem (models/resnet.py).
+// space-to-depth input of the 4x4 stride-1 form of the 7x7/2 stem (models/resnet.py), S = 4 /
+// Cq = 3 TResNet's SpaceToDepth(4) stem input (models/tresnet.py; timm's channel order).
 template <int S, int CQ>
 __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict__ src, int is_u8, int nchw, int N,
                                                           int C, int H, int W, float in_scale,
@@ -285,17 +286,24 @@ __global__ void __launch_bounds__(256) to_nhwc_pix_kernel(const void* __restrict
   }
 }
 
+// block 2: [N][H/2][W/2][16] (2x2, 4 channel slots: the ResNet s2d stem); block 4:
+// [N][H/4][W/4][48] (4x4, 3 channels: TResNet's SpaceToDepth(4) stem, written straight from the
+// images instead of an NHWC pass plus a space_to_depth pass)
 void launch_to_nhwc_s2d(const void* src, int is_u8, int nchw, int N, int C, int H, int W, float in_scale,
-                        const float* mean, const float* stdv, bf16* dst, hipStream_t s) {
-  size_t total = (size_t)N * (H / 2) * (W / 2);
+                        const float* mean, const float* stdv, bf16* dst, hipStream_t s, int block) {
+  size_t total = (size_t)N * (H / block) * (W / block);
   if (total >= (1ull << 31)) {
     fprintf(stderr, "to_nhwc_s2d: %zu output pixels exceed the 32-bit index range\n", total);
     abort();
   }
   size_t g = (total + 255) / 256;
   if (g > (1u << 20)) g = 1u << 20;
-  hipLaunchKernelGGL((to_nhwc_pix_kernel<2, 4>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
-                     in_scale, mean, stdv, dst);
+  if (block == 4)
+    hipLaunchKernelGGL((to_nhwc_pix_kernel<4, 3>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
+                       in_scale, mean, stdv, dst);
+  else
+    hipLaunchKernelGGL((to_nhwc_pix_kernel<2, 4>), dim3((int)g), dim3(256), 0, s, src, is_u8, nchw, N, C, H, W,
+                       in_scale, mean, stdv, dst);
 }
 
 void launch_to_nhwc(const void* src, int is_u8, int nchw, int N, int C, int H, int W, int Cp, float in_scale,

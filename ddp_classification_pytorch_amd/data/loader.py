@@ -64,7 +64,7 @@ class DevicePrefetcher:
         imgs = imgs.to(self.device, non_blocking=True)
         labels = labels.to(self.device, non_blocking=True)
         x = Fn.to_device_nhwc(imgs, self.mean, self.std, cpad=self.cpad, nchw=False, in_scale=1.0 / 255.0,
-                              s2d=self.s2d and imgs.shape[1] % 2 == 0 and imgs.shape[2] % 2 == 0)
+                              s2d=Fn.s2d_for(self.s2d, imgs.shape[1], imgs.shape[2]))
         rest = tuple(b.to(self.device, non_blocking=True) for b in batch[2:])
         return (x, labels) + rest
 
@@ -100,7 +100,7 @@ class SyntheticLoader:
                  mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad=8, return_index=False, s2d=False):
         self.device = torch.device(device)
         self.steps, self.cpad, self.return_index, self.batch_size = steps, cpad, return_index, batch_size
-        self.s2d = s2d and size % 2 == 0
+        self.s2d = Fn.s2d_for(s2d, size, size)
         g = torch.Generator(device="cpu")
         g.manual_seed(seed)
         self.imgs = [torch.randint(0, 256, (batch_size, size, size, 3), dtype=torch.uint8, generator=g).to(self.device)

@@ -271,14 +271,14 @@ class ShardLoader:
 
     def __init__(self, path: str, batch_size: int, sampler=None, aug: AugSpec = None, out_size: int = 224,
                  device="cuda", threads: int = 8, prefetch: int = 3, seed: int = 0, drop_last: bool = False,
-                 mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad: int = 8, s2d: bool = False, return_index: bool = False):
+                 mean=IMAGENET_MEAN, std=IMAGENET_STD, cpad: int = 8, s2d=False, return_index: bool = False):
         self.gather = NativeGather(path, threads)
         self.batch_size, self.sampler, self.out_size = int(batch_size), sampler, int(out_size)
         self.aug = aug if aug is not None else AugSpec(MODE_WHOLE, 0, 0, 1, 1, 1, 1, 0.0)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.prefetch, self.seed, self.drop_last = max(1, int(prefetch)), int(seed), drop_last
-        self.cpad, self.s2d, self.return_index = cpad, s2d and self.out_size % 2 == 0, return_index
+        self.cpad, self.s2d, self.return_index = cpad, Fn.s2d_for(s2d, self.out_size, self.out_size), return_index
         self.mean = torch.tensor(mean, dtype=torch.float32, device=self.device)
         self.std = torch.tensor(std, dtype=torch.float32, device=self.device)
         self.epoch = 0

@@ -109,8 +109,8 @@ def _shard_loaders(args, rt, tr, va, tr_s, va_s, mean, std, cpad, s2d, drop_last
     kw = dict(device=rt.device, threads=args.loader_threads, seed=args.seed, mean=mean, std=std, cpad=cpad,
               return_index=idx)
     tr_l = ShardLoader(tr.path, args.batchsize, tr_s, tr_aug, tr_size, drop_last=drop_last_train,
-                       s2d=s2d and tr_size % 2 == 0, **kw)
-    va_l = ShardLoader(va.path, args.batchsize, va_s, va_aug, va_size, s2d=s2d and va_size % 2 == 0, **kw)
+                       s2d=s2d, **kw)
+    va_l = ShardLoader(va.path, args.batchsize, va_s, va_aug, va_size, s2d=s2d, **kw)
     return tr_l, va_l
 
 
@@ -120,7 +120,8 @@ def build_data(args, rt: Runtime, drop_last_train=False):
         tr, va = WithIndex(tr), WithIndex(va)
     mean, std = norm_stats(args.dataset if "CIFAR" in args.dataset.upper() else "imagenet")
     cpad = 3 if str(args.model).startswith("tresnet") else 8
-    s2d = str(args.model).startswith(("resnet", "resnext"))  # ImageNet ResNets: space-to-depth stem input
+    # space-to-depth stem inputs written by the input kernel: ImageNet ResNets 2x2, TResNet 4x4
+    s2d = 4 if str(args.model).startswith("tresnet") else str(args.model).startswith(("resnet", "resnext"))
     tr_s = ShardSampler(tr, rt.world, rt.rank, shuffle=True, seed=args.seed, drop_last=drop_last_train)
     va_s = ShardSampler(va, rt.world, rt.rank, shuffle=False, seed=args.seed)
     if args.data == "shards":

@@ -29,7 +29,7 @@ def input_layout(model) -> dict:
     if any(getattr(m, "stem_s2d", False) for m in mods):
         return {"cpad": 8, "s2d": True}
     if any(type(m).__name__ == "TResNet" for m in mods):
-        return {"cpad": 3, "s2d": False}
+        return {"cpad": 3, "s2d": 4}  # SpaceToDepth(4) stem input written by the input kernel
     return {"cpad": 8, "s2d": False}
 
 

@@ -189,8 +189,10 @@ class TResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward_features(self, x):
-        """x: NHWC [N,H,W,3] (H, W divisible by 32)."""
-        x = Fn.space_to_depth(x, 4)
+        """x: NHWC [N,H,W,3] (H, W divisible by 32), or already the SpaceToDepth(4) input
+        [N,H/4,W/4,48] (``input_layout``: the input kernel writes it straight from the images)."""
+        if x.shape[-1] != 48:
+            x = Fn.space_to_depth(x, 4)
         x = self.stem(x)
         x = self.layer1(x)
         x = self.layer2(x)

@@ -449,10 +449,10 @@ def crop_resize(src, meta, Ho, Wo):
     return out
 
 
-def to_nhwc_s2d(src, nchw, in_scale, mean, std):
-    x = to_nhwc(src, nchw, 4, in_scale, mean, std)
-    N, H, W, _ = x.shape
-    return x.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 16).contiguous()
+def to_nhwc_s2d(src, nchw, in_scale, mean, std, block=2):
+    cq = 4 if block == 2 else 3
+    x = to_nhwc(src, nchw, cq, in_scale, mean, std)
+    return space_to_depth(x, block, False).contiguous()
 
 
 def act_bwd(dy, y, act):

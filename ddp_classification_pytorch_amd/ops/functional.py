@@ -1369,17 +1369,33 @@ def arcface_loss(x, weight, labels, s=30.0, m=0.5, easy_margin=True, return_logi
 
 
 # ----------------------------------------------------------------------------- misc
+def s2d_block(s2d) -> int:
+    """The space-to-depth block of an input-layout ``s2d`` value: False / 0 none, True / 2 the
+    ResNet s2d stem's 2x2 (16 channels), 4 TResNet's SpaceToDepth(4) (48 channels)."""
+    if s2d is True:
+        return 2
+    return int(s2d or 0)
+
+
+def s2d_for(s2d, h: int, w: int) -> int:
+    """``s2d``'s block if an h x w image divides into it, else 0 (plain NHWC input)."""
+    b = s2d_block(s2d)
+    return b if b and h % b == 0 and w % b == 0 else 0
+
+
 def to_device_nhwc(images: torch.Tensor, mean=None, std=None, cpad: int = 8, nchw: bool = True, in_scale: float = 1.0,
-                   s2d: bool = False):
+                   s2d=False):
     """Image batch (uint8 or fp32, NCHW/NHWC, already on the target device) -> normalised
-    NHWC activations with channels zero-padded to ``cpad``; ``s2d=True`` emits the 2x2
-    space-to-depth layout [N, H/2, W/2, 16] of the s2d stem (:func:`stem_conv_s2d`)."""
+    NHWC activations with channels zero-padded to ``cpad``; ``s2d=True`` (or 2) emits the 2x2
+    space-to-depth layout [N, H/2, W/2, 16] of the s2d stem (:func:`stem_conv_s2d`), ``s2d=4``
+    TResNet's 4x4 space-to-depth input [N, H/4, W/4, 48] (one pass from the images)."""
     if mean is not None and not torch.is_tensor(mean):
         mean = torch.tensor(mean, dtype=torch.float32, device=images.device)
     if std is not None and not torch.is_tensor(std):
         std = torch.tensor(std, dtype=torch.float32, device=images.device)
-    if s2d:
-        out = K(images).to_nhwc_s2d(images.contiguous(), nchw, in_scale, mean, std)
+    blk = s2d_block(s2d)
+    if blk:
+        out = K(images).to_nhwc_s2d(images.contiguous(), nchw, in_scale, mean, std, blk)
     else:
         out = K(images).to_nhwc(images.contiguous(), nchw, cpad, in_scale, mean, std)
     return out.to(act_dtype(images.device)) if not images.is_cuda else out

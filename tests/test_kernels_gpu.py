@@ -482,6 +482,21 @@ def test_to_nhwc_s2d(K, nchw):
     assert (y.view(-1, 4, 4)[:, :, 3] == 0).all()  # the pad channel of every phase
 
 
+@pytest.mark.parametrize("nchw", [True, False])
+def test_to_nhwc_s2d4_tresnet(K, nchw):
+    """TResNet's SpaceToDepth(4) input in one pass from the images: [N, H/4, W/4, 48] ==
+    space_to_depth(to_nhwc(images), 4) of the fp32 reference."""
+    img = torch.randint(0, 256, (3, 3, 20, 24), dtype=torch.uint8)
+    if not nchw:
+        img = img.permute(0, 2, 3, 1).contiguous()
+    mean = torch.tensor([0.485, 0.456, 0.406])
+    std = torch.tensor([0.229, 0.224, 0.225])
+    y = K.to_nhwc_s2d(img.to(DEV), nchw, 1 / 255.0, mean.to(DEV), std.to(DEV), 4)
+    yr = _ref.space_to_depth(_ref.to_nhwc(img, nchw, 3, 1 / 255.0, mean, std), 4, False)
+    assert y.shape == (3, 5, 6, 48)
+    assert relerr(y, yr) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,Ci,Co,k,pad", [(4, 112, 16, 64, 4, 2), (2, 9, 16, 72, 4, 2), (3, 15, 64, 64, 3, 1)])
 def test_conv_geo(K, N, H, Ci, Co, k, pad):
     """explicit-grid conv (the s2d stem: 4x4 taps, top/left pad 2, output grid = input grid)"""

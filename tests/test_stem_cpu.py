@@ -62,3 +62,22 @@ def test_resnet_s2d_stem_matches_plain_stem():
         out.append((loss.item(), m.conv1.weight.grad.clone()))
     assert abs(out[0][0] - out[1][0]) < 1e-4
     assert ((out[0][1] - out[1][1]).norm() / out[1][1].norm()).item() < 1e-3
+
+
+def test_tresnet_s2d4_input_matches_model_space_to_depth():
+    """TResNet's SpaceToDepth(4) stem input written by the input kernel (``input_layout`` s2d=4:
+    [N, H/4, W/4, 48], channel (py*4 + px)*3 + c, timm's order) == the model's own
+    space_to_depth of the plain 3-channel NHWC input, and the model gives the same output."""
+    torch.manual_seed(0)
+    m = build_model("tresnet_m", num_classes=10).eval()
+    lay = input_layout(m)
+    assert lay == {"cpad": 3, "s2d": 4}
+    img = torch.randint(0, 256, (2, 3, 64, 96), dtype=torch.uint8)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    x3 = Fn.to_device_nhwc(img, mean, std, cpad=3, in_scale=1 / 255.0)
+    x48 = Fn.to_device_nhwc(img, mean, std, in_scale=1 / 255.0, **lay)
+    assert x48.shape == (2, 16, 24, 48)
+    assert torch.equal(x48, _ref.space_to_depth(x3, 4, False))
+    with torch.no_grad():
+        assert torch.allclose(m(x48), m(x3), atol=1e-5)
+    assert Fn.s2d_for(4, 224, 224) == 4 and Fn.s2d_for(4, 226, 224) == 0 and Fn.s2d_for(True, 6, 8) == 2

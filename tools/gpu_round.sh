@@ -10,6 +10,8 @@
 #   pmc             three PMC passes (SQ: MFMA busy / LDS conflicts / waits; FETCH_SIZE; WRITE_SIZE)
 #   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
+#   stock1024       the same at batch 1024 (the headline batch)
+#   stockfp32       the same in fp32 (the reference's own precision), batch 256
 #   sweep           headline batch sweep 128..2048
 #   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
 #   convbench32     the same at batch 32 (the reference's per-process batch)
@@ -68,6 +70,12 @@ for step in "$@"; do
     stock)
       timeout -k 10 600 python -u tools/bench_torch_reference.py --batch 256 --warmup 3 > $O/stock_r50_b256.log 2>&1
       tail -1 $O/stock_r50_b256.log ;;
+    stock1024)
+      timeout -k 10 600 python -u tools/bench_torch_reference.py --batch 1024 --warmup 3 > $O/stock_r50_b1024.log 2>&1
+      tail -1 $O/stock_r50_b1024.log ;;
+    stockfp32)
+      timeout -k 10 600 python -u tools/bench_torch_reference.py --batch 256 --warmup 3 --fp32 > $O/stock_r50_b256_fp32.log 2>&1
+      tail -1 $O/stock_r50_b256_fp32.log ;;
     sweep)
       for b in 128 256 512 1024 2048; do
         timeout -k 10 240 python -u bench.py --batch $b --steps 10 --warmup 3 > $O/sweep_b$b.log 2>&1
