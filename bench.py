@@ -71,6 +71,9 @@ def parse(argv=None):
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--graph", action="store_true",
                     help="1 GPU: capture the whole step in a HIP graph and replay it (launch-bound small batches)")
+    ap.add_argument("--no-autotune", dest="autotune", action="store_false",
+                    help="fixed heuristic conv configurations instead of the per-shape timing on the warm-up "
+                         "steps (the reference's cudnn.benchmark=True, BASELINE/main.py:40)")
     return ap.parse_args(argv)
 
 
@@ -159,6 +162,10 @@ def main(argv=None):
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     kops = _ext.hip_ops()  # fail loudly if the gfx950 library is missing
+    # per-shape conv configuration autotuning on the (untimed) warm-up steps, as the reference's
+    # torch.backends.cudnn.benchmark = True (BASELINE/main.py:40); DCP_AUTOTUNE=0 / --no-autotune off
+    autotune = a.autotune and os.environ.get("DCP_AUTOTUNE", "1") != "0"
+    kops.set_tuning(25, 1 if autotune else 0)
     # A/B experiments only: DCP_TUNE="idx=value,..." sets the kernel-config overrides
     # (conv_igemm.hip g_tune: 0 BN tile, 1 LDS stages, 3 8-wave kernel)
     for kv in filter(None, os.environ.get("DCP_TUNE", "").split(",")):
@@ -286,6 +293,7 @@ def main(argv=None):
                 "num_classes": a.num_classes,
                 "parallelism": f"dp{world}",
                 "hip_graph": bool(a.graph),
+                "autotune": bool(autotune),
                 "syncbn": bool(a.syncbn),
                 "grad_comm": a.grad_comm,
                 "bucket_cap_mb": a.bucket_cap_mb,

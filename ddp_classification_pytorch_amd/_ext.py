@@ -7,7 +7,8 @@ math in :mod:`ddp_classification_pytorch_amd.ops._ref` (tests and gloo
 plumbing only).
 
 Set ``DCP_AUTOBUILD=1`` to compile the library on first use when it is
-missing (needs hipcc).
+missing (needs hipcc), ``DCP_AUTOTUNE=1`` to time the conv GEMM configurations per problem
+shape on first use and keep the fastest (like ``cudnn.benchmark``).
 """
 from __future__ import annotations
 
@@ -45,6 +46,9 @@ def try_load() -> bool:
             _state["error"] = f"failed to load {LIB_PATH}: {e}"
             return False
         _state["loaded"] = True
+        if os.environ.get("DCP_AUTOTUNE", "0") == "1":
+            # per-shape timing of the conv GEMM configurations on first use (conv_igemm.hip)
+            torch.ops.dcp.set_tuning(25, 1)
         return True
 
 

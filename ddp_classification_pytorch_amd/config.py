@@ -19,17 +19,18 @@ import os
 WORKLOAD_DEFAULTS = {
     "baseline": dict(model="tresnet_m", batchsize=16, lr=1e-3, epochs=100, optimizer="sgd", momentum=0.9,
                      weight_decay=0.0, imgs_limited=500, step_size=10, gamma=0.1, hidden=512, syncbn=True,
-                     transform="baseline"),
+                     transform="baseline", autotune=True),
     "arcface": dict(model="resnet50", batchsize=32, lr=1e-3, epochs=100, optimizer="adam", momentum=0.9,
                     weight_decay=5e-4, imgs_limited=400, step_size=10, gamma=0.1, hidden=512, syncbn=True,
-                    transform="arcface"),
+                    transform="arcface", autotune=True),
     "cdr": dict(model="resnet50", batchsize=128, lr=1e-3, epochs=200, optimizer="sgd", momentum=0.9,
                 weight_decay=0.0, imgs_limited=500, hidden=512, syncbn=False, transform="cdr",
-                milestones=[10, 20], gamma=0.1),
+                milestones=[10, 20], gamma=0.1, autotune=False),
     "nested": dict(model="resnet50", batchsize=128, lr=1e-2, epochs=150, optimizer="sgd", momentum=0.9,
-                   weight_decay=5e-4, syncbn=False, transform="nested", milestones=[20, 30, 40, 120], gamma=0.1),
+                   weight_decay=5e-4, syncbn=False, transform="nested", milestones=[20, 30, 40, 120], gamma=0.1,
+                   autotune=False),
     "plc": dict(model="resnet50", batchsize=64, lr=1e-2, epochs=10, optimizer="sgd", momentum=0.9, weight_decay=5e-4,
-                syncbn=False, transform="plc"),
+                syncbn=False, transform="plc", autotune=False),
 }
 
 
@@ -96,6 +97,12 @@ def build_parser() -> argparse.ArgumentParser:
     a("--heartbeat-every", dest="heartbeat_every", type=int, default=0,
       help="every N steps append a line to <out-dir>/heartbeat_rank<r>.txt")
     a("--profile", action="store_true", help="torch.profiler (roctracer) trace of 4 steps into <out-dir>/profile")
+    a("--autotune", dest="autotune", action="store_true", default=None,
+      help="time the conv kernel configurations per layer shape on first use and keep the fastest "
+           "(default for baseline / arcface, whose reference scripts set cudnn.benchmark=True: "
+           "BASELINE/main.py:40, ARCFACE/arc_main.py:51)")
+    a("--no-autotune", dest="autotune", action="store_false",
+      help="fixed heuristic kernel configurations (bit-reproducible run to run)")
     # ARCFACE
     a("--s", "--arc-s", dest="arc_s", type=float, default=30.0)
     a("--m", "--arc-m", dest="arc_m", type=float, default=0.5)

@@ -10,6 +10,8 @@
 #include <torch/library.h>
 
 #include <mutex>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "launchers.h"
@@ -512,6 +514,37 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   return {dx, sums};
 }
 
+// Weight-gradient configurations the autotuner (g_tune[25] = 1, DCP_AUTOTUNE) times per problem,
+// as g_tune overrides: [5] workgroups per CU of the split-K plan, [7] = 2 no 256-tile kernel,
+// [12] = 32 32-row k-tiles, [15] = 1 no direct 3x3 kernel.  The split count changes the partial
+// slabs, so the choice is made here, where they are allocated (see launch_tap_gemm for the
+// forward / data-gradient side).  Every configuration reduces the split partials in a fixed
+// order, but a different split count sums the rows in another order (fp32 rounding).
+namespace {
+struct WgCfg {
+  int t5, t7, t12, t15;
+};
+const WgCfg kWgCfgs[] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, 0, 0, 0}, {4, 0, 0, 0},
+                         {8, 0, 0, 0}, {0, 2, 0, 0}, {0, 0, 32, 0}, {0, 0, 0, 1}};
+std::mutex g_wg_mu;
+std::unordered_map<std::string, int> g_wg_choice;
+struct WgOverride {
+  int saved[4];
+  explicit WgOverride(const WgCfg& c) {
+    saved[0] = dcp::g_tune[5]; saved[1] = dcp::g_tune[7]; saved[2] = dcp::g_tune[12]; saved[3] = dcp::g_tune[15];
+    dcp::g_tune[5] = c.t5; dcp::g_tune[7] = c.t7; dcp::g_tune[12] = c.t12; dcp::g_tune[15] = c.t15;
+  }
+  ~WgOverride() {
+    dcp::g_tune[5] = saved[0]; dcp::g_tune[7] = saved[1]; dcp::g_tune[12] = saved[2]; dcp::g_tune[15] = saved[3];
+  }
+};
+}  // namespace
+
+int64_t wgrad_autotune_entries() {
+  std::lock_guard<std::mutex> lk(g_wg_mu);
+  return (int64_t)g_wg_choice.size();
+}
+
 // dy [N,Ho,Wo,Co], x [N,H,W,C] -> dw fp32 [Co,KH,KW,C]
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
   CHECK_ACT(dy);
@@ -525,10 +558,70 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   auto dw = at::empty({Co, KH, KW, C}, f32_like(dy));
   const auto taps = fwd_taps(KH, KW, pad);
   const int ncu = num_cus(dy.get_device());
-  const int splits = dcp::wgrad_plan_splits(N, Ho, Wo, Co, H, W, C, stride, taps, ncu);
-  auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
-  dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
-                    part.data_ptr<float>(), zero_page(dy.get_device()), ncu, cur_stream());
+  auto st = cur_stream();
+  auto run = [&]() {
+    const int splits = dcp::wgrad_plan_splits(N, Ho, Wo, Co, H, W, C, stride, taps, ncu);
+    auto part = at::empty({splits > 1 ? (int64_t)(splits + (splits + 63) / 64) * dw.numel() : 4}, f32_like(dy));
+    dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
+                      part.data_ptr<float>(), zero_page(dy.get_device()), ncu, st);
+  };
+  if (dcp::g_tune[25] != 1 || dcp::g_tune[5] || dcp::g_tune[7] || dcp::g_tune[12] || dcp::g_tune[15] ||
+      (int64_t)N * Ho * Wo == 0) {
+    run();
+    return dw;
+  }
+  const std::string key = std::to_string(N) + " " + std::to_string(Ho) + " " + std::to_string(Wo) + " " +
+                          std::to_string(Co) + " " + std::to_string(H) + " " + std::to_string(W) + " " +
+                          std::to_string(C) + " " + std::to_string(KH) + " " + std::to_string(KW) + " " +
+                          std::to_string(stride) + " " + std::to_string(pad);
+  int choice = -1;
+  {
+    std::lock_guard<std::mutex> lk(g_wg_mu);
+    auto it = g_wg_choice.find(key);
+    if (it != g_wg_choice.end()) choice = it->second;
+  }
+  if (choice < 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      run();
+      return dw;
+    }
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e30f, t_heur = 1e30f;
+    choice = 0;
+    for (int c = 0; c < (int)(sizeof(kWgCfgs) / sizeof(kWgCfgs[0])); ++c) {
+      WgOverride ov(kWgCfgs[c]);
+      run();  // warm
+      float t = 1e30f;
+      for (int r = 0; r < 3; ++r) {
+        hipEventRecord(e0, st);
+        run();
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        t = std::min(t, ms);
+      }
+      if (c == 0) {
+        t_heur = best = t;
+      } else if (t < best && t < 0.98f * t_heur) {  // must beat the heuristic by 2 % to replace it
+        best = t;
+        choice = c;
+      }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    {
+      std::lock_guard<std::mutex> lk(g_wg_mu);
+      g_wg_choice[key] = choice;
+    }
+    if (getenv("DCP_AUTOTUNE_LOG"))
+      fprintf(stderr, "[dcp-autotune] wgrad %s -> cfg %d (%.1f us)\n", key.c_str(), choice, best * 1e3f);
+  }
+  WgOverride ov(kWgCfgs[choice]);
+  run();
   return dw;
 }
 
@@ -1395,6 +1488,8 @@ Tensor table_fill(const Tensor& host, const Tensor& device_like) {
   return out;
 }
 
+int64_t autotune_entries() { return dcp::tap_gemm_tuned_count() + wgrad_autotune_entries(); }
+
 void set_tuning(int64_t idx, int64_t value) {
   TORCH_CHECK(idx >= 0 && idx < 32, "tuning index");
   dcp::g_tune[idx] = (int)value;
@@ -1402,6 +1497,7 @@ void set_tuning(int64_t idx, int64_t value) {
 
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
+  m.def("autotune_entries() -> int", &autotune_entries);
   m.def("table_fill(Tensor host, Tensor device_like) -> Tensor", &table_fill);
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);

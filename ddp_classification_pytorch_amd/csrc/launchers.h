@@ -53,6 +53,8 @@ struct AffineEpi {
   float slope;
 };
 
+// number of problems the tap-GEMM autotuner (g_tune[25] = 1) has measured in this process
+int tap_gemm_tuned_count();
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,

@@ -37,7 +37,9 @@ def setup(args) -> Runtime:
     if want_cuda:
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
-        _ext.hip_ops()  # GPU path requires the gfx950 library: fail loudly here, not mid-epoch
+        kops = _ext.hip_ops()  # GPU path requires the gfx950 library: fail loudly here, not mid-epoch
+        # per-shape conv configuration autotuning (the reference's cudnn.benchmark=True)
+        kops.set_tuning(25, 1 if getattr(args, "autotune", False) else 0)
     else:
         device = torch.device("cpu")
     set_seed(args.seed + rank)

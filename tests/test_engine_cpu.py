@@ -89,3 +89,17 @@ def test_warmup_heartbeat_profile_and_auto_resume(tmp_path):
     entry.main(base + ["--out-dir", str(out), "--auto-resume"])
     text = open(out / "output.txt").read()
     assert "resumed from" in text and "VAL Epoch 2" in text
+
+
+def test_autotune_defaults_follow_reference_cudnn_benchmark():
+    """--autotune (per-shape conv configuration timing, the cudnn.benchmark of these kernels)
+    defaults on where the reference sets torch.backends.cudnn.benchmark=True (BASELINE/main.py:40,
+    ARCFACE/arc_main.py:51) and off elsewhere; both directions can be forced."""
+    from ddp_classification_pytorch_amd.config import parse_args
+
+    assert parse_args(["--workload", "baseline"]).autotune is True
+    assert parse_args(["--workload", "arcface"]).autotune is True
+    for w in ("cdr", "nested", "plc"):
+        assert parse_args(["--workload", w]).autotune is False
+    assert parse_args(["--workload", "baseline", "--no-autotune"]).autotune is False
+    assert parse_args(["--workload", "cdr", "--autotune"]).autotune is True

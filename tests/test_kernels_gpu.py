@@ -1246,3 +1246,40 @@ def test_iabn_gamma_and_sign_mul(K):
     rge, rrg = _ref.iabn_gamma(g, 1e-5)
     assert torch.allclose(ge.cpu(), rge) and torch.allclose(rg.cpu(), rrg, rtol=1e-6)
     assert torch.equal(K.sign_mul(d.to(DEV), g.to(DEV)).cpu(), _ref.sign_mul(d, g))
+
+
+def test_conv_autotune_same_results(K):
+    """g_tune[25] = 1 (DCP_AUTOTUNE): the first call of each conv problem times the candidate
+    configurations and keeps one; forward and data gradient are bitwise the untuned results (every
+    candidate accumulates in the same k order), the BN statistics equal them to fp32 rounding (a
+    64-channel tile sums a slab's rows in another order), the weight gradient too (another split-K
+    plan), and later calls reuse the choice."""
+    torch.manual_seed(0)
+    shapes = [(5, 14, 14, 256, 256, 3, 1, 1), (3, 28, 28, 128, 512, 1, 1, 0), (3, 28, 28, 256, 512, 1, 2, 0)]
+    for N, H, W, Ci, Co, k, s, p in shapes:
+        x = rnd(N, H, W, Ci).to(DEV)
+        w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        dy = rnd(N, Ho, Wo, Co).to(DEV)
+        wb, wt = K.weight_prep(w.float(), 0, True)
+        K.set_tuning(25, 0)  # (a workload run earlier in this process may have left it on)
+        y0, s0 = K.conv_fwd(x, wb, s, p, True)
+        d0 = K.conv_dgrad(dy, wt, H, W, s, p)
+        g0 = K.conv_wgrad(dy, x, k, k, s, p)
+        n0 = K.autotune_entries()
+        try:
+            K.set_tuning(25, 1)
+            y1, s1 = K.conv_fwd(x, wb, s, p, True)
+            d1 = K.conv_dgrad(dy, wt, H, W, s, p)
+            g1 = K.conv_wgrad(dy, x, k, k, s, p)
+            n1 = K.autotune_entries()
+            y2, _ = K.conv_fwd(x, wb, s, p, True)
+            assert K.autotune_entries() == n1 > n0
+        finally:
+            K.set_tuning(25, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y0) and torch.equal(y2, y0), (N, H, Ci, Co, k, s)
+        assert torch.equal(d1, d0), (N, H, Ci, Co, k, s)
+        st0, st1 = K.bn_stats(y0, s0), K.bn_stats(y1, s1)
+        assert relerr(st1[0, 1:], st0[0, 1:]) < 1e-5
+        assert relerr(g1, g0) < 1e-5  # another split count sums the rows in another order
