@@ -62,6 +62,7 @@ for step in "$@"; do
       echo prof $c done ;;
     pmc)
       prof_env
+      export DCP_AUTOTUNE=0  # the heuristic's kernels: no tuning dispatches inside the counted steps
       PASS1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
       timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $PASS1 --output-format csv -d $O/pmc1 -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/pmc1.log 2>&1
       timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmc2 -o run -- python3 -u bench.py --steps 2 --warmup 1 > $O/pmc2.log 2>&1
