@@ -51,7 +51,7 @@ def table_to_device(rows, dtype, device) -> torch.Tensor:
     copy, so a table built while a step is being captured into a HIP graph replays correctly
     (a captured memcpy would re-read a host buffer that is gone, and pinning memory is not
     allowed during capture)."""
-    host = torch.tensor(rows, dtype=dtype)
+    host = rows.to(dtype).contiguous() if torch.is_tensor(rows) else torch.tensor(rows, dtype=dtype)
     device = torch.device(device)
     if device.type != "cuda":
         return host.to(device)

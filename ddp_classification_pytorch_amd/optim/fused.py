@@ -32,22 +32,31 @@ CHUNK = 4096
 
 
 class _TableCache:
+    """Device tables of one launch: the (param, grad, state..., numel) entries, rebuilt when a
+    pointer changes (every eager step when grads are set to None), and the (entry, chunk) work
+    list, which depends only on the tensor sizes and is built once (a per-step Python loop over
+    ResNet-50's 6,240 chunks cost milliseconds of host time per eager step)."""
+
     def __init__(self):
         self.key = None
+        self.sizes = None
         self.table = None
         self.chunks = None
 
     def get(self, entries, device):
         key = tuple((e[0], e[1], e[2], e[3], e[5]) for e in entries)
         if key != self.key:
-            ch = []
-            for i, e in enumerate(entries):
-                n = e[5]
-                ch.extend((i, c) for c in range((n + CHUNK - 1) // CHUNK))
+            sizes = tuple(e[5] for e in entries)
+            if sizes != self.sizes:
+                counts = torch.tensor([(n + CHUNK - 1) // CHUNK for n in sizes], dtype=torch.int64)
+                ent = torch.repeat_interleave(torch.arange(len(sizes), dtype=torch.int64), counts)
+                first = torch.repeat_interleave(torch.cumsum(counts, 0) - counts, counts)
+                ch = torch.stack([ent, torch.arange(ent.numel(), dtype=torch.int64) - first], 1)
+                self.chunks = Fn.table_to_device(ch.to(torch.int32), torch.int32, device).view(-1, 2)
+                self.sizes = sizes
             # graph-capture safe uploads (grads of a captured step live in the graph pool: the
-            # table is rebuilt once during capture and replayed from its pinned host copy)
+            # table is rebuilt once during capture and replayed from the fill kernel's arguments)
             self.table = Fn.table_to_device([list(e) for e in entries], torch.int64, device).view(-1, 6)
-            self.chunks = Fn.table_to_device(ch, torch.int32, device).view(-1, 2)
             self.key = key
         return self.table, self.chunks
 
