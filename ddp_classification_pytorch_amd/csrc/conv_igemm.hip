@@ -178,8 +178,11 @@ __device__ __forceinline__ void tile_stats(const TapGemmParams& p, char* E, int 
 // row 0 (one shift per channel for every thread, so the partial sums add) -> wave shuffles ->
 // LDS behind row 7 of the image -> one thread per channel.  Replaces 64 two-byte reads and a
 // two-pass per thread (tile_stats) with 8 (BN = 128) or 4 (BN = 64) chunk reads.
+// vv: this thread's image chunks (chunk tid % NCH of rows tid / NCH + G k), already in registers
+// from the store pass (tg_image_store reads exactly these) -- the image is not read twice
 template <int BN>
-__device__ __forceinline__ void tile_stats128(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
+__device__ __forceinline__ void tile_stats128_vv(const TapGemmParams& p, char* E, int m0, int n0, int tid,
+                                                 const bf16x8 (&vv)[128 / (256 / (BN / 8))]) {
   constexpr int NCH = BN / 8, G = 256 / NCH, RPT = 128 / G, RB = BN * 2;
   const int c = tid % NCH, g = tid / NCH, lane = tid & 63, wave = tid >> 6;
   const int nvalid = min(128, p.M - m0);
@@ -192,9 +195,6 @@ __device__ __forceinline__ void tile_stats128(const TapGemmParams& p, char* E, i
       s1[e] = s2[e] = 0.f;
     }
   }
-  bf16x8 vv[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) vv[k] = eimg_chunk<NCH>(E, g + G * k, c);
 #pragma unroll
   for (int k = 0; k < RPT; ++k)
     if (g + G * k < nvalid)
@@ -368,8 +368,9 @@ __device__ __forceinline__ void tg_image_store(const TapGemmParams& p, char* E, 
         *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
       }
     }
+    // the statistics of the bf16 outputs, from the chunks this pass already holds
+    if constexpr (EPI == 1) tile_stats128_vv<BN>(p, E, m0, n0, tid, vv);
   }
-  if constexpr (EPI == 1) tile_stats128<BN>(p, E, m0, n0, tid);
 }
 
 // EPI: 0 = bf16 store, 1 = store + per-64-row BN statistics, 2 = bias / activation (linear heads)
@@ -927,7 +928,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// tile_stats128 with LDS-only barriers (the persistent kernel keeps loads / stores in flight)
+// tile_stats128_vv with LDS-only barriers (the persistent kernel keeps loads / stores in flight)
 template <int BN>
 __device__ __forceinline__ void tile_stats128_nb(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
   constexpr int NCH = BN / 8, G = 256 / NCH, RPT = 128 / G, RB = BN * 2;
@@ -1521,7 +1522,7 @@ tap_gemm_big_kernel(const TapGemmParams p) {
   }
   __syncthreads();
   // group g (threads 256g ..) stores quadrants g*QPG ..; every group passes the same barriers
-  // (tile_stats128's), so the quadrant loop stays uniform
+  // (tile_stats128_vv's), so the quadrant loop stays uniform
   const int g = tid >> 8, gtid = tid & 255;
 #pragma unroll
   for (int k = 0; k < QPG; ++k) {
@@ -2050,7 +2051,7 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   const size_t full = (size_t)NS * stage;
   size_t epi = 0;
   if (EPI == 0) epi = (size_t)128 * 2 * BN;
-  if (EPI == 1) epi = (size_t)128 * 2 * BN;  // tile_stats128 keeps its scratch inside the image
+  if (EPI == 1) epi = (size_t)128 * 2 * BN;  // tile_stats128_vv keeps its scratch inside the image
   // image, then the sums' [2][8][256 + 4] fp32 in its space
   if (EPI == 3 || EPI == 4) epi = std::max((size_t)128 * 2 * BN, (size_t)2 * 8 * 260 * 4);
   size_t lds = std::max((size_t)std::min(NS, std::max(p.nkt, 1)) * stage, epi);
