@@ -2324,6 +2324,9 @@ static const TgCfg kTgCfgs[] = {
     {0, 2, 32, 2},  // 32-deep k-tiles, double buffer
     {0, 3, 64, 2},  // 3-stage ring of 64-deep k-tiles
     {64, 0, 0, 2},  // 64-channel tiles
+    {64, 2, 32, 2}, // 64-channel tiles, 32-deep k-tiles
+    {64, 3, 64, 2}, // 64-channel tiles, 3-stage ring
+    {0, 4, 64, 2},  // 4-stage ring of 64-deep k-tiles
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
 };
@@ -2390,7 +2393,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
       const TgCfg& cfg = kTgCfgs[c];
       if (cfg.big == 3 && !big_ok) continue;
       if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;
-      if (cfg.bn == 64 && Co <= 64) continue;  // the heuristic's tile already
+      if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
       TuneOverride ov(cfg);
       run();  // warm
       float t = 1e30f;
