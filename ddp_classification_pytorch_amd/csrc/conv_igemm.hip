@@ -2359,8 +2359,9 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   };
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
+  // (an add source aliasing the output would accumulate over the timing runs: never tuned)
   if (g_tune[25] != 1 || !fast || pscale != nullptr || g_tune[0] || g_tune[1] || g_tune[8] || g_tune[24] ||
-      (long)N * Hy * Wy == 0) {
+      (long)N * Hy * Wy == 0 || (addsrc != nullptr && addsrc == dst)) {
     run();
     return;
   }
