@@ -72,6 +72,16 @@ __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __res
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = r0 + w;
+    for (; r + 60 < r1; r += 64) {  // 16 slabs' loads in flight per wave, merged in order
+      float mb[16], m2b[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
+    }
     for (; r + 12 < r1; r += 16) {
       float mb[4], m2b[4];
 #pragma unroll
@@ -162,6 +172,15 @@ __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int p = w;
+    for (; p + 15 * NW < P; p += 16 * NW) {  // 16 partials' loads in flight, merged in order
+      float v[16][3];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[u][q] = part[((size_t)(p + u * NW) * 3 + q) * C + c];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a.merge(v[u][0], v[u][1], v[u][2]);
+    }
     for (; p + 3 * NW < P; p += 4 * NW) {
       float v[4][3];
 #pragma unroll
@@ -196,6 +215,18 @@ __device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, 
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = w;
+    // 16 slabs' loads in flight per wave before the (in-order, so deterministic) merges: the merge
+    // of a small batch's <= 1024 slabs is bound by load round trips, not by the merge math
+    for (; r + 15 * kMergeWaves < R; r += 16 * kMergeWaves) {
+      float mb[16], m2b[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        mb[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + u * kMergeWaves)), mb[u], m2b[u]);
+    }
     for (; r + 3 * kMergeWaves < R; r += 4 * kMergeWaves) {
       float mb[4], m2b[4];
 #pragma unroll
@@ -308,6 +339,16 @@ __global__ void __launch_bounds__(256) bn_slab_partial_finalize_kernel(
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = r0 + w;
+    for (; r + 60 < r1; r += 64) {  // 16 slabs' loads in flight per wave, merged in order
+      float mb[16], m2b[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
+    }
     for (; r + 12 < r1; r += 16) {
       float mb[4], m2b[4];
 #pragma unroll
@@ -350,6 +391,20 @@ __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restric
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (k < K) {
     int p = w;
+    // 16 loads in flight per wave (a small batch's BN sums reduce ~800 partials: load round trips,
+    // not adds, set the time); each accumulator still adds its rows in the same order
+    for (; p + 60 < P; p += 64) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = part[(size_t)(p + 4 * u) * K + k];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        s0 += v[u];
+        s1 += v[u + 1];
+        s2 += v[u + 2];
+        s3 += v[u + 3];
+      }
+    }
     for (; p + 12 < P; p += 16) {
       s0 += part[(size_t)p * K + k];
       s1 += part[(size_t)(p + 4) * K + k];

@@ -24,3 +24,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _kernel_tuning_off_between_tests():
+    """Per-shape autotuning (g_tune[25]) is process-global state that a workload run switches on
+    (the baseline / arcface workloads default to it): every test starts and ends with it off, so
+    tuning dispatches and their scratch never land inside another test's measurements."""
+    from ddp_classification_pytorch_amd import _ext
+
+    if _ext.is_loaded():
+        _ext.hip_ops().set_tuning(25, 0)
+    yield
+    if _ext.is_loaded():
+        _ext.hip_ops().set_tuning(25, 0)
