@@ -7,6 +7,8 @@
 #   bench           headline bench.py (20 steps)              configs every BASELINE.json config
 #   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
 #   profcfg=CFG     the same for another bench config (e.g. arcface)
+#   profsmall       the same for the batch-32 HIP-graph step (200 replays)
+#   graphs          HIP-graph batch 32 / 128 twice, then the headline batch
 #   pmc             three PMC passes (SQ: MFMA busy / LDS conflicts / waits; FETCH_SIZE; WRITE_SIZE)
 #   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
 #   stock           stock PyTorch-ROCm ResNet-50 step (MIOpen / hipBLASLt) at batch 256
@@ -60,6 +62,22 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run -- python3 -u bench.py --config $c --steps 8 --warmup 2 \
         > $O/prof_$c.log 2>&1
       echo prof $c done ;;
+    profsmall)
+      # rocprofv3 kernel statistics of the batch-32 HIP-graph step, 200 replays (tuning diluted)
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_small -o run -- python3 -u bench.py --batch 32 --graph --steps 200 --warmup 5 \
+        > $O/prof_small.log 2>&1
+      echo prof small done ;;
+    graphs)
+      # HIP-graph batch 32 / 128 (x2) and the headline batch
+      for r in 1 2; do
+        timeout -k 10 240 python -u bench.py --batch 32 --graph --steps 50 --warmup 5 > $O/g32_$r.log 2>&1
+        echo "b32 graph $(grep -o '"value": [0-9.]*' $O/g32_$r.log)"
+        timeout -k 10 240 python -u bench.py --batch 128 --graph --steps 30 --warmup 5 > $O/g128_$r.log 2>&1
+        echo "b128 graph $(grep -o '"value": [0-9.]*' $O/g128_$r.log)"
+      done
+      timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > $O/b1024.log 2>&1
+      echo "b1024 $(grep -o '"value": [0-9.]*' $O/b1024.log)" ;;
     pmc)
       prof_env
       export DCP_AUTOTUNE=0  # the heuristic's kernels: no tuning dispatches inside the counted steps
