@@ -17,7 +17,8 @@ import threading
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dcp_kernels.so")
+# DCP_LIB: load another build of the library (same-box A/B of two kernel versions)
+LIB_PATH = os.environ.get("DCP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dcp_kernels.so")
 _lock = threading.Lock()
 _state = {"loaded": False, "error": None}
 

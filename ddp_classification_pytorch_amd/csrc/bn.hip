@@ -72,16 +72,6 @@ __global__ void __launch_bounds__(256) bn_slab_partial_kernel(const float* __res
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = r0 + w;
-    for (; r + 60 < r1; r += 64) {  // 16 slabs' loads in flight per wave, merged in order
-      float mb[16], m2b[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
-        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
-    }
     for (; r + 12 < r1; r += 16) {
       float mb[4], m2b[4];
 #pragma unroll
@@ -172,15 +162,6 @@ __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int p = w;
-    for (; p + 15 * NW < P; p += 16 * NW) {  // 16 partials' loads in flight, merged in order
-      float v[16][3];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) v[u][q] = part[((size_t)(p + u * NW) * 3 + q) * C + c];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) a.merge(v[u][0], v[u][1], v[u][2]);
-    }
     for (; p + 3 * NW < P; p += 4 * NW) {
       float v[4][3];
 #pragma unroll
@@ -216,7 +197,9 @@ __device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, 
   if (c < C) {
     int r = w;
     // 16 slabs' loads in flight per wave before the (in-order, so deterministic) merges: the merge
-    // of a small batch's <= 1024 slabs is bound by load round trips, not by the merge math
+    // of a small batch's <= 1024 slabs is bound by load round trips, not by the merge math.  (The
+    // large-batch two-level merges keep 4: 16 there measured 0.6 % slower end to end at batch
+    // 1024, profiles/r3/bn_reduce_pipelining_ab.txt.)
     for (; r + 15 * kMergeWaves < R; r += 16 * kMergeWaves) {
       float mb[16], m2b[16];
 #pragma unroll
@@ -339,16 +322,6 @@ __global__ void __launch_bounds__(256) bn_slab_partial_finalize_kernel(
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = r0 + w;
-    for (; r + 60 < r1; r += 64) {  // 16 slabs' loads in flight per wave, merged in order
-      float mb[16], m2b[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
-        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
-    }
     for (; r + 12 < r1; r += 16) {
       float mb[4], m2b[4];
 #pragma unroll
