@@ -919,7 +919,12 @@ static inline int rows_grid(int M, int C, int rows_per_thread, int cap) {
 // 4096-workgroup grid-stride loop over 8 rows per thread -- HBM wants the whole tensor's loads
 // spread over many short-lived waves.  g_tune[9] / [10] override cap / rows (A/B only).
 static inline dim3 ew_grid(int M, int C) {
-  return dim3(rows_grid(M, C, g_tune[10] > 0 ? g_tune[10] : 2, g_tune[9] > 0 ? g_tune[9] : (1 << 20)));
+  // 4 rows per thread where that still leaves >= 2048 workgroups (8 per CU): R50 b1024 +0.4 % over
+  // 2 (same box, 4 pairs; 8 rows -0.6 %, 1 row -5 %: profiles/r3/ew_rows_ab.txt); small tensors 2
+  const int cap = g_tune[9] > 0 ? g_tune[9] : (1 << 20);
+  if (g_tune[10] > 0) return dim3(rows_grid(M, C, g_tune[10], cap));
+  const int g4 = rows_grid(M, C, 4, cap);
+  return dim3(g4 >= 2048 ? g4 : rows_grid(M, C, 2, cap));
 }
 
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y,
