@@ -936,7 +936,9 @@ void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const
                        mask, rscale, rshift);
 }
 
-int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, 512); }
+// g_tune[28] overrides the workgroup cap (A/B only: 256 and 1024 measured 0.5-1.2 % slower end to end
+// at b1024, profiles/r3/ew_rows_ab.txt)
+int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, g_tune[28] > 0 ? g_tune[28] : 512); }
 
 // partials must hold bn_bwd_reduce_blocks(M, C) x 2 x C floats; out [2][C]
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
