@@ -18,12 +18,18 @@ from ..parallel.ddp import wrap_ddp
 
 
 def build_classifier(args, log_softmax=False):
+    """TResNet / VGG carry their own classifier (timm / torchvision heads); the ResNets get the
+    reference's MLP head.  ``--pretrained FILE`` loads a local torchvision / timm / reference file
+    into the backbone (BASELINE/main.py:135,143-144) and raises if it does not fit the model."""
+    from ..models.pretrained import load_pretrained
+
     if args.model.startswith("tresnet") or args.model.startswith("vgg"):
-        return build_model(args.model, num_classes=args.num_classes)
+        model = build_model(args.model, num_classes=args.num_classes)
+        if args.pretrained:
+            load_pretrained(model, args.pretrained)  # the classifier is skipped when the class count differs
+        return model
     backbone = build_model(args.model, num_classes=0)
     if args.pretrained:
-        from ..models.pretrained import load_pretrained
-
         load_pretrained(backbone, args.pretrained)
     head = MLPHead(backbone.feat_dim, args.hidden, args.num_classes, log_softmax=log_softmax)
     return ClassifierModel(backbone, head)

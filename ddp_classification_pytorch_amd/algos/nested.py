@@ -92,7 +92,7 @@ def test_standard(net_feat, net_cls, val_data, nb_cls):
     net_feat.eval()
     net_cls.eval()
     dev = next(net_cls.parameters()).device
-    acc = torch.zeros(3, dtype=torch.float64, device=dev)
+    acc = torch.zeros(4, dtype=torch.float64, device=dev)
     left = valid_count(getattr(val_data, "sampler", None), float("inf"))
     for batch in val_data:
         x, y = batch[0], batch[1]
@@ -101,12 +101,10 @@ def test_standard(net_feat, net_cls, val_data, nb_cls):
         if k <= 0:
             continue
         _, rank = Fn.cross_entropy_rows(net_cls(net_feat(x)), y, nb_cls)
-        rank = rank[:k]
-        acc += torch.stack([(rank < 1).sum().double(), (rank < 3).sum().double(),
-                            torch.tensor(float(k), device=dev, dtype=torch.float64)])
+        Fn.metric_accum(acc, rank[:0].float(), 0.0, rank, k)  # [loss 0, top-1, top-3, count]
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(acc)
-    a = acc.tolist()
+    a = acc.tolist()[1:]
     return a[0] / max(a[2], 1), a[1] / max(a[2], 1)
 
 

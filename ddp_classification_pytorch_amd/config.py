@@ -49,7 +49,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--device", default=None, help="cuda (default when available) or cpu")
     a("--graph", action="store_true", help="1 GPU: replay the training step as a HIP graph (launch-bound small batches)")
     # data
-    a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "shards"])
+    a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "synthetic-device", "shards"],
+      help="synthetic: random images through the host DataLoader path; synthetic-device: random uint8 batches "
+           "generated once on the GPU (the bench.py input, no host pipeline in the step)")
     a("--shard-train", dest="shard_train", default=None, help="--data shards: train shard (default <folder>/train.dcps)")
     a("--shard-val", dest="shard_val", default=None, help="--data shards: val shard (default <folder>/test.dcps)")
     a("--loader-threads", dest="loader_threads", type=int, default=8, help="native shard loader host threads")
@@ -64,6 +66,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--image-size", dest="image_size", type=int, default=None)
     a("--synthetic-train-size", type=int, default=2048)
     a("--synthetic-val-size", type=int, default=512)
+    a("--synthetic-learnable", action="store_true",
+      help="--data synthetic: images carry their class (per-class colour template + noise) so the loss can fall")
     # model
     a("--model", default=None)
     a("--arch", default=None, help="NESTED alias of --model")
@@ -136,6 +140,8 @@ def build_parser() -> argparse.ArgumentParser:
 def resolve(args: argparse.Namespace) -> argparse.Namespace:
     """Fill workload defaults, environment-provided ranks and aliases."""
     d = WORKLOAD_DEFAULTS[args.workload]
+    if getattr(args, "autotune", None) is None and os.environ.get("DCP_AUTOTUNE") in ("0", "1"):
+        args.autotune = os.environ["DCP_AUTOTUNE"] == "1"  # the env switch, when no flag was given
     for k, v in d.items():
         if getattr(args, k, None) is None:
             setattr(args, k, v)

@@ -1318,6 +1318,17 @@ std::tuple<Tensor, Tensor> xent_fwd(const Tensor& logits, const Tensor& labels, 
   return {loss, rank};
 }
 
+// acc (fp64 [4]) += [loss_scale * sum(loss), #(rank < 1), #(rank < 3), nrows] over rank[:nrows]
+void metric_accum(const Tensor& acc, const Tensor& loss, double loss_scale, const Tensor& rank, int64_t nrows) {
+  CHECK_DEV(acc);
+  TORCH_CHECK(acc.scalar_type() == at::kDouble && acc.is_contiguous() && acc.numel() >= 4, "acc: fp64 [4]");
+  TORCH_CHECK(rank.scalar_type() == at::kInt && rank.is_contiguous() && rank.is_cuda(), "rank: int32 on GPU");
+  TORCH_CHECK(nrows >= 0 && nrows <= rank.numel(), "metric_accum: nrows");
+  const Tensor l = loss.to(at::kFloat).contiguous();
+  dcp::launch_metric_accum(acc.data_ptr<double>(), l.data_ptr<float>(), (int)l.numel(), (float)loss_scale,
+                           rank.data_ptr<int>(), (int)nrows, cur_stream());
+}
+
 // logits may be a column slice of a wider (padded) buffer: row stride = stride(0)
 Tensor xent_bwd(const Tensor& logits, const Tensor& labels, int64_t C, const Tensor& grad_out, double scale,
                 double smoothing, bool out_bf16) {
@@ -1590,6 +1601,7 @@ TORCH_LIBRARY(dcp, m) {
         "Tensor)",
         &chan_scale_bwd);
   m.def("xent_fwd(Tensor logits, Tensor labels, int C, float smoothing) -> (Tensor, Tensor)", &xent_fwd);
+  m.def("metric_accum(Tensor(a!) acc, Tensor loss, float loss_scale, Tensor rank, int nrows) -> ()", &metric_accum);
   m.def(
       "xent_bwd(Tensor logits, Tensor labels, int C, Tensor grad_out, float scale, float smoothing, bool out_bf16) "
       "-> Tensor",

@@ -185,6 +185,8 @@ void launch_s2d(const bf16* x, bf16* y, int N, int H, int W, int C, int b, int i
 
 void launch_xent_fwd(const void* logits, bool is_bf16, int B, int ld, int C, const int64_t* labels, float* loss,
                      int* rank, float smoothing, hipStream_t s);
+void launch_metric_accum(double* acc, const float* loss, int nloss, float loss_scale, const int* rank, int nrows,
+                         hipStream_t s);
 void launch_xent_bwd(const void* logits, bool in_bf16, int B, int ld, int C, const int64_t* labels,
                      const float* grad_out, float scale, float smoothing, void* dlogits, int ldo, bool out_bf16,
                      hipStream_t s);

@@ -334,4 +334,35 @@ void launch_arcface_bwd(const bf16* cosv, int B, int ld, int C, const int64_t* l
                      easy, lab_dphi, grad_out, scale, dcos);
 }
 
+// Training / validation metric accumulation in one launch (replaces the per-step compare / sum /
+// cast / stack / add chain and the host->device count copy of the loops): with one workgroup,
+//   acc[0] += loss_scale * sum(loss[0 .. nloss)),  acc[1] += #{rank[i] < 1},  acc[2] += #{rank[i] < 3},
+//   acc[3] += nrows        (i < nrows; acc fp64, the count a kernel argument -- no host copy)
+__global__ void __launch_bounds__(256) metric_accum_kernel(double* __restrict__ acc, const float* __restrict__ loss,
+                                                           int nloss, float loss_scale, const int* __restrict__ rank,
+                                                           int nrows) {
+  __shared__ float red[16];
+  float ls = 0.f, t1 = 0.f, t3 = 0.f;
+  for (int i = threadIdx.x; i < nloss; i += blockDim.x) ls += loss[i];
+  for (int i = threadIdx.x; i < nrows; i += blockDim.x) {
+    const int r = rank[i];
+    t1 += r < 1 ? 1.f : 0.f;
+    t3 += r < 3 ? 1.f : 0.f;
+  }
+  ls = block_sum(ls, red);
+  t1 = block_sum(t1, red);
+  t3 = block_sum(t3, red);
+  if (threadIdx.x == 0) {
+    acc[0] += (double)ls * (double)loss_scale;
+    acc[1] += (double)t1;
+    acc[2] += (double)t3;
+    acc[3] += (double)nrows;
+  }
+}
+
+void launch_metric_accum(double* acc, const float* loss, int nloss, float loss_scale, const int* rank, int nrows,
+                         hipStream_t s) {
+  metric_accum_kernel<<<1, 256, 0, s>>>(acc, loss, nloss, loss_scale, rank, nrows);
+}
+
 }  // namespace dcp

@@ -129,21 +129,35 @@ def write_label_files(data_root, split_lists: dict, out_dir="annotations"):
 
 
 class SyntheticImages(torch.utils.data.Dataset):
-    """n random uint8 HWC images of shape (size, size, 3) with labels in [0, num_classes)."""
+    """n random uint8 HWC images of shape (size, size, 3) with labels in [0, num_classes).
 
-    def __init__(self, n, size=224, num_classes=1000, seed=0, return_index=False):
+    ``learnable``: each image is its class's colour template (a coarse 4 x 4 grid of per-class
+    colours, the same for every split) plus noise, so the label is a function of the image and a
+    few epochs of training must lower the loss (the workload learning tests); otherwise pixels and
+    labels are independent (throughput runs)."""
+
+    def __init__(self, n, size=224, num_classes=1000, seed=0, return_index=False, learnable=False):
         self.n, self.size, self.num_classes, self.seed = n, size, num_classes, seed
         self.return_index = return_index
+        self.learnable = bool(learnable)
         g = np.random.RandomState(seed)
         self.labels = g.randint(0, num_classes, size=n).tolist()
         self.targets = self.labels
+        if self.learnable:
+            t = np.random.RandomState(12345).randint(0, 256, size=(num_classes, 4, 4, 3)).astype(np.float32)
+            rep = -(-size // 4)
+            self.templates = np.repeat(np.repeat(t, rep, axis=1), rep, axis=2)[:, :size, :size]
 
     def __len__(self):
         return self.n
 
     def __getitem__(self, i):
         g = np.random.RandomState(self.seed * 1000003 + i)
-        img = g.randint(0, 256, size=(self.size, self.size, 3), dtype=np.uint8)
+        if self.learnable:
+            noise = g.randint(-40, 41, size=(self.size, self.size, 3)).astype(np.float32)
+            img = np.clip(self.templates[self.labels[i]] + noise, 0, 255).astype(np.uint8)
+        else:
+            img = g.randint(0, 256, size=(self.size, self.size, 3), dtype=np.uint8)
         if self.return_index:
             return img, self.labels[i], i
         return img, self.labels[i]

@@ -31,6 +31,7 @@ import time
 import torch
 import torch.distributed as dist
 
+from ..ops import functional as Fn
 from ..optim.schedulers import LinearWarmup
 from .checkpoint import load_checkpoint, save_checkpoint
 from .logger import MetricsLogger
@@ -70,6 +71,7 @@ class ClassificationLoop:
         self.train_modules = train_modules or list(models.values())
         self.start_epoch, self.global_step, self.best = 0, 0, -1.0
         self.warmup = None
+        self._warmup_state = None  # LinearWarmup.state_dict() from a resumed checkpoint
 
     # ------------------------------------------------------------------ persistence
     def _ckpt(self, name):
@@ -89,10 +91,12 @@ class ClassificationLoop:
         self.start_epoch = int(extra.get("epoch", -1)) + 1
         self.global_step = int(extra.get("global_step", 0))
         self.best = float(extra.get("best", -1.0))
+        self._warmup_state = extra.get("warmup")
         self.logger.line(f"resumed from {path}: epoch {self.start_epoch}, step {self.global_step}")
 
     def save(self, epoch, val_top1):
         kw = dict(epoch=epoch, global_step=self.global_step, best=max(self.best, val_top1),
+                  warmup=self.warmup.state_dict() if self.warmup is not None else None,
                   config={k: v for k, v in vars(self.args).items() if isinstance(v, (int, float, str, bool, list))})
         sched = {"sched": self.scheduler} if self.scheduler is not None else None
         save_checkpoint(self._ckpt("last.pth"), self.models, {"opt": self.optimizer}, sched, **kw)
@@ -126,11 +130,20 @@ class ClassificationLoop:
             self._grapher = StepGrapher(self._train_step, warmup=2, counters=HostCounters(mods, [self.optimizer]))
 
     def _setup_warmup(self):
+        """The ramp's target is the configured ``--lr`` (or the scheduler's base LR), never the
+        optimizer's current LR: a checkpoint written mid-ramp restores a partial-ramp LR into the
+        optimizer, and ramping towards that would leave a resumed run below the uninterrupted one."""
         iters = int(getattr(self.args, "warmup_iters", 0) or 0)
         if iters > 0 and self.global_step < iters and self.warmup is None:
-            target = self.optimizer.param_groups[0]["lr"]
-            self.warmup = LinearWarmup(self.optimizer, iters, target, start_lr=1e-6)
+            target = getattr(self.args, "lr", None)
+            if target is None and self.scheduler is not None and getattr(self.scheduler, "base_lrs", None):
+                target = self.scheduler.base_lrs[0]
+            if target is None:
+                target = self.optimizer.param_groups[0].get("initial_lr", self.optimizer.param_groups[0]["lr"])
+            self.warmup = LinearWarmup(self.optimizer, iters, float(target), start_lr=1e-6)
             self.warmup.n = self.global_step  # resumed mid-warm-up: continue the ramp
+            if self._warmup_state is not None and self._warmup_state.get("iters") == iters:
+                self.warmup.load_state_dict(self._warmup_state)
 
     def _heartbeat(self, epoch):
         """Host-only (no device sync): wall time and step, so a stalled rank stops advancing."""
@@ -169,7 +182,7 @@ class ClassificationLoop:
         n_steps = len(self.train_data)
         if a.max_steps_per_epoch:
             n_steps = min(n_steps, a.max_steps_per_epoch)
-        t0 = time.time()
+        t0 = t_win = time.time()
         for i, batch in enumerate(self.train_data):
             if i >= n_steps:
                 break
@@ -192,23 +205,25 @@ class ClassificationLoop:
             if prof is not None:
                 prof.step()
             B = rank.numel()
-            step_stats = torch.stack([loss.detach().double() * B, (rank < 1).sum().double(),
-                                      (rank < 3).sum().double(), torch.tensor(float(B), device=dev,
-                                                                                dtype=torch.float64)])
-            acc += step_stats
-            win += step_stats
+            # one launch, no host->device copy (a torch.tensor(B, device=...) here synchronised the
+            # stream every step); the window folds into the epoch totals at each log point
+            Fn.metric_accum(win, loss, B, rank, B)
             self.global_step += 1
             self._heartbeat(epoch)
             if (i + 1) % a.log_interval == 0 or i + 1 == n_steps:
                 gpu_ms = None
                 if timing:
                     ev1.record()
+                acc += win
                 w = _allreduce(win.clone()).tolist()
                 if timing:
                     ev1.synchronize()
                     gpu_ms = ev0.elapsed_time(ev1) / max(win_steps, 1)
+                now = time.time()
+                win_ips = win_steps * B * self.rt.world / max(now - t_win, 1e-9)  # window wall rate (synced above)
+                t_win = now
                 win_steps = 0
-                dt = time.time() - t0
+                dt = now - t0
                 eta = dt / (i + 1) * (n_steps - i - 1)
                 lr = self.optimizer.param_groups[0]["lr"]
                 self.logger.progress(
@@ -217,7 +232,8 @@ class ClassificationLoop:
                     f"{(i + 1) * B * self.rt.world / max(dt, 1e-9):.0f} img/s "
                     f"eta {eta:.0f}s")
                 self.logger.log("train_iter", epoch=epoch, step=self.global_step, loss=w[0] / max(w[3], 1),
-                                top1=w[1] / max(w[3], 1), top3=w[2] / max(w[3], 1), lr=lr, gpu_ms_per_step=gpu_ms)
+                                top1=w[1] / max(w[3], 1), top3=w[2] / max(w[3], 1), lr=lr, gpu_ms_per_step=gpu_ms,
+                                img_per_s=win_ips)
                 win.zero_()
         if prof is not None:
             prof.__exit__(None, None, None)
@@ -248,9 +264,7 @@ class ClassificationLoop:
             left -= k
             if k <= 0:
                 continue
-            loss_rows, rank = loss_rows[:k], rank[:k]
-            acc += torch.stack([loss_rows.double().sum(), (rank < 1).sum().double(), (rank < 3).sum().double(),
-                                torch.tensor(float(k), device=dev, dtype=torch.float64)])
+            Fn.metric_accum(acc, loss_rows[:k], 1.0, rank, k)
         tot = _allreduce(acc).tolist()
         n = max(tot[3], 1)
         return {"loss": tot[0] / n, "top1": tot[1] / n, "top3": tot[2] / n, "count": tot[3]}

@@ -54,10 +54,11 @@ def _datasets(args):
     if args.data == "synthetic":
         n_tr, n_va = args.synthetic_train_size, args.synthetic_val_size
         size = args.image_size if args.transform != "baseline" or args.image_size != 224 else 224
+        learn = getattr(args, "synthetic_learnable", False)
         tr = SyntheticImages(n_tr, size=size, num_classes=args.num_classes, seed=args.seed,
-                             return_index=args.workload == "plc")
+                             return_index=args.workload == "plc", learnable=learn)
         va = SyntheticImages(n_va, size=size, num_classes=args.num_classes, seed=args.seed + 1,
-                             return_index=args.workload == "plc")
+                             return_index=args.workload == "plc", learnable=learn)
         return tr, va
     if args.data == "shards":
         from ..data.shards import ShardDataset
@@ -116,7 +117,28 @@ def _shard_loaders(args, rt, tr, va, tr_s, va_s, mean, std, cpad, s2d, drop_last
     return tr_l, va_l
 
 
+def _device_synthetic(args, rt: Runtime):
+    """--data synthetic-device: on-device uint8 batches (a pool of two per split, different per rank),
+    normalised by the input kernel every step -- the input bench.py times, so a main.py run measures
+    the training loop itself."""
+    from ..data import SyntheticLoader
+
+    if args.workload == "plc":
+        raise ValueError("--data synthetic-device has no per-sample dataset labels (PLC relabels its dataset)")
+    mean, std = norm_stats(args.dataset if "CIFAR" in args.dataset.upper() else "imagenet")
+    cpad = 3 if str(args.model).startswith("tresnet") else 8
+    s2d = 4 if str(args.model).startswith("tresnet") else str(args.model).startswith(("resnet", "resnext"))
+    kw = dict(size=args.image_size, num_classes=args.num_classes, device=rt.device, mean=mean, std=std, cpad=cpad,
+              s2d=s2d)
+    B = args.batchsize
+    tr = SyntheticLoader(B, max(1, args.synthetic_train_size // B), seed=args.seed + 17 * rt.rank, **kw)
+    va = SyntheticLoader(B, max(1, args.synthetic_val_size // B), seed=args.seed + 17 * rt.rank + 7, **kw)
+    return tr, va, None, None
+
+
 def build_data(args, rt: Runtime, drop_last_train=False):
+    if args.data == "synthetic-device":
+        return _device_synthetic(args, rt)
     tr, va = _datasets(args)
     if args.workload == "plc" and args.data != "synthetic" and not isinstance(tr, ListDataset):
         tr, va = WithIndex(tr), WithIndex(va)

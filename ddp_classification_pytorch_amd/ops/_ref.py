@@ -534,6 +534,12 @@ def xent_fwd(logits, labels, C, smoothing):
     return loss, rank
 
 
+def metric_accum(acc, loss, loss_scale, rank, nrows):
+    r = rank[:nrows]
+    acc += torch.stack([loss.double().sum() * loss_scale, (r < 1).sum().double(), (r < 3).sum().double(),
+                        torch.full((), float(nrows), dtype=torch.float64, device=acc.device)])
+
+
 def xent_bwd(logits, labels, C, grad_out, scale, smoothing, out_bf16):
     B, ld = logits.shape
     x = _f(logits)[:, :C]

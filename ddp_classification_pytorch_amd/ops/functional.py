@@ -925,9 +925,19 @@ _EVAL_COEFF = weakref.WeakKeyDictionary()
 def bn_eval_coefficients(bn):
     """(mean, invstd, scale, shift) of a BatchNorm2d's running statistics, cached until any of the
     four source tensors changes (frozen BN recomputes nothing per step; a HIP-graph replay reads the
-    same cached tensors)."""
+    same cached tensors).
+
+    On the GPU two writers change those tensors without bumping ``_version``: the BN statistics
+    kernels update running_mean / running_var in place, and the fused optimizers update gamma /
+    beta through pointer tables.  So the key also carries the weight generation (bumped by every
+    optimizer step and state load) and the BN's training-forward count (``_nbt_pending`` grows by
+    one per statistics forward and is flushed into ``num_batches_tracked``, whose ``_version`` the
+    flush bumps: the pair never repeats)."""
     g, b, rm, rv = bn.weight, bn.bias, bn.running_mean, bn.running_var
     key = tuple((t._version, t.data_ptr()) if t is not None else None for t in (g, b, rm, rv)) + (bn.eps,)
+    nbt = getattr(bn, "num_batches_tracked", None)
+    trainable = any(t is not None and t.requires_grad for t in (g, b))  # frozen BN: no per-step refresh
+    key += (_GEN[0] if trainable else None, getattr(bn, "_nbt_pending", 0), nbt._version if nbt is not None else None)
     hit = _EVAL_COEFF.get(bn)
     if hit is not None and hit[0] == key:
         return hit[1]
@@ -1267,6 +1277,18 @@ def cross_entropy(logits, labels, num_classes=None, smoothing=0.0, reduction="me
 
 
 @torch.no_grad()
+def metric_accum(acc: torch.Tensor, loss: torch.Tensor, loss_scale: float, rank: torch.Tensor, nrows: int):
+    """acc (fp64 [4], on the device) += [loss_scale * sum(loss), #(rank < 1), #(rank < 3), nrows] over
+    ``rank[:nrows]``: the loops' per-step top-1 / top-3 / loss bookkeeping as ONE launch, with the
+    row count a kernel argument (no host->device copy, so no stream sync)."""
+    loss = loss.detach().reshape(-1)
+    rank = rank.detach().reshape(-1)
+    if rank.dtype != torch.int32:
+        rank = rank.int()
+    K(acc).metric_accum(acc, loss.contiguous(), float(loss_scale), rank.contiguous(), int(nrows))
+    return acc
+
+
 def cross_entropy_rows(logits, labels, num_classes=None):
     """Per-sample CE loss and label rank (evaluation; no autograd)."""
     return K(logits).xent_fwd(logits, labels, num_classes or logits.shape[1], 0.0)
@@ -1529,7 +1551,9 @@ class _PrefixMask(Function):
 
 def nested_mask(feature, k_index):
     """feature * 1[:k+1] (nested dropout, NESTED/train.py:247-250); k_index int."""
-    keep = torch.tensor([int(k_index) + 1], dtype=torch.int32, device=feature.device)
+    # a fill kernel with K as its argument: torch.tensor(..., device=) would be a pageable
+    # host->device copy, which synchronises the stream every step
+    keep = torch.full((1,), int(k_index) + 1, dtype=torch.int32, device=feature.device)
     return _PrefixMask.apply(feature, keep)
 
 

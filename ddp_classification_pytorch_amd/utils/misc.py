@@ -73,7 +73,7 @@ def accuracy_from_rank(rank: torch.Tensor, topk=(1, 3)):
 
 
 def format_time(seconds: float) -> str:
-    """NESTED/utils.py:102-132 style: '1D2h3m4s5ms'."""
+    """NESTED/utils.py:102-132: the two leading non-zero units, e.g. "1D2h", "3m4s", "5ms"."""
     days = int(seconds / 3600 / 24)
     seconds -= days * 3600 * 24
     hours = int(seconds / 3600)
@@ -84,7 +84,7 @@ def format_time(seconds: float) -> str:
     millis = int((seconds - secondsf) * 1000)
     out, n = "", 0
     for v, u in ((days, "D"), (hours, "h"), (minutes, "m"), (secondsf, "s"), (millis, "ms")):
-        if v > 0 and n <= 2:
+        if v > 0 and n < 2:  # at most two units, as the reference (its counter starts at 1)
             out += f"{v}{u}"
             n += 1
     return out or "0ms"

@@ -201,3 +201,13 @@ def test_arcfacenet_and_newfc_heads():
     assert torch.allclose(out, torch.log(num / den), atol=1e-5)
     fc = NewFC(5, 3)
     assert torch.allclose(fc(x), F.linear(x, fc.fc.weight, fc.fc.bias), atol=1e-6)
+
+
+def test_format_time_two_units_like_reference():
+    """NESTED/utils.py:102-132 emits at most the two leading non-zero units."""
+    from ddp_classification_pytorch_amd.utils.misc import format_time
+
+    assert format_time(90061.5) == "1D1h"          # 1 day 1 h 1 min 1.5 s
+    assert format_time(3723.25) == "1h2m"
+    assert format_time(4.25) == "4s250ms"
+    assert format_time(0.0) == "0ms"

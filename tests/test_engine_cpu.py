@@ -103,3 +103,58 @@ def test_autotune_defaults_follow_reference_cudnn_benchmark():
         assert parse_args(["--workload", w]).autotune is False
     assert parse_args(["--workload", "baseline", "--no-autotune"]).autotune is False
     assert parse_args(["--workload", "cdr", "--autotune"]).autotune is True
+
+
+def test_resume_mid_warmup_is_equivalent(tmp_path):
+    """A checkpoint written while the LR ramp is still running (warm-up longer than an epoch)
+    restores a partial-ramp LR into the optimizer; the resumed run must still ramp to --lr and
+    end where the uninterrupted run ends."""
+    base = ["--workload", "baseline", "--model", "cifar_resnet18", "--epochs", "3", "--optimizer", "SGD",
+            "--lr", "0.05", "--warmup-iters", "7"] + SYN
+    torch.manual_seed(0)
+    entry.main(base + ["--out-dir", str(tmp_path / "ref")])
+    ref = torch.load(tmp_path / "ref" / "last.pth", weights_only=True)
+    with pytest.raises(InjectedFailure):
+        entry.main(base + ["--out-dir", str(tmp_path / "ft"), "--fail-at-step", "5"])  # epoch 2, step 5 of 7
+    mid = torch.load(tmp_path / "ft" / "last.pth", weights_only=True)
+    assert mid["warmup"]["n"] == 4 and mid["optimizers"]["opt"]["param_groups"][0]["lr"] < 0.05
+    entry.main(base + ["--out-dir", str(tmp_path / "ft"), "--resume", str(tmp_path / "ft" / "last.pth")])
+    got = torch.load(tmp_path / "ft" / "last.pth", weights_only=True)
+    assert got["optimizers"]["opt"]["param_groups"][0]["lr"] == pytest.approx(
+        ref["optimizers"]["opt"]["param_groups"][0]["lr"])
+    for k, v in ref["models"]["model"].items():
+        if v.dtype.is_floating_point:
+            assert torch.allclose(v, got["models"]["model"][k], atol=1e-5), k
+
+
+def test_autotune_env_switch_applies_without_flag(monkeypatch):
+    from ddp_classification_pytorch_amd.config import parse_args
+
+    monkeypatch.setenv("DCP_AUTOTUNE", "1")
+    assert parse_args(["--workload", "cdr"]).autotune is True
+    monkeypatch.setenv("DCP_AUTOTUNE", "0")
+    assert parse_args(["--workload", "baseline"]).autotune is False
+    assert parse_args(["--workload", "baseline", "--autotune"]).autotune is True  # the flag wins
+
+
+@pytest.mark.parametrize("workload", ["baseline", "cdr"])
+def test_workload_learns_cpu(tmp_path, workload):
+    """Plumbing half of the GPU learning tests: class-carrying synthetic images, 3 epochs, the
+    train loss falls by at least 30 %."""
+    out = tmp_path / "o"
+    entry.main(["--workload", workload, "--model", "resnet18", "--data", "synthetic", "--synthetic-learnable",
+                "--device", "cpu", "--batchsize", "16", "--synthetic-train-size", "64", "--synthetic-val-size", "16",
+                "--epochs", "3", "--out-dir", str(out), "--image-size", "64", "--num-classes", "10", "--dataset", "food",
+                "--workers", "0", "--log-interval", "4", "--lr", "0.05"])
+    losses = [json.loads(x)["loss"] for x in open(out / "metrics.jsonl") if '"train_iter"' in x]
+    assert len(losses) == 3 and losses[-1] <= 0.7 * losses[0], losses
+
+
+def test_device_synthetic_data_runs(tmp_path):
+    """--data synthetic-device (bench.py's on-device input) through main.py."""
+    out = tmp_path / "o"
+    entry.main(["--workload", "baseline", "--model", "resnet18", "--data", "synthetic-device", "--device", "cpu",
+                "--batchsize", "8", "--synthetic-train-size", "16", "--synthetic-val-size", "8", "--epochs", "1",
+                "--out-dir", str(out), "--dataset", "CIFAR10", "--log-interval", "1"])
+    recs = [json.loads(x) for x in open(out / "metrics.jsonl") if '"train_iter"' in x]
+    assert len(recs) == 2 and all(r["img_per_s"] > 0 for r in recs)

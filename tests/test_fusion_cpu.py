@@ -339,3 +339,33 @@ def test_tresnet_inplace_abn_matches_stored_input_backward(train):
     (l1, g1), (l0, g0) = out
     assert abs(l1 - l0) < 1e-5
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-4
+
+
+def test_eval_coefficient_cache_sees_untracked_bn_updates():
+    """On the GPU the BN statistics kernels rewrite running_mean / running_var and the fused
+    optimizers rewrite gamma / beta without bumping ``_version``.  The eval-coefficient cache must
+    still refresh: after a training-stats forward (``_nbt_pending``) and after an optimizer step
+    (weight generation).  ``.data`` writes reproduce the version-less update on the CPU."""
+    from ddp_classification_pytorch_amd.models.layers import BatchNorm2d
+
+    bn = BatchNorm2d(8)
+    bn.eval()
+    c0 = [t.clone() for t in Fn.bn_eval_coefficients(bn)]
+    bn.running_mean.data.add_(1.0)  # a statistics kernel: no version bump
+    bn._nbt_pending += 1            # ... during a training forward, which counts itself
+    c1 = Fn.bn_eval_coefficients(bn)
+    assert not torch.allclose(c0[0], c1[0])
+    assert torch.allclose(c1[0], bn.running_mean)
+    bn.flush_batches_tracked()      # pending -> num_batches_tracked: the key must stay fresh
+    c1b = Fn.bn_eval_coefficients(bn)
+    assert torch.allclose(c1b[0], bn.running_mean)
+    bn.weight.data.mul_(2.0)        # a fused optimizer step: pointer-table update, no version bump
+    Fn.bump_weight_generation()     # ... which every optimizer step does
+    c2 = Fn.bn_eval_coefficients(bn)
+    assert torch.allclose(c2[2], c1b[2] * 2.0)
+    # frozen BN (gamma / beta without grad): nothing changes, the cached tensors are reused
+    bn.weight.requires_grad_(False)
+    bn.bias.requires_grad_(False)
+    c3 = Fn.bn_eval_coefficients(bn)
+    Fn.bump_weight_generation()
+    assert Fn.bn_eval_coefficients(bn)[2] is c3[2]

@@ -237,6 +237,6 @@ def test_torchvision_format_weights_load(tmp_path):
     torch.save(sd, f)
     torch.manual_seed(3)
     dst = build_model("resnet18", num_classes=0)
-    missing, unexpected = load_pretrained(dst, str(f))
+    missing, unexpected, _ = load_pretrained(dst, str(f))
     for k, v in src.state_dict().items():
         assert torch.equal(dst.state_dict()[k], v), k
