@@ -66,7 +66,14 @@ def parse(argv=None):
                     help="N > 1: skip the second, SyncBN-timed phase")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
-                    help="DDP gradient all-reduce precision (bf16 = bf16_compress_hook: half the xGMI bytes)")
+                    help="gradient all-reduce precision (bf16: half the xGMI bytes; bucket engine: bf16 buckets, "
+                         "torch engine: bf16_compress_hook)")
+    ap.add_argument("--ddp-engine", default="dcp", choices=["dcp", "torch"],
+                    help="dcp: this framework's bucket engine (optimizer fused per bucket, HIP-graph capturable); "
+                         "torch: DistributedDataParallel's C++ Reducer")
+    ap.add_argument("--telemetry-steps", type=int, default=5,
+                    help="N > 1, dcp engine: untimed steps after the timed phase that record per-bucket HIP events "
+                         "(exposed communication per rank)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--graph", action="store_true",
@@ -175,14 +182,18 @@ def main(argv=None):
     torch.manual_seed(1234 + rank)
     model = build_bench_model(a).to(dev)
     if world > 1:
-        model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb)
+        model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb, engine=a.ddp_engine,
+                              comm_dtype=torch.bfloat16 if a.grad_comm == "bf16" else torch.float32)
         # created collectively now (every rank, same order) so the SyncBN phase can switch to it
         bn_group = pddp.bn_process_group()
-        if a.grad_comm == "bf16":
+        if a.grad_comm == "bf16" and a.ddp_engine == "torch":
             from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
 
             model.register_comm_hook(None, default_hooks.bf16_compress_hook)
     opt = FusedSGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+    # bucket engine: the SGD kernel runs per gradient bucket right behind its all-reduce (its
+    # step() after backward is then a no-op); torch DDP / one GPU: one launch after backward
+    pddp.attach_optimizer(model, opt)
 
     B, S = a.batch, a.image_size
     g = torch.Generator(device=dev)
@@ -207,11 +218,11 @@ def main(argv=None):
 
     run = step
     if a.graph:
-        if world > 1:
-            raise SystemExit("--graph is single-GPU only (DDP reducer hooks are not captured)")
+        if world > 1 and a.ddp_engine != "dcp":
+            raise SystemExit("--graph with N > 1 needs the bucket engine (torch DDP's reducer is not capturable)")
         from ddp_classification_pytorch_amd.engine.graph import GraphedStep
 
-        graphed = GraphedStep(step, warmup=max(1, a.warmup))  # warm-up steps run inside
+        graphed = GraphedStep(step, warmup=max(1, a.warmup), distributed=world > 1)  # warm-up steps run inside
         run = graphed
     else:
         for _ in range(a.warmup):
@@ -251,6 +262,27 @@ def main(argv=None):
         with open(os.path.join(a.profile_dir, "bench_profile.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     dt, per_rank = gather_max(dt)
+    comm = None
+    if world > 1 and a.ddp_engine == "dcp" and a.telemetry_steps > 0:
+        # untimed: per-step HIP events around the bucket engine (backward end on the compute stream,
+        # first bucket start / last bucket done on the communication stream), eager steps
+        red = model.reducer
+        red.telemetry = True
+        for _ in range(a.telemetry_steps):
+            step()
+        red.telemetry = False
+        summ = red.telemetry_summary() or {}
+        t = torch.tensor([summ.get("exposed_comm_ms", 0.0), summ.get("comm_span_ms", 0.0)], device=dev,
+                         dtype=torch.float64)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        comm = {"engine": "dcp", "buckets": summ.get("buckets"), "bucket_mb": summ.get("bucket_mb"),
+                "optimizer_per_bucket": True, "telemetry_steps": summ.get("steps"),
+                "exposed_comm_ms_per_rank": [round(float(v[0]), 4) for v in allt],
+                "comm_span_ms_per_rank": [round(float(v[1]), 4) for v in allt],
+                "grad_comm": a.grad_comm}
+    elif world > 1:
+        comm = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
     sync = None
     if world > 1 and not a.syncbn and a.syncbn_phase and not a.graph:
         # second phase: the reference's SyncBN (BASELINE/main.py:148) on the dedicated BN communicator
@@ -284,6 +316,7 @@ def main(argv=None):
             "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
             "syncbn_value": sync["value"] if sync else None,
             "syncbn_ms_per_step": sync["ms_per_step"] if sync else None,
+            "comm": comm,
             "config": {
                 "model": a.model,
                 "global_batch": B * world,
@@ -296,6 +329,7 @@ def main(argv=None):
                 "autotune": bool(autotune),
                 "syncbn": bool(a.syncbn),
                 "grad_comm": a.grad_comm,
+                "ddp_engine": a.ddp_engine if world > 1 else None,
                 "bucket_cap_mb": a.bucket_cap_mb,
                 "optimizer": "fused SGD momentum 0.9 wd 1e-4",
                 "final_loss": round(loss_v, 4),

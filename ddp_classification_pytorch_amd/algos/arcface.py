@@ -22,7 +22,7 @@ from ..models import build_model
 from ..models.heads import ArcMarginProduct, MLPHead
 from ..ops import functional as Fn
 from ..optim import StepLR, build_optimizer
-from ..parallel.ddp import wrap_ddp
+from ..parallel.ddp import attach_optimizer, wrap_ddp
 
 
 class ArcFaceModel(nn.Module):
@@ -58,6 +58,7 @@ def run(args):
     name = args.optimizer.lower()
     wd = args.weight_decay if name == "sgd" else 0.0  # ARCFACE/arc_main.py:249-253
     opt = build_optimizer(name, model.parameters(), args.lr, args.momentum, wd)
+    attach_optimizer(net, opt)
     sched = StepLR(opt, step_size=args.step_size, gamma=args.gamma)
 
     def fwd_train(batch):

@@ -14,7 +14,7 @@ from ..models import build_model
 from ..models.heads import ClassifierModel, MLPHead
 from ..ops import functional as Fn
 from ..optim import StepLR, build_optimizer
-from ..parallel.ddp import wrap_ddp
+from ..parallel.ddp import attach_optimizer, wrap_ddp
 
 
 def build_classifier(args, log_softmax=False):
@@ -43,6 +43,7 @@ def run(args):
                    first_bucket_mb=args.first_bucket_mb)
     opt = build_optimizer(args.optimizer, model.parameters(), args.lr, args.momentum, args.weight_decay,
                           args.nesterov)
+    attach_optimizer(net, opt)  # multi-GPU: the step runs per gradient bucket behind its all-reduce
     sched = StepLR(opt, step_size=args.step_size, gamma=args.gamma)
     C = args.num_classes
 

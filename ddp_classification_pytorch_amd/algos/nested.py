@@ -34,7 +34,7 @@ from ..models.heads import NetClassifier
 from ..models.nested import NetFeat
 from ..ops import functional as Fn
 from ..optim import FusedSGD, MultiStepLR
-from ..parallel.ddp import wrap_ddp
+from ..parallel.ddp import attach_optimizer, wrap_ddp
 from ..utils.misc import AverageMeter, ProgressBar
 
 
@@ -130,6 +130,8 @@ def run(args):
     ddp_kw = dict(syncbn=False, bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
     feat_net = wrap_ddp(net_feat, rt.local_rank, **ddp_kw)
     cls_net = wrap_ddp(net_cls, rt.local_rank, **ddp_kw)
+    attach_optimizer(feat_net, opt_feat)
+    attach_optimizer(cls_net, opt_cls)
     rng = np.random.RandomState(args.seed + rt.rank)
     bar = ProgressBar(stream=None) if rt.is_main else None
 

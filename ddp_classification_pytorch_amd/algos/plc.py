@@ -29,7 +29,7 @@ from ..engine.loop import ClassificationLoop
 from ..engine.runtime import build_data, setup
 from ..ops import functional as Fn
 from ..optim import FusedSGD
-from ..parallel.ddp import wrap_ddp
+from ..parallel.ddp import attach_optimizer, wrap_ddp
 
 
 def label_noise(targets, eta, noise_type=0, factor=1.2, rng=None):
@@ -178,6 +178,7 @@ def run(args):
         logger.line(f"Corrupted Size {changed} | Noisy Level {100.0 * changed / max(n, 1):.3f}%")
         labels = noisy
     delta = args.plc_delta
+    attach_optimizer(net, opt)  # after the posterior-estimation phase, which steps its own optimizer
 
     def fwd_train(batch):
         x, idx = batch[0], batch[2]

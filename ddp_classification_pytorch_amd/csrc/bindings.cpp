@@ -1425,6 +1425,15 @@ Tensor arcface_bwd(const Tensor& cosv, const Tensor& labels, int64_t C, double s
 // ---------------------------------------------------------------------------
 // optimizers (multi-tensor). table: int64 [n,6] = (p, g, s1, s2, shadow, numel); chunks int32 [k,2]
 // ---------------------------------------------------------------------------
+// table: MTEntry rows (dst, src, -, -, -, n); mode bit 0 = src bf16, bit 1 = dst bf16
+void mt_copy(const Tensor& table, const Tensor& chunks, double scale, int64_t mode) {
+  CHECK_DEV(table);
+  CHECK_DEV(chunks);
+  dcp::launch_mt_copy(reinterpret_cast<const dcp::MTEntry*>(table.data_ptr()),
+                      reinterpret_cast<const int2*>(chunks.data_ptr()), chunks.size(0), (float)scale, (int)mode,
+                      cur_stream());
+}
+
 void mt_sgd(const Tensor& table, const Tensor& chunks, double lr, double momentum, double dampening, double wd,
             bool nesterov, bool first, double grad_scale) {
   CHECK_DEV(table);
@@ -1628,6 +1637,7 @@ TORCH_LIBRARY(dcp, m) {
       "decoupled, float grad_scale, Tensor? step_dev=None) -> ()",
       &mt_adam);
   m.def("cdr_threshold(Tensor table, Tensor chunks, Tensor state) -> Tensor", &cdr_threshold);
+  m.def("mt_copy(Tensor table, Tensor chunks, float scale, int mode) -> ()", &mt_copy);
   m.def(
       "conv_fwd_affine(Tensor x, Tensor w, int stride, int pad, Tensor scale, Tensor shift, int act, float slope, "
       "Tensor? res) -> Tensor",

@@ -222,6 +222,8 @@ struct AdamHyper {
   int decoupled;
   const int* step_dev;  // optional device step count: bc1/bc2 computed in-kernel from it
 };
+// mode: bit 0 = source bf16, bit 1 = destination bf16 (MTEntry.p = destination, .g = source)
+void launch_mt_copy(const MTEntry* tab, const int2* chunks, int nchunks, float scale, int mode, hipStream_t s);
 void launch_mt_sgd(const MTEntry* tab, const int2* chunks, int nchunks, SgdHyper h, hipStream_t s);
 void launch_mt_adam(const MTEntry* tab, const int2* chunks, int nchunks, AdamHyper h, hipStream_t s);
 void launch_cdr_threshold(const MTEntry* tab, const int2* chunks, int nchunks, uint32_t* state, uint32_t* hist,

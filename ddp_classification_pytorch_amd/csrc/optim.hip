@@ -140,6 +140,40 @@ __global__ void __launch_bounds__(256) cdr_mask_kernel(const MTEntry* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// Multi-tensor scaled copy: dst_t[i] = src_t[i] * scale for every table entry (MTEntry.p = dst,
+// MTEntry.g = src, raw pointers; SRC_BF16 / DST_BF16 pick the element types).  The gradient
+// bucket engine (parallel/reducer.py) packs a bucket's parameter gradients into its flat
+// all-reduce buffer with one launch (pre-divided by the world size; optionally rounded to bf16
+// for a half-size all-reduce) and, for a bf16 bucket, unpacks the reduced values into the fp32
+// gradient views in one launch.
+template <bool SRC_BF16, bool DST_BF16>
+__global__ void __launch_bounds__(256) mt_copy_kernel(const MTEntry* __restrict__ tab, const int2* __restrict__ chunks,
+                                                      float scale) {
+  const int2 ck = chunks[blockIdx.x];
+  const MTEntry e = tab[ck.x];
+  const int64_t base = (int64_t)ck.y * kChunk;
+  const int64_t end = min(e.n, base + kChunk);
+  const void* src = (const void*)e.g;
+  void* dst = (void*)e.p;
+  for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
+    const float v = (SRC_BF16 ? bf2f(((const bf16*)src)[i]) : ((const float*)src)[i]) * scale;
+    if (DST_BF16)
+      ((bf16*)dst)[i] = f2bf(v);
+    else
+      ((float*)dst)[i] = v;
+  }
+}
+
+void launch_mt_copy(const MTEntry* tab, const int2* chunks, int nchunks, float scale, int mode, hipStream_t s) {
+  if (!nchunks) return;
+  switch (mode & 3) {
+    case 0: hipLaunchKernelGGL((mt_copy_kernel<false, false>), dim3(nchunks), dim3(256), 0, s, tab, chunks, scale); break;
+    case 1: hipLaunchKernelGGL((mt_copy_kernel<true, false>), dim3(nchunks), dim3(256), 0, s, tab, chunks, scale); break;
+    case 2: hipLaunchKernelGGL((mt_copy_kernel<false, true>), dim3(nchunks), dim3(256), 0, s, tab, chunks, scale); break;
+    default: hipLaunchKernelGGL((mt_copy_kernel<true, true>), dim3(nchunks), dim3(256), 0, s, tab, chunks, scale); break;
+  }
+}
+
 void launch_mt_sgd(const MTEntry* tab, const int2* chunks, int nchunks, SgdHyper h, hipStream_t s) {
   if (nchunks) hipLaunchKernelGGL(mt_sgd_kernel, dim3(nchunks), dim3(256), 0, s, tab, chunks, h);
 }

@@ -25,7 +25,9 @@ from ..ops import functional as Fn
 
 
 def _unwrap(m):
-    return m.module if isinstance(m, torch.nn.parallel.DistributedDataParallel) else m
+    from ..parallel.reducer import GradSyncDDP
+
+    return m.module if isinstance(m, (torch.nn.parallel.DistributedDataParallel, GradSyncDDP)) else m
 
 
 def rng_state():

@@ -11,8 +11,10 @@ graph pool.
 
 Constraints (checked or documented): inputs and labels must live in the static tensors the
 step closes over (copy new batches into them); hyper-parameters baked into kernel arguments
-(the learning rate) are those at capture time -- recapture after changing them; single
-process (DDP's reducer hooks are not captured here).
+(the learning rate) are those at capture time -- recapture after changing them.  Multi-process
+steps are capturable with this framework's bucket engine (parallel/reducer.py: its packing,
+all-reduces, per-bucket optimizer and the SyncBN collectives are all stream-ordered launches);
+torch's DistributedDataParallel Reducer is not.
 
 Host-side counters: a replay runs no Python, so counters the step advances on the host --
 BatchNorm2d's pending ``num_batches_tracked`` and FusedAdam's ``state["step"]`` -- would
@@ -67,9 +69,11 @@ class GraphedStep:
     (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
     returns the captured step's output tensors (overwritten by every replay)."""
 
-    def __init__(self, step_fn, warmup: int = 3, device=None, counters: HostCounters = None):
-        if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1:
-            raise RuntimeError("GraphedStep captures single-process steps (DDP reducer hooks are not graph-safe)")
+    def __init__(self, step_fn, warmup: int = 3, device=None, counters: HostCounters = None,
+                 distributed: bool = False):
+        if torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1 and not distributed:
+            raise RuntimeError("GraphedStep: a multi-process step is capturable only through the bucket engine "
+                               "(pass distributed=True for a GradSyncDDP model; torch DDP's reducer is not)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))

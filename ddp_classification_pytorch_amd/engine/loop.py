@@ -123,7 +123,8 @@ class ClassificationLoop:
         after the LR warm-up (its steps run eagerly: the LR changes every iteration)."""
         a = self.args
         self._grapher = None
-        if getattr(a, "graph", False) and self.rt.device.type == "cuda" and self.rt.world == 1:
+        graph_safe = not any(isinstance(m, torch.nn.parallel.DistributedDataParallel) for m in self.train_modules)
+        if getattr(a, "graph", False) and self.rt.device.type == "cuda" and (self.rt.world == 1 or graph_safe):
             from .graph import HostCounters, StepGrapher
 
             mods = list(self.models.values()) + list(self.train_modules)

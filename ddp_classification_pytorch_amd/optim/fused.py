@@ -70,6 +70,13 @@ class FusedSGD(torch.optim.Optimizer):
                         nesterov=nesterov, grad_scale=grad_scale)
         super().__init__(params, defaults)
         self._tables = {}
+        self._reducer_stepped = False
+
+    def mark_stepped_by_reducer(self):
+        """The bucket engine (parallel/reducer.py) already applied this step per bucket: the next
+        ``step()`` is a no-op (the training loop's call after backward)."""
+        self._reducer_stepped = True
+        Fn.bump_weight_generation()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -77,8 +84,22 @@ class FusedSGD(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._reducer_stepped:
+            self._reducer_stepped = False
+            return loss
+        self._step_subset(None)
+        Fn.bump_weight_generation()
+        return loss
+
+    @torch.no_grad()
+    def step_params(self, params):
+        """Update only ``params`` (one bucket, right behind its all-reduce); every group's
+        hyper-parameters apply to its own members.  The caller bumps the weight generation."""
+        self._step_subset({id(p) for p in params})
+
+    def _step_subset(self, ids):
         for gi, group in enumerate(self.param_groups):
-            params = [p for p in group["params"] if p.grad is not None]
+            params = [p for p in group["params"] if p.grad is not None and (ids is None or id(p) in ids)]
             if not params:
                 continue
             mom = group["momentum"]
@@ -94,8 +115,6 @@ class FusedSGD(torch.optim.Optimizer):
             for first, sub in ((True, [p for p in params if p in fresh]), (False, [p for p in params if p not in fresh])):
                 if sub:
                     self._update(gi, group, sub, first)
-        Fn.bump_weight_generation()
-        return loss
 
     def _update(self, gi, group, params, first):
         mom = group["momentum"]
@@ -109,7 +128,8 @@ class FusedSGD(torch.optim.Optimizer):
                 buf = self.state[p].get("momentum_buffer")
                 entries.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr() if buf is not None else 0, 0, 0,
                                 p.numel()))
-            table, chunks = self._tables.setdefault((gi, first), _TableCache()).get(entries, params[0].device)
+            key = (gi, first, len(params), params[0].data_ptr())  # one table per bucket subset
+            table, chunks = self._tables.setdefault(key, _TableCache()).get(entries, params[0].device)
             _ext.hip_ops().mt_sgd(table, chunks, group["lr"], mom, group["dampening"], group["weight_decay"],
                                   group["nesterov"], first, group["grad_scale"])
             return
@@ -136,6 +156,13 @@ class FusedAdam(torch.optim.Optimizer):
         self._tables = {}
         self._dsteps = {}        # launch key -> [device int32 step, host mirror, params]
         self._captured = None    # launch keys of the step being / last captured into a HIP graph
+        self._reducer_stepped = False
+        self._bucket_capture_open = False
+
+    def mark_stepped_by_reducer(self):
+        self._reducer_stepped = True
+        self._bucket_capture_open = False
+        Fn.bump_weight_generation()
 
     def on_graph_replay(self):
         """A captured step was replayed: its kernels advanced the device step counters; advance the
@@ -158,11 +185,27 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._reducer_stepped:
+            self._reducer_stepped = False
+            return loss
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         if capturing:
             self._captured = []
+        self._step_subset(None)
+        Fn.bump_weight_generation()
+        return loss
+
+    @torch.no_grad()
+    def step_params(self, params):
+        """Update only ``params`` (one bucket of the bucket engine); see FusedSGD.step_params."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and not self._bucket_capture_open:
+            self._captured = []  # the first bucket of a captured backward: this capture's launch keys
+            self._bucket_capture_open = True
+        self._step_subset({id(p) for p in params})
+
+    def _step_subset(self, ids):
         for gi, group in enumerate(self.param_groups):
-            params = [p for p in group["params"] if p.grad is not None]
+            params = [p for p in group["params"] if p.grad is not None and (ids is None or id(p) in ids)]
             if not params:
                 continue
             for p in params:
@@ -178,8 +221,6 @@ class FusedAdam(torch.optim.Optimizer):
                 by_step.setdefault(self.state[p]["step"], []).append(p)
             for step, sub in sorted(by_step.items()):
                 self._update(gi, group, sub, step)
-        Fn.bump_weight_generation()
-        return loss
 
     def _update(self, gi, group, params, step):
         b1, b2 = group["betas"]

@@ -82,10 +82,18 @@ def convert_sync_batchnorm(model: nn.Module, process_group=None) -> nn.Module:
     return model
 
 
+DEFAULT_ENGINE = os.environ.get("DCP_DDP_ENGINE", "dcp")
+
+
 def wrap_ddp(model: nn.Module, local_rank: int = None, syncbn: bool = False, bucket_cap_mb: float = 25.0,
              first_bucket_mb: float = 4.0, find_unused: bool = False, static_graph: bool = False,
-             force: bool = False):
-    """DDP over the default group (RCCL on GPU, gloo on CPU).
+             force: bool = False, engine: str = None, comm_dtype=torch.float32, telemetry: bool = False):
+    """Data parallelism over the default group (RCCL on GPU, gloo on CPU).
+
+    ``engine="dcp"`` (default; ``DCP_DDP_ENGINE``): this framework's bucket engine
+    (:class:`parallel.reducer.GradSyncDDP`): graph-capturable, optimizer fusable per bucket
+    (:func:`attach_optimizer`), bf16 all-reduce with ``comm_dtype=torch.bfloat16``.
+    ``engine="torch"``: torch's ``DistributedDataParallel`` (C++ Reducer), configured as below.
 
     Bucket limits: torch's Reducer honours a separate first-bucket limit only when the
     DDP constructor sees ``bucket_cap_mb=None`` (its 25 MiB default,
@@ -98,6 +106,15 @@ def wrap_ddp(model: nn.Module, local_rank: int = None, syncbn: bool = False, buc
         convert_sync_batchnorm(model)
     if not force and (not dist.is_initialized() or dist.get_world_size() == 1 and not syncbn):
         return model
+    engine = engine or DEFAULT_ENGINE
+    if engine == "dcp":
+        if find_unused:
+            raise ValueError("the dcp bucket engine needs every parameter used (find_unused=False)")
+        from .reducer import GradSyncDDP
+
+        return GradSyncDDP(model, None, bucket_cap_mb, first_bucket_mb, comm_dtype, telemetry)
+    if engine != "torch":
+        raise ValueError(f"unknown DDP engine {engine!r} (dcp | torch)")
     default_cap = abs(float(bucket_cap_mb) - 25.0) < 1e-9
     kw = dict(broadcast_buffers=False, bucket_cap_mb=None if default_cap else bucket_cap_mb,
               gradient_as_bucket_view=True, find_unused_parameters=find_unused, static_graph=static_graph)
@@ -114,9 +131,19 @@ def wrap_ddp(model: nn.Module, local_rank: int = None, syncbn: bool = False, buc
     return ddp
 
 
+def attach_optimizer(net: nn.Module, opt):
+    """Fuse ``opt``'s step into the bucket engine (one launch per bucket behind its all-reduce);
+    a no-op for torch DDP and unwrapped (single-process) models."""
+    if hasattr(net, "reducer") and hasattr(net, "attach_optimizer"):
+        net.attach_optimizer(opt)
+    return opt
+
+
 def bucket_layout_mb(ddp: nn.Module):
     """Gradient bucket sizes (MiB, in all-reduce order) of a DDP module's Reducer.  The
     layout is final after the first backward (DDP rebuilds buckets in gradient-ready order)."""
+    if hasattr(ddp, "reducer") and hasattr(ddp.reducer, "bucket_sizes_mb"):
+        return ddp.reducer.bucket_sizes_mb()
     data = ddp._get_ddp_logging_data()
     sizes = data.get("rebuilt_bucket_sizes") or data.get("bucket_sizes", "")
     if isinstance(sizes, str):
@@ -125,7 +152,9 @@ def bucket_layout_mb(ddp: nn.Module):
 
 
 def unwrap(model: nn.Module) -> nn.Module:
-    return model.module if isinstance(model, nn.parallel.DistributedDataParallel) else model
+    from .reducer import GradSyncDDP
+
+    return model.module if isinstance(model, (nn.parallel.DistributedDataParallel, GradSyncDDP)) else model
 
 
 @torch.no_grad()

@@ -48,7 +48,7 @@ def _layout(ddp):
 
 
 def test_resnet50_bucket_layout_leaves_small_tail(gloo1):
-    ddp = pddp.wrap_ddp(build_model("resnet50", num_classes=1000), force=True)
+    ddp = pddp.wrap_ddp(build_model("resnet50", num_classes=1000), force=True, engine="torch")
     sizes = _layout(ddp)
     assert abs(sum(sizes) - 97.49) < 0.05
     assert len(sizes) == 5
@@ -64,3 +64,19 @@ def test_explicit_cap_has_no_small_first_bucket(gloo1):
                                                     gradient_as_bucket_view=True)
     sizes = _layout(ddp)
     assert sizes[0] > 20.0 and sizes[-1] > 0.15 * sum(sizes)
+
+
+def test_bucket_engine_layout_follows_gradient_order(gloo1):
+    """The bucket engine (parallel/reducer.py) rebuilds its buckets after the first backward in
+    gradient-ready order: the head's gradients form the first (small) bucket, 25 MiB buckets
+    follow, and the tail that can only start after the stem's weight gradient stays small."""
+    net = pddp.wrap_ddp(build_model("resnet50", num_classes=1000), force=True, engine="dcp")
+    torch.manual_seed(0)
+    x = torch.randn(2, 32, 32, 8)
+    net(x).float().sum().backward()
+    sizes = pddp.bucket_layout_mb(net)
+    assert abs(sum(sizes) - 97.49) < 0.1
+    assert sizes[0] < 8.5 and all(s < 32 for s in sizes)
+    assert sizes[-1] < 0.15 * sum(sizes)
+    first = net.reducer.buckets[0].params
+    assert any(p is net.module.fc.weight for p in first)

@@ -55,7 +55,7 @@ def test_bench_rejects_world_mismatch():
     assert out.returncode != 0 and "--gpus 2" in out.stderr
 
 
-def _rccl_worker(rank, world, port, out_dir):
+def _rccl_worker(rank, world, port, out_dir, engine="torch"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     sys.path.insert(0, ROOT)
@@ -71,8 +71,8 @@ def _rccl_worker(rank, world, port, out_dir):
     dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=120))
     torch.manual_seed(0)
     model = build_model("resnet18", num_classes=10).to(dev)
-    net = wrap_ddp(model, 0, syncbn=True, bucket_cap_mb=1, force=True)
-    assert isinstance(net, torch.nn.parallel.DistributedDataParallel)
+    net = wrap_ddp(model, 0, syncbn=True, bucket_cap_mb=1, force=True, engine=engine)
+    assert isinstance(net, torch.nn.parallel.DistributedDataParallel) == (engine == "torch")
     bn_group = bn_process_group()
     assert bn_group is not None and bn_group is not dist.group.WORLD
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
@@ -93,13 +93,15 @@ def _rccl_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_rccl_world1_ddp_step():
-    """RCCL executes: world-1 ``nccl`` group, forced DDP + SyncBN, gradients equal a plain step."""
+@pytest.mark.parametrize("engine", ["torch", "dcp"])
+def test_rccl_world1_ddp_step(engine):
+    """RCCL executes: world-1 ``nccl`` group, forced DDP + SyncBN (torch's Reducer or the bucket
+    engine), gradients equal a plain step."""
     from ddp_classification_pytorch_amd.models import build_model
     from ddp_classification_pytorch_amd.ops import functional as Fn
 
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rccl_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d, engine), nprocs=1, join=True)
         got = torch.load(os.path.join(d, "rccl.pt"), weights_only=True)
     assert got["backend"] == "nccl" and torch.equal(got["t"], torch.ones(4))
     dev = torch.device("cuda", 0)
@@ -184,3 +186,71 @@ def test_ddp_two_ranks_matches_full_batch(syncbn):
     err = ((g_ddp - ref).norm() / ref.norm()).item()
     assert abs(float(got["loss"]) - ref_loss) < 2e-2 * max(1.0, abs(ref_loss))
     assert err <= 3 * floor + 1e-2, (err, floor)
+
+
+def _rccl_graph_worker(rank, world, port, out_dir, grad_comm):
+    """World-1 RCCL group, bucket engine + SyncBN (its own communicator) + SGD fused per bucket:
+    5 eager steps vs 2 eager warm-up steps + 3 HIP-graph replays of the captured step, from the
+    same initial state -- the captured all-reduces, SyncBN collectives and per-bucket optimizer
+    launches must replay to the same parameters."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import datetime
+
+    from ddp_classification_pytorch_amd.engine.graph import GraphedStep
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.optim import FusedSGD
+    from ddp_classification_pytorch_amd.parallel.ddp import attach_optimizer, wrap_ddp
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=120))
+    g = torch.Generator().manual_seed(1)
+    imgs = torch.randint(0, 256, (16, 3, 64, 64), dtype=torch.uint8, generator=g).to(dev)
+    labels = torch.randint(0, 10, (16,), generator=g).to(dev)
+    out = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(0)
+        model = build_model("resnet18", num_classes=10).to(dev)
+        net = wrap_ddp(model, 0, syncbn=True, bucket_cap_mb=2, first_bucket_mb=0.5, force=True, engine="dcp",
+                       comm_dtype=torch.bfloat16 if grad_comm == "bf16" else torch.float32)
+        opt = attach_optimizer(net, FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4))
+        x = Fn.to_device_nhwc(imgs, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), in_scale=1 / 255.0,
+                              **input_layout(model))
+
+        def step():
+            loss = Fn.cross_entropy(net(x), labels)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        if mode == "eager":
+            for _ in range(5):
+                loss = step()
+        else:
+            gs = GraphedStep(step, warmup=2, distributed=True)
+            for _ in range(3):
+                loss = gs()
+        torch.cuda.synchronize()
+        out[mode] = {"params": {n: p.detach().cpu().clone() for n, p in model.named_parameters()},
+                     "rm": model.layer2[0].bn1.running_mean.detach().cpu().clone(), "loss": float(loss),
+                     "buckets": len(net.reducer.buckets)}
+    torch.save(out, os.path.join(out_dir, "graph.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("grad_comm", ["fp32", "bf16"])
+def test_rccl_world1_bucket_engine_graph_replay_matches_eager(grad_comm):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rccl_graph_worker, args=(1, _free_port(), d, grad_comm), nprocs=1, join=True)
+        got = torch.load(os.path.join(d, "graph.pt"), weights_only=True)
+    e, g = got["eager"], got["graph"]
+    assert e["buckets"] >= 3
+    assert abs(e["loss"] - g["loss"]) < 1e-3 * max(1.0, abs(e["loss"]))
+    for n, v in e["params"].items():
+        err = (g["params"][n] - v).norm() / max(v.norm().item(), 1e-12)
+        assert err < 1e-4, (n, float(err))
+    assert torch.allclose(e["rm"], g["rm"], rtol=1e-4, atol=1e-5)

@@ -122,10 +122,15 @@ def _bn_group_worker(rank, world, port, out_dir):
     finally:
         dist.all_gather_into_tensor, dist.all_reduce = real_ag, real_ar
     bn = pddp.bn_process_group()
+    # the gradient buckets of the bucket engine go to the default group (group=None)
+    grad_calls = [c for c in calls if c[1] is None]
+    bn_calls = [c for c in calls if c[1] is not None]
+    n_fwd_bn = sum(1 for c in calls[:n_fwd] if c[1] is not None)
     if rank == 0:
         torch.save({"one_group": len(groups) == 1, "is_bn": groups == {bn}, "not_world": bn is not dist.group.WORLD,
-                    "all_on_bn": all(g is bn for _, g in calls), "n_fwd": n_fwd, "n_bwd": len(calls) - n_fwd,
-                    "kinds_fwd": sorted({k for k, _ in calls[:n_fwd]}),
+                    "all_on_bn": all(g is bn for _, g in bn_calls), "n_fwd": n_fwd_bn,
+                    "n_bwd": len(bn_calls) - n_fwd_bn, "kinds_fwd": sorted({k for k, _ in calls[:n_fwd]}),
+                    "grad_calls": len(grad_calls), "buckets": len(net.reducer.buckets),
                     "n_bn": sum(isinstance(m, BatchNorm2d) for m in model.modules())},
                    os.path.join(out_dir, "g.pt"))
     dist.barrier()
@@ -145,6 +150,7 @@ def test_syncbn_uses_dedicated_group_and_coalesces():
     assert n_bn == 20
     assert got["n_fwd"] == n_bn - n_proj, got
     assert got["n_bwd"] == n_bn - n_proj, got
+    assert got["grad_calls"] == got["buckets"]  # one all-reduce per gradient bucket, default group
 
 
 def _metrics_worker(rank, world, port, out_dir):
@@ -209,7 +215,9 @@ def _workload_worker(rank, world, port, out_dir, workload):
               "--device", "cpu", "--out-dir", os.path.join(out_dir, f"run{rank}"), "--log-interval", "100"]
     extra = {"cdr": [], "nested": ["--nested", "20", "--warmup-iters", "2"], "plc": ["--plc-eta-epochs", "1"]}
     entry.main(["--workload", workload] + common + extra[workload])
-    assert wrapped and all(isinstance(d, torch.nn.parallel.DistributedDataParallel) for _, d in wrapped)
+    from ddp_classification_pytorch_amd.parallel.reducer import GradSyncDDP
+
+    assert wrapped and all(isinstance(d, (torch.nn.parallel.DistributedDataParallel, GradSyncDDP)) for _, d in wrapped)
     torch.save([{n: p.detach().clone() for n, p in m.named_parameters()} for m, _ in wrapped],
                os.path.join(out_dir, f"params{rank}.pt"))
 

@@ -1,0 +1,127 @@
+"""The bucket engine (parallel/reducer.py) on the CPU: gradients averaged over ranks (gloo, world
+size 2) equal torch's DistributedDataParallel; the optimizer fused per bucket gives the same
+parameters as a plain FusedSGD / FusedAdam step after backward; bucket layout follows the
+gradient-ready order; bf16 all-reduce stays within bf16 rounding."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(rank, step):
+    g = torch.Generator().manual_seed(100 * step + rank)
+    return torch.randn(4, 3, 32, 32, generator=g), torch.randint(0, 10, (4,), generator=g)
+
+
+def _train(net, model, opt, rank, steps, attach):
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.parallel.ddp import attach_optimizer
+
+    if attach:
+        attach_optimizer(net, opt)
+    for s in range(steps):
+        x, y = _data(rank, s)
+        loss = Fn.cross_entropy(net(Fn.to_device_nhwc(x, cpad=8)), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    return {n: p.detach().clone() for n, p in model.named_parameters()}
+
+
+def _worker(rank, world, port, out_dir, engine, attach, comm, optname, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.optim import FusedAdam, FusedSGD
+    from ddp_classification_pytorch_amd.parallel.ddp import wrap_ddp
+
+    torch.manual_seed(0)
+    model = build_model("cifar_resnet18", num_classes=10)
+    net = wrap_ddp(model, None, bucket_cap_mb=8, first_bucket_mb=1, engine=engine,
+                   comm_dtype=torch.bfloat16 if comm == "bf16" else torch.float32)
+    if optname == "sgd":
+        opt = FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+    else:
+        opt = FusedAdam(model.parameters(), lr=1e-3)
+    init = {n: p.detach().clone() for n, p in model.named_parameters()}
+    params = _train(net, model, opt, rank, steps, attach)
+    info = {}
+    if engine == "dcp":
+        info = {"buckets": net.reducer.bucket_sizes_mb(), "grad_is_view": all(
+            p.grad is not None and p.grad.data_ptr() >= 0 for p in model.parameters())}
+    if rank == 0:
+        torch.save({"params": params, "init": init, "info": info}, os.path.join(out_dir, f"{engine}_{attach}_{comm}_{optname}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(d, engine, attach, comm="fp32", optname="sgd", steps=3):
+    mp.spawn(_worker, args=(2, _free_port(), d, engine, attach, comm, optname, steps), nprocs=2, join=True)
+    return torch.load(os.path.join(d, f"{engine}_{attach}_{comm}_{optname}.pt"), weights_only=True)
+
+
+@pytest.mark.parametrize("optname", ["sgd", "adam"])
+def test_bucket_engine_matches_torch_ddp(optname):
+    """3 steps, 2 ranks, different data per rank: torch DDP + optimizer.step() == our engine with the
+    optimizer fused per bucket == our engine without it."""
+    with tempfile.TemporaryDirectory() as d:
+        ref = _run(d, "torch", False, optname=optname)["params"]
+        fused = _run(d, "dcp", True, optname=optname)
+        plain = _run(d, "dcp", False, optname=optname)["params"]
+    assert len(fused["info"]["buckets"]) >= 3  # small buckets: the per-bucket path really runs
+    for k, v in ref.items():
+        assert torch.allclose(fused["params"][k], v, rtol=1e-5, atol=1e-6), k
+        assert torch.allclose(plain[k], v, rtol=1e-5, atol=1e-6), k
+
+
+def test_bucket_engine_bf16_allreduce_close():
+    """One step with bf16 gradient buckets: the update differs from the fp32 all-reduce's by about
+    bf16 rounding (2^-8 relative)."""
+    with tempfile.TemporaryDirectory() as d:
+        ref = _run(d, "dcp", True, steps=1)
+        got = _run(d, "dcp", True, comm="bf16", steps=1)
+    init = ref["init"]
+    num = sum(((got["params"][k] - v) ** 2).sum() for k, v in ref["params"].items())
+    den = sum(((v - init[k]) ** 2).sum() for k, v in ref["params"].items())
+    assert (num / den).sqrt().item() < 1e-2
+
+
+def test_single_process_engine_equals_plain_training():
+    """World size 1 (no process group): the engine's per-bucket SGD == FusedSGD after backward,
+    bit for bit; buckets are rebuilt in gradient-ready order (head first)."""
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.optim import FusedSGD
+    from ddp_classification_pytorch_amd.parallel.reducer import GradSyncDDP
+
+    def make():
+        torch.manual_seed(0)
+        m = build_model("cifar_resnet18", num_classes=10)
+        return m, FusedSGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+
+    m0, o0 = make()
+    ref = _train(m0, m0, o0, 0, 3, False)
+    m1, o1 = make()
+    net = GradSyncDDP(m1, bucket_cap_mb=4, first_bucket_mb=0.5)
+    got = _train(net, m1, o1, 0, 3, True)
+    for k, v in ref.items():
+        assert torch.equal(got[k], v), k
+    r = net.reducer
+    assert r._rebuilt and len(r.buckets) >= 3
+    first = r.buckets[0].params
+    assert any(p is m1.fc.weight or p is m1.fc.bias for p in first)  # the head's gradients are ready first
+    # p.grad are views into the reduced bucket buffers
+    b = r.buckets[1]
+    assert b.params[0].grad.data_ptr() == b.grad_buf.data_ptr()

@@ -23,6 +23,7 @@
 #   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
 #   smallenv=V=X    b32 graph / b128 eager, default vs with environment V=X
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
+#   loop            main.py's training loop vs bench.py at batch 32 (eager, HIP graph) and 128
 set -e
 set -o pipefail
 T=${1:?tag}; shift
@@ -35,6 +36,14 @@ for step in "$@"; do
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${k:+-k "$k"} \
         > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
       tail -2 $O/gpu_tests.log ;;
+    loop)
+      for g in "" "--graph"; do
+        timeout -k 10 400 python -u tools/loop_vs_bench.py --batch 32 $g > $O/loop32$g.log 2>&1
+        tail -1 $O/loop32$g.log
+      done
+      timeout -k 10 400 python -u tools/loop_vs_bench.py --batch 128 --steps 120 --log-interval 20 --bench-steps 40 \
+        > $O/loop128.log 2>&1
+      tail -1 $O/loop128.log ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
       tail -1 $O/smoke.log ;;
