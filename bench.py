@@ -71,6 +71,10 @@ def parse(argv=None):
     ap.add_argument("--ddp-engine", default="dcp", choices=["dcp", "torch"],
                     help="dcp: this framework's bucket engine (optimizer fused per bucket, HIP-graph capturable); "
                          "torch: DistributedDataParallel's C++ Reducer")
+    ap.add_argument("--force-ddp", action="store_true",
+                    help="1 GPU: still run the data-parallel path -- a world-size-1 RCCL process group, the DDP "
+                         "engine, the SyncBN phase and telemetry (measures the engine's own cost and its HIP-graph "
+                         "capture on one box)")
     ap.add_argument("--telemetry-steps", type=int, default=5,
                     help="N > 1, dcp engine: untimed steps after the timed phase that record per-bucket HIP events "
                          "(exposed communication per rank)")
@@ -159,8 +163,12 @@ def main(argv=None):
     # several ranks on one GPU (RCCL refuses duplicate devices).
     backend = os.environ.get("DCP_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    dist_on = world > 1 or a.force_ddp
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -181,8 +189,9 @@ def main(argv=None):
 
     torch.manual_seed(1234 + rank)
     model = build_bench_model(a).to(dev)
-    if world > 1:
+    if dist_on:
         model = pddp.wrap_ddp(model, local, syncbn=a.syncbn, bucket_cap_mb=a.bucket_cap_mb, engine=a.ddp_engine,
+                              force=a.force_ddp,
                               comm_dtype=torch.bfloat16 if a.grad_comm == "bf16" else torch.float32)
         # created collectively now (every rank, same order) so the SyncBN phase can switch to it
         bn_group = pddp.bn_process_group()
@@ -218,11 +227,11 @@ def main(argv=None):
 
     run = step
     if a.graph:
-        if world > 1 and a.ddp_engine != "dcp":
+        if dist_on and a.ddp_engine != "dcp":
             raise SystemExit("--graph with N > 1 needs the bucket engine (torch DDP's reducer is not capturable)")
         from ddp_classification_pytorch_amd.engine.graph import GraphedStep
 
-        graphed = GraphedStep(step, warmup=max(1, a.warmup), distributed=world > 1)  # warm-up steps run inside
+        graphed = GraphedStep(step, warmup=max(1, a.warmup), distributed=dist_on)  # warm-up steps run inside
         run = graphed
     else:
         for _ in range(a.warmup):
@@ -263,7 +272,7 @@ def main(argv=None):
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     dt, per_rank = gather_max(dt)
     comm = None
-    if world > 1 and a.ddp_engine == "dcp" and a.telemetry_steps > 0:
+    if dist_on and a.ddp_engine == "dcp" and a.telemetry_steps > 0:
         # untimed: per-step HIP events around the bucket engine (backward end on the compute stream,
         # first bucket start / last bucket done on the communication stream), eager steps
         red = model.reducer
@@ -281,10 +290,10 @@ def main(argv=None):
                 "exposed_comm_ms_per_rank": [round(float(v[0]), 4) for v in allt],
                 "comm_span_ms_per_rank": [round(float(v[1]), 4) for v in allt],
                 "grad_comm": a.grad_comm}
-    elif world > 1:
+    elif dist_on:
         comm = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
     sync = None
-    if world > 1 and not a.syncbn and a.syncbn_phase and not a.graph:
+    if dist_on and not a.syncbn and a.syncbn_phase and not a.graph:
         # second phase: the reference's SyncBN (BASELINE/main.py:148) on the dedicated BN communicator
         pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group)
         for _ in range(2):
@@ -310,8 +319,8 @@ def main(argv=None):
             "vs_baseline": None,  # the reference publishes no throughput
             "dtype": "bf16",
             "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
-            "dist_backend": (dist.get_backend() if world > 1 else None),
-            "world_size": (dist.get_world_size() if world > 1 else 1),
+            "dist_backend": (dist.get_backend() if dist_on else None),
+            "world_size": (dist.get_world_size() if dist_on else 1),
             "rccl_version": rccl_version(),
             "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
             "syncbn_value": sync["value"] if sync else None,
@@ -329,7 +338,8 @@ def main(argv=None):
                 "autotune": bool(autotune),
                 "syncbn": bool(a.syncbn),
                 "grad_comm": a.grad_comm,
-                "ddp_engine": a.ddp_engine if world > 1 else None,
+                "ddp_engine": a.ddp_engine if dist_on else None,
+                "force_ddp": bool(a.force_ddp),
                 "bucket_cap_mb": a.bucket_cap_mb,
                 "optimizer": "fused SGD momentum 0.9 wd 1e-4",
                 "final_loss": round(loss_v, 4),
@@ -337,7 +347,7 @@ def main(argv=None):
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -24,6 +24,8 @@
 #   smallenv=V=X    b32 graph / b128 eager, default vs with environment V=X
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
 #   loop            main.py's training loop vs bench.py at batch 32 (eager, HIP graph) and 128
+#   ddp1            world-1 RCCL through the bucket engine (--force-ddp): b32 graph / eager, b1024 (+ SyncBN phase,
+#                   comm telemetry), bf16 buckets
 set -e
 set -o pipefail
 T=${1:?tag}; shift
@@ -36,6 +38,15 @@ for step in "$@"; do
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${k:+-k "$k"} \
         > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
       tail -2 $O/gpu_tests.log ;;
+    ddp1)
+      timeout -k 10 300 python -u bench.py --force-ddp --batch 32 --graph --steps 100 --warmup 5 > $O/ddp1_b32g.log 2>&1
+      tail -1 $O/ddp1_b32g.log
+      timeout -k 10 300 python -u bench.py --force-ddp --batch 32 --steps 100 --warmup 5 > $O/ddp1_b32.log 2>&1
+      tail -1 $O/ddp1_b32.log
+      timeout -k 10 300 python -u bench.py --force-ddp --steps 20 --warmup 5 > $O/ddp1_b1024.log 2>&1
+      tail -1 $O/ddp1_b1024.log
+      timeout -k 10 300 python -u bench.py --force-ddp --batch 128 --grad-comm bf16 --steps 30 --warmup 5 > $O/ddp1_b128bf16.log 2>&1
+      tail -1 $O/ddp1_b128bf16.log ;;
     loop)
       for g in "" "--graph"; do
         timeout -k 10 400 python -u tools/loop_vs_bench.py --batch 32 $g > $O/loop32$g.log 2>&1
