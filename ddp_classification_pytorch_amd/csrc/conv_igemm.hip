@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 
 #include "common.cuh"
@@ -1531,6 +1532,253 @@ tap_gemm_big_kernel(const TapGemmParams p) {
   }
 }
 
+// compile-time interleave for the scheduler: NREAD groups of (one LDS read, then the k-th share of
+// NMFMA MFMAs): the reads go out early, the MFMAs behind them use the OTHER register set -- sched_group_barrier takes constant arguments only, hence the recursion
+template <int NREAD, int NMFMA, int K = 0>
+__device__ __forceinline__ void sched_mfma_reads() {
+  if constexpr (K < NREAD) {
+    constexpr int n = (K + 1) * NMFMA / NREAD - K * NMFMA / NREAD;
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                       // DS read
+    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x008, n, 0);  // MFMA
+    sched_mfma_reads<NREAD, NMFMA, K + 1>();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined 8-wave tap GEMM (FAST shapes: Cs % 64 == 0, one tap per 64-deep k-tile; plain /
+// statistics epilogue, optional eval-BN fold / add source).  Workgroup tile BM = 256 pixel rows
+// x BN = 64 * WN output channels, WM x WN waves, each owning PW = 256 / WM pixels x 64 channels.
+//
+// What the 128-row kernels and tap_gemm_big_kernel leave exposed (profiles/r3 PMC: 11-36 % MFMA
+// busy) is the serial chain per k-step: barrier -> LDS fragment reads -> lgkmcnt(0) -> MFMA burst,
+// with both waves of a SIMD in lockstep (so neither covers the other's read latency), one barrier
+// per 32-deep k-step, and a vmcnt drain whenever the ring is shallow.  Here:
+//   * 64-deep k-tiles (128-byte LDS rows, XOR-swizzled on the source address as everywhere in
+//     this file) in an NS-slot ring: ONE raw s_barrier per 64-deep k-tile;
+//   * the fragments of each k-tile are read in two halves (k 0..31, 32..63) into two register
+//     sets: the reads of one half are issued while the MFMAs of the other run -- the LDS latency
+//     hides behind the matrix pipe instead of stalling it (sched_group_barrier interleave when
+//     SCHED); the next k-tile's first half is read right after the barrier, under the current
+//     k-tile's second-half MFMAs;
+//   * a slot is restaged as soon as every wave has read it (the barrier of the same k-tile), so
+//     NS - 1 k-tiles of LDS-DMA stay in flight across every barrier, retired by a counted vmcnt
+//     (never 0 in the loop);
+//   * M32: v_mfma_f32_32x32x16_bf16 (2 x 2 fragments of 32 x 32 per 64 x 64 wave tile, K = 16 per
+//     instruction) instead of 16x16x32 (4 x 4 fragments): half the MFMA instructions for the same
+//     LDS bytes; which shape holds the higher clock is measured, not assumed (MI355X DVFS).
+// The accumulators leave through the LDS image in 128 x 128 quadrants and the 256-thread store
+// epilogue of the other tap GEMMs (tg_image_store: coalesced 16-byte stores, BN statistics).
+// ---------------------------------------------------------------------------
+template <int WM, int WN, int NS, int EPI, bool M32, bool SCHED>
+__global__ void __launch_bounds__(512, 1)
+tap_gemm_p8_kernel(const TapGemmParams p) {
+  constexpr int NW = WM * WN;
+  static_assert(NW == 8, "8 waves");
+  constexpr int BM = 256, BN = 64 * WN, PW = BM / WM;
+  constexpr int FD = M32 ? 32 : 16;             // fragment edge
+  constexpr int PF = PW / FD, CF = 64 / FD;     // pixel / channel fragments per wave
+  constexpr int KS = M32 ? 2 : 1;               // MFMA k-steps per 32-deep half k-tile
+  constexpr int AI = BM * 8 / 512, BI = BN * 8 / 512, LPT = AI + BI;  // LDS-DMA per thread per k-tile
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int QN = BN / 128;                  // 128-channel quadrants across the tile
+  static_assert(BN % 128 == 0 && NS >= 2, "tile geometry");
+  using accT = typename std::conditional<M32, f32x16, f32x4>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-slot source pointers + tap-validity masks (tap_gemm_kernel's FAST path)
+  const bf16* fa_ptr[AI];
+  uint32_t fa_vm[AI];
+  const bf16* fb_ptr[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * 8 + (lane >> 3);
+    const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const uint32_t x = mm - q * p.Wy;
+    const uint32_t n = fdiv(q, p.div_hy);
+    const uint32_t y = q - n * p.Hy;
+    const int ys = y * p.ss, xs = x * p.ss;
+    fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane & 7) ^ swz_chunk<64>(r)) * 8;
+    uint32_t vm = 0;
+    for (int t = 0; t < p.ntaps; ++t) {
+      const int tv = p.tap[t];
+      const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+      vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+    }
+    fa_vm[i] = vm;
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int r = (wave * BI + i) * 8 + (lane >> 3);
+    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane & 7) ^ swz_chunk<64>(r)) * 8;
+  }
+  // the tap table lives in one VGPR (lane t holds tap t; <= 64 taps), read with v_readlane: no
+  // scalar-memory load inside the k-loop (an SMEM result forces lgkmcnt(0), which would drain
+  // the in-flight LDS fragment reads); the (tap, channel chunk) of the next k-tile to stage is
+  // advanced with scalar selects instead of a division
+  const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
+  int st_t = 0, st_c = 0;  // tap / channel base of the next k-tile to stage
+  auto stage = [&](int slot) {
+    char* As = smem + slot * STAGE;
+    char* Bs = As + A_BYTES;
+    const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
+    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
+    const long boff = (long)tap_w(tv) * p.Cs + st_c;
+    const uint32_t tbit = 1u << st_t;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16,
+                                       0, 0);
+    st_c += 64;
+    const bool wrap = st_c >= p.Cs;
+    st_t += wrap ? 1 : 0;
+    st_c = wrap ? 0 : st_c;
+  };
+
+  accT acc[CF][PF];
+#pragma unroll
+  for (int j = 0; j < CF; ++j)
+#pragma unroll
+    for (int i = 0; i < PF; ++i) acc[j][i] = accT{};
+
+  // fragment reads of half h (k 32h .. 32h + 31) of the k-tile in `slot`: the 16x16x32 operand is
+  // 16 rows x one 16-byte chunk per lane (chunk 4h + lane / 16), the 32x32x16 operand 32 rows x
+  // one chunk per lane (chunk 4h + 2s + lane / 32) per k-step s
+  const int fr = M32 ? (lane & 31) : (lane & 15);
+  const int fc = M32 ? (lane >> 5) : (lane >> 4);
+  auto read_half = [&](int slot, int h, bf16x8 (&wf)[KS][CF], bf16x8 (&af)[KS][PF]) {
+    const char* As = smem + slot * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint32_t c = h * 4 + s * 2 * (M32 ? 1 : 0) + fc;
+#pragma unroll
+      for (int j = 0; j < CF; ++j) wf[s][j] = *(const bf16x8*)(Bs + swzk<64>(wn * 64 + j * FD + fr, c));
+#pragma unroll
+      for (int i = 0; i < PF; ++i) af[s][i] = *(const bf16x8*)(As + swzk<64>(wm * PW + i * FD + fr, c));
+    }
+  };
+  auto mfma_half = [&](const bf16x8 (&wf)[KS][CF], const bf16x8 (&af)[KS][PF]) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < CF; ++j)
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+          if constexpr (M32)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
+          else
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
+        }
+  };
+  // read / MFMA interleave for the scheduler (the MFMAs' operands were read one half k-tile earlier)
+  constexpr int NREAD = KS * (CF + PF), NMFMA = KS * CF * PF;
+  auto interleave = [&]() {
+    if constexpr (SCHED) sched_mfma_reads<NREAD, NMFMA>();
+  };
+  auto ring_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's fragment reads retired
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+  };
+
+  const int nkt = p.nkt;  // 64-deep k-tiles
+  bf16x8 w0[KS][CF], a0[KS][PF], w1[KS][CF], a1[KS][PF];
+#pragma unroll
+  for (int i = 0; i < NS; ++i)
+    if (i < nkt) stage(i);
+  if (nkt > 0) {
+    wait_vmcnt(LPT * (min(NS, nkt) - 1));  // k-tile 0 landed (this wave's share)
+    ring_barrier();                        // ... for every wave
+    read_half(0, 0, w0, a0);
+  }
+  // tiles issued so far at iteration kt: 0 .. min(kt + NS - 1, nkt - 1); before reading k-tile
+  // kt + 1 it must have landed: NS - 2 younger k-tiles may stay in flight in the steady state
+  int kt = 0;
+  for (; kt + NS < nkt; ++kt) {  // steady state: one k-tile staged per iteration
+    const int slot = kt % NS;
+    mfma_half(w0, a0);
+    read_half(slot, 1, w1, a1);  // second half of this k-tile, under the first half's MFMAs
+    interleave();
+    wait_vmcnt(LPT * (NS - 2));
+    ring_barrier();              // every wave: k-tile kt + 1 landed, slot kt fully read
+    mfma_half(w1, a1);
+    read_half((kt + 1) % NS, 0, w0, a0);  // next k-tile's first half, under this one's second
+    interleave();
+    // k-tile kt + NS into the slot just freed, issued behind the fragment reads: an LDS-DMA issued
+    // between an LDS read and its first use makes the compiler's wait for that read lgkmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    stage(slot);
+  }
+  for (; kt < nkt; ++kt) {  // the last NS k-tiles: nothing left to stage
+    const int slot = kt % NS;
+    mfma_half(w0, a0);
+    read_half(slot, 1, w1, a1);
+    interleave();
+    if (kt + 1 < nkt) {
+      wait_vmcnt(LPT * (nkt - 2 - kt));
+      ring_barrier();
+      mfma_half(w1, a1);
+      read_half((kt + 1) % NS, 0, w0, a0);
+      interleave();
+    } else {
+      mfma_half(w1, a1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
+#pragma unroll
+  for (int i = 0; i < PF; ++i) {
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      const int px = wm * PW + i * FD + fr;  // tile pixel of this lane's column
+      char* Q = smem + ((px >> 7) * QN + ((wn * 64) >> 7)) * 32768;
+      const uint32_t pl = px & 127;
+      if constexpr (M32) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t cl = ((wn * 64) & 127) + j * 32 + q * 8 + fc * 4;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][q * 4 + r]);
+          *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+        }
+      } else {
+        const uint32_t cl = ((wn * 64) & 127) + j * 16 + fc * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+      }
+    }
+  }
+  __syncthreads();
+  // group g (threads 256g ..) stores quadrants g*QN ..; both groups pass the same barriers
+  const int g = tid >> 8, gtid = tid & 255;
+#pragma unroll
+  for (int k = 0; k < QN; ++k) {
+    const int q = g * QN + k;
+    tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------
@@ -2086,6 +2334,38 @@ static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
   else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
 }
 
+// pipelined 8-wave kernel (tap_gemm_p8_kernel); variant v: 1 = 256 x 128 16x16x32, 2 = 256 x 128
+// 32x32x16, 3 / 4 = the same with the sched_group_barrier read/MFMA interleave (a 256 x 256 tile at
+// 8 waves -- 128 x 64 per wave -- spills with two fragment register sets)
+template <int WM, int WN, int NS, bool M32, bool SCHED>
+static void launch_p8_cfg(const TapGemmParams& p, int epi, hipStream_t stream) {
+  constexpr int BM = 256, BN = 64 * WN;
+  constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 128, (size_t)2 * (BN / 128) * 32768);
+  const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)tap_gemm_p8_kernel<WM, WN, NS, 0, M32, SCHED>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_p8_kernel<WM, WN, NS, 1, M32, SCHED>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  if (epi == 1)
+    hipLaunchKernelGGL((tap_gemm_p8_kernel<WM, WN, NS, 1, M32, SCHED>), dim3(grid), dim3(512), lds, stream, p);
+  else
+    hipLaunchKernelGGL((tap_gemm_p8_kernel<WM, WN, NS, 0, M32, SCHED>), dim3(grid), dim3(512), lds, stream, p);
+}
+
+static void launch_p8(TapGemmParams p, int variant, int epi, hipStream_t stream) {
+  p.nkt = p.ntaps * p.cpt / 8;  // 64-deep k-tiles (cpt % 8 == 0 on FAST shapes)
+  switch (variant) {
+    case 2: launch_p8_cfg<4, 2, 3, true, false>(p, epi, stream); break;
+    case 3: launch_p8_cfg<4, 2, 3, false, true>(p, epi, stream); break;
+    case 4: launch_p8_cfg<4, 2, 3, true, true>(p, epi, stream); break;
+    default: launch_p8_cfg<4, 2, 3, false, false>(p, epi, stream); break;
+  }
+}
+
 // 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[24]
 // (0 = this heuristic).  Per-shape A/B at b1024 (profiles/r3/big_tile_ab_b1024_pipelined.txt): the
 // big tiles win where the 128-row kernels' grid is short or their k-loop is exposed, and lose on
@@ -2240,6 +2520,12 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
+  // pipelined 8-wave kernel: g_tune[26] = variant (A/B; 0 = off)
+  const int p8 = g_tune[26];
+  if (big_ok && p8 > 0 && p8 <= 4) {
+    launch_p8(p, p8, epi, stream);
+    return;
+  }
   const int big = big_ok ? big_tile_pick(g_tune[24], p.M, Co, taps.n, ds) : 0;
   if (big != 0) {
     p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)

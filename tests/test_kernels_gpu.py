@@ -1150,6 +1150,48 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
     assert relerr(d1, dxr) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 1, 1), (3, 28, 28, 128, 512, 1, 1, 0),
+                                   (2, 7, 7, 512, 2048, 1, 1, 0), (2, 28, 28, 256, 512, 1, 2, 0),
+                                   (3, 9, 11, 128, 128, 3, 1, 1), (1, 13, 13, 256, 384, 3, 2, 1),
+                                   (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1),
+                                   (4, 14, 14, 64, 128, 1, 1, 0), (2, 14, 14, 128, 192, 3, 1, 1)])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_pipelined_p8_tap_gemm_matches(K, shape, variant):
+    """The pipelined 8-wave 256 x 128 tap GEMM (g_tune[26]: 1 = 16x16x32, 2 = 32x32x16, 3 / 4 with
+    the read/MFMA interleave) == the 128-row kernel and the fp32 reference: forward with BN
+    statistics and the data gradient (stride 1, the stride-2 parity classes, ragged M and Co,
+    1..36 k-tiles: the steady ring loop, its tail and the no-steady-state short-K path)."""
+    N, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co).to(DEV)
+    wb, wt = K.weight_prep(w.float(), 0, True)
+    outs = []
+    try:
+        for v in (0, variant):
+            K.set_tuning(24, 2)  # the 128-row kernel as the comparison
+            K.set_tuning(26, v)
+            y, slabs = K.conv_fwd(x, wb, s, p, True)
+            st = K.bn_stats(y, slabs)
+            dx = K.conv_dgrad(dy, wt, H, W, s, p)
+            torch.cuda.synchronize()
+            outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
+    finally:
+        K.set_tuning(24, 0)
+        K.set_tuning(26, 0)
+    (y0, s0, d0), (y1, s1, d1) = outs
+    assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
+    assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
+    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
+    assert relerr(y1, yr) < 1e-2
+    sr = _ref.bn_stats(y1, None)
+    assert relerr(s1[0, 1], sr[0, 1]) < 1e-4 and relerr(s1[0, 2], sr[0, 2]) < 1e-4
+    dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().cpu().permute(3, 1, 2, 0), H, W, s, p)
+    assert relerr(d1, dxr) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [
     (2, 56, 56, 64, 256),    # stage-1 conv3: one 64-deep k-tile, 128-wide tiles
     (3, 28, 28, 128, 512),   # stage 2: 32-deep k-tiles

@@ -23,6 +23,7 @@
 #   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
 #   smallenv=V=X    b32 graph / b128 eager, default vs with environment V=X
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
+#   convab=CFGS     tools/conv_bench.py --cfgs CFGS at b1024 (in-process interleaved A/B of g_tune configs)
 #   loop            main.py's training loop vs bench.py at batch 32 (eager, HIP graph) and 128
 #   ddp1            world-1 RCCL through the bucket engine (--force-ddp): b32 graph / eager, b1024 (+ SyncBN phase,
 #                   comm telemetry), bf16 buckets
@@ -47,6 +48,11 @@ for step in "$@"; do
       tail -1 $O/ddp1_b1024.log
       timeout -k 10 300 python -u bench.py --force-ddp --batch 128 --grad-comm bf16 --steps 30 --warmup 5 > $O/ddp1_b128bf16.log 2>&1
       tail -1 $O/ddp1_b128bf16.log ;;
+    convab=*)
+      c=${step#convab=}
+      timeout -k 10 900 python -u tools/conv_bench.py --batch 1024 --iters 10 --only 1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19,20,21,22 --cfgs "$c" \
+        > $O/convab.log 2>&1
+      tail -3 $O/convab.log ;;
     loop)
       for g in "" "--graph"; do
         timeout -k 10 400 python -u tools/loop_vs_bench.py --batch 32 $g > $O/loop32$g.log 2>&1
