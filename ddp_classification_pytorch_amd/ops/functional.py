@@ -543,8 +543,23 @@ def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
     st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
     gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
     dist.all_gather_into_tensor(gathered, st, group=cfg.group)
-    count = count * cfg.world  # DistributedSampler keeps per-rank batches equal
+    _check_equal_counts(gathered, count)
+    # the forward merge is exact for any counts; the backward normaliser assumes equal per-rank
+    # batches (the sharded sampler pads every rank to the same length; parallel/ddp.py)
+    count = count * cfg.world
     return (*k.bn_finalize(gathered, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
+
+
+_SYNCBN_CHECK = [os.environ.get("DCP_SYNCBN_CHECK", "0") == "1"]
+
+
+def _check_equal_counts(gathered, count):
+    """DCP_SYNCBN_CHECK=1: every rank's gathered count must equal this rank's (a host sync)."""
+    if _SYNCBN_CHECK[0]:
+        n = gathered[:, 0, 0].float().cpu()
+        if not bool((n == float(count)).all()):
+            raise RuntimeError(f"SyncBN: unequal per-rank batch counts {n.tolist()} (the backward assumes equal "
+                               "counts; pad the shards to equal length)")
 
 
 class _BNAct(Function):
@@ -775,6 +790,7 @@ class _BNAddBNAct(Function):
             st = torch.cat([k.bn_stats(x, slabs), k.bn_stats(r, rslabs)], dim=2)
             gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
             dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+            _check_equal_counts(gathered, x.numel() // C)
             count = rcount = (x.numel() // C) * cfg.world
             mean, invstd, scale, shift = k.bn_finalize(gathered[..., :C].contiguous(), gamma, beta, run_mean, run_var,
                                                        cfg.momentum, cfg.eps)

@@ -19,8 +19,12 @@ MI355X choices:
   construction (SyncBN) or rank-local (local BN), so the per-forward buffer
   broadcast the reference pays (C3) is skipped;
 * SyncBN is our fused BN with a ``process_group``: forward all-gathers each rank's
-  per-channel (n, mean, M2) (Chan-merged, so unequal per-rank counts stay exact),
-  backward all-reduces (sum g, sum g*xhat); a projection block's two BNs share one
+  per-channel (n, mean, M2) and Chan-merges them (the forward statistics are exact for any
+  per-rank counts), backward all-reduces (sum g, sum g*xhat) and normalises them by
+  ``per-rank count x world``: the backward assumes EQUAL per-rank batches, which the
+  rank-sharded sampler guarantees (it pads every rank to the same number of samples, so every
+  step's per-rank batch is the same; ``DCP_SYNCBN_CHECK=1`` verifies the gathered counts at every
+  SyncBN forward, at the price of a host sync per layer); a projection block's two BNs share one
   collective in each direction.  Those collectives run on a DEDICATED process group
   (:func:`bn_process_group`: its own RCCL communicator and stream), so a 516 B..16 KB
   statistics exchange that sits on the critical path never queues behind a 25 MiB

@@ -236,3 +236,36 @@ def test_noisy_label_workloads_stay_in_sync_under_ddp(workload):
         assert a.keys() == b.keys()
         for n in a:
             assert torch.allclose(a[n], b[n], atol=1e-6, rtol=1e-5), n
+
+
+def _syncbn_count_worker(rank, world, port, out_dir, unequal):
+    _init(rank, world, port)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.parallel.ddp import convert_sync_batchnorm
+
+    Fn._SYNCBN_CHECK[0] = True
+    torch.manual_seed(0)
+    model = convert_sync_batchnorm(build_model("cifar_resnet18", num_classes=10))
+    n = 4 + (rank if unequal else 0)
+    x = Fn.to_device_nhwc(torch.randn(n, 3, 32, 32, generator=torch.Generator().manual_seed(rank)), cpad=8)
+    err = None
+    try:
+        model(x)
+    except RuntimeError as e:
+        err = str(e)
+    torch.save({"err": err}, os.path.join(out_dir, f"c{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("unequal", [False, True])
+def test_syncbn_equal_count_check(unequal):
+    """SyncBN's backward normalises by per-rank count x world (equal batches, which the padded
+    sharded sampler guarantees); DCP_SYNCBN_CHECK=1 turns a violation into an error."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_syncbn_count_worker, args=(2, _free_port(), d, unequal), nprocs=2, join=True)
+        errs = [torch.load(os.path.join(d, f"c{r}.pt"), weights_only=True)["err"] for r in range(2)]
+    if unequal:
+        assert all(e is not None and "unequal per-rank batch counts" in e for e in errs)
+    else:
+        assert errs == [None, None]
