@@ -1363,14 +1363,16 @@ Tensor log_softmax_bwd(const Tensor& y, const Tensor& dy, int64_t ldo, bool out_
   return dx;
 }
 
-std::tuple<Tensor, Tensor> l2norm_rows(const Tensor& x, int64_t ldo, double eps) {
+std::tuple<Tensor, Tensor> l2norm_rows(const Tensor& x, int64_t ldo, double eps, int64_t rows_out) {
   CHECK_DEV(x);
   CHECK_CONTIG(x);
   const int R = x.size(0), D = x.size(1);
-  auto y = at::empty({R, ldo}, x.options().dtype(at::kBFloat16));
-  auto inv = at::empty({R}, f32_like(x));
-  dcp::launch_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, R, D, ldo, bpm(y), inv.data_ptr<float>(),
-                          (float)eps, cur_stream());
+  const int Ro = rows_out < 0 ? R : (int)rows_out;
+  TORCH_CHECK(Ro >= R && ldo >= D, "l2norm_rows: output smaller than input");
+  auto y = at::empty({Ro, ldo}, x.options().dtype(at::kBFloat16));
+  auto inv = at::empty({Ro}, f32_like(x));
+  dcp::launch_l2norm_rows(x.data_ptr(), x.scalar_type() == at::kBFloat16, R, Ro, D, ldo, bpm(y),
+                          inv.data_ptr<float>(), (float)eps, cur_stream());
   return {y, inv};
 }
 
@@ -1617,7 +1619,7 @@ TORCH_LIBRARY(dcp, m) {
       &xent_bwd);
   m.def("log_softmax_fwd(Tensor x, int C) -> Tensor", &log_softmax_fwd);
   m.def("log_softmax_bwd(Tensor y, Tensor dy, int ldo, bool out_bf16) -> Tensor", &log_softmax_bwd);
-  m.def("l2norm_rows(Tensor x, int ldo, float eps) -> (Tensor, Tensor)", &l2norm_rows);
+  m.def("l2norm_rows(Tensor x, int ldo, float eps, int rows_out=-1) -> (Tensor, Tensor)", &l2norm_rows);
   m.def("l2norm_bwd(Tensor dy, Tensor y, Tensor inv, int D, bool out_bf16) -> Tensor", &l2norm_bwd);
   m.def("transpose2d(Tensor x) -> Tensor", &transpose2d);
   m.def(

@@ -193,7 +193,7 @@ void launch_xent_bwd(const void* logits, bool in_bf16, int B, int ld, int C, con
 void launch_log_softmax_fwd(const void* x, bool is_bf16, int B, int ld, int C, float* y, hipStream_t s);
 void launch_log_softmax_bwd(const float* y, const float* dy, int B, int C, int ldo, void* dx, bool out_bf16,
                             hipStream_t s);
-void launch_l2norm_rows(const void* x, bool is_bf16, int R, int D, int ldo, bf16* y, float* inv_norm, float eps,
+void launch_l2norm_rows(const void* x, bool is_bf16, int R, int Rout, int D, int ldo, bf16* y, float* inv_norm, float eps,
                         hipStream_t s);
 void launch_l2norm_bwd(const void* dy, bool dy_bf16, int ldd, const bf16* y, int ldy, const float* inv_norm, int R,
                        int D, void* dx, bool out_bf16, hipStream_t s);

@@ -126,14 +126,19 @@ __global__ void __launch_bounds__(256) log_softmax_bwd_kernel(const float* __res
 // softmax-CE with its backward through the margin (guarding cos = +-1).
 // ---------------------------------------------------------------------------
 
-// rows of x [R][D] (fp32 or bf16) -> bf16 normalised rows [R][ldo] (zero-padded), inverse norms
+// rows of x [R][D] (fp32 or bf16) -> bf16 normalised rows [Rout][ldo] (zero-padded in both
+// dimensions, Rout >= R), inverse norms [Rout]
 template <typename T>
 __global__ void __launch_bounds__(256) l2norm_rows_kernel(const T* __restrict__ x, int R, int D, int ldo,
                                                           bf16* __restrict__ y, float* __restrict__ inv_norm,
                                                           float eps) {
   __shared__ float red[16];
   const int r = blockIdx.x;
-  if (r >= R) return;
+  if (r >= R) {  // padding rows of the GEMM operand (R rounded up to the tile): zero, inverse norm 0
+    for (int j = threadIdx.x; j < ldo; j += blockDim.x) y[(size_t)r * ldo + j] = f2bf(0.f);
+    if (threadIdx.x == 0) inv_norm[r] = 0.f;
+    return;
+  }
   const T* row = x + (size_t)r * D;
   float s = 0.f;
   for (int j = threadIdx.x; j < D; j += blockDim.x) {
@@ -294,13 +299,13 @@ void launch_log_softmax_bwd(const float* y, const float* dy, int B, int C, int l
     hipLaunchKernelGGL(log_softmax_bwd_kernel<float>, dim3(B), dim3(256), 0, s, y, dy, C, ldo, (float*)dx);
 }
 
-void launch_l2norm_rows(const void* x, bool is_bf16, int R, int D, int ldo, bf16* y, float* inv_norm, float eps,
-                        hipStream_t s) {
+void launch_l2norm_rows(const void* x, bool is_bf16, int R, int Rout, int D, int ldo, bf16* y, float* inv_norm,
+                        float eps, hipStream_t s) {
   if (is_bf16)
-    hipLaunchKernelGGL(l2norm_rows_kernel<bf16>, dim3(R), dim3(256), 0, s, (const bf16*)x, R, D, ldo, y, inv_norm,
+    hipLaunchKernelGGL(l2norm_rows_kernel<bf16>, dim3(Rout), dim3(256), 0, s, (const bf16*)x, R, D, ldo, y, inv_norm,
                        eps);
   else
-    hipLaunchKernelGGL(l2norm_rows_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)x, R, D, ldo, y,
+    hipLaunchKernelGGL(l2norm_rows_kernel<float>, dim3(Rout), dim3(256), 0, s, (const float*)x, R, D, ldo, y,
                        inv_norm, eps);
 }
 

@@ -562,13 +562,16 @@ def log_softmax_bwd(y, dy, ldo, out_bf16):
     return out.to(torch.bfloat16 if out_bf16 else torch.float32)
 
 
-def l2norm_rows(x, ldo, eps):
+def l2norm_rows(x, ldo, eps, rows_out=-1):
     xf = _f(x)
     n = xf.norm(dim=1).clamp_min(eps)
     y = xf / n.unsqueeze(1)
-    if ldo > y.shape[1]:
-        y = F.pad(y, (0, ldo - y.shape[1]))
-    return y, 1.0 / n
+    inv = 1.0 / n
+    pad_r = max(0, rows_out - y.shape[0])
+    if ldo > y.shape[1] or pad_r:
+        y = F.pad(y, (0, ldo - y.shape[1], 0, pad_r))
+        inv = F.pad(inv, (0, pad_r))
+    return y, inv
 
 
 def l2norm_bwd(dy, y, inv, D, out_bf16):

@@ -1319,10 +1319,7 @@ def arcface_rows(x, weight, labels, s=30.0, m=0.5, easy_margin=True, with_margin
     Dp = round_up(D, 8) if x.is_cuda else D
     Cp = round_up(C, 64) if x.is_cuda else C
     xn, _ = k.l2norm_rows(x.contiguous(), Dp, 1e-12)
-    w = weight.detach()
-    if Cp > C:
-        w = F.pad(w, (0, 0, 0, Cp - C))
-    wn, _ = k.l2norm_rows(w.contiguous(), Dp, 1e-12)
+    wn, _ = k.l2norm_rows(weight.detach().contiguous(), Dp, 1e-12, Cp)  # zero rows C..Cp
     if not x.is_cuda:
         xn, wn = xn.float(), wn.float()
     cos = k.linear_fwd(xn, wn, None, 0)
@@ -1367,10 +1364,7 @@ class _ArcFace(Function):
         Dp = round_up(D, 8) if x.is_cuda else D
         Cp = round_up(C, 64) if x.is_cuda else C
         xn, inv_x = k.l2norm_rows(x.contiguous(), Dp, 1e-12)
-        wsrc = weight.detach()
-        if Cp > C:
-            wsrc = F.pad(wsrc, (0, 0, 0, Cp - C))
-        wn, inv_w = k.l2norm_rows(wsrc.contiguous(), Dp, 1e-12)
+        wn, inv_w = k.l2norm_rows(weight.detach().contiguous(), Dp, 1e-12, Cp)  # zero rows C..Cp
         if not x.is_cuda:
             xn, wn = xn.float(), wn.float()
         cos = k.linear_fwd(xn, wn, None, 0)  # [B, Cp]
@@ -1397,7 +1391,7 @@ class _ArcFace(Function):
             dx = k.l2norm_bwd(dxn, xn, inv_x, D, False)
         if ctx.needs_input_grad[1]:
             dwn = k.linear_wgrad(dcos, xn)  # [Cp, Dp] fp32
-            dw = k.l2norm_bwd(dwn.contiguous(), wn, inv_w, D, False)[:C]
+            dw = k.l2norm_bwd(dwn[:C].contiguous(), wn, inv_w, D, False)  # the C real rows only
         return dx, dw, None, None, None, None, None
 
 
