@@ -293,9 +293,15 @@ def main(argv=None):
     elif dist_on:
         comm = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
     sync = None
-    if dist_on and not a.syncbn and a.syncbn_phase and not a.graph:
+    if dist_on and not a.syncbn and a.syncbn_phase:
         # second phase: the reference's SyncBN (BASELINE/main.py:148) on the dedicated BN communicator
         pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group)
+        if a.graph:  # recapture: the BN collectives (on the BN communicator) go into the new graph
+            from ddp_classification_pytorch_amd.engine.graph import GraphedStep
+
+            run = graphed = None
+            torch.cuda.empty_cache()
+            run = GraphedStep(step, warmup=2, distributed=True)
         for _ in range(2):
             run()
         sdt, _ = timed(a.steps)

@@ -516,26 +516,31 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
 
 // Weight-gradient configurations the autotuner (g_tune[25] = 1, DCP_AUTOTUNE) times per problem,
 // as g_tune overrides: [5] workgroups per CU of the split-K plan, [7] = 2 no 256-tile kernel,
-// [12] = 32 32-row k-tiles, [15] = 1 no direct 3x3 kernel.  The split count changes the partial
+// [12] = 32 32-row k-tiles, [15] = 1 no direct 3x3 kernel, [27] = 64 at most 64 splits (one reduce
+// launch instead of two: pays at small batches, where the launches dominate).  The split count changes the partial
 // slabs, so the choice is made here, where they are allocated (see launch_tap_gemm for the
 // forward / data-gradient side).  Every configuration reduces the split partials in a fixed
 // order, but a different split count sums the rows in another order (fp32 rounding).
 namespace {
 struct WgCfg {
-  int t5, t7, t12, t15;
+  int t5, t7, t12, t15, t27;
 };
-const WgCfg kWgCfgs[] = {{0, 0, 0, 0}, {1, 0, 0, 0}, {2, 0, 0, 0}, {4, 0, 0, 0},
-                         {8, 0, 0, 0}, {0, 2, 0, 0}, {0, 0, 32, 0}, {0, 0, 0, 1}};
+const WgCfg kWgCfgs[] = {{0, 0, 0, 0, 0}, {1, 0, 0, 0, 0}, {2, 0, 0, 0, 0},  {4, 0, 0, 0, 0},
+                         {8, 0, 0, 0, 0}, {0, 2, 0, 0, 0}, {0, 0, 32, 0, 0}, {0, 0, 0, 1, 0},
+                         {0, 0, 0, 0, 64}, {0, 2, 0, 0, 64}, {0, 0, 0, 1, 64}};
 std::mutex g_wg_mu;
 std::unordered_map<std::string, int> g_wg_choice;
 struct WgOverride {
-  int saved[4];
+  int saved[5];
   explicit WgOverride(const WgCfg& c) {
     saved[0] = dcp::g_tune[5]; saved[1] = dcp::g_tune[7]; saved[2] = dcp::g_tune[12]; saved[3] = dcp::g_tune[15];
+    saved[4] = dcp::g_tune[27];
     dcp::g_tune[5] = c.t5; dcp::g_tune[7] = c.t7; dcp::g_tune[12] = c.t12; dcp::g_tune[15] = c.t15;
+    dcp::g_tune[27] = c.t27;
   }
   ~WgOverride() {
     dcp::g_tune[5] = saved[0]; dcp::g_tune[7] = saved[1]; dcp::g_tune[12] = saved[2]; dcp::g_tune[15] = saved[3];
+    dcp::g_tune[27] = saved[4];
   }
 };
 }  // namespace
@@ -566,7 +571,7 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
                       part.data_ptr<float>(), zero_page(dy.get_device()), ncu, st);
   };
   if (dcp::g_tune[25] != 1 || dcp::g_tune[5] || dcp::g_tune[7] || dcp::g_tune[12] || dcp::g_tune[15] ||
-      (int64_t)N * Ho * Wo == 0) {
+      dcp::g_tune[27] || (int64_t)N * Ho * Wo == 0) {
     run();
     return dw;
   }

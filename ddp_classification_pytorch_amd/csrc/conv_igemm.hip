@@ -2879,6 +2879,9 @@ int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_spl
   int splits = target / tiles;
   int max_splits = (M + 255) / 256;
   if (splits > max_splits) splits = max_splits;
+  // g_tune[27] > 0: at most that many splits (64: the one-level reduction, no second launch --
+  // small batches, where every launch counts; an autotuner candidate)
+  if (g_tune[27] > 0 && splits > g_tune[27]) splits = g_tune[27];
   if (splits < 1) splits = 1;
   int rps = (M + splits - 1) / splits;
   rps = (rps + 63) / 64 * 64;

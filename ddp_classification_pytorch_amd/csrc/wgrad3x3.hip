@@ -192,7 +192,8 @@ int wgrad3x3_splits(int N, int H, int W, int C, int Co, int num_cu) {
   const int R = w3_rows(H, W);
   if (R == 0) return 0;
   const int strips = N * ((H + R - 1) / R);
-  const int splits = std::max(1, std::min(strips, num_cu / pairs));
+  int splits = std::max(1, std::min(strips, num_cu / pairs));
+  if (g_tune[27] > 1) splits = std::max(1, std::min(splits, g_tune[27] / 2));  // cap on the slices (2 per split)
   const int sps = (strips + splits - 1) / splits;
   return 2 * ((strips + sps - 1) / sps);
 }

@@ -64,6 +64,14 @@ class HostCounters:
             o.on_graph_replay()
 
 
+def _capture_mode():
+    """With a process group, capture thread-locally: the RCCL process group's watchdog thread polls
+    the HIP events of collectives issued before the capture (the warm-up steps' all-reduces), and a
+    global-mode capture turns that query in another thread into a capture error that aborts the
+    process.  The capturing thread itself is still checked."""
+    return "thread_local" if torch.distributed.is_initialized() else "global"
+
+
 class GraphedStep:
     """``GraphedStep(step_fn, warmup=3)``: runs ``step_fn`` ``warmup`` times on a side stream
     (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
@@ -87,7 +95,7 @@ class GraphedStep:
         if counters is not None:
             counters.begin_capture()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
             self.out = step_fn()
         if counters is not None:
             counters.end_capture()
@@ -148,7 +156,7 @@ class StepGrapher:
             if self.counters is not None:
                 self.counters.begin_capture()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=_capture_mode()):
                 self.out = self.fn(*self.static)
             if self.counters is not None:
                 self.counters.end_capture()

@@ -30,6 +30,8 @@ bucket", §5.8 items 1-3):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -38,9 +40,18 @@ from .. import _ext
 
 _COMM_STREAMS = {}
 CHUNK = 4096
+# Where the bucket work (pack, all-reduce, per-bucket optimizer) runs: a side stream overlapping
+# the rest of backward when there is communication to hide (world size > 1), the compute stream at
+# world size 1 -- the side stream's fork / join edges cost ~0.15 ms per bucket in a replayed HIP
+# graph at batch 32 (6.13 ms plain, 6.30 compute stream, 6.85-6.94 side stream with 5 buckets:
+# profiles/r4/ddp_stream_ab_b32.txt).  DCP_COMM_STREAM=1 / 0 forces either.
+_SIDE_STREAM_ENV = os.environ.get("DCP_COMM_STREAM", "auto")
 
 
-def _comm_stream(device):
+def _comm_stream(device, world=2):
+    side = _SIDE_STREAM_ENV == "1" or (_SIDE_STREAM_ENV != "0" and world > 1)
+    if not side:
+        return torch.cuda.current_stream(device)
     s = _COMM_STREAMS.get(device)
     if s is None:
         s = _COMM_STREAMS[device] = torch.cuda.Stream(device=device)
@@ -87,6 +98,9 @@ class BucketReducer:
         self.cuda = self.device.type == "cuda"
         self.group = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # a process group of any size all-reduces (world 1 included: a forced single-GPU DDP run
+        # then measures the real RCCL launches); no group at all (plain single process) does not
+        self.reduce = dist.is_initialized()
         self.cap = int(bucket_cap_mb * 2**20)
         self.first_cap = int(first_bucket_mb * 2**20) if first_bucket_mb else self.cap
         self.comm_dtype = comm_dtype
@@ -208,7 +222,7 @@ class BucketReducer:
         grads = [p.grad for p in b.params]
         present = [g is not None for g in grads]
         if self.cuda:
-            comm = _comm_stream(self.device)
+            comm = _comm_stream(self.device, self.world)
             comm.wait_stream(self._compute)
             with torch.cuda.stream(comm):
                 if self._ev is not None and not any(x.launched for x in self.buckets if x is not b):
@@ -236,7 +250,7 @@ class BucketReducer:
         for g, v in zip(grads, b.views):
             if g.data_ptr() != v.data_ptr():
                 g.record_stream(comm)  # the fresh autograd gradient is read here, freed by the compute side
-        if self.world > 1:
+        if self.reduce:
             dist.all_reduce(b.comm_buf, group=self.group)
         if unpack is not None:
             K.mt_copy(unpack, chunks, 1.0, 1)
@@ -249,7 +263,7 @@ class BucketReducer:
                     dst.zero_()
                 else:
                     dst.copy_(g.reshape(-1).to(torch.float32) / self.world)
-            if self.world > 1:
+            if self.reduce:
                 dist.all_reduce(b.comm_buf, group=self.group)
             if b.comm_buf is not b.grad_buf:
                 b.grad_buf.copy_(b.comm_buf.float())
@@ -265,7 +279,7 @@ class BucketReducer:
         if not by_opt:
             return
         if self.cuda:
-            with torch.cuda.stream(_comm_stream(self.device)):
+            with torch.cuda.stream(_comm_stream(self.device, self.world)):
                 for o, ps in by_opt.values():
                     o.step_params(ps)
         else:
@@ -279,7 +293,7 @@ class BucketReducer:
             if not b.launched:
                 self._launch(b)
         if self.cuda:
-            comm = _comm_stream(self.device)
+            comm = _comm_stream(self.device, self.world)
             if self._ev is not None:
                 self._ev[0].record(self._compute)
                 self._ev[2].record(comm)

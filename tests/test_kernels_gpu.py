@@ -780,12 +780,14 @@ def test_bn_act_mask_and_masked_dgrad_bn(K):
     assert relerr(s1, s0) < 1e-5
 
 
-@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4)), ((14, 4),), ((14, 3),), ((12, 32), (14, 3))])
+@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4)), ((14, 4),), ((14, 3),), ((12, 32), (14, 3)),
+                                 ((27, 8),), ((27, 8), (15, 1))])
 @pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
                                    (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1)])
 def test_conv_wgrad_variants(K, cfg, shape):
-    """Weight gradient with 32-row k-tiles, another split plan, and the narrow (Co <= 64) kernel's
-    256- / 192-column tiles (g_tune[14] = 4 / 3), against the fp32 reference."""
+    """Weight gradient with 32-row k-tiles, another split plan, the narrow (Co <= 64) kernel's
+    256- / 192-column tiles (g_tune[14] = 4 / 3) and a capped split count (g_tune[27]; direct 3x3
+    and implicit GEMM), against the fp32 reference."""
     N, H, W, Ci, Co, k, s, p = shape
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     dy, x = rnd(N, Ho, Wo, Co), rnd(N, H, W, Ci)

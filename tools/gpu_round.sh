@@ -8,6 +8,8 @@
 #   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
 #   profcfg=CFG     the same for another bench config (e.g. arcface)
 #   profsmall       the same for the batch-32 HIP-graph step (200 replays)
+#   ddpab           batch-32 graph: no DDP vs world-1 bucket engine variants (side stream, same stream, 100 MB buckets)
+#   profddp         the same for the world-1 RCCL bucket-engine batch-32 HIP-graph step
 #   graphs          HIP-graph batch 32 / 128 twice, then the headline batch
 #   pmc             three PMC passes (SQ: MFMA busy / LDS conflicts / waits; FETCH_SIZE; WRITE_SIZE)
 #   gloo2           bench.py --gpus 2 over gloo on this one GPU (self-launched ranks)
@@ -94,6 +96,25 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_small -o run -- python3 -u bench.py --batch 32 --graph --steps 200 --warmup 5 \
         > $O/prof_small.log 2>&1
       echo prof small done ;;
+    profddp)
+      # rocprofv3 kernel statistics of the world-1 RCCL bucket-engine batch-32 HIP-graph step
+      prof_env
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_ddp -o run -- python3 -u bench.py --force-ddp --batch 32 --graph --steps 200 --warmup 5 --no-syncbn-phase --telemetry-steps 0 \
+        > $O/prof_ddp.log 2>&1
+      echo prof ddp done ;;
+    ddpab)
+      # batch-32 HIP-graph step: no DDP, world-1 bucket engine (default / compute-stream buckets /
+      # one 100 MB bucket), interleaved twice
+      for r in 1 2; do
+        timeout -k 10 240 python -u bench.py --batch 32 --graph --steps 100 --warmup 5 > $O/ddpab_plain_$r.log 2>&1
+        echo "plain: $(grep -o '"ms_per_step": [0-9.]*' $O/ddpab_plain_$r.log)"
+        timeout -k 10 240 python -u bench.py --force-ddp --no-syncbn-phase --telemetry-steps 0 --batch 32 --graph --steps 100 --warmup 5 > $O/ddpab_ddp_$r.log 2>&1
+        echo "ddp: $(grep -o '"ms_per_step": [0-9.]*' $O/ddpab_ddp_$r.log)"
+        DCP_COMM_STREAM=0 timeout -k 10 240 python -u bench.py --force-ddp --no-syncbn-phase --telemetry-steps 0 --batch 32 --graph --steps 100 --warmup 5 > $O/ddpab_same_$r.log 2>&1
+        echo "ddp same stream: $(grep -o '"ms_per_step": [0-9.]*' $O/ddpab_same_$r.log)"
+        timeout -k 10 240 python -u bench.py --force-ddp --no-syncbn-phase --telemetry-steps 0 --bucket-cap-mb 100 --batch 32 --graph --steps 100 --warmup 5 > $O/ddpab_big_$r.log 2>&1
+        echo "ddp 100MB buckets: $(grep -o '"ms_per_step": [0-9.]*' $O/ddpab_big_$r.log)"
+      done ;;
     graphs)
       # HIP-graph batch 32 / 128 (x2) and the headline batch
       for r in 1 2; do
