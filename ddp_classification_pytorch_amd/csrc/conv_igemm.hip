@@ -2806,6 +2806,45 @@ __global__ void __launch_bounds__(256) split_reduce2_kernel(const float4* __rest
   }
 }
 
+// One launch for a narrow reduction (few columns, up to a few thousand splits: the BN-backward sums
+// of a small batch's dgrad epilogue, 2C columns over one partial row per 128-pixel tile): a
+// 1024-thread workgroup per 64 float4 columns, its 16 waves striding over the split rows with 8
+// loads in flight each, then a fixed-order LDS combine -- deterministic, no second launch.
+__global__ void __launch_bounds__(1024) split_reduce_rows_kernel(const float4* __restrict__ part, int splits, int n4,
+                                                                 float4* __restrict__ out) {
+  __shared__ float4 red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+    int k = w;
+    for (; k + 7 * 16 < splits; k += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 16 * u) * n4 + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+      }
+    }
+    for (; k < splits; k += 16) {
+      const float4 v = part[(size_t)k * n4 + col];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < n4) {
+    float4 t = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      const float4 v = red[q][lane];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    out[col] = t;
+  }
+}
+
 unsigned* ticket_counters(int n) {
   static std::mutex mu;
   static unsigned* pool[64] = {nullptr};
@@ -2830,6 +2869,13 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
   const int chunks = (splits + 63) / 64;
   if (chunks == 1) {
     hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, 1), dim3(256), 0, stream, (const float4*)part,
+                       splits, n4, (float4*)out);
+    return;
+  }
+  // narrow and not too deep (a small batch's BN-backward sums: 2C <= 4096 columns, <= 2048 tiles):
+  // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[29] = 2 off
+  if (n4 <= 1024 && splits <= 2048 && g_tune[29] != 2) {
+    hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 63) / 64), dim3(1024), 0, stream, (const float4*)part,
                        splits, n4, (float4*)out);
     return;
   }

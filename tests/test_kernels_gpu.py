@@ -347,6 +347,8 @@ def test_conv_dgrad_fused_add(K, Ci, Co, k, s):
     (2, 14, 128, 512, 1, False, False, 1),  # conv3 consuming BN2, 128-channel tiles
     (3, 9, 72, 40, 3, True, False, 0),      # ragged M / channels, identity activation
     (8, 7, 512, 2048, 1, False, True, 1),   # layer4: M = 392 (not a multiple of 128)
+    (4, 56, 256, 64, 1, True, True, 1),     # batch-4 layer1: 98 tiles -> the one-launch row reduction
+    (40, 56, 64, 64, 3, False, False, 1),   # 980 tiles: the row reduction's 8-deep loop and tail
 ])
 def test_conv_dgrad_bn_fused(K, N, H, Ci, Co, k, add, res, act):
     """dgrad epilogue fused with the BN(+ReLU)(+residual) backward reduction: the masked
@@ -783,7 +785,8 @@ def test_bn_act_mask_and_masked_dgrad_bn(K):
 @pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4)), ((14, 4),), ((14, 3),), ((12, 32), (14, 3)),
                                  ((27, 8),), ((27, 8), (15, 1))])
 @pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
-                                   (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1)])
+                                   (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1),
+                                   (8, 56, 56, 64, 64, 1, 1, 0)])  # > 64 splits: one-launch row reduction
 def test_conv_wgrad_variants(K, cfg, shape):
     """Weight gradient with 32-row k-tiles, another split plan, the narrow (Co <= 64) kernel's
     256- / 192-column tiles (g_tune[14] = 4 / 3) and a capped split count (g_tune[27]; direct 3x3
