@@ -19,6 +19,8 @@
 //    slab pass.
 #include <algorithm>
 
+#include <type_traits>
+
 #include "common.cuh"
 #include "launchers.h"
 #include "pool_gather.cuh"
@@ -363,7 +365,12 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float g3[4] = {0.f, 0.f, 0.f, 0.f};  // G3 = sum X: plain adds of the B fragments (VALU, beside MFMAs)
+  // G3 = sum X: an MFMA of a ones A-fragment (k-padding pixels 0) with the B fragments -- every
+  // row of the 16 x 16 result is the column sum (the VALU adds it replaced were a quarter of the
+  // kernel's VALU work, which sets its time)
+  f32x4 g3[4];
+#pragma unroll
+  for (int tx = 0; tx < 4; ++tx) g3[tx] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // phase-E operands of a row, loaded a barrier interval ahead (their HBM latency overlaps the
   // previous interval's MFMAs).  An item is a pixel pair (2j, 2j + 1) x an 8-channel chunk: pixel
@@ -400,10 +407,12 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
   };
   // ---- phase E of row gg: g' and z - mu into the A images of set gg & 1 (same masking, order
   // of the window sum and rounding as gather_pool_grad + maxpool_bn_bwd) ----
-  auto phase_e = [&](int gg) {
+  // ROW1: the row lies in two pooled rows (odd y, not the last): a uniform branch per row, so an
+  // even row's items test 1 (even pixel) + 2 (odd pixel) windows instead of 2 + 4
+  auto phase_e_rows = [&](int gg, auto row1_tag) {
+    constexpr bool row1 = decltype(row1_tag)::value;
     const int y = gg - (gg / H) * H;
     const int h0 = y >> 1, h1 = (y + 1) >> 1;
-    const bool row1 = (h1 != h0) & (h1 < p.Ho);
     char* ag = smem + (gg & 1) * 32768;
 #pragma unroll
     for (int k = 0; k < NIT; ++k) {
@@ -458,6 +467,14 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
       }
     }
   };
+  auto phase_e = [&](int gg) {
+    const int y = gg - (gg / H) * H;
+    const int h0 = y >> 1, h1 = (y + 1) >> 1;
+    if ((h1 != h0) & (h1 < p.Ho))
+      phase_e_rows(gg, std::true_type{});
+    else
+      phase_e_rows(gg, std::false_type{});
+  };
   // ---- phase M of row gg: this wave's A image of set gg & 1 against input row y + ty - 2 ----
   auto phase_m = [&](int gg) {
     const int n = gg / H, y = gg - n * H;
@@ -471,14 +488,16 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
 #pragma unroll
       for (int tx = 0; tx < 4; ++tx)
         bf[tx] = sb_tr(brow + (ra + tx) * 32 + pp * 8, brow + (rb + tx) * 32 + pp * 8);
-      if (half == 0)  // wave-uniform
+      if (half == 0) {  // wave-uniform: G3 = sum X on the matrix pipe, A = 1 on the row's W pixels
+        bf16x8 one;
 #pragma unroll
-        for (int tx = 0; tx < 4; ++tx)
+        for (int j = 0; j < 4; ++j) {
+          one[j] = f2bf(base + j < (uint32_t)W ? 1.f : 0.f);
+          one[4 + j] = f2bf(base + 8 + j < (uint32_t)W ? 1.f : 0.f);
+        }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            g3[tx] += (base + j < (uint32_t)W) ? bf2f(bf[tx][j]) : 0.f;
-            g3[tx] += (base + 8 + j < (uint32_t)W) ? bf2f(bf[tx][4 + j]) : 0.f;
-          }
+        for (int tx = 0; tx < 4; ++tx) g3[tx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(one, bf[tx], g3[tx], 0, 0, 0);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t col = i * 16 + pp * 4;
@@ -538,14 +557,9 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         part[(half * 64 + i * 16 + (int)kq * 4 + r) * 256 + col + tx * 16] = acc[i][tx][r];
-  if (half == 0)
+  if (half == 0 && kq == 0)  // row 0 of the result (lanes 0..15, register 0)
 #pragma unroll
-    for (int tx = 0; tx < 4; ++tx) {
-      float t = g3[tx];
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      if (kq == 0) part[128 * 256 + col + tx * 16] = t;
-    }
+    for (int tx = 0; tx < 4; ++tx) part[128 * 256 + col + tx * 16] = g3[tx][0];
   float* red = (float*)smem;  // [2][512][8] (the A images are free)
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
