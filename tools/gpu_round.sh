@@ -8,6 +8,7 @@
 #   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
 #   profcfg=CFG     the same for another bench config (e.g. arcface)
 #   profsmall       the same for the batch-32 HIP-graph step (200 replays)
+#   pmcconv=S:CFGS  PMC passes (SQ / TCC hit-miss / FETCH_SIZE) over forward convs of shapes S under configs CFGS
 #   ddpab           batch-32 graph: no DDP vs world-1 bucket engine variants (side stream, same stream, 100 MB buckets)
 #   profddp         the same for the world-1 RCCL bucket-engine batch-32 HIP-graph step
 #   graphs          HIP-graph batch 32 / 128 twice, then the headline batch
@@ -115,6 +116,18 @@ for step in "$@"; do
         timeout -k 10 240 python -u bench.py --force-ddp --no-syncbn-phase --telemetry-steps 0 --bucket-cap-mb 100 --batch 32 --graph --steps 100 --warmup 5 > $O/ddpab_big_$r.log 2>&1
         echo "ddp 100MB buckets: $(grep -o '"ms_per_step": [0-9.]*' $O/ddpab_big_$r.log)"
       done ;;
+    pmcconv=*)
+      # PMC passes over forward convs of chosen shapes under chosen configs, e.g.
+      # pmcconv=13,16:26=0,26=1 (tools/pmc_conv.py; kernels told apart by name)
+      a=${step#pmcconv=}; shp=${a%%:*}; cf=${a#*:}
+      prof_env
+      export DCP_AUTOTUNE=0
+      timeout -s KILL 60 rocprofv3 -L > $O/pmc_counters_avail.txt 2>&1 || true
+      P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $P1 --output-format csv -d $O/pmcc1 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc1.log 2>&1
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc2 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc2.log 2>&1
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc3 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc3.log 2>&1
+      echo pmcconv done ;;
     graphs)
       # HIP-graph batch 32 / 128 (x2) and the headline batch
       for r in 1 2; do
