@@ -49,10 +49,15 @@ __device__ __forceinline__ float dpp_f(float v) {
 }
 }  // namespace
 
-template <int NSUB>  // W = 16 * NSUB output columns
+// W output columns in NSUB 16-pixel MFMA tiles (W a multiple of 8: the last tile of a W = 56 row --
+// the 112 px ArcFace input -- is half valid; its other lanes compute unused columns, skipped in
+// the stores and the statistics)
+template <int NSUB, int W = NSUB * 16>
 __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
-  constexpr int W = NSUB * 16;
+  constexpr bool PART = W != NSUB * 16;
+  constexpr int NST = PART ? (16 * W - 192 + 255) / 256 : NSUB;  // 16-byte stores per step, last wave
   static_assert(W + 4 <= kPlanePx, "row does not fit a plane");
+  static_assert(W % 8 == 0 && W > 16 * (NSUB - 1) && W <= 16 * NSUB, "W in the last tile");
   // [kSlots * kSlotBytes ring][2 * W * 128 B output staging of one row pair]
   extern __shared__ __attribute__((aligned(16))) char ring[];
   char* stage = ring + kSlots * kSlotBytes;
@@ -109,7 +114,9 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // also publishes the zeroed padding
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSUB) : "memory");
+      // (PART: the last store instruction has no lanes in the upper waves, which then issued
+      // NST stores -- the fewest of any wave; a smaller count only waits longer)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
@@ -154,7 +161,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
         const uint32_t px = rp * W + i * 16 + l16;
         const uint32_t slot = (((2 * cg + j) * 4 + kq) ^ (px & 15));
-        *(bf16x4*)(stage + px * 128 + slot * 8) = o;
+        if (!PART || i * 16 + (int)l16 < W) *(bf16x4*)(stage + px * 128 + slot * 8) = o;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // not __syncthreads: keep the loads in flight
     __builtin_amdgcn_s_barrier();
@@ -163,6 +170,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
 #pragma unroll
     for (int k = 0; k < NSUB; ++k) {
       const uint32_t q = k * 256 + tid, px = q >> 3, c = q & 7, sw = px & 15;
+      if (PART && q >= 16u * W) break;  // 2 W pixels x 8 chunks
       u32x4 v = *(const u32x4*)(stage + px * 128 + ((c ^ (sw >> 1)) << 4));
       if (sw & 1) v = u32x4{v[2], v[3], v[0], v[1]};
       *(u32x4*)(ydst + (size_t)q * 8) = v;
@@ -175,6 +183,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
       for (int c = 0; c < 8; ++c)
 #pragma unroll
         for (int i = 0; i < NSUB; ++i) {
+          if (PART && i == NSUB - 1 && (int)l16 >= W - 16 * (NSUB - 1)) continue;
           const float d = acc[c >> 2][i][c & 3] - shf[c];
           s1[c] += d;
           s2[c] = fmaf(d, d, s2[c]);
@@ -185,7 +194,9 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
   if (p.part) {
     // lane (n, mean, M2) per channel, merged over the 16 lanes of the pixel group (equal counts),
     // then across the two row waves of each channel half through LDS
-    float n = (float)(NSUB * nsteps), mean[8], m2[8];
+    // lanes of a partial last tile hold one column fewer: count-weighted merges (PART)
+    const int lane_cols = (PART && (int)l16 >= W - 16 * (NSUB - 1)) ? NSUB - 1 : NSUB;
+    float n = (float)(lane_cols * nsteps), mean[8], m2[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const float a1 = s1[c], a2 = s2[c];
@@ -193,14 +204,26 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
       m2[c] = fmaxf(a2 - a1 * a1 / n, 0.f);
     }
     auto level = [&](auto partner) {
+      if constexpr (PART) {
+        const float nb = partner(n), nt = n + nb, f = nb / nt;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float mb = partner(mean[c]), m2b = partner(m2[c]);
-        const float d = mb - mean[c];
-        mean[c] += 0.5f * d;
-        m2[c] += m2b + d * d * (0.5f * n);
+        for (int c = 0; c < 8; ++c) {
+          const float mb = partner(mean[c]), m2b = partner(m2[c]);
+          const float d = mb - mean[c];
+          mean[c] += d * f;
+          m2[c] += m2b + d * d * n * f;
+        }
+        n = nt;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const float mb = partner(mean[c]), m2b = partner(m2[c]);
+          const float d = mb - mean[c];
+          mean[c] += 0.5f * d;
+          m2[c] += m2b + d * d * (0.5f * n);
+        }
+        n *= 2.f;
       }
-      n *= 2.f;
     };
     level([](float v) { return dpp_f<0x128>(v); });
     level([](float v) { return dpp_f<0x124>(v); });
@@ -301,12 +324,12 @@ __device__ __forceinline__ bf16x8 sb_tr(const char* a, const char* b) {
 }
 }  // namespace
 
-template <int NSUB>  // W = 16 NSUB output columns
+template <int W>  // output columns (a multiple of 8)
 // one workgroup of 8 waves per CU (two per SIMD, so the gather phase's dependent VALU chains
 // and the MFMAs of one wave hide behind the other's): wave w owns tap row ty = w & 3 and the g'
 // (w < 4) or the z - mu image (w >= 4): 16 accumulator tiles
 __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
-  constexpr int W = NSUB * 16, NKS = (W + 31) / 32;
+  constexpr int NKS = (W + 31) / 32;
   static_assert(W + 4 <= kSbRing && NKS * 32 <= 128, "row does not fit");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // A images, double-buffered by row parity: set b at smem + b * 32 KB = {g' [128 px][64],
@@ -594,7 +617,8 @@ __global__ void stem_bwd_dw_kernel(const float* __restrict__ tot, const float* _
 }
 
 bool stem_bwd_supported(int H, int W, int C, int Ho, int Wo) {
-  return C == kStemCo && H % 2 == 0 && W % 16 == 0 && W >= 16 && W + 4 <= kSbRing && Ho == H / 2 && Wo == W / 2;
+  return C == kStemCo && H % 2 == 0 && (W % 16 == 0 || W == 56) && W >= 16 && W + 4 <= kSbRing && Ho == H / 2 &&
+         Wo == W / 2;
 }
 int stem_bwd_blocks(int N, int H, int num_cu) { return std::min(N * H, num_cu); }
 int stem_bwd_part_floats() { return kSbPart; }
@@ -606,13 +630,13 @@ void launch_stem_bwd(const bf16* z, const bf16* x16, const bf16* dy, const uint8
   p.rpb = (N * H + nblocks - 1) / nblocks;
   p.ablate = g_tune[17];
   constexpr int lds = 65536 + 9 * kSbSlot + 768;
-  switch (W / 16) {
-#define DCP_STEMB(NS_)                                                                                  \
-  case NS_:                                                                                             \
-    (void)hipFuncSetAttribute((const void*)stem_bwd_kernel<NS_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
-    hipLaunchKernelGGL(stem_bwd_kernel<NS_>, dim3(nblocks), dim3(512), lds, s, p);                      \
+  switch (W) {
+#define DCP_STEMB(W_)                                                                                  \
+  case W_:                                                                                             \
+    (void)hipFuncSetAttribute((const void*)stem_bwd_kernel<W_>, hipFuncAttributeMaxDynamicSharedMemorySize, lds); \
+    hipLaunchKernelGGL(stem_bwd_kernel<W_>, dim3(nblocks), dim3(512), lds, s, p);                      \
     break;
-    DCP_STEMB(1) DCP_STEMB(2) DCP_STEMB(3) DCP_STEMB(4) DCP_STEMB(5) DCP_STEMB(6) DCP_STEMB(7)
+    DCP_STEMB(16) DCP_STEMB(32) DCP_STEMB(48) DCP_STEMB(56) DCP_STEMB(64) DCP_STEMB(80) DCP_STEMB(96) DCP_STEMB(112)
 #undef DCP_STEMB
     default: break;
   }
@@ -630,14 +654,18 @@ void launch_stem_bwd_dw(const float* tot, const float* sums, const float* scale,
 int stem_fwd_blocks(int N, int H) { return N * ((H + kStemRows - 1) / kStemRows); }
 
 bool stem_fwd_supported(int H, int W, int C, int Co, int KH, int KW) {
-  return C == 16 && Co == kStemCo && KH == 4 && KW == 4 && H % 2 == 0 && H > 0 && W % 16 == 0 && W >= 16 &&
-         W + 4 <= kPlanePx;
+  return C == 16 && Co == kStemCo && KH == 4 && KW == 4 && H % 2 == 0 && H > 0 && (W % 16 == 0 || W == 56) &&
+         W >= 16 && W + 4 <= kPlanePx;
 }
 
 void launch_stem_fwd(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
                      hipStream_t s) {
   StemParams p{x, w, y, part, zero, H, (H + kStemRows - 1) / kStemRows};
   const dim3 grid(stem_fwd_blocks(N, H)), block(256);
+  if (W == 56) {  // the 112 px input (ArcFace): 3.5 tiles per row
+    hipLaunchKernelGGL((stem_fwd_kernel<4, 56>), grid, block, kSlots * kSlotBytes + 4 * 16 * 256, s, p);
+    return;
+  }
   switch (W / 16) {
 #define DCP_STEM(NS_) \
   case NS_: hipLaunchKernelGGL(stem_fwd_kernel<NS_>, grid, block, kSlots * kSlotBytes + NS_ * 16 * 256, s, p); break;

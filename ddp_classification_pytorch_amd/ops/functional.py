@@ -1526,7 +1526,7 @@ class _StemBNPool(Function):
 
 def stem_bn_pool_fusable(x16: torch.Tensor, act: str = "relu") -> bool:
     """Whether stem_bn_pool's fused kernels cover this input (GPU, training, ReLU/identity,
-    even H, W a multiple of 16 up to 112)."""
+    even H, W a multiple of 16 up to 112, or 56: the 112 px input)."""
     if not (x16.is_cuda and x16.dim() == 4 and x16.shape[-1] == 16 and act in ("relu", "none")
             and torch.is_grad_enabled()):
         return False

@@ -514,9 +514,10 @@ def test_conv_geo(K, N, H, Ci, Co, k, pad):
     assert relerr(dw, _ref.conv_wgrad_geo(dy.float(), x.float(), k, k, 1, pad)) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W", [(4, 112, 112), (3, 30, 48), (2, 8, 16), (2, 9, 9)])
+@pytest.mark.parametrize("N,H,W", [(4, 112, 112), (3, 30, 48), (2, 8, 16), (2, 9, 9), (3, 56, 56)])
 def test_stem_fwd(K, N, H, W):
-    """dedicated s2d stem kernel (stem.hip; (2, 9, 9) takes the implicit-GEMM fallback): output
+    """dedicated s2d stem kernel (stem.hip; (2, 9, 9) takes the implicit-GEMM fallback, W = 56 the
+    half-tile rows of the 112 px input): output
     vs the fp32 conv, its BN partials (taken from the fp32 accumulators) vs statistics of the
     fp32 conv, and BN finalize from the partials vs from the stored bf16 activations"""
     torch.manual_seed(0)
@@ -568,7 +569,7 @@ def test_s2d_stem_gpu_matches_plain_stem():
     assert relerr(g1, g0) < 1e-2
 
 
-@pytest.mark.parametrize("size,batch", [(64, 4), (96, 3), (224, 2)])
+@pytest.mark.parametrize("size,batch", [(64, 4), (96, 3), (224, 2), (112, 3)])  # 112: W = 56, half tiles
 def test_fused_stem_matches_unfused(size, batch):
     """The one-op stem (stem conv + BN + ReLU + max pool, one-pass fused backward in stem.hip)
     against the unfused chain (stem conv, BN+ReLU+pool, two-pass BN/pool backward, implicit-GEMM
