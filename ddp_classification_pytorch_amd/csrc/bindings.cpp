@@ -658,15 +658,18 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias
   TORCH_CHECK(K % 8 == 0 && Np % 8 == 0, "linear needs K and N multiples of 8");
   if (bias.has_value()) {
     CHECK_F32(*bias);
-    TORCH_CHECK(bias->numel() >= Np, "bias must be padded to the output width");
+    CHECK_CONTIG(*bias);
+    TORCH_CHECK(bias->numel() >= 1 && bias->numel() <= Np, "bias longer than the output width");
   }
   auto y = at::empty({B, Np}, bf16_like(x));
   dcp::TapList t;
   t.n = 1;
   t.dy[0] = t.dx[0] = t.widx[0] = 0;
   TORCH_CHECK(act >= 0 && act <= 2, "linear act must be 0 (none), 1 (relu) or 2 (sigmoid)");
+  // an unpadded bias (the output width rounded up for the GEMM): columns past it add 0
   dcp::launch_tap_gemm(bp(x), B, 1, 1, K, bp(w), Np, 1, bpm(y), 1, 1, 1, 1, 1, 1, 0, 0, t, nullptr, fp(bias),
-                       (int)act, zero_page(x.get_device()), cur_stream());
+                       (int)act, zero_page(x.get_device()), cur_stream(), nullptr, nullptr, nullptr, nullptr,
+                       nullptr, bias.has_value() ? (int)bias->numel() : 0);
   return y;
 }
 
@@ -869,6 +872,32 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
                                 (float)eps, fp(gamma), fp(beta), cp, cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean),
                                 fpm(run_var), (float)momentum, cur_stream());
   return {coef[0], coef[1], coef[2], coef[3]};
+}
+
+// stem weight: 7x7 master [Co,7,7,C<=4] fp32 -> its s2d form written into w16 [Co,4,4,16] (in place)
+void s2d_weight(const Tensor& w7, const Tensor& w16) {
+  CHECK_DEV(w7);
+  CHECK_F32(w7);
+  CHECK_CONTIG(w7);
+  CHECK_DEV(w16);
+  CHECK_F32(w16);
+  CHECK_CONTIG(w16);
+  TORCH_CHECK(w7.dim() == 4 && w7.size(1) == 7 && w7.size(2) == 7 && w7.size(3) <= 4 && w16.dim() == 4 &&
+                  w16.size(0) == w7.size(0) && w16.size(1) == 4 && w16.size(2) == 4 && w16.size(3) == 16,
+              "s2d_weight shapes");
+  dcp::launch_s2d_weight(w7.data_ptr<float>(), w7.size(0), w7.size(3), w16.data_ptr<float>(), cur_stream());
+}
+
+// gradient of the s2d form [Co,4,4,16] -> gradient of the 7x7 master [Co,7,7,C]
+Tensor s2d_weight_bwd(const Tensor& g16, int64_t C) {
+  CHECK_DEV(g16);
+  CHECK_F32(g16);
+  CHECK_CONTIG(g16);
+  TORCH_CHECK(g16.dim() == 4 && g16.size(1) == 4 && g16.size(2) == 4 && g16.size(3) == 16 && C >= 1 && C <= 4,
+              "s2d_weight_bwd shapes");
+  auto g7 = at::empty({g16.size(0), 7, 7, C}, g16.options());
+  dcp::launch_s2d_weight_bwd(g16.data_ptr<float>(), g16.size(0), (int)C, g7.data_ptr<float>(), cur_stream());
+  return g7;
 }
 
 Tensor colsum(const Tensor& x) {
@@ -1624,6 +1653,8 @@ TORCH_LIBRARY(dcp, m) {
       &xent_bwd);
   m.def("log_softmax_fwd(Tensor x, int C) -> Tensor", &log_softmax_fwd);
   m.def("log_softmax_bwd(Tensor y, Tensor dy, int ldo, bool out_bf16) -> Tensor", &log_softmax_bwd);
+  m.def("s2d_weight(Tensor w7, Tensor(a!) w16) -> ()", &s2d_weight);
+  m.def("s2d_weight_bwd(Tensor g16, int C) -> Tensor", &s2d_weight_bwd);
   m.def("l2norm_rows(Tensor x, int ldo, float eps, int rows_out=-1) -> (Tensor, Tensor)", &l2norm_rows);
   m.def("l2norm_bwd(Tensor dy, Tensor y, Tensor inv, int D, bool out_bf16) -> Tensor", &l2norm_bwd);
   m.def("transpose2d(Tensor x) -> Tensor", &transpose2d);

@@ -56,6 +56,7 @@ struct TapGemmParams {
   int ntaps, cpt, nkt, ldw;
   int relu;          // fused activation on the stored output: 0 none, 1 ReLU, 2 sigmoid (linear heads)
   const float* bias; // optional per-output-channel bias (linear heads)
+  int nbias;         // bias entries (channels past it add 0: an unpadded bias of a padded GEMM)
   const bf16* addsrc;  // optional: added to the stored output (same layout as dst; fused residual-gradient sum)
   FastDiv div_wy, div_hy, div_cpt;
   // per tap: dy (int8) | dx (int8) << 8 | weight tap index << 16.  Dword entries so a
@@ -755,7 +756,7 @@ tap_gemm_kernel(const TapGemmParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float t = acc[j][i][r];
-        if (p.bias) t += (co + r < p.Co) ? p.bias[co + r] : 0.f;
+        if (p.bias) t += (co + r < p.nbias) ? p.bias[co + r] : 0.f;
         if (p.relu == 1) t = fmaxf(t, 0.f);
         else if (p.relu == 2) t = 1.f / (1.f + __expf(-t));
         v[r] = t;
@@ -1357,11 +1358,13 @@ tap_gemm8_kernel(const TapGemmParams p) {
 // add source): the accumulators go to a whole-tile LDS image cut into 128 x 128 quadrants, which
 // the 256-thread groups store through tg_image_store (the 4-wave kernel's epilogue).
 // ---------------------------------------------------------------------------
-template <int WM, int WN, int NS, int EPI>
-__global__ void __launch_bounds__(64 * WM * WN, 2)
+// CFW = 8: 128 channels per wave (8 x 8 accumulator fragments, 256 registers: AGPRs at one wave
+// per SIMD) -- the 4-wave 256 x 256 tile, 64 MACs per staged byte
+template <int WM, int WN, int NS, int EPI, int CFW = 4>
+__global__ void __launch_bounds__(64 * WM * WN, CFW == 8 ? 1 : 2)
 tap_gemm_big_kernel(const TapGemmParams p) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
-  constexpr int BM = 128 * WM, BN = 64 * WN, BK = 32;
+  constexpr int BM = 128 * WM, BN = 16 * CFW * WN, BK = 32;
   constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;  // 64-byte rows, 16 rows per LDS-DMA
   constexpr int AI = BM / (NW * RPI), BI = BN / (NW * RPI), LPT = AI + BI;
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
@@ -1427,19 +1430,20 @@ tap_gemm_big_kernel(const TapGemmParams p) {
                                        0, 0);
   };
 
-  f32x4 acc[4][8];  // [16-channel fragment][16-pixel fragment]
+  f32x4 acc[CFW][8];  // [16-channel fragment][16-pixel fragment]
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < CFW; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = p.nkt;
   const uint32_t c = lane >> 4;
-  bf16x8 wf[4], af[8];
+  bf16x8 wf[CFW], af[8];
   auto frag_w = [&](int slot) {
     const char* Bs = smem + slot * STAGE + A_BYTES;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * 64 + j * 16 + (lane & 15), c));
+    for (int j = 0; j < CFW; ++j)
+      wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (16 * CFW) + j * 16 + (lane & 15), c));
   };
   auto frag_a = [&](int slot, int i0) {
     const char* As = smem + slot * STAGE;
@@ -1448,7 +1452,7 @@ tap_gemm_big_kernel(const TapGemmParams p) {
   };
   auto mfma_half = [&](int i0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < CFW; ++j)
 #pragma unroll
       for (int i = i0; i < i0 + 4; ++i)
         acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
@@ -1506,13 +1510,13 @@ tap_gemm_big_kernel(const TapGemmParams p) {
 
   // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
   {
-    char* Q = smem + (wm * QN + (wn * 64) / 128) * 32768;
-    const uint32_t cb = (wn * 64) % 128;
+    char* Q = smem + (wm * QN + (wn * 16 * CFW) / 128) * 32768;
+    const uint32_t cb = (wn * 16 * CFW) % 128;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint32_t pl = i * 16 + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < CFW; ++j) {
         const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
         bf16x4 o;
 #pragma unroll
@@ -2329,21 +2333,23 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>), dim3(grid), dim3(256), lds, stream, p);
 }
 
-template <int WM, int WN, int NS>
+template <int WM, int WN, int NS, int CFW = 4>
 static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
-  constexpr int BM = 128 * WM, BN = 64 * WN;
+  constexpr int BM = 128 * WM, BN = 16 * CFW * WN;
   constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 64, (size_t)WM * (BN / 128) * 32768);
   const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
-    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 0, CFW>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 1, CFW>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  if (epi == 1) hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 1>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
-  else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
+  if (epi == 1)
+    hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 1, CFW>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
+  else
+    hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0, CFW>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
 }
 
 // pipelined 8-wave kernel (tap_gemm_p8_kernel); variant v: 1 = 256 x 128 16x16x32, 2 = 256 x 128
@@ -2391,6 +2397,7 @@ static void launch_p8(TapGemmParams p, int variant, int epi, hipStream_t stream)
 // convs are 14 256 x 256 tiles (122 us against the 128-row kernel's 52-workgroup grid).
 static int big_tile_pick(int mode, int M, int Co, int ntaps, int ds) {
   if (mode == 2) return 0;
+  if (mode == 4) return Co >= 256 ? 4 : 0;  // 4-wave 256 x 256 (128 x 128 per wave): A/B and autotuner
   if (mode == 1) return Co >= 256 ? 1 : 2;
   if (mode == 3) return 2;
   int pick = 0;
@@ -2406,7 +2413,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
                           bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                           const TapList& taps, float* stats, const float* bias, int relu,
                           const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb,
-                          const AffineEpi* aff, const float* pscale, const float* pshift) {
+                          const AffineEpi* aff, const float* pscale, const float* pshift, int nbias) {
   TapGemmParams p;
   p.pscale = pscale;
   p.pshift = pshift;
@@ -2426,7 +2433,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   p.Co = Co; p.T = T; p.M = N * Hy * Wy;
   p.ntaps = taps.n; p.cpt = Cs / 8; p.ldw = T * Cs;
   p.nkt = (taps.n * p.cpt + 7) / 8;
-  p.relu = relu; p.bias = bias;
+  p.relu = relu; p.bias = bias; p.nbias = (nbias > 0 && nbias < Co) ? nbias : Co;
   p.div_wy = make_fastdiv(Wy); p.div_hy = make_fastdiv(Hy); p.div_cpt = make_fastdiv(p.cpt);
   for (int i = 0; i < taps.n; ++i)
     p.tap[i] = (taps.dy[i] & 0xff) | ((taps.dx[i] & 0xff) << 8) | ((taps.widx[i] & 0xffff) << 16);
@@ -2542,6 +2549,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   if (big != 0) {
     p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)
     if (big == 1) launch_big<2, 4, 4>(p, epi, stream);
+    else if (big == 4) launch_big<2, 2, 4, 8>(p, epi, stream);
     else launch_big<2, 2, 3>(p, epi, stream);
     return;
   }
@@ -2627,6 +2635,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 4, 64, 2},  // 4-stage ring of 64-deep k-tiles
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
+    {0, 0, 0, 4},   // 256 x 256 at 4 waves, 128 x 128 per wave (Co >= 256)
 };
 static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
@@ -2650,10 +2659,10 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
                      const TapList& taps, float* stats, const float* bias, int relu,
                      const bf16* zero, hipStream_t stream, const bf16* addsrc, const BnBwdEpi* bnb,
-                     const AffineEpi* aff, const float* pscale, const float* pshift) {
+                     const AffineEpi* aff, const float* pscale, const float* pshift, int nbias) {
   auto run = [&]() {
     tap_gemm_impl(src, N, Hs, Ws, Cs, wt, Co, T, dst, Hd, Wd, Hy, Wy, ss, ds, oy, ox, taps, stats, bias, relu, zero,
-                  stream, addsrc, bnb, aff, pscale, pshift);
+                  stream, addsrc, bnb, aff, pscale, pshift, nbias);
   };
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
@@ -2691,7 +2700,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     for (int c = 0; c < (int)(sizeof(kTgCfgs) / sizeof(kTgCfgs[0])); ++c) {
       const TgCfg& cfg = kTgCfgs[c];
       if (cfg.big == 3 && !big_ok) continue;
-      if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;
+      if ((cfg.big == 1 || cfg.big == 4) && !(big_ok && Co >= 256)) continue;
       if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
       TuneOverride ov(cfg);
       run();  // warm

@@ -59,7 +59,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16*
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,
                      const BnBwdEpi* bnb = nullptr, const AffineEpi* aff = nullptr,
-                     const float* pscale = nullptr, const float* pshift = nullptr);
+                     const float* pscale = nullptr, const float* pshift = nullptr, int nbias = 0);
 // (pscale, pshift: BN + ReLU prologue on the input of a 1x1 stride-1 forward, K5 -- the input is
 // the BN's input x and the conv sees bf16(relu(x * pscale[c] + pshift[c])))
 // backward of act(c * scale + shift [+ r]) from its output y: g = dy * act'(y) and dc = g * scale
@@ -273,5 +273,9 @@ void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* 
                            hipStream_t st);
 void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg, float* part,
                            bf16* dres, int N, int HW, int C, int relu, hipStream_t st);
+
+// stem weight 7x7/2 [Co][7][7][C<=4] <-> space-to-depth 4x4 [Co][4][4][16] (misc.hip)
+void launch_s2d_weight(const float* w7, int Co, int C, float* w16, hipStream_t s);
+void launch_s2d_weight_bwd(const float* g16, int Co, int C, float* g7, hipStream_t s);
 
 }  // namespace dcp

@@ -448,4 +448,40 @@ void launch_sign_mul(const float* d, const float* g, float* out, int C, hipStrea
   hipLaunchKernelGGL(sign_mul_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d, g, out, C);
 }
 
+
+// ---------------------------------------------------------------------------
+// The stem weight between its 7x7 / stride-2 master form [Co][7][7][C <= 4] and the 4x4 / stride-1
+// form over the 2x2 space-to-depth input [Co][4][4][16] (ops/functional.py stem_s2d_weight):
+//   w16[co][ta][tb][(py * 2 + px) * 4 + c] = w7[co][2 ta + py - 1][2 tb + px - 1][c]
+// (0 outside the 7x7 window or past C).  Forward: refresh the persistent s2d buffer every step in
+// one launch; backward: the 4x4 weight gradient back onto the 7x7 master (each 7x7 element has
+// exactly one 4x4 image, so a gather).
+__global__ void __launch_bounds__(256) s2d_weight_kernel(const float* __restrict__ w7, int Co, int C,
+                                                         float* __restrict__ w16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Co * 256) return;
+  const int co = i >> 8, k = i & 255;
+  const int ta = k >> 6, tb = (k >> 4) & 3, q = k & 15, py = q >> 3, px = (q >> 2) & 1, c = q & 3;
+  const int kh = 2 * ta + py - 1, kw = 2 * tb + px - 1;
+  const bool ok = kh >= 0 && kh < 7 && kw >= 0 && kw < 7 && c < C;
+  w16[i] = ok ? w7[((co * 7 + kh) * 7 + kw) * C + c] : 0.f;
+}
+
+__global__ void __launch_bounds__(256) s2d_weight_bwd_kernel(const float* __restrict__ g16, int Co, int C,
+                                                             float* __restrict__ g7) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Co * 49 * C) return;
+  const int c = i % C, t = i / C, kw = t % 7, kh = (t / 7) % 7, co = t / 49;
+  const int u = kh + 1, v = kw + 1;  // 8 x 8 padded index
+  const int ta = u >> 1, py = u & 1, tb = v >> 1, px = v & 1;
+  g7[i] = g16[co * 256 + ta * 64 + tb * 16 + (py * 2 + px) * 4 + c];
+}
+
+void launch_s2d_weight(const float* w7, int Co, int C, float* w16, hipStream_t s) {
+  hipLaunchKernelGGL(s2d_weight_kernel, dim3((Co * 256 + 255) / 256), dim3(256), 0, s, w7, Co, C, w16);
+}
+void launch_s2d_weight_bwd(const float* g16, int Co, int C, float* g7, hipStream_t s) {
+  hipLaunchKernelGGL(s2d_weight_bwd_kernel, dim3((Co * 49 * C + 255) / 256), dim3(256), 0, s, g16, Co, C, g7);
+}
+
 }  // namespace dcp

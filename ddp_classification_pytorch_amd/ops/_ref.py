@@ -127,7 +127,10 @@ def conv_wgrad(dy, x, KH, KW, stride, pad):
 def linear_fwd(x, w, bias, act):
     y = _f(x) @ _f(w).t()
     if bias is not None:
-        y = y + _f(bias)[: y.shape[1]]
+        b = _f(bias)[: y.shape[1]]
+        if b.numel() < y.shape[1]:  # an unpadded bias of a padded GEMM
+            b = F.pad(b, (0, y.shape[1] - b.numel()))
+        y = y + b
     if int(act) == 1:
         y = torch.relu(y)
     elif int(act) == 2:
@@ -666,3 +669,17 @@ def iabn_gamma(g, eps):
 
 def sign_mul(d, g):
     return d * torch.sign(g)
+
+
+def s2d_weight(w7, w16):
+    """In place: w16 = the space-to-depth 4x4 form of the 7x7 stem weight (functional.stem_s2d_weight)."""
+    from .functional import stem_s2d_weight
+
+    w16.copy_(stem_s2d_weight(w7.float()))
+
+
+def s2d_weight_bwd(g16, C):
+    Co = g16.shape[0]
+    g8 = g16.float().reshape(Co, 4, 4, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Co, 8, 8, 4)
+    return g8[:, 1:, 1:, :C].contiguous()
+

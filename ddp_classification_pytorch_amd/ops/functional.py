@@ -495,7 +495,7 @@ class _Linear(Function):
         if ctx.needs_input_grad[1]:
             dw = k.linear_wgrad(dy, x)[: ctx.out]
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = k.colsum(dy)  # grad of the padded bias (F.pad backward slices it)
+            db = k.colsum(dy)[: ctx.out]  # the padded GEMM's column sums, the real outputs only
         return dx, dw, db, None, None, None
 
 
@@ -510,10 +510,8 @@ def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
         raise ValueError(f"linear: input width {x.shape[1]} != {inf}")
     npad = round_up(out, 64) if x.is_cuda else out
     wb, wt = prepared_weight(weight, npad, True)
-    bias_p = None
-    if bias is not None:
-        bias_p = F.pad(bias, (0, npad - out)) if npad > out else bias
-    y = _Linear.apply(x, weight, bias_p, wb, wt, act_code)
+    # the bias goes in unpadded: the GEMM epilogue adds 0 past its length (no per-step pad copy)
+    y = _Linear.apply(x, weight, bias, wb, wt, act_code)
     return y if keep_padded or npad == out else y[:, :out]
 
 
@@ -1458,11 +1456,21 @@ def stem_s2d_weight(w: torch.Tensor) -> torch.Tensor:
     return w8.reshape(co, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(co, 4, 4, 16)
 
 
+def _s2d_weight_refresh(weight, buf):
+    """buf <- the s2d form of the 7x7 master, one launch (no pad / permute / copy chain per step)."""
+    with torch.no_grad():
+        K(weight).s2d_weight(weight.detach().contiguous(), buf)
+
+
 class _StemS2D(Function):
+    """The s2d stem conv; autograd input is the 7x7 master itself (the 4x4 weight gradient goes
+    back onto it through s2d_weight_bwd)."""
+
     @staticmethod
-    def forward(ctx, x, w16, wb, stats):
+    def forward(ctx, x, w7, wb, stats):
         y, slabs = K(x).stem_fwd(x, wb, stats)  # slabs: BN partials [P,3,64] or conv slabs
         ctx.save_for_backward(x)
+        ctx.c7 = w7.shape[3]
         ctx.mark_non_differentiable(slabs)
         ctx.set_materialize_grads(False)
         return y, slabs
@@ -1472,7 +1480,10 @@ class _StemS2D(Function):
         if dy is None:
             return None, None, None, None
         (x,) = ctx.saved_tensors
-        dw = K(dy).conv_wgrad_geo(dy.contiguous(), x, 4, 4, 1, 2) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            k = K(dy)
+            dw = k.s2d_weight_bwd(k.conv_wgrad_geo(dy.contiguous(), x, 4, 4, 1, 2).float().contiguous(), ctx.c7)
         return None, dw, None, None
 
 
@@ -1481,10 +1492,9 @@ def stem_conv_s2d(x16: torch.Tensor, weight: torch.Tensor, buf: torch.Tensor, st
     K = 16 taps x 16 channels = 256 (4 MFMA k-tiles) instead of 49 taps x 8 padded
     channels = 392 (7 k-tiles).  ``buf``: persistent fp32 [Co,4,4,16] holding the
     transformed master weight (its bf16 copy rides the multi-tensor weight cache)."""
-    with torch.no_grad():
-        buf.copy_(stem_s2d_weight(weight.detach()))
+    _s2d_weight_refresh(weight, buf)
     wb, _ = prepared_weight(buf, 0, False)
-    return _StemS2D.apply(x16, stem_s2d_weight(weight), wb, bool(stats and x16.is_cuda))
+    return _StemS2D.apply(x16, weight, wb, bool(stats and x16.is_cuda))
 
 
 class _StemBNPool(Function):
@@ -1495,8 +1505,9 @@ class _StemBNPool(Function):
     neither the full-resolution activation gradient nor a second BN-backward pass exists."""
 
     @staticmethod
-    def forward(ctx, x16, w16, wb, gamma, beta, run_mean, run_var, cfg: BNConfig):
+    def forward(ctx, x16, w7, wb, gamma, beta, run_mean, run_var, cfg: BNConfig):
         k = K(x16)
+        ctx.c7 = w7.shape[3]
         z, part = k.stem_fwd(x16, wb, True)
         mean, invstd, scale, shift, count = _bn_train_coeff(k, z, part, gamma, beta, run_mean, run_var, cfg)
         y, idx = k.bn_act_maxpool(z, scale, shift, cfg.act, 3, 2, 1)
@@ -1518,7 +1529,9 @@ class _StemBNPool(Function):
         if cfg.group is not None:
             sums = local.clone()
             dist.all_reduce(sums, group=cfg.group)
-        dw = k.stem_bwd_dw(tot, sums, scale, invstd, float(ctx.count)) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:  # the 4x4 s2d weight gradient, onto the 7x7 master
+            dw = k.s2d_weight_bwd(k.stem_bwd_dw(tot, sums, scale, invstd, float(ctx.count)), ctx.c7)
         dgamma = local[1] if ctx.needs_input_grad[3] else None
         dbeta = local[0] if ctx.needs_input_grad[4] else None
         return None, dw, None, dgamma, dbeta, None, None, None
@@ -1540,10 +1553,9 @@ def stem_bn_pool(x16, weight, buf, gamma, beta, run_mean, run_var, momentum, eps
     of its s2d form (as stem_conv_s2d)."""
     world = dist.get_world_size(group) if group is not None else 1
     cfg = BNConfig(True, momentum, eps, ACT[act], 0.0, group, world)
-    with torch.no_grad():
-        buf.copy_(stem_s2d_weight(weight.detach()))
+    _s2d_weight_refresh(weight, buf)
     wb, _ = prepared_weight(buf, 0, False)
-    y, _ = _StemBNPool.apply(x16, stem_s2d_weight(weight), wb, gamma, beta, run_mean, run_var, cfg)
+    y, _ = _StemBNPool.apply(x16, weight, wb, gamma, beta, run_mean, run_var, cfg)
     return y
 
 

@@ -123,6 +123,28 @@ def test_linear(K, B, K_, N, relu, bias):
     assert relerr(dw, dy.float().t() @ x.float()) < 5e-3
 
 
+def test_linear_unpadded_bias(K):
+    """A 1000-way head on the 1024-wide padded GEMM with its 1000-entry bias: the columns past the
+    bias get none (the epilogue reads only nbias entries); Fn.linear's bias gradient has 1000."""
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    x = rnd(64, 512)
+    w = torch.randn(1000, 512) / math.sqrt(512)
+    b = torch.randn(1000)
+    wb, _ = K.weight_prep(w.to(DEV), 1024, True)
+    y = K.linear_fwd(x.to(DEV), wb, b.to(DEV), 0)
+    assert y.shape == (64, 1024)
+    yr = x.float() @ w.bfloat16().float().t() + b
+    assert relerr(y[:, :1000], yr) < 1e-2
+    # padded weight rows are zero and no bias is added there
+    assert y[:, 1000:].float().abs().max().item() == 0.0
+    wd, bd = w.clone().to(DEV).requires_grad_(True), b.clone().to(DEV).requires_grad_(True)
+    out = Fn.linear(x.to(DEV), wd, bd)
+    assert out.shape == (64, 1000)
+    g = rnd(64, 1000).to(DEV)
+    out.backward(g)
+    assert bd.grad.shape == (1000,) and relerr(bd.grad, g.float().sum(0)) < 1e-2
+
+
 @pytest.mark.parametrize("act,res,shape", [(1, False, (4, 14, 14, 256)), (1, True, (4, 14, 14, 256)),
                                            (0, False, (4, 14, 14, 256)), (2, True, (4, 14, 14, 256)),
                                            (1, True, (8, 2, 2, 512)), (1, False, (8, 2, 2, 512)),
@@ -1117,11 +1139,12 @@ def test_persistent_tap_gemm_matches(K, shape, bk):
                                    (2, 7, 7, 512, 2048, 1, 1, 0), (2, 28, 28, 256, 512, 1, 2, 0),
                                    (3, 9, 11, 128, 128, 3, 1, 1), (1, 13, 13, 256, 384, 3, 2, 1),
                                    (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1)])
-@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("mode", [1, 3, 4])
 @pytest.mark.parametrize("cvar", [0, 2])
 def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
-    """The 8-wave 256 x 256 (g_tune[24] = 1; 256 x 128 below 256 channels) and 4-wave 256 x 128
-    (g_tune[24] = 3) big-tile tap GEMMs, fragments read across the barrier or (g_tune[4] = 2)
+    """The 8-wave 256 x 256 (g_tune[24] = 1; 256 x 128 below 256 channels), 4-wave 256 x 128
+    (g_tune[24] = 3) and 4-wave 256 x 256 (g_tune[24] = 4: 128 x 128 per wave, AGPR accumulators;
+    Co >= 256 only) big-tile tap GEMMs, fragments read across the barrier or (g_tune[4] = 2)
     after it, == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
     M: quadrants past M write no slab) and the data gradient (stride 1 and the stride-2 parity
     classes), channel counts that are not a multiple of the tile."""
