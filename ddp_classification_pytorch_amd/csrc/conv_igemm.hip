@@ -2635,7 +2635,8 @@ static const TgCfg kTgCfgs[] = {
     {0, 4, 64, 2},  // 4-stage ring of 64-deep k-tiles
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
-    {0, 0, 0, 4},   // 256 x 256 at 4 waves, 128 x 128 per wave (Co >= 256)
+    // (the 4-wave 256 x 256 tile, g_tune[24] = 4, is not a candidate: slower on every R50 shape,
+    // profiles/r4/big4_tile_ab_b1024.txt)
 };
 static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
