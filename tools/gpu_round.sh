@@ -81,7 +81,7 @@ for step in "$@"; do
       tail -1 $O/bench_gloo2.log ;;
     prof)
       prof_env
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 2 \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 30 --warmup 3 \
         > $O/prof.log 2>&1
       echo prof done ;;
     profcfg=*)
