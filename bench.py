@@ -78,6 +78,9 @@ def parse(argv=None):
     ap.add_argument("--telemetry-steps", type=int, default=5,
                     help="N > 1, dcp engine: untimed steps after the timed phase that record per-bucket HIP events "
                          "(exposed communication per rank)")
+    ap.add_argument("--no-comm-probe", dest="comm_probe", action="store_false",
+                    help="distributed runs: skip the untimed collective probe after the timed phases (RCCL "
+                         "all-reduce bus bandwidth per bucket size; SyncBN-sized all-gather / all-reduce latency)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
     ap.add_argument("--graph", action="store_true",
@@ -144,6 +147,41 @@ def self_launch(n, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+def comm_probe(dev, world, bn_group, reps=5):
+    """Untimed microbenchmark of the collectives this step issues, on the job's own communicators
+    (SURVEY.md §5.8 items 1, 4, 6): all-reduce bus bandwidth at gradient-bucket sizes (ring
+    convention 2 (n-1)/n x bytes / time) and the latency of SyncBN-sized all-gathers (forward
+    statistics, 3 x 2048 floats per rank) and all-reduces (backward sums, 2 x 2048 floats) on the
+    dedicated BN communicator.  The per-bucket numbers say where bucket size stops paying on xGMI."""
+    out = {"allreduce_busbw_gbs": {}, "allreduce_ms": {}, "world": world}
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn, n):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        ev0.record()
+        for _ in range(n):
+            fn()
+        ev1.record()
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / n * 1e-3  # s per call
+
+    for mb in (4, 25, 100):
+        t = torch.empty(mb * 2**20 // 4, dtype=torch.float32, device=dev)
+        sec = timed(lambda: dist.all_reduce(t), reps)
+        out["allreduce_ms"][f"{mb}MB"] = round(sec * 1e3, 4)
+        out["allreduce_busbw_gbs"][f"{mb}MB"] = round(2.0 * (world - 1) / max(world, 1) * t.numel() * 4 / sec / 1e9, 1)
+        del t
+    st = torch.empty(3 * 2048, dtype=torch.float32, device=dev)
+    gathered = torch.empty(world * st.numel(), dtype=torch.float32, device=dev)
+    out["syncbn_allgather_us"] = round(timed(lambda: dist.all_gather_into_tensor(gathered, st, group=bn_group), 20) * 1e6, 1)
+    sums = torch.empty(2 * 2048, dtype=torch.float32, device=dev)
+    out["syncbn_allreduce_us"] = round(timed(lambda: dist.all_reduce(sums, group=bn_group), 20) * 1e6, 1)
+    return out
 
 
 def main(argv=None):
@@ -308,6 +346,9 @@ def main(argv=None):
         sdt, sper = gather_max(sdt)
         sync = {"value": round(B * world * a.steps / sdt, 2), "ms_per_step": round(sdt / a.steps * 1000.0, 3),
                 "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in sper]}
+    probe = None
+    if dist_on and a.comm_probe and dist.get_backend() == "nccl":
+        probe = comm_probe(dev, world, bn_group)
     loss_v = float(loss.item())
     ms = dt / a.steps * 1000.0
     ips = B * world * a.steps / dt
@@ -332,6 +373,7 @@ def main(argv=None):
             "syncbn_value": sync["value"] if sync else None,
             "syncbn_ms_per_step": sync["ms_per_step"] if sync else None,
             "comm": comm,
+            "comm_probe": probe,
             "config": {
                 "model": a.model,
                 "global_batch": B * world,
