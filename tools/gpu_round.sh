@@ -42,6 +42,10 @@ for step in "$@"; do
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${k:+-k "$k"} \
         > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
       tail -2 $O/gpu_tests.log ;;
+    probe)
+      # world-1 RCCL DDP step with the collective probe in its JSON (comm_probe)
+      timeout -k 10 300 python -u bench.py --force-ddp --steps 20 --warmup 5 > $O/ddp1_probe.log 2>&1
+      tail -1 $O/ddp1_probe.log | grep -o '"comm_probe": {[^}]*}[^}]*}[^}]*}' ;;
     ddp1)
       timeout -k 10 300 python -u bench.py --force-ddp --batch 32 --graph --steps 100 --warmup 5 > $O/ddp1_b32g.log 2>&1
       tail -1 $O/ddp1_b32g.log
