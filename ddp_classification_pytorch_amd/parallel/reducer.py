@@ -113,6 +113,7 @@ class BucketReducer:
         self._order = []            # hook order of the current backward
         self._rebuilt = False
         self._compute = None
+        self._next = 0              # the next bucket index to launch this backward
         self._build(list(reversed(range(len(ps)))))
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
 
@@ -190,7 +191,12 @@ class BucketReducer:
         b = self.buckets[self.bucket_of[i]]
         b.pending -= 1
         if b.pending == 0 and self._rebuilt_ready():
-            self._launch(b)
+            # collectives go out in bucket-index order on every rank (one communicator needs the
+            # same call sequence everywhere): a bucket that completes early waits for the ones
+            # before it -- with buckets built in gradient-ready order that is rarely a delay
+            while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+                self._launch(self.buckets[self._next])
+                self._next += 1
 
     def _rebuilt_ready(self):
         # the first backward only records the ready order; its buckets launch together at the end
@@ -289,7 +295,7 @@ class BucketReducer:
     def _finalize(self):
         if not self._rebuilt:
             self._rebuild_from_observed()
-        for b in self.buckets:
+        for b in self.buckets:  # the rest (unused parameters, the first backward) in index order
             if not b.launched:
                 self._launch(b)
         if self.cuda:
@@ -303,6 +309,7 @@ class BucketReducer:
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
+        self._next = 0
         for o in self.optimizers:
             o.mark_stepped_by_reducer()
         self._armed = False

@@ -125,3 +125,34 @@ def test_single_process_engine_equals_plain_training():
     # p.grad are views into the reduced bucket buffers
     b = r.buckets[1]
     assert b.params[0].grad.data_ptr() == b.grad_buf.data_ptr()
+
+
+def test_buckets_launch_in_index_order():
+    """A bucket whose gradients complete early waits for the buckets before it: every rank issues
+    its collectives in bucket-index order whatever order the gradients arrive in (one communicator
+    needs the same call sequence on all ranks)."""
+    import torch.nn as nn
+
+    from ddp_classification_pytorch_amd.parallel.reducer import BucketReducer
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(64, 64), nn.Linear(64, 64), nn.Linear(64, 64))
+    r = BucketReducer(m.parameters(), bucket_cap_mb=0.01, first_bucket_mb=0.01)  # ~one bucket per tensor
+    x = torch.randn(4, 64)
+    m(x).sum().backward()  # first backward: buckets rebuilt in gradient-ready order
+    nb = len(r.buckets)
+    assert nb >= 3
+    launched = []
+    orig = r._launch
+    r._launch = lambda b: (launched.append(b.index), orig(b))
+    # gradients arriving in reverse bucket order: nothing may launch until bucket 0 is complete
+    r._armed, r._compute = True, None
+    order = [p for b in reversed(r.buckets) for p in b.params]
+    for k, p in enumerate(order):
+        p.grad = torch.ones_like(p)
+        r._hook(p)
+        if k < len(order) - len(r.buckets[0].params):
+            assert launched == [], launched
+    assert launched == list(range(nb))
+    r._finalize()
+    assert launched == list(range(nb))
