@@ -47,6 +47,30 @@ def test_bench_two_ranks_one_gpu():
     assert len(rec["per_rank_ms"]) == 2
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_bench_force_ddp_rccl_world1(graph):
+    """bench.py --force-ddp: a world-1 RCCL group through the bucket engine, eager and HIP-graph
+    replay, with the SyncBN phase, the bucket telemetry (eager) and the collective probe in the
+    JSON line."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-ddp", "--steps", "3", "--warmup", "2",
+           "--batch", "8", "--image-size", "64"] + (["--graph"] if graph else [])
+    out = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["dist_backend"] == "nccl" and rec["world_size"] == 1 and rec["value"] > 0
+    assert rec["syncbn_value"] > 0 and rec["config"]["hip_graph"] == graph
+    probe = rec["comm_probe"]
+    assert probe["world"] == 1 and set(probe["allreduce_ms"]) == {"4MB", "25MB", "100MB"}
+    assert probe["syncbn_allgather_us"] > 0 and probe["syncbn_allreduce_us"] > 0
+    if not graph:
+        assert rec["comm"]["engine"] == "dcp" and rec["comm"]["buckets"] >= 1
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
