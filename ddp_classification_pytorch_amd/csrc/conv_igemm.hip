@@ -2883,8 +2883,10 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
     return;
   }
   // narrow and not too deep (a small batch's BN-backward sums: 2C <= 4096 columns, <= 2048 tiles):
-  // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[29] = 2 off
-  if (n4 <= 1024 && splits <= 2048 && g_tune[29] != 2) {
+  // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[29] = 2 off,
+  // > 2: the depth limit (A/B)
+  const int row_max = g_tune[29] > 2 ? g_tune[29] : 2048;
+  if (n4 <= 1024 && splits <= row_max && g_tune[29] != 2) {
     hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 63) / 64), dim3(1024), 0, stream, (const float4*)part,
                        splits, n4, (float4*)out);
     return;
