@@ -198,7 +198,7 @@ def _workload_worker(rank, world, port, out_dir, workload):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import main as entry
-    from ddp_classification_pytorch_amd.algos import nested, plc
+    from ddp_classification_pytorch_amd.algos import arcface, baseline, nested, plc
     from ddp_classification_pytorch_amd.parallel import ddp as pddp
 
     wrapped = []
@@ -209,11 +209,12 @@ def _workload_worker(rank, world, port, out_dir, workload):
         wrapped.append((model, out))
         return out
 
-    pddp.wrap_ddp = nested.wrap_ddp = plc.wrap_ddp = recording_wrap
+    pddp.wrap_ddp = nested.wrap_ddp = plc.wrap_ddp = arcface.wrap_ddp = baseline.wrap_ddp = recording_wrap
     common = ["--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10", "--batchsize", "4",
               "--synthetic-train-size", "16", "--synthetic-val-size", "8", "--workers", "0", "--epochs", "1",
               "--device", "cpu", "--out-dir", os.path.join(out_dir, f"run{rank}"), "--log-interval", "100"]
-    extra = {"cdr": [], "nested": ["--nested", "20", "--warmup-iters", "2"], "plc": ["--plc-eta-epochs", "1"]}
+    extra = {"cdr": [], "nested": ["--nested", "20", "--warmup-iters", "2"], "plc": ["--plc-eta-epochs", "1"],
+             "arcface": ["--num-classes", "10"], "baseline": ["--lr", "0.05"]}
     entry.main(["--workload", workload] + common + extra[workload])
     from ddp_classification_pytorch_amd.parallel.reducer import GradSyncDDP
 
@@ -222,7 +223,7 @@ def _workload_worker(rank, world, port, out_dir, workload):
                os.path.join(out_dir, f"params{rank}.pt"))
 
 
-@pytest.mark.parametrize("workload", ["cdr", "nested", "plc"])
+@pytest.mark.parametrize("workload", ["cdr", "nested", "plc", "arcface", "baseline"])
 def test_noisy_label_workloads_stay_in_sync_under_ddp(workload):
     """Ranks start from rank 0's weights (DDP broadcast) and apply all-reduced gradients, so
     after training on different shards (and different seed+rank RNG streams) every rank
