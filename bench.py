@@ -348,7 +348,10 @@ def main(argv=None):
                 "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in sper]}
     probe = None
     if dist_on and a.comm_probe and dist.get_backend() == "nccl":
-        probe = comm_probe(dev, world, bn_group)
+        try:  # diagnostics only: never let the probe cost the benchmark line
+            probe = comm_probe(dev, world, bn_group)
+        except Exception as e:  # noqa: BLE001
+            probe = {"error": f"{type(e).__name__}: {e}"[:300]}
     loss_v = float(loss.item())
     ms = dt / a.steps * 1000.0
     ips = B * world * a.steps / dt
