@@ -114,6 +114,8 @@ class BucketReducer:
         self._rebuilt = False
         self._compute = None
         self._next = 0              # the next bucket index to launch this backward
+        self._hold = []             # side-stream case: this backward's packed autograd gradients
+        self._bucket_opts = {}      # bucket index -> [(optimizer, its params in the bucket)]
         self._build(list(reversed(range(len(ps)))))
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
 
@@ -171,6 +173,7 @@ class BucketReducer:
         if not hasattr(opt, "step_params"):
             raise TypeError("attach_optimizer needs a FusedSGD / FusedAdam (step_params)")
         self.optimizers.append(opt)
+        self._bucket_opts = {}
         self._opt_params = {}
         for o in self.optimizers:
             for g in o.param_groups:
@@ -253,9 +256,10 @@ class BucketReducer:
         pack, chunks, unpack = self._pack_tables(b, grads)
         mode = 2 if self.comm_dtype == torch.bfloat16 else 0
         K.mt_copy(pack, chunks, 1.0 / self.world, mode)
-        for g, v in zip(grads, b.views):
-            if g.data_ptr() != v.data_ptr():
-                g.record_stream(comm)  # the fresh autograd gradient is read here, freed by the compute side
+        if comm != self._compute:
+            # the fresh autograd gradients are read on the side stream: keep them alive until the
+            # compute stream has joined it (_finalize) instead of one record_stream per tensor
+            self._hold.append(grads)
         if self.reduce:
             dist.all_reduce(b.comm_buf, group=self.group)
         if unpack is not None:
@@ -277,13 +281,17 @@ class BucketReducer:
     def _step_optimizers(self, b):
         if not self.optimizers:
             return
-        by_opt = {}
-        for p in b.params:
-            o = self._opt_params.get(id(p))
-            if o is not None:
-                by_opt.setdefault(id(o), (o, []))[1].append(p)
-        if not by_opt:
+        groups = self._bucket_opts.get(b.index)
+        if groups is None or groups[0] is not b:  # per bucket once (layout or optimizers changed)
+            by_opt = {}
+            for p in b.params:
+                o = self._opt_params.get(id(p))
+                if o is not None:
+                    by_opt.setdefault(id(o), (o, []))[1].append(p)
+            groups = self._bucket_opts[b.index] = (b, list(by_opt.values()))
+        if not groups[1]:
             return
+        by_opt = {id(o): (o, ps) for o, ps in groups[1]}
         if self.cuda:
             with torch.cuda.stream(_comm_stream(self.device, self.world)):
                 for o, ps in by_opt.values():
@@ -306,6 +314,7 @@ class BucketReducer:
                 self.records.append(self._ev)
                 self._ev = None
             self._compute.wait_stream(comm)
+            self._hold = []  # freed on the compute stream, which now follows the side stream's reads
         for b in self.buckets:
             b.pending = len(b.params)
             b.launched = False
