@@ -194,6 +194,7 @@ class FusedAdam(torch.optim.Optimizer):
         self._captured = None    # launch keys of the step being / last captured into a HIP graph
         self._reducer_stepped = False
         self._bucket_capture_open = False
+        self._gid = None
 
     def mark_stepped_by_reducer(self):
         self._reducer_stepped = True
@@ -237,26 +238,35 @@ class FusedAdam(torch.optim.Optimizer):
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() and not self._bucket_capture_open:
             self._captured = []  # the first bucket of a captured backward: this capture's launch keys
             self._bucket_capture_open = True
-        self._step_subset({id(p) for p in params})
+        gid = FusedSGD._group_index(self)
+        by_group = {}
+        for p in params:
+            gi = gid.get(id(p))
+            if gi is not None and p.grad is not None:
+                by_group.setdefault(gi, []).append(p)
+        for gi in sorted(by_group):
+            self._step_group(gi, self.param_groups[gi], by_group[gi])
 
     def _step_subset(self, ids):
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None and (ids is None or id(p) in ids)]
-            if not params:
-                continue
-            for p in params:
-                st = self.state[p]
-                if "step" not in st:
-                    st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["step"] += 1
-            # bias correction is per parameter (torch.optim.Adam): one launch per distinct step count
-            by_step = {}
-            for p in params:
-                by_step.setdefault(self.state[p]["step"], []).append(p)
-            for step, sub in sorted(by_step.items()):
-                self._update(gi, group, sub, step)
+            if params:
+                self._step_group(gi, group, params)
+
+    def _step_group(self, gi, group, params):
+        for p in params:
+            st = self.state[p]
+            if "step" not in st:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            st["step"] += 1
+        # bias correction is per parameter (torch.optim.Adam): one launch per distinct step count
+        by_step = {}
+        for p in params:
+            by_step.setdefault(self.state[p]["step"], []).append(p)
+        for step, sub in sorted(by_step.items()):
+            self._update(gi, group, sub, step)
 
     def _update(self, gi, group, params, step):
         b1, b2 = group["betas"]
