@@ -9,6 +9,7 @@
 #   profcfg=CFG     the same for another bench config (e.g. arcface)
 #   profsmall       the same for the batch-32 HIP-graph step (200 replays)
 #   pmcconv=S:CFGS  PMC passes (SQ / TCC hit-miss / FETCH_SIZE) over forward convs of shapes S under configs CFGS
+#   graph1024       headline batch eager vs HIP graph, interleaved twice
 #   ddpab           batch-32 graph: no DDP vs world-1 bucket engine variants (side stream, same stream, 100 MB buckets)
 #   profddp         the same for the world-1 RCCL bucket-engine batch-32 HIP-graph step
 #   graphs          HIP-graph batch 32 / 128 twice, then the headline batch
@@ -132,6 +133,14 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc2 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc2.log 2>&1
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc3 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc3.log 2>&1
       echo pmcconv done ;;
+    graph1024)
+      # headline batch: eager vs HIP-graph replay, interleaved twice
+      for r in 1 2; do
+        timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > $O/g1024_eager_$r.log 2>&1
+        echo "eager: $(grep -o '"value": [0-9.]*' $O/g1024_eager_$r.log)"
+        timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --graph > $O/g1024_graph_$r.log 2>&1
+        echo "graph: $(grep -o '"value": [0-9.]*' $O/g1024_graph_$r.log)"
+      done ;;
     graphs)
       # HIP-graph batch 32 / 128 (x2) and the headline batch
       for r in 1 2; do
