@@ -83,8 +83,12 @@ def parse(argv=None):
                          "all-reduce bus bandwidth per bucket size; SyncBN-sized all-gather / all-reduce latency)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace here")
-    ap.add_argument("--graph", action="store_true",
-                    help="1 GPU: capture the whole step in a HIP graph and replay it (launch-bound small batches)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
+                    help="capture the whole step in a HIP graph and replay it (default on one GPU: +0.5 %% at the "
+                         "headline batch, profiles/r4/graph1024_ab.txt; more at small batches)")
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="launch the step eagerly (the default with several ranks: a captured side-stream bucket "
+                         "fork / join costs more than replay saves at batch 1024)")
     ap.add_argument("--no-autotune", dest="autotune", action="store_false",
                     help="fixed heuristic conv configurations instead of the per-shape timing on the warm-up "
                          "steps (the reference's cudnn.benchmark=True, BASELINE/main.py:40)")
@@ -202,6 +206,8 @@ def main(argv=None):
     backend = os.environ.get("DCP_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
     dist_on = world > 1 or a.force_ddp
+    if a.graph is None:  # default: HIP-graph replay on one GPU without a process group, eager otherwise
+        a.graph = not dist_on
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))

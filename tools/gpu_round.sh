@@ -136,7 +136,7 @@ for step in "$@"; do
     graph1024)
       # headline batch: eager vs HIP-graph replay, interleaved twice
       for r in 1 2; do
-        timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > $O/g1024_eager_$r.log 2>&1
+        timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --eager > $O/g1024_eager_$r.log 2>&1
         echo "eager: $(grep -o '"value": [0-9.]*' $O/g1024_eager_$r.log)"
         timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 --graph > $O/g1024_graph_$r.log 2>&1
         echo "graph: $(grep -o '"value": [0-9.]*' $O/g1024_graph_$r.log)"
@@ -175,7 +175,7 @@ for step in "$@"; do
       done ;;
     small)
       for b in 32 128; do
-        timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 > $O/small_b$b.log 2>&1
+        timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 --eager > $O/small_b$b.log 2>&1
         tail -1 $O/small_b$b.log | grep -o '"value": [0-9.]*'
         timeout -k 10 240 python -u bench.py --batch $b --steps 30 --warmup 5 --graph > $O/small_b${b}_graph.log 2>&1
         tail -1 $O/small_b${b}_graph.log | grep -o '"value": [0-9.]*'
@@ -183,7 +183,7 @@ for step in "$@"; do
     smallenv=*)
       # b32 HIP-graph and b128 eager, default vs with an environment assignment
       c=${step#smallenv=}
-      for args in "--batch 32 --graph" "--batch 128"; do
+      for args in "--batch 32 --graph" "--batch 128 --eager"; do
         tag=$(echo "$args" | tr -d ' -')
         timeout -k 10 240 python -u bench.py $args --steps 30 --warmup 5 > $O/smallenv_${tag}_default.log 2>&1
         echo "$args default: $(grep -o '"value": [0-9.]*' $O/smallenv_${tag}_default.log)"

@@ -40,8 +40,7 @@ def run_loop(a, out):
 def run_bench(a):
     cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--batch", str(a.batch), "--steps",
            str(a.bench_steps), "--warmup", "10"]
-    if a.graph:
-        cmd.append("--graph")
+    cmd.append("--graph" if a.graph else "--eager")  # bench.py defaults to graph replay on one GPU
     out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
     line = [x for x in out.splitlines() if x.startswith("{")][-1]
     return json.loads(line)
