@@ -2566,6 +2566,17 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
     else hipLaunchKernelGGL(tap_gemm8_kernel<0>, dim3(grid8), dim3(512), lds8, stream, p);
     return;
   }
+  // 256-channel tiles (g_tune[0] = 256, A/B and autotuner): each wave 64 rows x 128 channels, the
+  // A tile read once per 256 output channels -- for the short-K expansion 1x1 convs, whose A reads
+  // are half of their bytes at 128-channel tiles.  Plain / statistics epilogue only.
+  if (bn == 256 && !(fast && (epi == 0 || epi == 1) && pscale == nullptr && Co > 128)) bn = 128;
+  if (bn == 256) {
+    // (32-deep k-tiles only: the 64-deep variant spills at the 168-register cap)
+    const int grid256 = ntm * ((Co + 255) / 256);
+    if (epi == 1) launch_tg<256, 1, true, 2, 32>(p, grid256, stream);
+    else launch_tg<256, 0, true, 2, 32>(p, grid256, stream);
+    return;
+  }
   const int grid = ntm * ((Co + bn - 1) / bn);
   if (pscale != nullptr) {
     // BN prologue on the A operand: 1x1 / stride-1 / FAST, plain or statistics epilogue,

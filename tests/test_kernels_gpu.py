@@ -1354,3 +1354,32 @@ def test_conv_autotune_same_results(K):
         st0, st1 = K.bn_stats(y0, s0), K.bn_stats(y1, s1)
         assert relerr(st1[0, 1:], st0[0, 1:]) < 1e-5
         assert relerr(g1, g0) < 1e-5  # another split count sums the rows in another order
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 64, 256, 1, 1, 0), (3, 9, 11, 128, 320, 1, 1, 0),
+                                   (2, 7, 7, 256, 1024, 1, 1, 0), (2, 14, 14, 128, 256, 3, 1, 1),
+                                   (2, 28, 28, 256, 512, 1, 2, 0)])
+def test_conv_fwd_256_channel_tiles(K, shape):
+    """256-channel tap-GEMM tiles (g_tune[0] = 256: 64 x 128 outputs per wave, statistics
+    epilogue) == the fp32 reference and the 128-channel tiles, ragged M and channel counts that are
+    not a multiple of 256 included; dgrad is unaffected (falls back to 128)."""
+    N, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+    wb, _ = K.weight_prep(w.float(), 0, True)
+    outs = []
+    try:
+        for bn in (0, 256):
+            K.set_tuning(0, bn)
+            y, slabs = K.conv_fwd(x, wb, s, p, True)
+            st = K.bn_stats(y, slabs)
+            torch.cuda.synchronize()
+            outs.append((y.float().cpu(), st.cpu()))
+    finally:
+        K.set_tuning(0, 0)
+    (y0, s0), (y1, s1) = outs
+    assert torch.equal(y1, y0)  # same k order: bit-identical outputs
+    assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-4
+    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
+    assert relerr(y1, yr) < 1e-2
