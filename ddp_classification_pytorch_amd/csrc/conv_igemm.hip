@@ -2646,6 +2646,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 4, 64, 2},  // 4-stage ring of 64-deep k-tiles
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
+    {256, 2, 32, 2},  // 256-channel tiles, 32-deep k-tiles (2-3 % on two R50 shapes: profiles/r4/bn256_tile_ab_b1024.txt)
     // (the 4-wave 256 x 256 tile, g_tune[24] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };
@@ -2713,6 +2714,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
       const TgCfg& cfg = kTgCfgs[c];
       if (cfg.big == 3 && !big_ok) continue;
       if ((cfg.big == 1 || cfg.big == 4) && !(big_ok && Co >= 256)) continue;
+      if (cfg.bn == 256 && !(Co > 128 && bnb == nullptr && bias == nullptr && relu == 0)) continue;
       if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
       TuneOverride ov(cfg);
       run();  // warm
