@@ -58,6 +58,28 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (uint32_t)(((uint64_t)hi + n) >> f.shr);
 }
 
+// 16-byte LDS-DMA per lane (global_load_lds_dwordx4: lane data lands at the wave-uniform LDS
+// base + 16 * lane), issued as inline asm.  The compiler's waitcnt pass treats the builtin form
+// as a FLAT access that may touch LDS: while one is in flight, every wait it places for an LDS
+// read becomes lgkmcnt(0), so a software-pipelined fragment prefetch is drained before each
+// MFMA group.  Untracked, the LDS reads get exact counted waits; the caller orders the DMA
+// itself (its own s_waitcnt vmcnt + barrier before any read of the destination), as every
+// ring here already does for the other waves' DMA.  M0 is saved and restored around it.
+__device__ __forceinline__ void dma16(const void* g, const char* lds) {
+  const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)LDS_PTR(char, lds));
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(g), "s"(a)
+      : "memory");
+}
+
+// The same DMA through the builtin (tracked by the compiler's waitcnt pass).
+__device__ __forceinline__ void dma16_tracked(const void* g, const char* lds) {
+  __builtin_amdgcn_global_load_lds(g, LDS_PTR(void, lds), 16, 0, 0);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -16,9 +16,13 @@
 //    output-channel subtiles); waves 0/1 and 2/3 split the subtiles by parity and process two
 //    at a time (four independent accumulator chains);
 //  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
-//    (the numbers the BN normalises), and writes through a per-wave LDS staging tile as 32-byte
-//    row pieces; two workgroups per CU overlap one's window load with the other's MFMAs
-//    (g_tune[19] = 2: double-buffered windows, measured slower: 366 vs 345 us at b1024).
+//    (the numbers the BN normalises) and writes through a per-wave LDS staging tile as 32-byte
+//    row pieces (g_tune[30] = 1: c3_tile_direct stores each lane's 4 channels straight from the
+//    accumulators, weights as the MFMA A operand); the next strip's window streams in behind this strip's
+//    MFMAs (8 waves, two window buffers; g_tune[19] = 1 / 2: 4-wave variants, not faster);
+//  * the window DMA is untracked (dma16), so the fragment prefetch gets exact lgkmcnt waits.
+//    Timing ablations (g_tune[2]) at b1024: no stores 251 us, no window loads 232, neither 210,
+//    full 284 -- the MFMA loop itself, not memory, is the bound (~45 % of MFMA peak).
 #include <algorithm>
 
 #include "common.cuh"
@@ -30,6 +34,7 @@ namespace {
 constexpr int kC3WinMax = 48 * 1024;        // single window buffer: bytes per workgroup
 constexpr int kC3WinBuf2 = 35 * 1024;       // each of two window buffers (two workgroups per CU)
 constexpr int kC3Stage = 4 * 32 * 64;       // per-wave 32 px x 32 ch bf16 staging tiles (4 waves)
+constexpr int kC3WinDirect = 72 * 1024;     // each of two window buffers, direct epilogue (no staging)
 
 struct C3Params {
   const bf16* x;     // [N][H][W][64]
@@ -42,6 +47,7 @@ struct C3Params {
   int strips, sps;   // strips in total, strips per workgroup
   int Wp, xq;        // window pitch (c3_pitch) and its 16-byte chunk count
   int wbytes, nbuf;  // bytes per window buffer (1 KB aligned), window buffers (1 or 2)
+  int ablate;        // timing ablations (g_tune[2], direct epilogue only): 1 no stores, 2 no window loads
   FastDiv div_wp, div_w, div_spi;
 };
 
@@ -137,9 +143,89 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
   __builtin_amdgcn_wave_barrier();
 }
 
+// Same tile with the MFMA operands swapped (weights as A, window as B): the accumulator then
+// holds D[co 32 ch + 16 n + 4 lg + i][pixel 16 sub + lr], i.e. each lane owns 4 consecutive
+// output channels of one pixel and stores them as one 8-byte piece straight from registers --
+// no LDS staging round trip, no wave barriers.  Statistics are per (lane group, i) channel and
+// reduced across the 16 pixel lanes at the end.  g_tune[30] = 1 selects it: 2-7 % faster than
+// the staged epilogue at b1024 (profiles/r4/conv3x3_direct_epilogue_ab.txt), but its different
+// fp32 summation order flips the marginal 12-step ResNet-50 learning test
+// (tests/test_workloads_gpu.py), so it stays opt-in until that test is made robust.
+template <int NU>
+__device__ __forceinline__ void c3_tile_direct(const C3Params& p, const char* win, const bf16x8 (&bw)[9][2][2], int s0,
+                                               int du, int npix, size_t ybase, int ch, int lane, float (&K)[2][4],
+                                               float (&s1)[2][4], float (&s2)[2][4], float& cnt, bool& have_k) {
+  const uint32_t lr = lane & 15, lg = lane >> 4;
+  const int W = p.W, Wp = p.Wp;
+  uint32_t base[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const uint32_t pix = min((s0 + du * u) * 16 + (int)lr, npix - 1);
+    const uint32_t r = fdiv(pix, p.div_w), xp = pix - r * W;
+    base[u] = r * Wp + xp;
+  }
+  f32x4 acc[NU][2];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) acc[u][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto frag = [&](int st, int u) {
+    const int t = st >> 1, h = st & 1;
+    return *LDS_PTR(bf16x8, win + c3_addr(base[u] + (t / 3) * Wp + (t % 3), 4 * h + lg));
+  };
+  // fragments are read PD steps ahead (ring of PD + 1); the schedule-group barriers keep the
+  // scheduler from sinking the reads next to their MFMAs (that exposes the LDS latency per step)
+  constexpr int PD = 2;
+  bf16x8 a[PD + 1][NU];
+#pragma unroll
+  for (int st = 0; st < PD; ++st)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) a[st][u] = frag(st, u);
+#pragma unroll
+  for (int st = 0; st < 18; ++st) {
+    if (st + PD < 18)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) a[(st + PD) % (PD + 1)][u] = frag(st + PD, u);
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[u][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[st >> 1][st & 1][n], a[st % (PD + 1)][u], acc[u][n],
+                                                            0, 0, 0);
+    if (st + PD < 18) __builtin_amdgcn_sched_group_barrier(0x100, NU, 0);  // this step's reads, then
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * NU, 0);                // its MFMAs
+  }
+  if (!have_k) {  // shift: the wave's first output pixel (lane lr = 0 of the lane group)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) K[n][i] = __shfl(bf2f(f2bf(acc[0][n][i])), (int)lg * 16, 64);
+    have_k = true;
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int pix = (s0 + du * u) * 16 + (int)lr;
+    const bool valid = pix < npix;
+    bf16* dst = p.y + ybase + (size_t)pix * 64 + 32 * ch + 4 * lg;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = f2bf(acc[u][n][i]);
+        const float d = valid ? bf2f(v[i]) - K[n][i] : 0.f;
+        s1[n][i] += d;
+        s2[n][i] = fmaf(d, d, s2[n][i]);
+      }
+      if (valid && !(p.ablate & 1)) *(bf16x4*)(dst + 16 * n) = v;
+    }
+    cnt += valid ? 1.f : 0.f;
+  }
+}
+
 // NW waves per workgroup: wave w owns output-channel half w & 1 and pixel group w >> 1 (NW / 2
 // groups split a strip's 16-pixel subtiles); NW = 4 runs two workgroups per CU, NW = 8 one.
-template <int NW>
+template <int NW, bool DE>
 __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Params p) {
   constexpr int NPG = NW / 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -161,11 +247,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
         bw[t][h][n] = *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + t) * 64 + 32 * h + 8 * lg);
 
   float K[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, cnt = 0.f;
+  float K4[DE ? 2 : 1][4] = {}, t1[DE ? 2 : 1][4] = {}, t2[DE ? 2 : 1][4] = {};
   bool have_k = false;
   const int s_begin = blockIdx.x * p.sps, s_end = min(p.strips, s_begin + p.sps);
 
   // strip s's input window -> window buffer b (LDS-DMA; zero page outside the image)
   auto load_strip = [&](int s, int b) {
+    if (DE && (p.ablate & 2) && s != s_begin) return;
     char* wb = smem + b * p.wbytes;
     const int n_img = fdiv(s, p.div_spi);
     const int y0 = (s - n_img * p.spi) * p.R;
@@ -176,7 +264,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
       const bool ok = yy >= 0 && yy < H && xi >= 0 && xi < W;
       const uint32_t c = (qq & 7) ^ (P & 7u);
       const bf16* g = ok ? p.x + ((size_t)(n_img * H + yy) * W + xi) * 64 + c * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, wb + (qq - lane) * 16), 16, 0, 0);
+      dma16(g, wb + (qq - lane) * 16);
     }
   };
   if (p.nbuf == 2 && s_begin < s_end) load_strip(s_begin, 0);
@@ -199,36 +287,72 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
     const int nsub = (npix + 15) >> 4;
     const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
     for (int s0 = pg; s0 < nsub; s0 += 2 * NPG) {
-      if (s0 + NPG < nsub)
-        c3_tile<2>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
-      else  // odd tail: one subtile, no wasted MFMAs
-        c3_tile<1>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+      if constexpr (DE) {
+        if (s0 + NPG < nsub)
+          c3_tile_direct<2>(p, win, bw, s0, NPG, npix, ybase, ch, lane, K4, t1, t2, cnt, have_k);
+        else
+          c3_tile_direct<1>(p, win, bw, s0, NPG, npix, ybase, ch, lane, K4, t1, t2, cnt, have_k);
+      } else {
+        if (s0 + NPG < nsub)
+          c3_tile<2>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+        else  // odd tail: one subtile, no wasted MFMAs
+          c3_tile<1>(p, win, stage, bw, s0, NPG, npix, ybase, ch, lane, K, s1, s2, cnt, have_k);
+      }
     }
   }
   if (!p.part) return;
 
-  // per-wave channel sums: lanes lr share a channel across the 4 lane groups
+  if constexpr (DE) {
+    // direct epilogue: lanes lr (pixels) share channel 32 ch + 16 n + 4 lg + i -> reduce across them
 #pragma unroll
-  for (int off = 16; off < 64; off *= 2) {
+    for (int off = 1; off < 16; off *= 2) {
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      s1[n] += __shfl_xor(s1[n], off, 64);
-      s2[n] += __shfl_xor(s2[n], off, 64);
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          t1[n][i] += __shfl_xor(t1[n][i], off, 64);
+          t2[n][i] += __shfl_xor(t2[n][i], off, 64);
+        }
+      cnt += __shfl_xor(cnt, off, 64);
     }
-    cnt += __shfl_xor(cnt, off, 64);
+    __syncthreads();
+    float* sc = (float*)smem;
+    if (lr == 0)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float* e = sc + ((wave * 2 + n) * 16 + 4 * lg + i) * 4;
+          e[0] = cnt;
+          e[1] = K4[n][i];
+          e[2] = t1[n][i];
+          e[3] = t2[n][i];
+        }
+  } else {
+    // per-wave channel sums: lanes lr share a channel across the 4 lane groups
+#pragma unroll
+    for (int off = 16; off < 64; off *= 2) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        s1[n] += __shfl_xor(s1[n], off, 64);
+        s2[n] += __shfl_xor(s2[n], off, 64);
+      }
+      cnt += __shfl_xor(cnt, off, 64);
+    }
+    __syncthreads();  // window / staging no longer read: reuse as scratch
+    float* sc = (float*)smem;  // [NW waves][2 n][16][4]: cnt, K, s1, s2
+    if (lg == 0)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        float* e = sc + ((wave * 2 + n) * 16 + lr) * 4;
+        e[0] = cnt;
+        e[1] = K[n];
+        e[2] = s1[n];
+        e[3] = s2[n];
+      }
   }
-  __syncthreads();  // window / staging no longer read: reuse as scratch
-  float* sc = (float*)smem;  // [NW waves][2 n][16][4]: cnt, K, s1, s2
-  if (lg == 0)
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      float* e = sc + ((wave * 2 + n) * 16 + lr) * 4;
-      e[0] = cnt;
-      e[1] = K[n];
-      e[2] = s1[n];
-      e[3] = s2[n];
-    }
   __syncthreads();
+  const float* sc = (const float*)smem;
   if (tid < 64) {  // channel c = tid: waves (c >> 5) + 2 q hold it, n = (c >> 4) & 1
     const int c = tid, cw = c >> 5, n = (c >> 4) & 1, l = c & 15;
     float nt = 0.f, mean = 0.f, m2 = 0.f;
@@ -260,6 +384,8 @@ struct C3Cfg {
 static C3Cfg c3_cfg() {
   if (g_tune[19] == 1) return {4, 1, kC3WinMax};
   if (g_tune[19] == 2) return {4, 2, kC3WinBuf2};
+  if (g_tune[30] == 1)  // direct epilogue: no staging tiles, the LDS goes to taller windows
+    return {8, 2, g_tune[31] > 0 ? std::min(g_tune[31], 78) * 1024 : kC3WinDirect};
   return {8, 2, kC3WinMax};
 }
 
@@ -294,6 +420,7 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   C3Params p;
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
   p.H = H; p.W = W;
+  p.ablate = g_tune[2];
   p.R = c3_rows(H, W);
   p.spi = (H + p.R - 1) / p.R;
   p.strips = N * p.spi;
@@ -305,19 +432,31 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.div_wp = make_fastdiv(p.Wp);
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
-  const int lds = p.nbuf * p.wbytes + cfg.nw * 32 * 64;
+  const bool de = g_tune[30] == 1;
+  const int lds = p.nbuf * p.wbytes + (de ? 0 : cfg.nw * 32 * 64);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * kC3WinBuf2 + 2048 + kC3Stage);
-    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * kC3WinBuf2 + 2048 + kC3Stage);
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               2 * kC3WinMax + 2048 + 2 * kC3Stage);
+    (void)hipFuncSetAttribute((const void*)conv3x3_c64_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * 78 * 1024 + 2048);
     attr = true;
   }
-  if (cfg.nw == 8)
-    hipLaunchKernelGGL(conv3x3_c64_kernel<8>, dim3(blocks), dim3(512), lds, stream, p);
-  else
-    hipLaunchKernelGGL(conv3x3_c64_kernel<4>, dim3(blocks), dim3(256), lds, stream, p);
+  if (cfg.nw == 8) {
+    if (de)
+      hipLaunchKernelGGL((conv3x3_c64_kernel<8, true>), dim3(blocks), dim3(512), lds, stream, p);
+    else
+      hipLaunchKernelGGL((conv3x3_c64_kernel<8, false>), dim3(blocks), dim3(512), lds, stream, p);
+  } else {
+    if (de)
+      hipLaunchKernelGGL((conv3x3_c64_kernel<4, true>), dim3(blocks), dim3(256), lds, stream, p);
+    else
+      hipLaunchKernelGGL((conv3x3_c64_kernel<4, false>), dim3(blocks), dim3(256), lds, stream, p);
+  }
 }
 
 }  // namespace dcp

@@ -18,7 +18,10 @@
 // channels, K = taps x channels in 8-channel (16-byte) chunks.  Tiles are
 // staged global->LDS with `global_load_lds_dwordx4` (LDS-DMA, no VGPR
 // round trip); out-of-bounds / padding taps point the lane at a zero page so
-// the gather needs no branches.  LDS rows are XOR-swizzled on the source
+// the gather needs no branches.  The weight-gradient kernels issue it untracked
+// (dma16, common.cuh: exact lgkmcnt waits for their fragment prefetch, 10-15 %
+// faster); the forward / data-gradient families keep the compiler-tracked builtin
+// (dma16_tracked), which measured 1 % faster for them (profiles/r4/dma_untracked_ab.txt).  LDS rows are XOR-swizzled on the source
 // address so the MFMA fragment reads (`ds_read_b128`) are bank-conflict free.
 // The MFMA is v_mfma_f32_16x16x32_bf16 with the weight as the A operand, so
 // each lane ends up owning 4 consecutive output channels of one pixel
@@ -512,13 +515,11 @@ tap_gemm_kernel(const TapGemmParams p) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-        __builtin_amdgcn_global_load_lds((const void*)g,
-                                         LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+        dma16_tracked(g, As + (wave * AI + i) * 1024);
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff),
-                                         LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
+        dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
     } else {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
@@ -530,8 +531,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         const int hi = a_ys[i] + tap_dy(tv), wi = a_xs[i] + tap_dx(tv);
         ok = ok && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + ci0 : p.zero;
-        __builtin_amdgcn_global_load_lds((const void*)g,
-                                         LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+        dma16_tracked(g, As + (wave * AI + i) * 1024);
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
@@ -541,8 +541,7 @@ tap_gemm_kernel(const TapGemmParams p) {
         const bool ok = b_ok[i] && kc < kc_total;
         const bf16* g =
             ok ? p.wt + b_row[i] + (uint32_t)tap_w(*LDS_PTR(const int, tap_lds + t)) * p.Cs + ci0 : p.zero;
-        __builtin_amdgcn_global_load_lds((const void*)g,
-                                         LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16, 0, 0);
+        dma16_tracked(g, Bs + (wave * BI + i) * 1024);
       }
     }
   };
@@ -849,8 +848,7 @@ __global__ void __launch_bounds__(256, 2) tap_win_kernel(const TapGemmParams p) 
       const int k = (L & 7) ^ (w & 7);
       const int q = wbase + w;
       const bf16* g = (q >= 0 && q < p.M) ? p.src + (size_t)q * p.Cs + ch * BK + k * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, win0 + b * wbytes + (j * 256 + wave * 64) * 16),
-                                       16, 0, 0);
+      dma16_tracked(g, win0 + b * wbytes + (j * 256 + wave * 64) * 16);
     }
   };
   auto stage_b = [&](int kt, int b) {
@@ -858,8 +856,7 @@ __global__ void __launch_bounds__(256, 2) tap_win_kernel(const TapGemmParams p) 
     const long boff = (long)tap_w(p.tap[t]) * p.Cs + ch * BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff),
-                                       LDS_PTR(void, bst0 + b * B_BYTES + (wave * 4 + i) * 1024), 16, 0, 0);
+      dma16_tracked((fb_ptr[i] + boff), bst0 + b * B_BYTES + (wave * 4 + i) * 1024);
   };
 
   f32x4 acc[TN][4];
@@ -1058,12 +1055,11 @@ tap_gemm_ps_kernel(const TapGemmParams p) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+      dma16_tracked(g, As + (wave * AI + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024),
-                                       16, 0, 0);
+      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
     if (++iss_kt == nkt) {
       iss_kt = 0;
       if (++iss_tile < t1) setup_issue(iss_tile);
@@ -1229,12 +1225,12 @@ tap_gemm8_kernel(const TapGemmParams p) {
       const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
       const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
       const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * 4 + i) * 1024), 16, 0, 0);
+      dma16_tracked(g, As + (wave * 4 + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const bf16* g = b_ok[i] ? p.wt + b_row[i] + wofs + b_chunk[i] * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, Bs + (wave * 2 + i) * 1024), 16, 0, 0);
+      dma16_tracked(g, Bs + (wave * 2 + i) * 1024);
     }
   };
 
@@ -1422,12 +1418,11 @@ tap_gemm_big_kernel(const TapGemmParams p) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+      dma16_tracked(g, As + (wave * AI + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16,
-                                       0, 0);
+      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
   };
 
   f32x4 acc[CFW][8];  // [16-channel fragment][16-pixel fragment]
@@ -1640,12 +1635,11 @@ tap_gemm_p8_kernel(const TapGemmParams p) {
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, As + (wave * AI + i) * 1024), 16, 0, 0);
+      dma16_tracked(g, As + (wave * AI + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(fb_ptr[i] + boff), LDS_PTR(void, Bs + (wave * BI + i) * 1024), 16,
-                                       0, 0);
+      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
     st_c += 64;
     const bool wrap = st_c >= p.Cs;
     st_t += wrap ? 1 : 0;
@@ -1895,7 +1889,7 @@ wgrad_kernel(const WgradParams p) {
       const int m = mstart + kt * BK + r;
       const bool mok = m < mend;
       const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * SL + i) * 1024), 16, 0, 0);
+      dma16(ga, Ai + (wave * SL + i) * 1024);
       const bf16* gb;
       if (p.direct) {  // 1x1 stride 1: input pixel m is GEMM row m (no decode)
         gb = (mok && b_cok[i]) ? p.src + (size_t)m * p.Cs + b_ci[i] : p.zero;
@@ -1909,7 +1903,7 @@ wgrad_kernel(const WgradParams p) {
         const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
       }
-      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SL + i) * 1024), 16, 0, 0);
+      dma16(gb, Bi + (wave * SL + i) * 1024);
     }
   };
 
@@ -2045,7 +2039,7 @@ wgrad256_kernel(const WgradParams p) {
       const int m = mstart + kt * BK + r;
       const bool mok = m < mend;
       const bf16* ga = (mok && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * 4 + i) * 1024), 16, 0, 0);
+      dma16(ga, Ai + (wave * 4 + i) * 1024);
       const bf16* gb;
       if (p.direct) {  // 1x1 stride 1: input pixel m is GEMM row m (no decode)
         gb = (mok && b_cok[i]) ? p.src + (size_t)m * p.Cs + b_ci[i] : p.zero;
@@ -2059,7 +2053,7 @@ wgrad256_kernel(const WgradParams p) {
         const bool ok = mok && b_cok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
         gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
       }
-      __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * 4 + i) * 1024), 16, 0, 0);
+      dma16(gb, Bi + (wave * 4 + i) * 1024);
     }
   };
 
@@ -2225,7 +2219,7 @@ wgrad64_kernel(const WgradParams p) {
       const int r = (wave * SA + i) * 8 + (lane >> 3);
       const int m = mstart + kt * BK + r;
       const bf16* ga = (m < mend && a_cok[i]) ? p.dy + (size_t)m * p.Co + a_col[i] : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)ga, LDS_PTR(void, Ai + (wave * SA + i) * 1024), 16, 0, 0);
+      dma16(ga, Ai + (wave * SA + i) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < SB; ++i) {
@@ -2246,7 +2240,7 @@ wgrad64_kernel(const WgradParams p) {
         gb = ok ? p.src + ((size_t)(n * p.Hs + hi) * p.Ws + wi) * p.Cs + b_ci[i] : p.zero;
       }
       if (NJ == 4 || b_in[i])
-        __builtin_amdgcn_global_load_lds((const void*)gb, LDS_PTR(void, Bi + (wave * SB + i) * 1024), 16, 0, 0);
+        dma16(gb, Bi + (wave * SB + i) * 1024);
     }
   };
 

@@ -84,8 +84,7 @@ __device__ __forceinline__ void stage_halo(const GconvParams& p, char* img, int 
   for (int e0 = wave * 64; e0 < total; e0 += 256) {
     const int e = e0 + lane;
     if (e < total)
-      __builtin_amdgcn_global_load_lds((const void*)(base + (size_t)(e / CH) * p.C + (e % CH) * 8),
-                                       LDS_PTR(void, img + SG * 2 + e0 * 16), 16, 0, 0);
+      dma16((base + (size_t)(e / CH) * p.C + (e % CH) * 8), img + SG * 2 + e0 * 16);
   }
 }
 
@@ -451,7 +450,7 @@ __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const GconvParams p) {
       const int e = e0 + lane;
       const int m = m0c + e / CH;
       const bf16* g = m <= m1c ? p.dy + (size_t)m * p.C + sg * SG + (e % CH) * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, buf + e0 * 16), 16, 0, 0);
+      dma16(g, buf + e0 * 16);
     }
     return R_lo;
   };

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256, 2) stem_fwd_kernel(StemParams p) {
   auto load_row = [&](int ir) {
     char* dst = ring + ((ir + kSlots) & (kSlots - 1)) * kSlotBytes + lq * (kPlanePx * 16) + (2 + (wave & 1) * 64) * 16;
     const bf16* g = (unsigned)ir < (unsigned)H ? p.x + ((size_t)(n * H + ir) * W + lpx) * 16 + lq * 8 : p.zero;
-    if (lpx < W) __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, dst), 16, 0, 0);
+    if (lpx < W) dma16(g, dst);
   };
 #pragma unroll
   for (int d = -2; d <= 2; ++d) load_row(r0 + d);

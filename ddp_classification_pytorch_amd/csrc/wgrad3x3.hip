@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(512, 1) wgrad3x3_kernel(const W3Params p) {
       const bool ok = (int)rr < rows + 2 && yy >= 0 && yy < H && xi >= 0 && xi < W;
       const uint32_t c = (qq & 7) ^ w3_g(xx);
       const bf16* g = ok ? p.x + ((size_t)(n * H + yy) * W + xi) * p.C + ci0 + c * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, ximg + (qq - lane) * 16), 16, 0, 0);
+      dma16(g, ximg + (qq - lane) * 16);
     }
     const int dq = ((npix + 31) >> 5) * 256;
     for (int qq = tid; qq < dq; qq += 512) {
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(512, 1) wgrad3x3_kernel(const W3Params p) {
       const uint32_t r = fdiv(P, p.div_w), xpx = P - r * W;
       const uint32_t c = (qq & 7) ^ w3_g(P);
       const bf16* g = (int)P < npix ? p.dy + ((size_t)(n * H + y0 + r) * W + xpx) * p.Co + co0 + c * 8 : p.zero;
-      __builtin_amdgcn_global_load_lds((const void*)g, LDS_PTR(void, dimg + (qq - lane) * 16), 16, 0, 0);
+      dma16(g, dimg + (qq - lane) * 16);
     }
   };
 

@@ -54,6 +54,7 @@ CONV_SHAPES = [
     (8, 4, 4, 256, 512, 3, 2, 1),
     (8, 2, 2, 512, 512, 1, 1, 0),
     (8, 4, 4, 256, 512, 1, 2, 0),
+    (16, 16, 16, 64, 64, 3, 1, 1),   # layer1 3x3 at 64 px: one direct-kernel strip per image
 ]
 
 
@@ -901,21 +902,25 @@ def test_bn2_bwd_elemt_matches_two_passes(K):
     assert relerr(dx, dx1) < 1e-3
 
 
+@pytest.mark.parametrize("de", [0, 1])
 @pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 7, 9), (1, 13, 30), (2, 28, 28), (1, 1, 5), (1, 4, 126),
-                                   (2, 64, 64)])
-def test_conv3x3_direct_c64(K, N, H, W, variant):
+                                   (2, 64, 64), (16, 16, 16)])
+def test_conv3x3_direct_c64(K, N, H, W, variant, de):
     """The direct 64->64 3x3 kernel (conv3x3.hip) against the reference conv and against the
-    implicit GEMM it replaces (g_tune[18] = 1 forces the latter); BN partials vs bn_stats."""
+    implicit GEMM it replaces (g_tune[18] = 1 forces the latter); BN partials vs bn_stats.
+    de = 1: the register-direct store epilogue (g_tune[30] = 1, opt-in)."""
     torch.manual_seed(7)
     x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
     w = rnd(64, 3, 3, 64, scale=1.0 / 24)
     K.set_tuning(19, variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double
+    K.set_tuning(30, de)
     try:
         y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
         y3, none = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, False)
     finally:
         K.set_tuning(19, 0)
+        K.set_tuning(30, 0)
     if W <= 100 and variant != 2:  # wider rows / the smaller windows of variant 2: implicit GEMM (slabs)
         assert part.shape[1:] == (3, 64)  # (n, mean, M2) partials of the direct kernel
     yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1, False)
