@@ -16,9 +16,9 @@
 //    output-channel subtiles); waves 0/1 and 2/3 split the subtiles by parity and process two
 //    at a time (four independent accumulator chains);
 //  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
-//    (the numbers the BN normalises) and writes through a per-wave LDS staging tile as 32-byte
-//    row pieces (g_tune[30] = 1: c3_tile_direct stores each lane's 4 channels straight from the
-//    accumulators, weights as the MFMA A operand); the next strip's window streams in behind this strip's
+//    (the numbers the BN normalises) and stores each lane's 4 channels straight from the
+//    accumulators (c3_tile_direct, weights as the MFMA A operand; g_tune[30] = 2: the older
+//    per-wave LDS staging tile); the next strip's window streams in behind this strip's
 //    MFMAs (8 waves, two window buffers; g_tune[19] = 1 / 2: 4-wave variants, not faster);
 //  * the window DMA is untracked (dma16), so the fragment prefetch gets exact lgkmcnt waits.
 //    Timing ablations (g_tune[2]) at b1024: no stores 251 us, no window loads 232, neither 210,
@@ -147,10 +147,9 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
 // holds D[co 32 ch + 16 n + 4 lg + i][pixel 16 sub + lr], i.e. each lane owns 4 consecutive
 // output channels of one pixel and stores them as one 8-byte piece straight from registers --
 // no LDS staging round trip, no wave barriers.  Statistics are per (lane group, i) channel and
-// reduced across the 16 pixel lanes at the end.  g_tune[30] = 1 selects it: 2-7 % faster than
-// the staged epilogue at b1024 (profiles/r4/conv3x3_direct_epilogue_ab.txt), but its different
-// fp32 summation order flips the marginal 12-step ResNet-50 learning test
-// (tests/test_workloads_gpu.py), so it stays opt-in until that test is made robust.
+// reduced across the 16 pixel lanes at the end.  The default: 2-7 % faster than the staged
+// epilogue at b1024 (profiles/r4/conv3x3_direct_epilogue_ab.txt); bit-identical outputs, BN
+// statistics equal up to fp32 summation order.  g_tune[30] = 2 selects the staged epilogue.
 template <int NU>
 __device__ __forceinline__ void c3_tile_direct(const C3Params& p, const char* win, const bf16x8 (&bw)[9][2][2], int s0,
                                                int du, int npix, size_t ybase, int ch, int lane, float (&K)[2][4],
@@ -384,7 +383,7 @@ struct C3Cfg {
 static C3Cfg c3_cfg() {
   if (g_tune[19] == 1) return {4, 1, kC3WinMax};
   if (g_tune[19] == 2) return {4, 2, kC3WinBuf2};
-  if (g_tune[30] == 1)  // direct epilogue: no staging tiles, the LDS goes to taller windows
+  if (g_tune[30] != 2)  // direct epilogue: no staging tiles, the LDS goes to taller windows
     return {8, 2, g_tune[31] > 0 ? std::min(g_tune[31], 78) * 1024 : kC3WinDirect};
   return {8, 2, kC3WinMax};
 }
@@ -432,7 +431,7 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.div_wp = make_fastdiv(p.Wp);
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
-  const bool de = g_tune[30] == 1;
+  const bool de = g_tune[30] != 2;
   const int lds = p.nbuf * p.wbytes + (de ? 0 : cfg.nw * 32 * 64);
   static bool attr = false;
   if (!attr) {

@@ -909,12 +909,12 @@ def test_bn2_bwd_elemt_matches_two_passes(K):
 def test_conv3x3_direct_c64(K, N, H, W, variant, de):
     """The direct 64->64 3x3 kernel (conv3x3.hip) against the reference conv and against the
     implicit GEMM it replaces (g_tune[18] = 1 forces the latter); BN partials vs bn_stats.
-    de = 1: the register-direct store epilogue (g_tune[30] = 1, opt-in)."""
+    de = 1: the register-direct store epilogue (default; g_tune[30] = 2: the LDS-staged one)."""
     torch.manual_seed(7)
     x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
     w = rnd(64, 3, 3, 64, scale=1.0 / 24)
     K.set_tuning(19, variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double
-    K.set_tuning(30, de)
+    K.set_tuning(30, 0 if de else 2)
     try:
         y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
         y3, none = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, False)

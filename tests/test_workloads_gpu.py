@@ -120,9 +120,12 @@ def test_bn_prologue_step_matches_separate_bn():
     assert p1 < p0, (p0, p1)
 
 
+# --no-autotune: the kernel choice must not depend on the box's timings -- 16-step trainings at
+# batch 16 amplify fp32 summation-order differences (e.g. a BN-statistics epilogue's) into
+# visibly different loss curves (profiles/r4/learning_test_sensitivity.txt)
 LEARN = ["--data", "synthetic", "--synthetic-learnable", "--batchsize", "16", "--synthetic-train-size", "64",
          "--synthetic-val-size", "16", "--workers", "0", "--log-interval", "4", "--device", "cuda", "--image-size",
-         "64", "--num-classes", "10", "--dataset", "food"]
+         "64", "--num-classes", "10", "--dataset", "food", "--no-autotune"]
 
 
 def _epoch_losses(out, workload, tmp_path):
@@ -136,7 +139,7 @@ def _epoch_losses(out, workload, tmp_path):
 
 
 @pytest.mark.parametrize("workload,model,extra", [
-    ("baseline", "resnet50", ["--lr", "0.05", "--epochs", "3"]),
+    ("baseline", "resnet50", ["--lr", "0.05", "--epochs", "4"]),  # 3 epochs ends at 0.66-0.70x: too close
     ("baseline", "tresnet_m", ["--lr", "0.05", "--epochs", "3"]),
     ("arcface", "resnet18", ["--epochs", "4", "--m", "0.2"]),  # Adam 1e-3, s=30 (a 0.5 margin needs more steps)
     ("cdr", "resnet50", ["--lr", "0.05", "--epochs", "5"]),  # CDR keeps only the top |g*w| gradients: slower
