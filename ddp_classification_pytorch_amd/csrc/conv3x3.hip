@@ -48,6 +48,7 @@ struct C3Params {
   int Wp, xq;        // window pitch (c3_pitch) and its 16-byte chunk count
   int wbytes, nbuf;  // bytes per window buffer (1 KB aligned), window buffers (1 or 2)
   int ablate;        // timing ablations (g_tune[2], direct epilogue only): 1 no stores, 2 no window loads
+  int sched;         // g_tune[19] = 3: s_setprio 1 for the upper wave half; 4: upper half out of phase
   FastDiv div_wp, div_w, div_spi;
 };
 
@@ -245,6 +246,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
       for (int n = 0; n < 2; ++n)
         bw[t][h][n] = *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + t) * 64 + 32 * h + 8 * lg);
 
+  if (p.sched == 3 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   float K[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, cnt = 0.f;
   float K4[DE ? 2 : 1][4] = {}, t1[DE ? 2 : 1][4] = {}, t2[DE ? 2 : 1][4] = {};
   bool have_k = false;
@@ -285,7 +287,13 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
 
     const int nsub = (npix + 15) >> 4;
     const size_t ybase = ((size_t)(n_img * H + y0) * W) * 64;
-    for (int s0 = pg; s0 < nsub; s0 += 2 * NPG) {
+    // sched = 4: the upper wave half (sharing each SIMD with a lower-half wave) walks its
+    // subtiles in reverse, so the two waves of a SIMD are out of phase (one reads / stores while
+    // the other runs MFMAs) instead of in lockstep
+    const bool rev = p.sched == 4 && wave >= NW / 2 && pg < nsub;
+    const int s_last = pg < nsub ? pg + 2 * NPG * ((nsub - 1 - pg) / (2 * NPG)) : pg;
+    for (int it = pg; it < nsub; it += 2 * NPG) {
+      const int s0 = rev ? s_last - (it - pg) : it;
       if constexpr (DE) {
         if (s0 + NPG < nsub)
           c3_tile_direct<2>(p, win, bw, s0, NPG, npix, ybase, ch, lane, K4, t1, t2, cnt, have_k);
@@ -420,6 +428,7 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
   p.H = H; p.W = W;
   p.ablate = g_tune[2];
+  p.sched = g_tune[19];
   p.R = c3_rows(H, W);
   p.spi = (H + p.R - 1) / p.R;
   p.strips = N * p.spi;

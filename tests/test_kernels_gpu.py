@@ -903,7 +903,7 @@ def test_bn2_bwd_elemt_matches_two_passes(K):
 
 
 @pytest.mark.parametrize("de", [0, 1])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 7, 9), (1, 13, 30), (2, 28, 28), (1, 1, 5), (1, 4, 126),
                                    (2, 64, 64), (16, 16, 16)])
 def test_conv3x3_direct_c64(K, N, H, W, variant, de):
@@ -913,7 +913,8 @@ def test_conv3x3_direct_c64(K, N, H, W, variant, de):
     torch.manual_seed(7)
     x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
     w = rnd(64, 3, 3, 64, scale=1.0 / 24)
-    K.set_tuning(19, variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double
+    K.set_tuning(19, variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double;
+    # 3 / 4: variant 0 with s_setprio for the upper wave half / the upper half's subtiles reversed
     K.set_tuning(30, 0 if de else 2)
     try:
         y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
