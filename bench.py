@@ -209,6 +209,8 @@ def main(argv=None):
     if a.graph is None:  # default: HIP-graph replay on one GPU without a process group, eager otherwise
         a.graph = not dist_on
     if dist_on:
+        if a.graph:
+            pddp.graph_safe_nccl_env()
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
         os.environ.setdefault("RANK", "0")

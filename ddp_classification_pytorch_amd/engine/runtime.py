@@ -17,7 +17,7 @@ import torch
 from .. import _ext
 from ..data import (CappedImageFolder, DevicePrefetcher, ImageFolder, ListDataset, ShardSampler, SyntheticImages,
                     build_loader, build_transform, norm_stats)
-from ..parallel.ddp import init_distributed
+from ..parallel.ddp import graph_safe_nccl_env, init_distributed
 from ..utils.misc import set_seed, worker_init_fn
 
 
@@ -33,6 +33,8 @@ class Runtime:
 def setup(args) -> Runtime:
     want_cuda = (args.device or ("cuda" if torch.cuda.is_available() else "cpu")).startswith("cuda")
     backend = args.dist_backend or ("nccl" if want_cuda else "gloo")
+    if getattr(args, "graph", False):
+        graph_safe_nccl_env()
     rank, local, world = init_distributed(backend)
     if want_cuda:
         torch.cuda.set_device(local)

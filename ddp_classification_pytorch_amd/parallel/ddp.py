@@ -43,6 +43,17 @@ import torch.nn as nn
 from ..models.layers import BatchNorm2d
 
 
+def graph_safe_nccl_env():
+    """Call before init_process_group when steps will be captured into HIP graphs.  The RCCL
+    process group's event cache hands a finished collective's events to the next collective; a
+    captured collective records them inside the graph, and the watchdog thread's later query of
+    such an event (from a work enqueued eagerly around the capture) fails with
+    hipErrorCapturedEvent and aborts the process (seen intermittently in
+    tests/test_ddp_gpu.py::test_bench_force_ddp_rccl_world1[True]).  Fresh events per collective
+    cost a few microseconds each; only the graph path pays it."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
+
 def init_distributed(backend: str = None, timeout_s: int = 1800):
     """torchrun / torch.distributed.launch compatible init.  Returns (rank, local_rank, world)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
