@@ -24,6 +24,8 @@ counter the captured step increments, optim/fused.py).
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 
@@ -72,6 +74,18 @@ def _capture_mode():
     return "thread_local" if torch.distributed.is_initialized() else "global"
 
 
+def _quiesce_watchdog():
+    """Before a capture with a process group: drain the device, then give the RCCL watchdog
+    thread (100 ms poll) time to retire the warm-up steps' finished collectives.  A finished work
+    still on its list is polled during the capture, and HIP refuses a query of an event whose
+    stream (the process group's RCCL stream, which the captured collectives join) is capturing:
+    hipErrorCapturedEvent, and the watchdog aborts the process (intermittent in
+    tests/test_ddp_gpu.py::test_bench_force_ddp_rccl_world1[True])."""
+    if torch.distributed.is_initialized():
+        torch.cuda.synchronize()
+        time.sleep(0.35)
+
+
 class GraphedStep:
     """``GraphedStep(step_fn, warmup=3)``: runs ``step_fn`` ``warmup`` times on a side stream
     (allocator / autograd / table warm-up), captures one call, then ``__call__`` replays it and
@@ -90,6 +104,7 @@ class GraphedStep:
                 step_fn()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        _quiesce_watchdog()
         _stale_weights()
         self.counters = counters
         if counters is not None:
@@ -151,6 +166,7 @@ class StepGrapher:
             return self._eager(tensors)
         if self.graph is None:
             torch.cuda.synchronize()
+            _quiesce_watchdog()
             _stale_weights()
             self.static = [t.clone() for t in tensors]
             if self.counters is not None:
