@@ -24,11 +24,13 @@ headline ``value`` is local BN (per-GPU batch 1024).
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -216,10 +218,13 @@ def main(argv=None):
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
+        # an explicit timeout: a rank that never arrives fails the job with a message in minutes
+        # instead of running into the driver's limit (DCP_PG_TIMEOUT seconds, default 300)
+        pg_timeout = datetime.timedelta(seconds=float(os.environ.get("DCP_PG_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     kops = _ext.hip_ops()  # fail loudly if the gfx950 library is missing
@@ -272,6 +277,7 @@ def main(argv=None):
         return loss
 
     run = step
+    graphed = None
     if a.graph:
         if dist_on and a.ddp_engine != "dcp":
             raise SystemExit("--graph with N > 1 needs the bucket engine (torch DDP's reducer is not capturable)")
@@ -317,8 +323,99 @@ def main(argv=None):
         with open(os.path.join(a.profile_dir, "bench_profile.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
     dt, per_rank = gather_max(dt)
-    comm = None
-    if dist_on and a.ddp_engine == "dcp" and a.telemetry_steps > 0:
+    loss_v = float(loss.item())
+    ms = dt / a.steps * 1000.0
+    ips = B * world * a.steps / dt
+    out = {
+        "metric": METRICS[a.config],
+        "value": round(ips, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,  # the reference publishes no throughput
+        "dtype": "bf16",
+        "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
+        "dist_backend": (dist.get_backend() if dist_on else None),
+        "world_size": (dist.get_world_size() if dist_on else 1),
+        "rccl_version": rccl_version(),
+        "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
+        "syncbn_value": None,
+        "syncbn_ms_per_step": None,
+        "comm": None,
+        "comm_probe": None,
+        "config": {
+            "model": a.model,
+            "global_batch": B * world,
+            "per_gpu_batch": B,
+            "seq_len": None,
+            "image_size": S,
+            "num_classes": a.num_classes,
+            "parallelism": f"dp{world}",
+            "hip_graph": bool(a.graph),
+            "autotune": bool(autotune),
+            "syncbn": bool(a.syncbn),
+            "grad_comm": a.grad_comm,
+            "ddp_engine": a.ddp_engine if dist_on else None,
+            "force_ddp": bool(a.force_ddp),
+            "bucket_cap_mb": a.bucket_cap_mb,
+            "optimizer": "fused SGD momentum 0.9 wd 1e-4",
+            "final_loss": round(loss_v, 4),
+            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+        },
+    }
+    # The headline is measured.  What follows (bucket telemetry, the SyncBN phase, the collective
+    # probe) is diagnostic and must never cost the line: each phase is guarded, and a deadline
+    # watchdog prints the line and ends the rank if a phase hangs (e.g. one rank failed inside a
+    # collective sequence the others are still in).
+    emitted = threading.Event()
+
+    def emit():
+        if rank == 0 and not emitted.is_set():
+            emitted.set()
+            print(json.dumps(out), flush=True)
+
+    errors = {}
+
+    def watchdog():
+        errors["deadline"] = f"diagnostic phases exceeded {extra_deadline:.0f} s; headline kept"
+        out["diagnostic_errors"] = dict(errors)
+        emit()
+        sys.stdout.flush()
+        sys.stderr.write(f"bench.py rank {rank}: {errors['deadline']}\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    extra_deadline = float(os.environ.get("DCP_BENCH_EXTRA_DEADLINE", "240"))
+    timer = threading.Timer(extra_deadline, watchdog) if dist_on else None
+    if timer is not None:
+        timer.daemon = True
+        timer.start()
+    inject = os.environ.get("DCP_BENCH_INJECT", "")  # tests: "phase" or "phase:rank" raises in that phase
+    inject_rank = int(inject.split(":")[1]) if ":" in inject else None
+
+    def guarded(name, fn):
+        """Run one diagnostic phase; an exception is recorded in the line instead of ending the run.
+        Afterwards the ranks agree (one all-reduce) whether any of them failed, so they all skip the
+        remaining phases together instead of entering mismatched collectives."""
+        ok = 1.0
+        try:
+            if inject.split(":")[0] == name and inject_rank in (None, rank):
+                raise RuntimeError(f"injected failure in the {name} phase (DCP_BENCH_INJECT)")
+            fn()
+        except Exception as e:  # noqa: BLE001
+            errors[name] = f"{type(e).__name__}: {e}"[:300]
+            ok = 0.0
+        if world > 1:
+            flag = torch.tensor([ok], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = float(flag.item())
+        return ok > 0
+
+    def telemetry_phase():
         # untimed: per-step HIP events around the bucket engine (backward end on the compute stream,
         # first bucket start / last bucket done on the communication stream), eager steps
         red = model.reducer
@@ -331,15 +428,14 @@ def main(argv=None):
                          dtype=torch.float64)
         allt = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allt, t)
-        comm = {"engine": "dcp", "buckets": summ.get("buckets"), "bucket_mb": summ.get("bucket_mb"),
-                "optimizer_per_bucket": True, "telemetry_steps": summ.get("steps"),
-                "exposed_comm_ms_per_rank": [round(float(v[0]), 4) for v in allt],
-                "comm_span_ms_per_rank": [round(float(v[1]), 4) for v in allt],
-                "grad_comm": a.grad_comm}
-    elif dist_on:
-        comm = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
-    sync = None
-    if dist_on and not a.syncbn and a.syncbn_phase:
+        out["comm"] = {"engine": "dcp", "buckets": summ.get("buckets"), "bucket_mb": summ.get("bucket_mb"),
+                       "optimizer_per_bucket": True, "telemetry_steps": summ.get("steps"),
+                       "exposed_comm_ms_per_rank": [round(float(v[0]), 4) for v in allt],
+                       "comm_span_ms_per_rank": [round(float(v[1]), 4) for v in allt],
+                       "grad_comm": a.grad_comm}
+
+    def syncbn_phase():
+        nonlocal run, graphed
         # second phase: the reference's SyncBN (BASELINE/main.py:148) on the dedicated BN communicator
         pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group)
         if a.graph:  # recapture: the BN collectives (on the BN communicator) go into the new graph
@@ -352,60 +448,27 @@ def main(argv=None):
             run()
         sdt, _ = timed(a.steps)
         sdt, sper = gather_max(sdt)
-        sync = {"value": round(B * world * a.steps / sdt, 2), "ms_per_step": round(sdt / a.steps * 1000.0, 3),
-                "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in sper]}
-    probe = None
-    if dist_on and a.comm_probe and dist.get_backend() == "nccl":
-        try:  # diagnostics only: never let the probe cost the benchmark line
-            probe = comm_probe(dev, world, bn_group)
-        except Exception as e:  # noqa: BLE001
-            probe = {"error": f"{type(e).__name__}: {e}"[:300]}
-    loss_v = float(loss.item())
-    ms = dt / a.steps * 1000.0
-    ips = B * world * a.steps / dt
-    if rank == 0:
-        out = {
-            "metric": METRICS[a.config],
-            "value": round(ips, 2),
-            "unit": "images/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,  # the reference publishes no throughput
-            "dtype": "bf16",
-            "data": "synthetic (uint8 ImageNet-shaped images generated on device, random labels; random-init weights)",
-            "dist_backend": (dist.get_backend() if dist_on else None),
-            "world_size": (dist.get_world_size() if dist_on else 1),
-            "rccl_version": rccl_version(),
-            "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
-            "syncbn_value": sync["value"] if sync else None,
-            "syncbn_ms_per_step": sync["ms_per_step"] if sync else None,
-            "comm": comm,
-            "comm_probe": probe,
-            "config": {
-                "model": a.model,
-                "global_batch": B * world,
-                "per_gpu_batch": B,
-                "seq_len": None,
-                "image_size": S,
-                "num_classes": a.num_classes,
-                "parallelism": f"dp{world}",
-                "hip_graph": bool(a.graph),
-                "autotune": bool(autotune),
-                "syncbn": bool(a.syncbn),
-                "grad_comm": a.grad_comm,
-                "ddp_engine": a.ddp_engine if dist_on else None,
-                "force_ddp": bool(a.force_ddp),
-                "bucket_cap_mb": a.bucket_cap_mb,
-                "optimizer": "fused SGD momentum 0.9 wd 1e-4",
-                "final_loss": round(loss_v, 4),
-                "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
-            },
-        }
-        print(json.dumps(out), flush=True)
+        out["syncbn_value"] = round(B * world * a.steps / sdt, 2)
+        out["syncbn_ms_per_step"] = round(sdt / a.steps * 1000.0, 3)
+        out["syncbn_per_rank_ms"] = [round(v / a.steps * 1000.0, 3) for v in sper]
+
+    def probe_phase():
+        out["comm_probe"] = comm_probe(dev, world, bn_group)
+
+    go = True
+    if dist_on and a.ddp_engine == "dcp" and a.telemetry_steps > 0:
+        go = guarded("telemetry", telemetry_phase)
+    elif dist_on:
+        out["comm"] = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
+    if go and dist_on and not a.syncbn and a.syncbn_phase:
+        go = guarded("syncbn", syncbn_phase)
+    if go and dist_on and a.comm_probe and dist.get_backend() == "nccl":
+        go = guarded("probe", probe_phase)
+    if timer is not None:
+        timer.cancel()
+    if errors:
+        out["diagnostic_errors"] = errors
+    emit()
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()

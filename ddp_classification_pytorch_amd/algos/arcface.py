@@ -53,8 +53,8 @@ def run(args):
     rt = setup(args)
     train_data, val_data, _, _ = build_data(args, rt)
     model = build_arcface(args).to(rt.device)
-    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
-                   first_bucket_mb=args.first_bucket_mb)
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and (rt.world > 1 or args.force_ddp), bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb, force=args.force_ddp)
     name = args.optimizer.lower()
     wd = args.weight_decay if name == "sgd" else 0.0  # ARCFACE/arc_main.py:249-253
     opt = build_optimizer(name, model.parameters(), args.lr, args.momentum, wd)

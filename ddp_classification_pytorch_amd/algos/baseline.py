@@ -39,8 +39,8 @@ def run(args):
     rt = setup(args)
     train_data, val_data, _, _ = build_data(args, rt)
     model = build_classifier(args).to(rt.device)
-    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
-                   first_bucket_mb=args.first_bucket_mb)
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and (rt.world > 1 or args.force_ddp), bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb, force=args.force_ddp)
     opt = build_optimizer(args.optimizer, model.parameters(), args.lr, args.momentum, args.weight_decay,
                           args.nesterov)
     attach_optimizer(net, opt)  # multi-GPU: the step runs per gradient bucket behind its all-reduce

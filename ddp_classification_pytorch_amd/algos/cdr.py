@@ -112,8 +112,8 @@ def run(args):
     model = build_classifier(args, log_softmax=True).to(rt.device)
     # one process per GPU: gradients are all-reduced by DDP before the mask, so every rank
     # selects the same critical parameters from the global-batch gradient
-    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
-                   first_bucket_mb=args.first_bucket_mb)
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and (rt.world > 1 or args.force_ddp), bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb, force=args.force_ddp)
     opt = build_optimizer("sgd", model.parameters(), args.lr, args.momentum, 0.0)
     sched = MultiStepLR(opt, milestones=args.milestones, gamma=args.gamma)
     C = args.num_classes

@@ -127,7 +127,8 @@ def run(args):
     # requiring grad in train(freeze_bn=True), which must happen before DDP registers the
     # parameters it all-reduces.
     net_feat.train(True, freeze_bn=args.freeze_bn)
-    ddp_kw = dict(syncbn=False, bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
+    ddp_kw = dict(syncbn=False, bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
+                  force=args.force_ddp)
     feat_net = wrap_ddp(net_feat, rt.local_rank, **ddp_kw)
     cls_net = wrap_ddp(net_cls, rt.local_rank, **ddp_kw)
     attach_optimizer(feat_net, opt_feat)

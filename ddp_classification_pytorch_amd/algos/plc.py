@@ -158,8 +158,8 @@ def run(args):
     logger = MetricsLogger(args.out_dir if rt.is_main else None)
     train_data, val_data, train_set, _ = build_data(args, rt)
     model = build_classifier(args).to(rt.device)
-    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and rt.world > 1, bucket_cap_mb=args.bucket_cap_mb,
-                   first_bucket_mb=args.first_bucket_mb)
+    net = wrap_ddp(model, rt.local_rank, syncbn=args.syncbn and (rt.world > 1 or args.force_ddp), bucket_cap_mb=args.bucket_cap_mb,
+                   first_bucket_mb=args.first_bucket_mb, force=args.force_ddp)
     opt = FusedSGD(model.parameters(), lr=args.lr, momentum=args.momentum, nesterov=True,
                    weight_decay=args.weight_decay)
     C = args.num_classes

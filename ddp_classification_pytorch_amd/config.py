@@ -44,10 +44,15 @@ def build_parser() -> argparse.ArgumentParser:
     a("--dist-backend", default=None, help="nccl (=RCCL) on GPU, gloo on CPU")
     a("--syncbn", dest="syncbn", action="store_true", default=None, help="cross-replica BN (reference default)")
     a("--no-syncbn", dest="syncbn", action="store_false")
+    a("--force-ddp", action="store_true",
+      help="one process: still create a (world-1) process group and train through the data-parallel engine "
+           "(measures the engine's own cost; tests its HIP-graph capture)")
     a("--bucket-cap-mb", type=float, default=25.0)
     a("--first-bucket-mb", type=float, default=4.0)
     a("--device", default=None, help="cuda (default when available) or cpu")
-    a("--graph", action="store_true", help="1 GPU: replay the training step as a HIP graph (launch-bound small batches)")
+    a("--graph", action="store_true",
+      help="replay the training step as a HIP graph (launch-bound small batches); with several ranks the "
+           "bucket engine's all-reduces and per-bucket optimizer are captured too")
     # data
     a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "synthetic-device", "shards"],
       help="synthetic: random images through the host DataLoader path; synthetic-device: random uint8 batches "

@@ -24,7 +24,7 @@ counter the captured step increments, optim/fused.py).
 """
 from __future__ import annotations
 
-import time
+import os
 
 import torch
 
@@ -69,21 +69,29 @@ class HostCounters:
 def _capture_mode():
     """With a process group, capture thread-locally: the RCCL process group's watchdog thread polls
     the HIP events of collectives issued before the capture (the warm-up steps' all-reduces), and a
-    global-mode capture turns that query in another thread into a capture error that aborts the
-    process.  The capturing thread itself is still checked."""
+    global-mode capture turns any such query from another thread into a capture error.  Stream
+    capture itself is per stream, so the kernels and collectives the autograd device thread issues
+    on the capturing streams are captured either way; what thread-local mode gives up is HIP's
+    unsafe-call check in threads other than the capturing one."""
     return "thread_local" if torch.distributed.is_initialized() else "global"
 
 
-def _quiesce_watchdog():
-    """Before a capture with a process group: drain the device, then give the RCCL watchdog
-    thread (100 ms poll) time to retire the warm-up steps' finished collectives.  A finished work
-    still on its list is polled during the capture, and HIP refuses a query of an event whose
-    stream (the process group's RCCL stream, which the captured collectives join) is capturing:
-    hipErrorCapturedEvent, and the watchdog aborts the process (intermittent in
-    tests/test_ddp_gpu.py::test_bench_force_ddp_rccl_world1[True])."""
-    if torch.distributed.is_initialized():
-        torch.cuda.synchronize()
-        time.sleep(0.35)
+def _check_capture_safe_pg():
+    """Before a capture with an RCCL process group: the group must have been created with its CUDA
+    event cache off (``parallel.ddp.graph_safe_nccl_env()`` before ``init_process_group``).  With
+    the cache on, a collective captured into the graph re-records a cached event object that the
+    watchdog may still be polling for an older, eager work; HIP refuses that query with
+    hipErrorCapturedEvent and the watchdog aborts the process (the intermittent abort of
+    tests/test_ddp_gpu.py::test_bench_force_ddp_rccl_world1[True] in round 4).  With fresh events
+    per work no event the watchdog polls is ever recorded inside a capture, and the captured works
+    themselves never reach the watchdog's list, so no timing condition remains to wait for."""
+    if not torch.distributed.is_initialized() or torch.distributed.get_backend() != "nccl":
+        return
+    if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE", "1") not in ("0", "false", "False"):
+        raise RuntimeError("HIP-graph capture with an RCCL process group needs TORCH_NCCL_CUDA_EVENT_CACHE=0 at "
+                           "process-group creation: call parallel.ddp.graph_safe_nccl_env() before "
+                           "init_process_group (bench.py --graph and main.py --graph do)")
+    torch.cuda.synchronize()
 
 
 class GraphedStep:
@@ -104,7 +112,7 @@ class GraphedStep:
                 step_fn()
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
-        _quiesce_watchdog()
+        _check_capture_safe_pg()
         _stale_weights()
         self.counters = counters
         if counters is not None:
@@ -166,7 +174,7 @@ class StepGrapher:
             return self._eager(tensors)
         if self.graph is None:
             torch.cuda.synchronize()
-            _quiesce_watchdog()
+            _check_capture_safe_pg()
             _stale_weights()
             self.static = [t.clone() for t in tensors]
             if self.counters is not None:

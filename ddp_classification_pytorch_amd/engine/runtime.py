@@ -35,13 +35,16 @@ def setup(args) -> Runtime:
     backend = args.dist_backend or ("nccl" if want_cuda else "gloo")
     if getattr(args, "graph", False):
         graph_safe_nccl_env()
-    rank, local, world = init_distributed(backend)
+    rank, local, world = init_distributed(backend, force=getattr(args, "force_ddp", False))
     if want_cuda:
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         kops = _ext.hip_ops()  # GPU path requires the gfx950 library: fail loudly here, not mid-epoch
-        # per-shape conv configuration autotuning (the reference's cudnn.benchmark=True)
-        kops.set_tuning(25, 1 if getattr(args, "autotune", False) else 0)
+        # per-shape conv configuration autotuning (the reference's cudnn.benchmark=True); the
+        # DCP_AUTOTUNE environment variable (_ext.py) overrides the flag either way
+        env = os.environ.get("DCP_AUTOTUNE")
+        tune = getattr(args, "autotune", False) if env is None else env == "1"
+        kops.set_tuning(25, 1 if tune else 0)
     else:
         device = torch.device("cpu")
     set_seed(args.seed + rank)

@@ -1460,6 +1460,9 @@ def _s2d_weight_refresh(weight, buf):
     """buf <- the s2d form of the 7x7 master, one launch (no pad / permute / copy chain per step)."""
     with torch.no_grad():
         K(weight).s2d_weight(weight.detach().contiguous(), buf)
+    # the kernel writes buf behind autograd's back: bump its version so the bf16 weight cache
+    # (stamped with buf._version) refreshes even without a weight-generation bump
+    torch.autograd.graph.increment_version(buf)
 
 
 class _StemS2D(Function):

@@ -54,14 +54,18 @@ def graph_safe_nccl_env():
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
-def init_distributed(backend: str = None, timeout_s: int = 1800):
-    """torchrun / torch.distributed.launch compatible init.  Returns (rank, local_rank, world)."""
+def init_distributed(backend: str = None, timeout_s: int = 1800, force: bool = False):
+    """torchrun / torch.distributed.launch compatible init.  Returns (rank, local_rank, world).
+    ``force``: create the process group at world size 1 too (``--force-ddp``: one process runs the
+    data-parallel engine over a real, single-rank RCCL communicator)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))

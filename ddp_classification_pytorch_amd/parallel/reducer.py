@@ -116,6 +116,7 @@ class BucketReducer:
         self._next = 0              # the next bucket index to launch this backward
         self._hold = []             # side-stream case: this backward's packed autograd gradients
         self._bucket_opts = {}      # bucket index -> [(optimizer, its params in the bucket)]
+        self._warned_unused = False
         self._build(list(reversed(range(len(ps)))))
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in ps]
 
@@ -172,6 +173,14 @@ class BucketReducer:
         over (a subset of) these parameters."""
         if not hasattr(opt, "step_params"):
             raise TypeError("attach_optimizer needs a FusedSGD / FusedAdam (step_params)")
+        # every trainable parameter of the optimizer must be reduced (and so stepped) here: its
+        # step() after backward becomes a no-op, so a parameter outside the wrapped module (an
+        # unwrapped head, a margin weight) would silently never be updated
+        outside = [p for g in opt.param_groups for p in g["params"] if p.requires_grad and id(p) not in self.index]
+        if outside:
+            raise ValueError(f"attach_optimizer: {len(outside)} optimizer parameter(s) are not in the wrapped module "
+                             f"(shapes {[tuple(p.shape) for p in outside[:4]]}); wrap them too, or give them their "
+                             "own optimizer")
         self.optimizers.append(opt)
         self._bucket_opts = {}
         self._opt_params = {}
@@ -239,11 +248,20 @@ class BucketReducer:
                 self._reduce_cuda(b, grads, comm)
         else:
             self._reduce_cpu(b, grads)
-        # a parameter without a gradient this step (unused, frozen) contributes zeros to the
-        # all-reduce but keeps grad None, so no optimizer touches it (weight decay included)
-        for p, v, had in zip(b.params, b.views, present):
-            if had:
-                p.grad = v
+        # a parameter without a gradient on THIS rank (unused in this forward) contributed zeros
+        # to the all-reduce; it still gets the reduced view as its gradient, on every rank, so
+        # the replicas apply the same update whether or not another rank used it (torch DDP
+        # gives every rank the reduced bucket view too).  Unlike DDP with find_unused_parameters,
+        # a parameter no rank used gets a zero gradient rather than None: weight decay and
+        # momentum still move it -- identically on every rank, so nothing drifts.
+        if not all(present) and not self._warned_unused:
+            self._warned_unused = True
+            import warnings
+
+            warnings.warn("BucketReducer: some parameters received no gradient on this rank; they are updated "
+                          "with the all-reduced bucket view (zero where no rank used them)", stacklevel=2)
+        for p, v in zip(b.params, b.views):
+            p.grad = v
         self._step_optimizers(b)
 
     def _reduce_cuda(self, b, grads, comm):

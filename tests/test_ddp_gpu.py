@@ -212,25 +212,32 @@ def test_ddp_two_ranks_matches_full_batch(syncbn):
     assert err <= 3 * floor + 1e-2, (err, floor)
 
 
-def _rccl_graph_worker(rank, world, port, out_dir, grad_comm):
-    """World-1 RCCL group, bucket engine + SyncBN (its own communicator) + SGD fused per bucket:
-    5 eager steps vs 2 eager warm-up steps + 3 HIP-graph replays of the captured step, from the
-    same initial state -- the captured all-reduces, SyncBN collectives and per-bucket optimizer
-    launches must replay to the same parameters."""
+def _rccl_graph_worker(rank, world, port, out_dir, grad_comm, optim="sgd", comm_stream="auto"):
+    """World-1 RCCL group, bucket engine + SyncBN (its own communicator) + the optimizer fused per
+    bucket: 5 eager steps vs 2 eager warm-up steps + 3 HIP-graph replays of the captured step, from
+    the same initial state -- the captured all-reduces, SyncBN collectives and per-bucket optimizer
+    launches must replay to the same parameters.  ``comm_stream="1"`` forces the side
+    communication stream that world > 1 uses (DCP_COMM_STREAM): the captured fork / join, the
+    all-reduce and the per-bucket SGD / Adam on that stream, the autograd gradients held to the
+    join."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), DCP_COMM_STREAM=comm_stream)
     sys.path.insert(0, ROOT)
     import datetime
 
     from ddp_classification_pytorch_amd.engine.graph import GraphedStep
     from ddp_classification_pytorch_amd.models import build_model, input_layout
     from ddp_classification_pytorch_amd.ops import functional as Fn
-    from ddp_classification_pytorch_amd.optim import FusedSGD
-    from ddp_classification_pytorch_amd.parallel.ddp import attach_optimizer, wrap_ddp
+    from ddp_classification_pytorch_amd.optim import FusedAdam, FusedSGD
+    from ddp_classification_pytorch_amd.parallel import reducer as R
+    from ddp_classification_pytorch_amd.parallel.ddp import attach_optimizer, graph_safe_nccl_env, wrap_ddp
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    graph_safe_nccl_env()
     dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=120))
+    side = R._comm_stream(dev, 1) != torch.cuda.current_stream(dev)
+    assert side == (comm_stream == "1"), (side, comm_stream)
     g = torch.Generator().manual_seed(1)
     imgs = torch.randint(0, 256, (16, 3, 64, 64), dtype=torch.uint8, generator=g).to(dev)
     labels = torch.randint(0, 10, (16,), generator=g).to(dev)
@@ -240,7 +247,9 @@ def _rccl_graph_worker(rank, world, port, out_dir, grad_comm):
         model = build_model("resnet18", num_classes=10).to(dev)
         net = wrap_ddp(model, 0, syncbn=True, bucket_cap_mb=2, first_bucket_mb=0.5, force=True, engine="dcp",
                        comm_dtype=torch.bfloat16 if grad_comm == "bf16" else torch.float32)
-        opt = attach_optimizer(net, FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4))
+        opt = (FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4) if optim == "sgd"
+               else FusedAdam(model.parameters(), lr=1e-3, weight_decay=1e-4))
+        attach_optimizer(net, opt)
         x = Fn.to_device_nhwc(imgs, (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), in_scale=1 / 255.0,
                               **input_layout(model))
 
@@ -266,10 +275,13 @@ def _rccl_graph_worker(rank, world, port, out_dir, grad_comm):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("grad_comm", ["fp32", "bf16"])
-def test_rccl_world1_bucket_engine_graph_replay_matches_eager(grad_comm):
+@pytest.mark.parametrize("grad_comm,optim,comm_stream", [
+    ("fp32", "sgd", "auto"), ("bf16", "sgd", "auto"),  # world 1: bucket work on the compute stream
+    ("fp32", "sgd", "1"), ("bf16", "sgd", "1"), ("fp32", "adam", "1"),  # the side stream N ranks use
+])
+def test_rccl_world1_bucket_engine_graph_replay_matches_eager(grad_comm, optim, comm_stream):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_rccl_graph_worker, args=(1, _free_port(), d, grad_comm), nprocs=1, join=True)
+        mp.spawn(_rccl_graph_worker, args=(1, _free_port(), d, grad_comm, optim, comm_stream), nprocs=1, join=True)
         got = torch.load(os.path.join(d, "graph.pt"), weights_only=True)
     e, g = got["eager"], got["graph"]
     assert e["buckets"] >= 3
@@ -278,3 +290,108 @@ def test_rccl_world1_bucket_engine_graph_replay_matches_eager(grad_comm):
         err = (g["params"][n] - v).norm() / max(v.norm().item(), 1e-12)
         assert err < 1e-4, (n, float(err))
     assert torch.allclose(e["rm"], g["rm"], rtol=1e-4, atol=1e-5)
+
+
+def test_main_graph_force_ddp_side_stream_matches_eager(tmp_path):
+    """main.py --graph through the bucket engine on a world-1 RCCL group with the side
+    communication stream forced (DCP_COMM_STREAM=1, the N-rank configuration): 2 epochs, the step
+    recaptured at the epoch boundary, SyncBN collectives and per-bucket SGD inside the graph --
+    the weights equal the eager run's."""
+    common = ["--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+              "--batchsize", "16", "--synthetic-train-size", "96", "--synthetic-val-size", "32", "--epochs", "2",
+              "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "SGD",
+              "--lr", "0.05", "--force-ddp", "--syncbn"]
+    outs = {}
+    for tag, flag in (("eager", []), ("graph", ["--graph"])):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(_free_port()), DCP_COMM_STREAM="1")
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
+        cmd = [sys.executable, os.path.join(ROOT, "main.py")] + common + ["--out-dir", str(tmp_path / tag)] + flag
+        r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[tag] = torch.load(tmp_path / tag / "last.pth", weights_only=True)
+    for name, me in outs["eager"]["models"].items():
+        mg = outs["graph"]["models"][name]
+        for k, v in me.items():
+            if v.dtype.is_floating_point:
+                assert torch.allclose(v, mg[k], rtol=2e-3, atol=2e-4), (name, k)
+            else:
+                assert torch.equal(v, mg[k]), (name, k)
+
+
+def _gloo_engine_worker(rank, world, port, engine, out_dir):
+    """2 gloo ranks on one GPU, 3 SGD steps through ``engine``: the dcp engine runs its buckets on
+    the side communication stream (world > 1) with the optimizer fused per bucket behind each
+    all-reduce while the rest of backward still runs; torch's DDP steps after backward."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    from ddp_classification_pytorch_amd.models import build_model
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+    from ddp_classification_pytorch_amd.optim import FusedSGD
+    from ddp_classification_pytorch_amd.parallel import reducer as R
+    from ddp_classification_pytorch_amd.parallel.ddp import attach_optimizer, wrap_ddp
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = build_model("resnet18", num_classes=10).to(dev)
+    net = wrap_ddp(model, 0, syncbn=False, bucket_cap_mb=1, first_bucket_mb=0.25, engine=engine)
+    opt = attach_optimizer(net, FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4))
+    if engine == "dcp":
+        assert R._comm_stream(dev, world) != torch.cuda.current_stream(dev)
+    g = torch.Generator().manual_seed(1)
+    imgs = torch.randint(0, 256, (3, 8, 3, 64, 64), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (3, 8), generator=g)
+    sl = slice(rank * 4, rank * 4 + 4)
+    for it in range(3):
+        x = Fn.to_device_nhwc(imgs[it, sl].to(dev), (0.485, 0.456, 0.406), (0.229, 0.224, 0.225), cpad=8,
+                              in_scale=1 / 255.0)
+        loss = Fn.cross_entropy(net(x), labels[it, sl].to(dev))
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    torch.cuda.synchronize()
+    params = {n: p.detach().cpu().clone() for n, p in model.named_parameters()}
+    torch.save({"params": params, "buckets": len(net.reducer.buckets) if engine == "dcp" else 0},
+               os.path.join(out_dir, f"{engine}{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_engine_two_ranks_side_stream_matches_torch_ddp():
+    """the bucket engine's world > 1 path (side stream, per-bucket optimizer during
+    backward, gradients held to the join) trains 2 ranks to the same weights as torch's DDP, and
+    both ranks stay identical."""
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        for engine in ("dcp", "torch"):
+            mp.spawn(_gloo_engine_worker, args=(2, _free_port(), engine, d), nprocs=2, join=True)
+            res[engine] = [torch.load(os.path.join(d, f"{engine}{r}.pt"), weights_only=True) for r in range(2)]
+    assert res["dcp"][0]["buckets"] >= 3
+    for n, v in res["torch"][0]["params"].items():
+        for r in range(2):
+            got = res["dcp"][r]["params"][n]
+            err = (got - v).norm() / max(v.norm().item(), 1e-12)
+            assert err < 1e-4, (n, r, float(err))
+        assert torch.equal(res["dcp"][0]["params"][n], res["dcp"][1]["params"][n]), n
+
+
+@pytest.mark.parametrize("inject", ["syncbn", "syncbn:1"])
+def test_bench_diagnostic_phase_failure_keeps_headline(inject):
+    """A failure in the optional SyncBN phase -- on every rank (caught, recorded) or on rank 1 only
+    (the ranks then wait in mismatched collectives until the diagnostic deadline) -- still prints
+    the one JSON line with the local-BN headline."""
+    env = dict(os.environ, DCP_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", DCP_BENCH_INJECT=inject,
+               DCP_BENCH_EXTRA_DEADLINE="40")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "8", "--image-size", "64"]
+    out = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["syncbn_value"] is None
+    errs = rec["diagnostic_errors"]
+    assert ("syncbn" in errs) if inject == "syncbn" else ("deadline" in errs or "syncbn" in errs), errs
