@@ -39,7 +39,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd import _ext, tuning  # noqa: E402
 from ddp_classification_pytorch_amd.models import build_model, input_layout  # noqa: E402
 from ddp_classification_pytorch_amd.ops import functional as Fn  # noqa: E402
 from ddp_classification_pytorch_amd.optim import FusedSGD  # noqa: E402
@@ -231,12 +231,9 @@ def main(argv=None):
     # per-shape conv configuration autotuning on the (untimed) warm-up steps, as the reference's
     # torch.backends.cudnn.benchmark = True (BASELINE/main.py:40); DCP_AUTOTUNE=0 / --no-autotune off
     autotune = a.autotune and os.environ.get("DCP_AUTOTUNE", "1") != "0"
-    kops.set_tuning(25, 1 if autotune else 0)
-    # A/B experiments only: DCP_TUNE="idx=value,..." sets the kernel-config overrides
-    # (conv_igemm.hip g_tune: 0 BN tile, 1 LDS stages, 3 8-wave kernel)
-    for kv in filter(None, os.environ.get("DCP_TUNE", "").split(",")):
-        i, v = kv.split("=")
-        kops.set_tuning(int(i), int(v))
+    kops.set_tuning(tuning.slot("autotune"), 1 if autotune else 0)
+    # A/B experiments only: DCP_TUNE="name=value,..." sets kernel-config overrides (csrc/tune.h)
+    tuning.apply(kops, os.environ.get("DCP_TUNE", ""))
 
     torch.manual_seed(1234 + rank)
     model = build_bench_model(a).to(dev)

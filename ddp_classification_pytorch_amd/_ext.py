@@ -8,7 +8,7 @@ plumbing only).
 
 Set ``DCP_AUTOBUILD=1`` to compile the library on first use when it is
 missing (needs hipcc), ``DCP_AUTOTUNE=1`` to time the conv GEMM configurations per problem
-shape on first use and keep the fastest (like ``cudnn.benchmark``), ``DCP_TUNE="i=v,..."``
+shape on first use and keep the fastest (like ``cudnn.benchmark``), ``DCP_TUNE="name=v,..."``
 to override kernel configuration slots (A/B experiments).
 """
 from __future__ import annotations
@@ -48,14 +48,15 @@ def try_load() -> bool:
             _state["error"] = f"failed to load {LIB_PATH}: {e}"
             return False
         _state["loaded"] = True
+        from . import tuning
+
+        tuning.verify(torch.ops.dcp)
         if os.environ.get("DCP_AUTOTUNE", "0") == "1":
             # per-shape timing of the conv GEMM configurations on first use (conv_igemm.hip)
-            torch.ops.dcp.set_tuning(25, 1)
-        # A/B experiments: DCP_TUNE="idx=value,..." sets kernel-config overrides (g_tune) in any
-        # process that loads the library (bench.py, main.py, tests)
-        for kv in filter(None, os.environ.get("DCP_TUNE", "").split(",")):
-            i, v = kv.split("=")
-            torch.ops.dcp.set_tuning(int(i), int(v))
+            torch.ops.dcp.set_tuning(tuning.slot("autotune"), 1)
+        # A/B experiments: DCP_TUNE="name=value,..." (csrc/tune.h names) sets kernel-config
+        # overrides in any process that loads the library (bench.py, main.py, tests)
+        tuning.apply(torch.ops.dcp, os.environ.get("DCP_TUNE", ""))
         return True
 
 

@@ -514,7 +514,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   return {dx, sums};
 }
 
-// Weight-gradient configurations the autotuner (g_tune[25] = 1, DCP_AUTOTUNE) times per problem,
+// Weight-gradient configurations the autotuner (g_tune[kAutotune] = 1, DCP_AUTOTUNE) times per problem,
 // as g_tune overrides: [5] workgroups per CU of the split-K plan, [7] = 2 no 256-tile kernel,
 // [12] = 32 32-row k-tiles, [15] = 1 no direct 3x3 kernel, [27] = 64 at most 64 splits (one reduce
 // launch instead of two: pays at small batches, where the launches dominate).  The split count changes the partial
@@ -533,14 +533,14 @@ std::unordered_map<std::string, int> g_wg_choice;
 struct WgOverride {
   int saved[5];
   explicit WgOverride(const WgCfg& c) {
-    saved[0] = dcp::g_tune[5]; saved[1] = dcp::g_tune[7]; saved[2] = dcp::g_tune[12]; saved[3] = dcp::g_tune[15];
-    saved[4] = dcp::g_tune[27];
-    dcp::g_tune[5] = c.t5; dcp::g_tune[7] = c.t7; dcp::g_tune[12] = c.t12; dcp::g_tune[15] = c.t15;
-    dcp::g_tune[27] = c.t27;
+    saved[0] = dcp::g_tune[dcp::kWgSplitsPerCu]; saved[1] = dcp::g_tune[dcp::kWgTileMode]; saved[2] = dcp::g_tune[dcp::kWgRows]; saved[3] = dcp::g_tune[dcp::kWg3x3];
+    saved[4] = dcp::g_tune[dcp::kWgSplitCap];
+    dcp::g_tune[dcp::kWgSplitsPerCu] = c.t5; dcp::g_tune[dcp::kWgTileMode] = c.t7; dcp::g_tune[dcp::kWgRows] = c.t12; dcp::g_tune[dcp::kWg3x3] = c.t15;
+    dcp::g_tune[dcp::kWgSplitCap] = c.t27;
   }
   ~WgOverride() {
-    dcp::g_tune[5] = saved[0]; dcp::g_tune[7] = saved[1]; dcp::g_tune[12] = saved[2]; dcp::g_tune[15] = saved[3];
-    dcp::g_tune[27] = saved[4];
+    dcp::g_tune[dcp::kWgSplitsPerCu] = saved[0]; dcp::g_tune[dcp::kWgTileMode] = saved[1]; dcp::g_tune[dcp::kWgRows] = saved[2]; dcp::g_tune[dcp::kWg3x3] = saved[3];
+    dcp::g_tune[dcp::kWgSplitCap] = saved[4];
   }
 };
 }  // namespace
@@ -570,8 +570,8 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
     dcp::launch_wgrad(bp(dy), N, Ho, Wo, Co, bp(x), H, W, C, stride, taps, dw.data_ptr<float>(),
                       part.data_ptr<float>(), zero_page(dy.get_device()), ncu, st);
   };
-  if (dcp::g_tune[25] != 1 || dcp::g_tune[5] || dcp::g_tune[7] || dcp::g_tune[12] || dcp::g_tune[15] ||
-      dcp::g_tune[27] || (int64_t)N * Ho * Wo == 0) {
+  if (dcp::g_tune[dcp::kAutotune] != 1 || dcp::g_tune[dcp::kWgSplitsPerCu] || dcp::g_tune[dcp::kWgTileMode] || dcp::g_tune[dcp::kWgRows] || dcp::g_tune[dcp::kWg3x3] ||
+      dcp::g_tune[dcp::kWgSplitCap] || (int64_t)N * Ho * Wo == 0) {
     run();
     return dw;
   }
@@ -1547,12 +1547,20 @@ Tensor table_fill(const Tensor& host, const Tensor& device_like) {
 int64_t autotune_entries() { return dcp::tap_gemm_tuned_count() + wgrad_autotune_entries(); }
 
 void set_tuning(int64_t idx, int64_t value) {
-  TORCH_CHECK(idx >= 0 && idx < 32, "tuning index");
+  TORCH_CHECK(idx >= 0 && idx < dcp::kTuneSlots, "tuning index");
   dcp::g_tune[idx] = (int)value;
+}
+
+// "name=slot;..." of every named slot (tune.h): the Python mirror (tuning.py) is checked against it
+std::string tuning_slots() {
+  std::string out;
+  for (const auto& t : dcp::kTuneSlotNames) out += std::string(t.name) + "=" + std::to_string(t.slot) + ";";
+  return out;
 }
 
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
+  m.def("tuning_slots() -> str", &tuning_slots);
   m.def("autotune_entries() -> int", &autotune_entries);
   m.def("table_fill(Tensor host, Tensor device_like) -> Tensor", &table_fill);
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);

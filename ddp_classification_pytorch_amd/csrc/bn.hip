@@ -306,55 +306,6 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
   finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
 }
 
-// Local BN from the conv slabs in ONE launch for any slab count: bn_slab_partial's workgroups
-// (grid (C/64, P)) store their split partials, and the last to arrive for each 64-channel group
-// (last_arrival) merges the P partials in split order and finalizes -- the bn_slab_partial +
-// bn_merge_finalize pair without the second launch.
-__global__ void __launch_bounds__(256) bn_slab_partial_finalize_kernel(
-    const float* __restrict__ slabs, int R, int M, int C, int tiles_per_split, float* __restrict__ part,
-    unsigned* __restrict__ ctr, float eps, const float* __restrict__ gamma, const float* __restrict__ beta,
-    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale, float* __restrict__ shift,
-    float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  const int r0 = blockIdx.y * tiles_per_split;
-  const int r1 = min(R, r0 + tiles_per_split);
-  Welford a{0.f, 0.f, 0.f};
-  if (c < C) {
-    int r = r0 + w;
-    for (; r + 12 < r1; r += 16) {
-      float mb[4], m2b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        mb[u] = slabs[((size_t)(r + 4 * u) * 2 + 0) * C + c];
-        m2b[u] = slabs[((size_t)(r + 4 * u) * 2 + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a.merge((float)min(128, M - 128 * (r + 4 * u)), mb[u], m2b[u]);
-    }
-    for (; r < r1; r += 4) {
-      const float nb = (float)min(128, M - 128 * r);
-      a.merge(nb, slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
-    }
-  }
-  __shared__ float red[3][4][64];
-  red[0][w][lane] = a.n;
-  red[1][w][lane] = a.mean;
-  red[2][w][lane] = a.m2;
-  __syncthreads();
-  if (w == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
-    part[((size_t)blockIdx.y * 3 + 0) * C + c] = a.n;
-    part[((size_t)blockIdx.y * 3 + 1) * C + c] = a.mean;
-    part[((size_t)blockIdx.y * 3 + 2) * C + c] = a.m2;
-  }
-  if (!last_arrival(ctr + blockIdx.x, gridDim.y)) return;
-  const Welford m = merge_partials<4>(part, gridDim.y, C);
-  if (w != 0 || c >= C) return;
-  Welford f{0.f, 0.f, 0.f};
-  f.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
-  finalize_channel(f, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
-}
 
 // [P][K] -> [K] column sums; one workgroup per 64 columns, 4 waves x 4-deep unroll over P
 __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restrict__ part, int P, int K,
@@ -828,16 +779,6 @@ void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, f
                        eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
     return;
   }
-  // one launch (merge + finalize in each channel group's last workgroup): g_tune[23] = 1 only, measured
-  // slower -- see launch_split_reduce
-  unsigned* ctr = (slabs && g_tune[23] == 1) ? ticket_counters((C + 63) / 64) : nullptr;
-  if (ctr) {
-    const int P = bn_stats_partials(M, C, true);
-    const int tps = (R + P - 1) / P;
-    hipLaunchKernelGGL(bn_slab_partial_finalize_kernel, dim3((C + 63) / 64, P), dim3(256), 0, s, slabs, R, M, C, tps,
-                       part, ctr, eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
-    return;
-  }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
   hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps, gamma, beta,
                      mean, invstd, scale, shift, rm, rv, momentum);
@@ -917,12 +858,12 @@ static inline int rows_grid(int M, int C, int rows_per_thread, int cap) {
 // Elementwise grid: two rows per thread and no practical cap on the workgroup count.  Measured
 // on the R50 b512 stage-1/2 tensors (tools/ew_bench.py): 5.7-6.0 TB/s against 4.5 TB/s for a
 // 4096-workgroup grid-stride loop over 8 rows per thread -- HBM wants the whole tensor's loads
-// spread over many short-lived waves.  g_tune[9] / [10] override cap / rows (A/B only).
+// spread over many short-lived waves.  g_tune[kEwGridCap] / [10] override cap / rows (A/B only).
 static inline dim3 ew_grid(int M, int C) {
   // 4 rows per thread where that still leaves >= 2048 workgroups (8 per CU): R50 b1024 +0.4 % over
   // 2 (same box, 4 pairs; 8 rows -0.6 %, 1 row -5 %: profiles/r3/ew_rows_ab.txt); small tensors 2
-  const int cap = g_tune[9] > 0 ? g_tune[9] : (1 << 20);
-  if (g_tune[10] > 0) return dim3(rows_grid(M, C, g_tune[10], cap));
+  const int cap = g_tune[kEwGridCap] > 0 ? g_tune[kEwGridCap] : (1 << 20);
+  if (g_tune[kEwRows] > 0) return dim3(rows_grid(M, C, g_tune[kEwRows], cap));
   const int g4 = rows_grid(M, C, 4, cap);
   return dim3(g4 >= 2048 ? g4 : rows_grid(M, C, 2, cap));
 }
@@ -932,13 +873,13 @@ void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const
                        const float* rscale, const float* rshift) {
   const int M = (int)(numel / C);
   const dim3 grid = ew_grid(M, C);
-  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[11],
+  DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[kBnActVariant],
                        mask, rscale, rshift);
 }
 
-// g_tune[28] overrides the workgroup cap (A/B only: 256 and 1024 measured 0.5-1.2 % slower end to end
+// g_tune[kBnBwdCap] overrides the workgroup cap (A/B only: 256 and 1024 measured 0.5-1.2 % slower end to end
 // at b1024, profiles/r3/ew_rows_ab.txt)
-int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, g_tune[28] > 0 ? g_tune[28] : 512); }
+int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, g_tune[kBnBwdCap] > 0 ? g_tune[kBnBwdCap] : 512); }
 
 // partials must hold bn_bwd_reduce_blocks(M, C) x 2 x C floats; out [2][C]
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,

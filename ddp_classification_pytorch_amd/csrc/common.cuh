@@ -129,32 +129,5 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
   return base + idx;
 }
 
-// Last-arrival ticket: the `total` workgroups of a group each call this after storing their
-// partial result; it returns true in exactly one of them, the last to arrive, which may then read
-// every other workgroup's partial (release fence before the counter increment, acquire fence
-// after it: the stores of workgroups on other XCDs are written back from their L2s and this CU's
-// caches are invalidated).  That workgroup leaves the counter at zero again, so one zeroed counter
-// pool serves every launch on a stream in turn (ticket_counters).  Lets a two-level reduction run
-// as ONE launch: the second level inside the first level's last workgroup.  Costly on MI355X: the
-// release fence writes back the XCD's L2 in every workgroup (measured: launch_split_reduce).
-__device__ __forceinline__ bool last_arrival(unsigned* ctr, unsigned total) {
-  __shared__ unsigned s_last;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = atomicAdd(ctr, 1u);
-    s_last = (t + 1 == total) ? 1u : 0u;
-    if (s_last) atomicExch(ctr, 0u);
-  }
-  __syncthreads();
-  const bool last = s_last != 0;
-  if (last) __threadfence();
-  return last;
-}
-
-constexpr int kTicketCounters = 1 << 16;
-// zeroed counters for last_arrival, one pool per device (allocated on first use: call it once
-// outside a stream capture -- every op's first, eager, call does); nullptr if n is too large
-unsigned* ticket_counters(int n);
 
 }  // namespace dcp

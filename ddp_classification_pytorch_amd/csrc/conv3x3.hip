@@ -17,11 +17,11 @@
 //    at a time (four independent accumulator chains);
 //  * the epilogue rounds to bf16, accumulates shifted per-channel sums of the rounded values
 //    (the numbers the BN normalises) and stores each lane's 4 channels straight from the
-//    accumulators (c3_tile_direct, weights as the MFMA A operand; g_tune[30] = 2: the older
+//    accumulators (c3_tile_direct, weights as the MFMA A operand; g_tune[kC3Epilogue] = 2: the older
 //    per-wave LDS staging tile); the next strip's window streams in behind this strip's
-//    MFMAs (8 waves, two window buffers; g_tune[19] = 1 / 2: 4-wave variants, not faster);
+//    MFMAs (8 waves, two window buffers; g_tune[kC3Variant] = 1 / 2: 4-wave variants, not faster);
 //  * the window DMA is untracked (dma16), so the fragment prefetch gets exact lgkmcnt waits.
-//    Timing ablations (g_tune[2]) at b1024: no stores 251 us, no window loads 232, neither 210,
+//    Timing ablations (g_tune[kAblate]) at b1024: no stores 251 us, no window loads 232, neither 210,
 //    full 284 -- the MFMA loop itself, not memory, is the bound (~45 % of MFMA peak).
 #include <algorithm>
 
@@ -47,8 +47,8 @@ struct C3Params {
   int strips, sps;   // strips in total, strips per workgroup
   int Wp, xq;        // window pitch (c3_pitch) and its 16-byte chunk count
   int wbytes, nbuf;  // bytes per window buffer (1 KB aligned), window buffers (1 or 2)
-  int ablate;        // timing ablations (g_tune[2], direct epilogue only): 1 no stores, 2 no window loads
-  int sched;         // g_tune[19] = 3: s_setprio 1 for the upper wave half; 4: upper half out of phase
+  int ablate;        // timing ablations (g_tune[kAblate], direct epilogue only): 1 no stores, 2 no window loads
+  int sched;         // g_tune[kC3Variant] = 3: s_setprio 1 for the upper wave half; 4: upper half out of phase
   FastDiv div_wp, div_w, div_spi;
 };
 
@@ -150,7 +150,7 @@ __device__ __forceinline__ void c3_tile(const C3Params& p, const char* win, char
 // no LDS staging round trip, no wave barriers.  Statistics are per (lane group, i) channel and
 // reduced across the 16 pixel lanes at the end.  The default: 2-7 % faster than the staged
 // epilogue at b1024 (profiles/r4/conv3x3_direct_epilogue_ab.txt); bit-identical outputs, BN
-// statistics equal up to fp32 summation order.  g_tune[30] = 2 selects the staged epilogue.
+// statistics equal up to fp32 summation order.  g_tune[kC3Epilogue] = 2 selects the staged epilogue.
 template <int NU>
 __device__ __forceinline__ void c3_tile_direct(const C3Params& p, const char* win, const bf16x8 (&bw)[9][2][2], int s0,
                                                int du, int npix, size_t ybase, int ch, int lane, float (&K)[2][4],
@@ -382,17 +382,17 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
 }
 
 // ---------------------------------------------------------------------------
-// variants (g_tune[19]): 0 = 8 waves, one workgroup per CU, double-buffered windows (the next
+// variants (g_tune[kC3Variant]): 0 = 8 waves, one workgroup per CU, double-buffered windows (the next
 // strip streams in behind this strip's MFMAs); 1 = 4 waves, two workgroups per CU, one window
 // each; 2 = 4 waves, two double-buffered smaller windows
 struct C3Cfg {
   int nw, nbuf, budget;  // waves, window buffers, bytes per window buffer
 };
 static C3Cfg c3_cfg() {
-  if (g_tune[19] == 1) return {4, 1, kC3WinMax};
-  if (g_tune[19] == 2) return {4, 2, kC3WinBuf2};
-  if (g_tune[30] != 2)  // direct epilogue: no staging tiles, the LDS goes to taller windows
-    return {8, 2, g_tune[31] > 0 ? std::min(g_tune[31], 78) * 1024 : kC3WinDirect};
+  if (g_tune[kC3Variant] == 1) return {4, 1, kC3WinMax};
+  if (g_tune[kC3Variant] == 2) return {4, 2, kC3WinBuf2};
+  if (g_tune[kC3Epilogue] != 2)  // direct epilogue: no staging tiles, the LDS goes to taller windows
+    return {8, 2, g_tune[kC3WindowKB] > 0 ? std::min(g_tune[kC3WindowKB], 78) * 1024 : kC3WinDirect};
   return {8, 2, kC3WinMax};
 }
 
@@ -410,7 +410,7 @@ static int c3_rows(int H, int W) {
 }
 
 bool conv3x3_c64_supported(int H, int W, int C, int Co) {
-  return g_tune[18] != 1 && C == 64 && Co == 64 && H >= 1 && W >= 1 && c3_rows(H, W) > 0;
+  return g_tune[kC3Off] != 1 && C == 64 && Co == 64 && H >= 1 && W >= 1 && c3_rows(H, W) > 0;
 }
 
 int conv3x3_c64_blocks(int N, int H, int W, int num_cu) {
@@ -427,8 +427,8 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   C3Params p;
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
   p.H = H; p.W = W;
-  p.ablate = g_tune[2];
-  p.sched = g_tune[19];
+  p.ablate = g_tune[kAblate];
+  p.sched = g_tune[kC3Variant];
   p.R = c3_rows(H, W);
   p.spi = (H + p.R - 1) / p.R;
   p.strips = N * p.spi;
@@ -440,7 +440,7 @@ void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, cons
   p.div_wp = make_fastdiv(p.Wp);
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
-  const bool de = g_tune[30] != 2;
+  const bool de = g_tune[kC3Epilogue] != 2;
   const int lds = p.nbuf * p.wbytes + (de ? 0 : cfg.nw * 32 * 64);
   static bool attr = false;
   if (!attr) {

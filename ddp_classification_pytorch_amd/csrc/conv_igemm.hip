@@ -44,7 +44,7 @@
 
 namespace dcp {
 
-int g_tune[32] = {0};
+int g_tune[kTuneSlots] = {0};
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
@@ -116,65 +116,6 @@ template <int NCH>
 __device__ __forceinline__ bf16x8 eimg_chunk(const char* E, uint32_t pl, uint32_t c) {
   const bf16x8 v = *LDS_PTR(const bf16x8, E + pl * (NCH * 16) + ((c ^ ((pl >> 1) & (NCH - 1))) << 4));
   return (pl & 1) ? bf16x8{v[4], v[5], v[6], v[7], v[0], v[1], v[2], v[3]} : v;
-}
-
-// Per 128-row slab and channel of the LDS output image E[rows][BN] (16-byte chunks
-// XOR-swizzled by row>>1): (mean, M2) of the bf16-rounded outputs.  A thread takes one
-// channel x 64 rows with two passes over register-resident values (no E[x^2]-E[x]^2
-// cancellation), then the two 64-row halves of a slab are merged with Chan's formula
-// through LDS (scratch behind the image).  NT = 64-row tiles in the block (even).
-template <int BN, int NT>
-__device__ __forceinline__ void tile_stats(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
-  constexpr int RB = BN * 2, NCH = BN / 8;
-  static_assert(NT % 2 == 0, "slabs pair 64-row tiles");
-  float* xch = (float*)(E + NT * 64 * RB);  // [NT/2][3][BN]
-  const int ch = tid % BN, h = tid / BN;
-  const int co = n0 + ch;
-  const bool active = h < NT && co < p.Co;
-  const int nvalid = active ? max(0, min(64, p.M - (m0 + h * 64))) : 0;
-  float mean = 0.f, m2 = 0.f;
-  if (nvalid > 0) {
-    const uint32_t coff = ((ch >> 3) << 4) + (ch & 7) * 2;
-    float v[64];
-#pragma unroll
-    for (int r = 0; r < 64; ++r) {
-      const uint32_t pl = h * 64 + r;
-      v[r] = bf2f(*LDS_PTR(bf16, E + pl * RB + ((coff ^ (((pl >> 1) & (NCH - 1)) << 4)) ^ ((pl & 1) << 3))));
-    }
-    float s[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s[k] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 64; ++r) s[r & 7] += r < nvalid ? v[r] : 0.f;
-    mean = ((s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]))) / (float)nvalid;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s[k] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 64; ++r) {
-      const float d = v[r] - mean;
-      s[r & 7] += r < nvalid ? d * d : 0.f;
-    }
-    m2 = (s[0] + s[1]) + (s[2] + s[3]) + ((s[4] + s[5]) + (s[6] + s[7]));
-  }
-  if (active && (h & 1)) {
-    xch[((h >> 1) * 3 + 0) * BN + ch] = (float)nvalid;
-    xch[((h >> 1) * 3 + 1) * BN + ch] = mean;
-    xch[((h >> 1) * 3 + 2) * BN + ch] = m2;
-  }
-  __syncthreads();
-  if (active && !(h & 1) && nvalid > 0) {
-    const float nb = xch[((h >> 1) * 3 + 0) * BN + ch];
-    if (nb > 0.f) {
-      const float mb = xch[((h >> 1) * 3 + 1) * BN + ch], m2b = xch[((h >> 1) * 3 + 2) * BN + ch];
-      const float na = (float)nvalid, n = na + nb;
-      const float d = mb - mean;
-      mean += d * (nb / n);
-      m2 += m2b + d * d * (na * nb / n);
-    }
-    const size_t rb = (size_t)(m0 / 128 + (h >> 1));
-    p.stats[(rb * 2 + 0) * p.Co + co] = mean;
-    p.stats[(rb * 2 + 1) * p.Co + co] = m2;
-  }
 }
 
 // (mean, M2) per channel of the 128-row slab of the LDS output image E (bf16-rounded outputs),
@@ -769,578 +710,6 @@ tap_gemm_kernel(const TapGemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// Window tap GEMM: 3x3-neighbourhood taps (|dy|, |dx| <= 1, stride 1, output grid == input grid:
-// the 3x3 / pad-1 forward conv and its data gradient), C % 64 == 0.
-//
-// tap_gemm_kernel gathers a fresh 128-row A tile for every (tap, 64-channel chunk) k-step, so
-// every input pixel crosses L2 -> LDS nine times.  Here a workgroup's 128 GEMM rows are 128
-// consecutive output pixels (NHWC order), and the input pixels any of their taps can touch form
-// ONE contiguous range, [m0 - W - 1, m0 + 128 + W + 1): that "window" is staged once per
-// 64-channel chunk (one LDS-DMA per 16-byte piece, pieces XOR-swizzled by the window pixel's low
-// three bits so a fragment read of 16 consecutive pixels is conflict free), and tap t reads it
-// shifted by dy * W + dx.  A tap whose source pixel lies outside the image (image edges, other
-// images of the batch) is masked to zero per fragment from a 9-bit validity mask computed once.
-// The k-steps run chunk-major (9 taps of one chunk, then the next): the next chunk's window
-// streams in one instruction per step over the first steps, the next step's weight tile
-// (128 channels x 64) is double-buffered; vmcnt(0) + barrier per step as in tap_gemm_kernel.
-// LDS: 2 windows of (128 + 2W + 2) x 128 B (rounded to 4 KB) + 2 x 16 KB weights: two workgroups
-// per CU up to W = 28.
-// Measured (profiles/r3/conv3x3_window_ab_b1024.txt): no faster than the gather kernel on the
-// ResNet-50 3x3 shapes (128 ch 28x28: 301.6 vs 299.8 us forward; 256 ch 14x14: 257.8 vs 249.2;
-// headline 14,236 -> 14,186 img/s) -- cutting the A staging to a ninth does not move a k-loop
-// bound by its per-step barrier and load latency.  Kept behind g_tune[22] = 1 (off by default).
-// ---------------------------------------------------------------------------
-constexpr int kWinMaxW = 64;  // widest image row (the next window streams in over <= 9 steps)
-
-__host__ __device__ constexpr int win_instrs(int W) { return ((128 + 2 * W + 2) * 8 + 255) / 256; }
-
-__device__ __forceinline__ uint32_t win_off(uint32_t w, uint32_t k) { return w * 128u + ((k ^ (w & 7u)) << 4); }
-
-template <int EPI>
-__global__ void __launch_bounds__(256, 2) tap_win_kernel(const TapGemmParams p) {
-  constexpr int BN = 128, BM = 128, BK = 64, TN = BN / 32;
-  constexpr int B_BYTES = BN * BK * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const uint32_t tn = bid % ntn, tm = bid / ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int W = p.Ws, H = p.Hs;
-  const int WP = BM + 2 * W + 2;
-  const int nwi = win_instrs(W);
-  const int wbytes = nwi * 4096;
-  char* const win0 = smem;
-  char* const bst0 = smem + 2 * wbytes;
-  const int wbase = m0 - W - 1;  // input pixel at window index 0
-  const int ntaps = p.ntaps;
-  const int nkt = (p.Cs / BK) * ntaps;
-
-  // per A fragment: which taps read a pixel inside the image (bit t)
-  uint32_t vm[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t mm = (uint32_t)min(m0 + wm * 64 + i * 16 + (int)(lane & 15), p.M - 1);
-    const uint32_t q = fdiv(mm, p.div_wy);
-    const int x = (int)(mm - q * p.Wy);
-    const int y = (int)(q - fdiv(q, p.div_hy) * p.Hy);
-    uint32_t v = 0;
-    for (int t = 0; t < ntaps; ++t) {
-      const int tv = p.tap[t];
-      v |= ((unsigned)(y + tap_dy(tv)) < (unsigned)H && (unsigned)(x + tap_dx(tv)) < (unsigned)W) ? (1u << t) : 0u;
-    }
-    vm[i] = v;
-  }
-  // weight tile rows (tap_gemm_kernel's FAST B staging, 64-deep)
-  const bf16* fb_ptr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (wave * 4 + i) * 8 + lane / 8;
-    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % 8) ^ swz_chunk<BK>(r)) * 8;
-  }
-
-  auto stage_win = [&](int ch, int b, int j) {
-    const int L = j * 256 + tid;  // physical 16-byte slot of the window buffer
-    const int w = L >> 3;
-    if (w < WP) {
-      const int k = (L & 7) ^ (w & 7);
-      const int q = wbase + w;
-      const bf16* g = (q >= 0 && q < p.M) ? p.src + (size_t)q * p.Cs + ch * BK + k * 8 : p.zero;
-      dma16_tracked(g, win0 + b * wbytes + (j * 256 + wave * 64) * 16);
-    }
-  };
-  auto stage_b = [&](int kt, int b) {
-    const int ch = kt / ntaps, t = kt - ch * ntaps;
-    const long boff = (long)tap_w(p.tap[t]) * p.Cs + ch * BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dma16_tracked((fb_ptr[i] + boff), bst0 + b * B_BYTES + (wave * 4 + i) * 1024);
-  };
-
-  f32x4 acc[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int j = 0; j < nwi; ++j) stage_win(0, 0, j);
-  stage_b(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int ch = kt / ntaps, t = kt - ch * ntaps;
-    // the next chunk's window: one instruction per step over this chunk's first nwi steps (its
-    // buffer was last read by the previous chunk, which ended behind a barrier)
-    if (t < nwi && (ch + 1) * ntaps < nkt) stage_win(ch + 1, (ch + 1) & 1, t);
-    if (kt + 1 < nkt) stage_b(kt + 1, (kt + 1) & 1);
-    const char* Wn = win0 + (ch & 1) * wbytes;
-    const char* Bs = bst0 + (kt & 1) * B_BYTES;
-    const int tv = p.tap[t];
-    const int shift = W + 1 + tap_dy(tv) * W + tap_dx(tv);
-    const uint32_t tbit = 1u << t;
-#pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
-      const uint32_t c = s * 4 + (lane >> 4);
-      bf16x8 wf[TN], af[4];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint32_t r = wn * (BN / 2) + j * 16 + (lane & 15);
-        wf[j] = *(const bf16x8*)(Bs + swzk<BK>(r, c));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t w = wm * 64 + i * 16 + (lane & 15) + shift;
-        const bf16x8 a = *(const bf16x8*)(Wn + win_off(w, c));
-        af[i] = (vm[i] & tbit) ? a : bf16x8{};
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  tg_store_epilogue<BN, EPI>(p, acc, smem, m0, n0, tid, lane, wm, wn);
-}
-
-// ---------------------------------------------------------------------------
-// Persistent tap GEMM (FAST shapes, EPI 0 / 1, no residual add): each workgroup walks a
-// contiguous run of output tiles (column tiles of one row block back to back, so the A rows
-// they share come from this XCD's L2), and its NS-stage LDS-DMA ring runs ACROSS tile
-// boundaries -- the first k-tiles of tile i+1 are in flight while tile i's epilogue writes its
-// image, stores the output and reduces the BN statistics.  In the one-tile-per-workgroup kernel
-// that epilogue (and the k-loop's load latency) is hidden only by the other workgroups on the CU;
-// the 1x1 "expansion" convs (the output 4x the input) and the deep-K shapes stall on it.
-// Synchronisation: LDS-only raw barriers (lgkmcnt(0) + s_barrier) everywhere -- a
-// __syncthreads() would drain vmcnt, i.e. the prefetched stages AND the epilogue's stores.  The
-// counted vmcnt before each k-step counts the stages issued after the needed one plus, for the
-// first k-steps of a tile, the previous epilogue's stores when they were issued after it
-// (counted only for full tiles, where every wave issues every store; otherwise 0 = wait longer).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// tile_stats128_vv with LDS-only barriers (the persistent kernel keeps loads / stores in flight)
-template <int BN>
-__device__ __forceinline__ void tile_stats128_nb(const TapGemmParams& p, char* E, int m0, int n0, int tid) {
-  constexpr int NCH = BN / 8, G = 256 / NCH, RPT = 128 / G, RB = BN * 2;
-  const int c = tid % NCH, g = tid / NCH, lane = tid & 63, wave = tid >> 6;
-  const int nvalid = min(128, p.M - m0);
-  float K[8], s1[8], s2[8];
-  {
-    const bf16x8 v = eimg_chunk<NCH>(E, 0, c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      K[e] = bf2f(v[e]);
-      s1[e] = s2[e] = 0.f;
-    }
-  }
-  bf16x8 vv[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) vv[k] = eimg_chunk<NCH>(E, g + G * k, c);
-#pragma unroll
-  for (int k = 0; k < RPT; ++k)
-    if (g + G * k < nvalid)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = bf2f(vv[k][e]) - K[e];
-        s1[e] += d;
-        s2[e] = fmaf(d, d, s2[e]);
-      }
-#pragma unroll
-  for (int off = NCH; off < 64; off *= 2)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += __shfl_xor(s1[e], off, 64);
-      s2[e] += __shfl_xor(s2[e], off, 64);
-    }
-  lds_barrier();  // every image read done: rows 8.. become scratch
-  float* xch = (float*)(E + 8 * RB);
-  if (lane < NCH)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      xch[(wave * 2 + 0) * BN + c * 8 + e] = s1[e];
-      xch[(wave * 2 + 1) * BN + c * 8 + e] = s2[e];
-    }
-  lds_barrier();
-  if (tid < BN && n0 + tid < p.Co) {
-    float S1 = 0.f, S2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      S1 += xch[(w * 2 + 0) * BN + tid];
-      S2 += xch[(w * 2 + 1) * BN + tid];
-    }
-    const float k0 = bf2f(eimg_chunk<NCH>(E, 0, tid >> 3)[tid & 7]);
-    const float n = (float)nvalid;
-    const size_t rb = (size_t)(m0 / 128);
-    p.stats[(rb * 2 + 0) * p.Co + n0 + tid] = k0 + S1 / n;
-    p.stats[(rb * 2 + 1) * p.Co + n0 + tid] = fmaxf(S2 - S1 * S1 / n, 0.f);
-  }
-}
-
-template <int BN, int EPI, int NS, int BK>
-__global__ void __launch_bounds__(256, 2)
-tap_gemm_ps_kernel(const TapGemmParams p) {
-  static_assert(EPI == 0 || EPI == 1, "persistent tap GEMM: plain / statistics epilogue");
-  static_assert(NS >= 3, "the ring keeps NS-2 stages in flight across each barrier");
-  constexpr int BM = 128;
-  constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;
-  constexpr int AI = BM / (4 * RPI), BI = BN / (4 * RPI), LPT = AI + BI;
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int TN = BN / 32, NCH = BN / 8, RB = BN * 2, R = 256 / NCH, SPT = BM / R;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* E = smem + NS * STAGE;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const uint32_t T = ntm * ntn;
-  const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * T) / gridDim.x);
-  const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * T) / gridDim.x);
-  if (t0 >= t1) return;
-  const int nkt = p.nkt, tiles_per_tap = p.cpt / CH;
-  const int G = (int)(t1 - t0) * nkt;  // k-steps of this workgroup
-
-  // ---- issue side: the tile whose k-tiles are being staged ----
-  const bf16* fa_ptr[AI];
-  uint32_t fa_vm[AI];
-  const bf16* fb_ptr[BI];
-  auto setup_issue = [&](uint32_t tile) {
-    const int m0 = (int)(tile / ntn) * BM, n0 = (int)(tile % ntn) * BN;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int r = (wave * AI + i) * RPI + lane / CH;
-      const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
-      const uint32_t q = fdiv(mm, p.div_wy);
-      const uint32_t x = mm - q * p.Wy;
-      const uint32_t n = fdiv(q, p.div_hy);
-      const uint32_t y = q - n * p.Hy;
-      const int ys = y * p.ss, xs = x * p.ss;
-      fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs +
-                  ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
-      uint32_t vm = 0;
-      for (int t = 0; t < p.ntaps; ++t) {
-        const int tv = p.tap[t];
-        const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
-        vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
-      }
-      fa_vm[i] = vm;
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int r = (wave * BI + i) * RPI + lane / CH;
-      fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
-    }
-  };
-  uint32_t iss_tile = t0;
-  int iss_kt = 0;
-  setup_issue(iss_tile);
-  auto issue = [&](int slot) {
-    char* As = smem + slot * STAGE;
-    char* Bs = As + A_BYTES;
-    const int t = iss_kt / tiles_per_tap;
-    const int cbase = (iss_kt - t * tiles_per_tap) * BK;
-    const int tv = p.tap[t];
-    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;
-    const long boff = (long)tap_w(tv) * p.Cs + cbase;
-    const uint32_t tbit = 1u << t;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      dma16_tracked(g, As + (wave * AI + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i)
-      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
-    if (++iss_kt == nkt) {
-      iss_kt = 0;
-      if (++iss_tile < t1) setup_issue(iss_tile);
-    }
-  };
-
-  f32x4 acc[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int issued = 0;
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (issued < G) issue(issued++ % NS);
-  int store_mark = 0, store_cnt = 0;  // the last epilogue's stores precede stage `store_mark`
-  uint32_t tile = t0;
-  int kt = 0;
-  for (int g = 0; g < G; ++g) {
-    wait_vmcnt(LPT * (issued - g - 1) + (g < store_mark ? store_cnt : 0));
-    lds_barrier();  // stage g landed for every wave; stage g-1's slot is free
-    if (issued < G) issue(issued++ % NS);
-    {
-      const char* As = smem + (g % NS) * STAGE;
-      const char* Bs = As + A_BYTES;
-#pragma unroll
-      for (int s = 0; s < BK / 32; ++s) {
-        const uint32_t c = s * 4 + (lane >> 4);
-        bf16x8 wf[TN], af[4];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (BN / 2) + j * 16 + (lane & 15), c));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 64 + i * 16 + (lane & 15), c));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-      }
-    }
-    if (++kt < nkt) continue;
-    // ---- epilogue of `tile` (its own LDS image: the ring keeps streaming) ----
-    kt = 0;
-    const int m0 = (int)(tile / ntn) * BM, n0 = (int)(tile % ntn) * BN;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint32_t cl = wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        *LDS_PTR(bf16x4, E + eimg_off8<NCH>(pl, cl)) = o;
-        acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    lds_barrier();
-    const int c = tid % NCH, pr0 = tid / NCH;
-    const bool cok = n0 + c * 8 < p.Co;
-    bf16x8 vv[SPT];
-#pragma unroll
-    for (int k = 0; k < SPT; ++k) vv[k] = eimg_chunk<NCH>(E, pr0 + k * R, c);
-#pragma unroll
-    for (int k = 0; k < SPT; ++k) {
-      const int m = m0 + pr0 + k * R;
-      if (m < p.M && cok) {
-        size_t drow;
-        if (p.ds == 1) {
-          drow = (size_t)m * (size_t)p.Co;
-        } else {
-          const uint32_t q = fdiv(m, p.div_wy);
-          const uint32_t x = m - q * p.Wy;
-          const uint32_t n = fdiv(q, p.div_hy);
-          const uint32_t y = q - n * p.Hy;
-          drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
-        }
-        *(bf16x8*)(p.dst + drow + n0 + c * 8) = vv[k];
-      }
-    }
-    const bool full = m0 + BM <= p.M && n0 + BN <= p.Co;
-    store_cnt = full ? SPT : 0;
-    if constexpr (EPI == 1) {
-      tile_stats128_nb<BN>(p, E, m0, n0, tid);
-      if (full && wave * 64 < BN) store_cnt += 2;
-    }
-    store_mark = issued;
-    ++tile;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 8-wave variant for the common one-tap-per-k-tile shapes with Co >= 128:
-// 256 pixel rows x 128 output channels per workgroup (the weight tile is shared
-// by twice the rows: 6 instead of 8 LDS-DMA instructions per thread per 64-deep
-// k-tile for the same 32 MFMAs per wave), 3 LDS stages (144 KB) so a tile's loads
-// are issued two k-tiles ahead and stay in flight across the raw barrier, drained
-// by a counted vmcnt.  One workgroup (2 waves per SIMD) per CU.
-// ---------------------------------------------------------------------------
-template <int EPI>
-__global__ void __launch_bounds__(512)
-tap_gemm8_kernel(const TapGemmParams p) {
-  constexpr int BM = 256, BN = 128, NS = 3;
-  constexpr int A_BYTES = BM * 128;       // pixel rows x 64 k (bf16)
-  constexpr int B_BYTES = BN * 128;       // channel rows x 64 k
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int TN = 4;
-  constexpr int LPT = 6;                  // LDS-DMA instructions per thread per k-tile
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;  // 64-pixel group, 64-channel group
-
-  const uint32_t ntn = (p.Co + BN - 1) / BN;
-  const uint32_t ntm = (p.M + BM - 1) / BM;
-  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const uint32_t tn = bid % ntn, tm = bid / ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  uint32_t a_pix[4];
-  int a_ys[4], a_xs[4];
-  uint32_t a_chunk[4];
-  bool a_ok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (wave * 4 + i) * 8 + (lane >> 3);
-    const int m = m0 + r;
-    a_ok[i] = m < p.M;
-    const uint32_t mm = a_ok[i] ? m : 0;
-    const uint32_t q = fdiv(mm, p.div_wy);
-    const uint32_t x = mm - q * p.Wy;
-    const uint32_t n = fdiv(q, p.div_hy);
-    const uint32_t y = q - n * p.Hy;
-    a_pix[i] = n * (uint32_t)(p.Hs * p.Ws);
-    a_ys[i] = y * p.ss;
-    a_xs[i] = x * p.ss;
-    a_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
-  }
-  uint32_t b_row[2], b_chunk[2];
-  bool b_ok[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = (wave * 2 + i) * 8 + (lane >> 3);
-    b_ok[i] = (n0 + r) < p.Co;
-    b_row[i] = (uint32_t)(n0 + r) * p.ldw;
-    b_chunk[i] = (lane & 7) ^ ((r >> 1) & 7);
-  }
-  const int tiles_per_tap = p.cpt >> 3;
-
-  auto stage = [&](int kt, int buf) {
-    char* As = smem + buf * STAGE;
-    char* Bs = As + A_BYTES;
-    const int t = kt / tiles_per_tap;
-    const int cbase = (kt - t * tiles_per_tap) * 64;
-    const int tv = p.tap[t];
-    const int dy = tap_dy(tv), dx = tap_dx(tv);
-    const uint32_t wofs = (uint32_t)tap_w(tv) * p.Cs + cbase;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int hi = a_ys[i] + dy, wi = a_xs[i] + dx;
-      const bool ok = a_ok[i] && (unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws;
-      const bf16* g = ok ? p.src + (size_t)(a_pix[i] + hi * p.Ws + wi) * p.Cs + cbase + a_chunk[i] * 8 : p.zero;
-      dma16_tracked(g, As + (wave * 4 + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bf16* g = b_ok[i] ? p.wt + b_row[i] + wofs + b_chunk[i] * 8 : p.zero;
-      dma16_tracked(g, Bs + (wave * 2 + i) * 1024);
-    }
-  };
-
-  f32x4 acc[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nkt = p.nkt;
-  stage(0, 0);
-  if (nkt > 1) stage(1, 1);
-  for (int kt = 0; kt < nkt; ++kt) {
-    wait_vmcnt(kt + 1 < nkt ? LPT : 0);  // tile kt landed (tile kt+1 may stay in flight)
-    if (!(p.ablate & 4)) __builtin_amdgcn_s_barrier();  // ... for every wave; tile kt-1's slot is free
-    asm volatile("" ::: "memory");
-    if (kt + 2 < nkt && !(p.ablate & 1)) stage(kt + 2, (kt + 2) % NS);
-    const char* As = smem + (kt % NS) * STAGE;
-    const char* Bs = As + A_BYTES;
-    if (p.ablate & 2) {
-    } else if (p.cvar == 0) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t c = s * 4 + (lane >> 4);
-        bf16x8 wf[TN], af[4];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-      }
-    } else {
-      // all 16 fragments of the k-tile in flight at once; counted lgkmcnt waits per MFMA group
-      bf16x8 wf[2][TN], af[2][4];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t c = s * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) wf[s][j] = *(const bf16x8*)(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[s][i] = *(const bf16x8*)(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
-      }
-      if (p.cvar == 2) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
-      if (p.cvar == 2) __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  __syncthreads();
-
-  // ---- epilogue through LDS (as tap_gemm_kernel): E[256 pixels][128 channels] ----
-  constexpr int RB = BN * 2, NCH = BN / 8;
-  char* E = smem;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t pl = wm * 64 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const uint32_t cl = wn * 64 + j * 16 + (lane >> 4) * 4;
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-      const uint32_t off = eimg_off8<NCH>(pl, cl);
-      *LDS_PTR(bf16x4, E + off) = o;
-    }
-  }
-  __syncthreads();
-  {
-    constexpr int R = 512 / NCH;
-    const int c = tid % NCH, pr0 = tid / NCH;
-    const bool cok = n0 + c * 8 < p.Co;
-#pragma unroll
-    for (int k = 0; k < BM / R; ++k) {
-      const int pl = pr0 + k * R;
-      const int m = m0 + pl;
-      const bf16x8 v = eimg_chunk<NCH>(E, pl, c);
-      if (m < p.M && cok) {
-        size_t drow;
-        if (p.ds == 1) {
-          drow = (size_t)m * (size_t)p.Co;
-        } else {
-          const uint32_t q = fdiv(m, p.div_wy);
-          const uint32_t x = m - q * p.Wy;
-          const uint32_t n = fdiv(q, p.div_hy);
-          const uint32_t y = q - n * p.Hy;
-          drow = (size_t)((n * p.Hd + y * p.ds + p.oy) * p.Wd + x * p.ds + p.ox) * (size_t)p.Co;
-        }
-        bf16x8 o = v;
-        if (p.addsrc) {
-          const bf16x8 a = *(const bf16x8*)(p.addsrc + drow + n0 + c * 8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(v[e]) + bf2f(a[e]));
-        }
-        *(bf16x8*)(p.dst + drow + n0 + c * 8) = o;
-      }
-    }
-  }
-  if constexpr (EPI == 1) tile_stats<BN, 4>(p, E, m0, n0, tid);
-}
-
-// ---------------------------------------------------------------------------
 // Big-tile tap GEMM: WM x WN waves, each owning 128 pixel rows x 64 output channels (8 x 4
 // accumulator fragments: 12 fragment reads feed 32 MFMAs per 32-deep k-step, against 8 for 16
 // in the 4-wave kernel); workgroup tile BM = 128 WM x BN = 64 WN, e.g. 256 x 256 at 8 waves,
@@ -1354,10 +723,10 @@ tap_gemm8_kernel(const TapGemmParams p) {
 // add source): the accumulators go to a whole-tile LDS image cut into 128 x 128 quadrants, which
 // the 256-thread groups store through tg_image_store (the 4-wave kernel's epilogue).
 // ---------------------------------------------------------------------------
-// CFW = 8: 128 channels per wave (8 x 8 accumulator fragments, 256 registers: AGPRs at one wave
-// per SIMD) -- the 4-wave 256 x 256 tile, 64 MACs per staged byte
+// (CFW: 16-channel accumulator fragments per wave; the 4-wave 256 x 256 tile at CFW = 8 measured
+// slower on every R50 shape, profiles/r4/big4_tile_ab_b1024.txt, and was removed)
 template <int WM, int WN, int NS, int EPI, int CFW = 4>
-__global__ void __launch_bounds__(64 * WM * WN, CFW == 8 ? 1 : 2)
+__global__ void __launch_bounds__(64 * WM * WN, 2)
 tap_gemm_big_kernel(const TapGemmParams p) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BM = 128 * WM, BN = 16 * CFW * WN, BK = 32;
@@ -1462,8 +831,52 @@ tap_gemm_big_kernel(const TapGemmParams p) {
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nkt) stage(i, i);
-  if (p.cvar == 2) {
-    // g_tune[4] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
+  if (WM == 2 && p.cvar == 3 && nkt > 0) {
+    // Ping-pong (g_tune[kTgBigCvar] = 3): the two row halves of the tile are two wave groups
+    // (waves 0-3: pixel rows 0-127, waves 4-7: 128-255), and the waves of a workgroup sit on the
+    // four SIMDs one from each group.  Group 1 runs one segment behind group 0, so in every
+    // interval between two workgroup barriers one wave of each SIMD runs its MFMA segment
+    // (k-tile kt's 32 MFMAs from registers) while its partner runs a load segment (the next
+    // k-tile's 12 fragment reads and its share of a later k-tile's LDS-DMA): the matrix pipe
+    // alternates between the two instead of idling through a common read phase.
+    // Synchronisation, counting workgroup barriers b (group 0 loads k-tile kt in (2kt, 2kt+1),
+    // computes it in (2kt+1, 2kt+2); group 1 one interval later):
+    //   RAW -- every wave retires its own DMA of k-tile kt (counted vmcnt) before barrier 2kt:
+    //   group 0 at the end of its compute segment kt-1, group 1 at the end of its load segment kt-1;
+    //   WAR -- k-tile kt's slot is last read in (2kt+1, 2kt+2) (each reader waits lgkmcnt(0)
+    //   before its next barrier) and is restaged (k-tile kt+NS) in load segments after 2kt+2.
+    // Each group passes the same number of barriers: group 1 one extra at the start, group 0 one
+    // extra at the end.
+    const int grp = wm;
+    auto pp_barrier = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    wait_vmcnt(LPT * min(NS - 2, nkt - 1));  // k-tile 0 (this wave's share)
+    pp_barrier();                            // ... every wave's
+    if (grp == 1) pp_barrier();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int slot = kt % NS;
+      frag_w(slot);
+      frag_a(slot, 0);
+      frag_a(slot, 4);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      mfma_half(0);
+      mfma_half(4);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+      pp_barrier();
+    }
+    if (grp == 0) pp_barrier();
+  } else if (p.cvar == 2) {
+    // g_tune[kTgBigCvar] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
     for (int kt = 0; kt < nkt; ++kt) {
       wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
       ring_barrier();  // ... for every wave; slot kt-1 is free
@@ -1527,264 +940,6 @@ tap_gemm_big_kernel(const TapGemmParams p) {
 #pragma unroll
   for (int k = 0; k < QPG; ++k) {
     const int q = g * QPG + k;
-    tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
-  }
-}
-
-// compile-time interleave for the scheduler: NREAD groups of (one LDS read, then the k-th share of
-// NMFMA MFMAs): the reads go out early, the MFMAs behind them use the OTHER register set -- sched_group_barrier takes constant arguments only, hence the recursion
-template <int NREAD, int NMFMA, int K = 0>
-__device__ __forceinline__ void sched_mfma_reads() {
-  if constexpr (K < NREAD) {
-    constexpr int n = (K + 1) * NMFMA / NREAD - K * NMFMA / NREAD;
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                       // DS read
-    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x008, n, 0);  // MFMA
-    sched_mfma_reads<NREAD, NMFMA, K + 1>();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pipelined 8-wave tap GEMM (FAST shapes: Cs % 64 == 0, one tap per 64-deep k-tile; plain /
-// statistics epilogue, optional eval-BN fold / add source).  Workgroup tile BM = 256 pixel rows
-// x BN = 64 * WN output channels, WM x WN waves, each owning PW = 256 / WM pixels x 64 channels.
-//
-// What the 128-row kernels and tap_gemm_big_kernel leave exposed (profiles/r3 PMC: 11-36 % MFMA
-// busy) is the serial chain per k-step: barrier -> LDS fragment reads -> lgkmcnt(0) -> MFMA burst,
-// with both waves of a SIMD in lockstep (so neither covers the other's read latency), one barrier
-// per 32-deep k-step, and a vmcnt drain whenever the ring is shallow.  Here:
-//   * 64-deep k-tiles (128-byte LDS rows, XOR-swizzled on the source address as everywhere in
-//     this file) in an NS-slot ring: ONE raw s_barrier per 64-deep k-tile;
-//   * the fragments of each k-tile are read in two halves (k 0..31, 32..63) into two register
-//     sets: the reads of one half are issued while the MFMAs of the other run -- the LDS latency
-//     hides behind the matrix pipe instead of stalling it (sched_group_barrier interleave when
-//     SCHED); the next k-tile's first half is read right after the barrier, under the current
-//     k-tile's second-half MFMAs;
-//   * a slot is restaged as soon as every wave has read it (the barrier of the same k-tile), so
-//     NS - 1 k-tiles of LDS-DMA stay in flight across every barrier, retired by a counted vmcnt
-//     (never 0 in the loop);
-//   * M32: v_mfma_f32_32x32x16_bf16 (2 x 2 fragments of 32 x 32 per 64 x 64 wave tile, K = 16 per
-//     instruction) instead of 16x16x32 (4 x 4 fragments): half the MFMA instructions for the same
-//     LDS bytes; which shape holds the higher clock is measured, not assumed (MI355X DVFS).
-// The accumulators leave through the LDS image in 128 x 128 quadrants and the 256-thread store
-// epilogue of the other tap GEMMs (tg_image_store: coalesced 16-byte stores, BN statistics).
-// ---------------------------------------------------------------------------
-template <int WM, int WN, int NS, int EPI, bool M32, bool SCHED>
-__global__ void __launch_bounds__(512, 1)
-tap_gemm_p8_kernel(const TapGemmParams p) {
-  constexpr int NW = WM * WN;
-  static_assert(NW == 8, "8 waves");
-  constexpr int BM = 256, BN = 64 * WN, PW = BM / WM;
-  constexpr int FD = M32 ? 32 : 16;             // fragment edge
-  constexpr int PF = PW / FD, CF = 64 / FD;     // pixel / channel fragments per wave
-  constexpr int KS = M32 ? 2 : 1;               // MFMA k-steps per 32-deep half k-tile
-  constexpr int AI = BM * 8 / 512, BI = BN * 8 / 512, LPT = AI + BI;  // LDS-DMA per thread per k-tile
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int QN = BN / 128;                  // 128-channel quadrants across the tile
-  static_assert(BN % 128 == 0 && NS >= 2, "tile geometry");
-  using accT = typename std::conditional<M32, f32x16, f32x4>::type;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const uint32_t tn = bid % ntn, tm = bid / ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // per-slot source pointers + tap-validity masks (tap_gemm_kernel's FAST path)
-  const bf16* fa_ptr[AI];
-  uint32_t fa_vm[AI];
-  const bf16* fb_ptr[BI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int r = (wave * AI + i) * 8 + (lane >> 3);
-    const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
-    const uint32_t q = fdiv(mm, p.div_wy);
-    const uint32_t x = mm - q * p.Wy;
-    const uint32_t n = fdiv(q, p.div_hy);
-    const uint32_t y = q - n * p.Hy;
-    const int ys = y * p.ss, xs = x * p.ss;
-    fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane & 7) ^ swz_chunk<64>(r)) * 8;
-    uint32_t vm = 0;
-    for (int t = 0; t < p.ntaps; ++t) {
-      const int tv = p.tap[t];
-      const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
-      vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
-    }
-    fa_vm[i] = vm;
-  }
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int r = (wave * BI + i) * 8 + (lane >> 3);
-    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane & 7) ^ swz_chunk<64>(r)) * 8;
-  }
-  // the tap table lives in one VGPR (lane t holds tap t; <= 64 taps), read with v_readlane: no
-  // scalar-memory load inside the k-loop (an SMEM result forces lgkmcnt(0), which would drain
-  // the in-flight LDS fragment reads); the (tap, channel chunk) of the next k-tile to stage is
-  // advanced with scalar selects instead of a division
-  const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
-  int st_t = 0, st_c = 0;  // tap / channel base of the next k-tile to stage
-  auto stage = [&](int slot) {
-    char* As = smem + slot * STAGE;
-    char* Bs = As + A_BYTES;
-    const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
-    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
-    const long boff = (long)tap_w(tv) * p.Cs + st_c;
-    const uint32_t tbit = 1u << st_t;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      dma16_tracked(g, As + (wave * AI + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i)
-      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
-    st_c += 64;
-    const bool wrap = st_c >= p.Cs;
-    st_t += wrap ? 1 : 0;
-    st_c = wrap ? 0 : st_c;
-  };
-
-  accT acc[CF][PF];
-#pragma unroll
-  for (int j = 0; j < CF; ++j)
-#pragma unroll
-    for (int i = 0; i < PF; ++i) acc[j][i] = accT{};
-
-  // fragment reads of half h (k 32h .. 32h + 31) of the k-tile in `slot`: the 16x16x32 operand is
-  // 16 rows x one 16-byte chunk per lane (chunk 4h + lane / 16), the 32x32x16 operand 32 rows x
-  // one chunk per lane (chunk 4h + 2s + lane / 32) per k-step s
-  const int fr = M32 ? (lane & 31) : (lane & 15);
-  const int fc = M32 ? (lane >> 5) : (lane >> 4);
-  auto read_half = [&](int slot, int h, bf16x8 (&wf)[KS][CF], bf16x8 (&af)[KS][PF]) {
-    const char* As = smem + slot * STAGE;
-    const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const uint32_t c = h * 4 + s * 2 * (M32 ? 1 : 0) + fc;
-#pragma unroll
-      for (int j = 0; j < CF; ++j) wf[s][j] = *(const bf16x8*)(Bs + swzk<64>(wn * 64 + j * FD + fr, c));
-#pragma unroll
-      for (int i = 0; i < PF; ++i) af[s][i] = *(const bf16x8*)(As + swzk<64>(wm * PW + i * FD + fr, c));
-    }
-  };
-  auto mfma_half = [&](const bf16x8 (&wf)[KS][CF], const bf16x8 (&af)[KS][PF]) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int j = 0; j < CF; ++j)
-#pragma unroll
-        for (int i = 0; i < PF; ++i) {
-          if constexpr (M32)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
-          else
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s][j], af[s][i], acc[j][i], 0, 0, 0);
-        }
-  };
-  // read / MFMA interleave for the scheduler (the MFMAs' operands were read one half k-tile earlier)
-  constexpr int NREAD = KS * (CF + PF), NMFMA = KS * CF * PF;
-  auto interleave = [&]() {
-    if constexpr (SCHED) sched_mfma_reads<NREAD, NMFMA>();
-  };
-  auto ring_barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's fragment reads retired
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-  };
-
-  // g_tune[4] (p.cvar) experiments: bit 0 = static priority 1 for waves 4..7 (the partner half
-  // of every SIMD, the arbitration loser at each barrier release; MI355X_MICROARCH "two waves per
-  // SIMD" item 4), bit 1 = s_setprio 1 around every MFMA region
-  const bool prio_region = (p.cvar & 2) != 0;
-  if ((p.cvar & 1) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  auto prio_on = [&]() { if (prio_region) __builtin_amdgcn_s_setprio(1); };
-  auto prio_off = [&]() { if (prio_region) __builtin_amdgcn_s_setprio(0); };
-
-  const int nkt = p.nkt;  // 64-deep k-tiles
-  bf16x8 w0[KS][CF], a0[KS][PF], w1[KS][CF], a1[KS][PF];
-#pragma unroll
-  for (int i = 0; i < NS; ++i)
-    if (i < nkt) stage(i);
-  if (nkt > 0) {
-    wait_vmcnt(LPT * (min(NS, nkt) - 1));  // k-tile 0 landed (this wave's share)
-    ring_barrier();                        // ... for every wave
-    read_half(0, 0, w0, a0);
-  }
-  // tiles issued so far at iteration kt: 0 .. min(kt + NS - 1, nkt - 1); before reading k-tile
-  // kt + 1 it must have landed: NS - 2 younger k-tiles may stay in flight in the steady state
-  int kt = 0;
-  for (; kt + NS < nkt; ++kt) {  // steady state: one k-tile staged per iteration
-    const int slot = kt % NS;
-    prio_on();
-    mfma_half(w0, a0);
-    read_half(slot, 1, w1, a1);  // second half of this k-tile, under the first half's MFMAs
-    interleave();
-    prio_off();
-    wait_vmcnt(LPT * (NS - 2));
-    ring_barrier();              // every wave: k-tile kt + 1 landed, slot kt fully read
-    prio_on();
-    mfma_half(w1, a1);
-    read_half((kt + 1) % NS, 0, w0, a0);  // next k-tile's first half, under this one's second
-    interleave();
-    prio_off();
-    // k-tile kt + NS into the slot just freed, issued behind the fragment reads: an LDS-DMA issued
-    // between an LDS read and its first use makes the compiler's wait for that read lgkmcnt(0)
-    __builtin_amdgcn_sched_barrier(0);
-    stage(slot);
-  }
-  for (; kt < nkt; ++kt) {  // the last NS k-tiles: nothing left to stage
-    const int slot = kt % NS;
-    mfma_half(w0, a0);
-    read_half(slot, 1, w1, a1);
-    interleave();
-    if (kt + 1 < nkt) {
-      wait_vmcnt(LPT * (nkt - 2 - kt));
-      ring_barrier();
-      mfma_half(w1, a1);
-      read_half((kt + 1) % NS, 0, w0, a0);
-      interleave();
-    } else {
-      mfma_half(w1, a1);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
-#pragma unroll
-  for (int i = 0; i < PF; ++i) {
-#pragma unroll
-    for (int j = 0; j < CF; ++j) {
-      const int px = wm * PW + i * FD + fr;  // tile pixel of this lane's column
-      char* Q = smem + ((px >> 7) * QN + ((wn * 64) >> 7)) * 32768;
-      const uint32_t pl = px & 127;
-      if constexpr (M32) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t cl = ((wn * 64) & 127) + j * 32 + q * 8 + fc * 4;
-          bf16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][q * 4 + r]);
-          *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
-        }
-      } else {
-        const uint32_t cl = ((wn * 64) & 127) + j * 16 + fc * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
-      }
-    }
-  }
-  __syncthreads();
-  // group g (threads 256g ..) stores quadrants g*QN ..; both groups pass the same barriers
-  const int g = tid >> 8, gtid = tid & 255;
-#pragma unroll
-  for (int k = 0; k < QN; ++k) {
-    const int q = g * QN + k;
     tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
   }
 }
@@ -2346,39 +1501,7 @@ static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
     hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0, CFW>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
 }
 
-// pipelined 8-wave kernel (tap_gemm_p8_kernel); variant v: 1 = 256 x 128 16x16x32, 2 = 256 x 128
-// 32x32x16, 3 / 4 = the same with the sched_group_barrier read/MFMA interleave (a 256 x 256 tile at
-// 8 waves -- 128 x 64 per wave -- spills with two fragment register sets)
-template <int WM, int WN, int NS, bool M32, bool SCHED>
-static void launch_p8_cfg(const TapGemmParams& p, int epi, hipStream_t stream) {
-  constexpr int BM = 256, BN = 64 * WN;
-  constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 128, (size_t)2 * (BN / 128) * 32768);
-  const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)tap_gemm_p8_kernel<WM, WN, NS, 0, M32, SCHED>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)tap_gemm_p8_kernel<WM, WN, NS, 1, M32, SCHED>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  if (epi == 1)
-    hipLaunchKernelGGL((tap_gemm_p8_kernel<WM, WN, NS, 1, M32, SCHED>), dim3(grid), dim3(512), lds, stream, p);
-  else
-    hipLaunchKernelGGL((tap_gemm_p8_kernel<WM, WN, NS, 0, M32, SCHED>), dim3(grid), dim3(512), lds, stream, p);
-}
-
-static void launch_p8(TapGemmParams p, int variant, int epi, hipStream_t stream) {
-  p.nkt = p.ntaps * p.cpt / 8;  // 64-deep k-tiles (cpt % 8 == 0 on FAST shapes)
-  switch (variant) {
-    case 2: launch_p8_cfg<4, 2, 3, true, false>(p, epi, stream); break;
-    case 3: launch_p8_cfg<4, 2, 3, false, true>(p, epi, stream); break;
-    case 4: launch_p8_cfg<4, 2, 3, true, true>(p, epi, stream); break;
-    default: launch_p8_cfg<4, 2, 3, false, false>(p, epi, stream); break;
-  }
-}
-
-// 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[24]
+// 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[kTgBig]
 // (0 = this heuristic).  Per-shape A/B at b1024 (profiles/r3/big_tile_ab_b1024_pipelined.txt): the
 // big tiles win where the 128-row kernels' grid is short or their k-loop is exposed, and lose on
 // the 1x1 stride-1 shapes and the 256-channel 3x3s (784 256 x 256 tiles = 3.06 rounds of 256 CUs):
@@ -2391,7 +1514,6 @@ static void launch_p8(TapGemmParams p, int variant, int epi, hipStream_t stream)
 // convs are 14 256 x 256 tiles (122 us against the 128-row kernel's 52-workgroup grid).
 static int big_tile_pick(int mode, int M, int Co, int ntaps, int ds) {
   if (mode == 2) return 0;
-  if (mode == 4) return Co >= 256 ? 4 : 0;  // 4-wave 256 x 256 (128 x 128 per wave): A/B and autotuner
   if (mode == 1) return Co >= 256 ? 1 : 2;
   if (mode == 3) return 2;
   int pick = 0;
@@ -2444,9 +1566,9 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   const bool fast = (p.cpt & 7) == 0 && taps.n <= 32;  // FAST: 32-bit tap-validity masks
   // config: BN (64/128 output channels per tile) and NS (LDS stages); g_tune overrides the
   // heuristic (tuning experiments only)
-  const int env_bn = g_tune[0], env_ns = g_tune[1];
-  p.ablate = g_tune[2];
-  p.cvar = g_tune[4];
+  const int env_bn = g_tune[kTgTileN], env_ns = g_tune[kTgStages];
+  p.ablate = g_tune[kAblate];
+  p.cvar = g_tune[kTgBigCvar];
   int bn = Co <= 64 ? 64 : 128, ns = 2;
   // a short grid (< 1.5 rounds of 256 CUs at 128-channel tiles: batch 32-128 from stage 2 on, the
   // stride-2 parity classes, the linear heads) takes 64-channel tiles, twice the workgroups: the
@@ -2459,108 +1581,27 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // 1x1 shapes with K <= 1024 and 128-channel tiles: 32-deep k-tiles, double-buffered (32 KB of
   // LDS: four workgroups per CU) beat the 64-deep double buffer (two per CU) by 5-25 % and the
   // 32-deep 3-stage ring by 2-12 %; 3x3 and deep-K shapes keep 64-deep tiles (tools/conv_bench.py
-  // --cfgs "1=2;8=32,1=3;8=32" per-shape A/B).  g_tune[8] = 32 forces 32-deep tiles (with [1]),
+  // --cfgs "1=2;8=32,1=3;8=32" per-shape A/B).  g_tune[kTgKDepth] = 32 forces 32-deep tiles (with [1]),
   // 64 disables the heuristic.
   // narrow-channel (non-FAST) shapes -- the space-to-depth stem -- take 32-deep tiles double-
-  // buffered only (their taps are looked up per lane; g_tune[13] = 32 / 64 selects, A/B)
-  bool bk32 = (fast && g_tune[8] == 32 && ns >= 2 && ns <= 4) || (!fast && g_tune[13] == 32);
+  // buffered only (their taps are looked up per lane; g_tune[kNarrowKDepth] = 32 / 64 selects, A/B)
+  bool bk32 = (fast && g_tune[kTgKDepth] == 32 && ns >= 2 && ns <= 4) || (!fast && g_tune[kNarrowKDepth] == 32);
   // (K = 64, one 64-deep k-tile, measured faster with the 64-deep tile: 487 vs 511 us on the R50
   // stage-1 expansion at b1024, tools/fwd_epi_bench.py)
-  if (fast && env_ns == 0 && g_tune[8] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
-  const bool use8 = g_tune[3] == 1 && aff == nullptr;  // measured slower than the 4-wave kernel (conv_bench --cfgs)
-  // window kernel (tap_win_kernel): 3x3-neighbourhood taps on a same-size stride-1 grid, C % 64 == 0,
-  // plain / statistics epilogue; g_tune[22] = 1 turns it on (measured no faster, A/B only)
-  bool win_ok = fast && (Cs % 64) == 0 && ss == 1 && ds == 1 && Hy == Hs && Wy == Ws && Hd == Hy && Wd == Wy &&
-                Ws <= kWinMaxW && taps.n > 1 && (epi == 0 || epi == 1) && addsrc == nullptr && aff == nullptr &&
-                bnb == nullptr && pscale == nullptr && g_tune[22] != 2;
-  for (int i = 0; i < taps.n && win_ok; ++i)
-    win_ok = taps.dy[i] >= -1 && taps.dy[i] <= 1 && taps.dx[i] >= -1 && taps.dx[i] <= 1;
-  if (win_ok && g_tune[22] == 1) {
-    const int grid = ntm * ((Co + 127) / 128);
-    const size_t lds = 2 * (size_t)win_instrs(Ws) * 4096 + 2 * 128 * 64 * 2;
-    static bool attr = false;
-    if (!attr) {
-      const int mx = 2 * win_instrs(kWinMaxW) * 4096 + 2 * 128 * 64 * 2;
-      hipFuncSetAttribute((const void*)tap_win_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      hipFuncSetAttribute((const void*)tap_win_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      attr = true;
-    }
-    if (epi == 1) hipLaunchKernelGGL(tap_win_kernel<1>, dim3(grid), dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL(tap_win_kernel<0>, dim3(grid), dim3(256), lds, stream, p);
-    return;
-  }
-  // persistent cross-tile-prefetch kernel (tap_gemm_ps_kernel): FAST shapes, plain / statistics
-  // epilogue, no residual add / fold; g_tune[20] = 1 on, 2 off (A/B), 0 = heuristic
-  const int ps_mode = g_tune[20];
-  // (a parity class with no taps -- stride-2 1x1 dgrad -- only writes zeros: the plain kernel)
-  const bool ps_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && addsrc == nullptr && aff == nullptr &&
-                     bnb == nullptr && pscale == nullptr;
-  if (ps_ok && ps_mode == 1) {
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      if (ncu <= 0) ncu = 256;
-    }
-    const int ps_bk = g_tune[21] == 64 ? 64 : 32;
-    const int tiles = ntm * ((Co + bn - 1) / bn);
-    const int grid = std::min(tiles, 2 * ncu);
-#define DCP_PS(BN_, EPI_, BK_)                                                                          \
-  {                                                                                                     \
-    p.nkt = (p.ntaps * p.cpt + BK_ / 8 - 1) / (BK_ / 8);                                                \
-    constexpr size_t lds = 3 * (size_t)(128 + BN_) * BK_ * 2 + (size_t)128 * 2 * BN_;                   \
-    static bool attr = false;                                                                           \
-    if (!attr) {                                                                                        \
-      hipFuncSetAttribute((const void*)tap_gemm_ps_kernel<BN_, EPI_, 3, BK_>,                            \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                        \
-      attr = true;                                                                                      \
-    }                                                                                                   \
-    hipLaunchKernelGGL((tap_gemm_ps_kernel<BN_, EPI_, 3, BK_>), dim3(grid), dim3(256), lds, stream, p); \
-  }
-    if (bn == 64) {
-      if (epi == 1) { if (ps_bk == 64) DCP_PS(64, 1, 64) else DCP_PS(64, 1, 32) }
-      else { if (ps_bk == 64) DCP_PS(64, 0, 64) else DCP_PS(64, 0, 32) }
-    } else {
-      if (epi == 1) { if (ps_bk == 64) DCP_PS(128, 1, 64) else DCP_PS(128, 1, 32) }
-      else { if (ps_bk == 64) DCP_PS(128, 0, 64) else DCP_PS(128, 0, 32) }
-    }
-#undef DCP_PS
-    return;
-  }
+  if (fast && env_ns == 0 && g_tune[kTgKDepth] != 64 && taps.n == 1 && Cs > 64 && Cs <= 1024 && bn == 128) bk32 = true;
   // big-tile kernel (tap_gemm_big_kernel): FAST, plain / statistics epilogue, >= 128 output
-  // channels.  g_tune[24]: 1 = on wherever it applies (256 x 256 for Co >= 256, else 256 x 128),
+  // channels.  g_tune[kTgBig]: 1 = on wherever it applies (256 x 256 for Co >= 256, else 256 x 128),
   // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
-  // pipelined 8-wave kernel: g_tune[26] = variant (A/B; 0 = off)
-  const int p8 = g_tune[26];
-  if (big_ok && p8 > 0 && p8 <= 4) {
-    launch_p8(p, p8, epi, stream);
-    return;
-  }
-  const int big = big_ok ? big_tile_pick(g_tune[24], p.M, Co, taps.n, ds) : 0;
+  const int big = big_ok ? big_tile_pick(g_tune[kTgBig], p.M, Co, taps.n, ds) : 0;
   if (big != 0) {
     p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)
     if (big == 1) launch_big<2, 4, 4>(p, epi, stream);
-    else if (big == 4) launch_big<2, 2, 4, 8>(p, epi, stream);
     else launch_big<2, 2, 3>(p, epi, stream);
     return;
   }
-  if (fast && Co >= 128 && epi < 2 && use8 && pscale == nullptr) {
-    const int grid8 = ((p.M + 255) / 256) * ((Co + 127) / 128);
-    constexpr size_t lds8 = 3 * (256 + 128) * 128;
-    static bool attr8 = false;
-    if (!attr8) {
-      hipFuncSetAttribute((const void*)tap_gemm8_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
-      hipFuncSetAttribute((const void*)tap_gemm8_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8);
-      attr8 = true;
-    }
-    if (epi == 1) hipLaunchKernelGGL(tap_gemm8_kernel<1>, dim3(grid8), dim3(512), lds8, stream, p);
-    else hipLaunchKernelGGL(tap_gemm8_kernel<0>, dim3(grid8), dim3(512), lds8, stream, p);
-    return;
-  }
-  // 256-channel tiles (g_tune[0] = 256, A/B and autotuner): each wave 64 rows x 128 channels, the
+  // 256-channel tiles (g_tune[kTgTileN] = 256, A/B and autotuner): each wave 64 rows x 128 channels, the
   // A tile read once per 256 output channels -- for the short-K expansion 1x1 convs, whose A reads
   // are half of their bytes at 128-channel tiles.  Plain / statistics epilogue only.
   if (bn == 256 && !(fast && (epi == 0 || epi == 1) && pscale == nullptr && Co > 128)) bn = 128;
@@ -2615,7 +1656,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 }
 
 // ---------------------------------------------------------------------------
-// Per-shape autotuning of the forward / data-gradient GEMM configuration (g_tune[25] = 1, set
+// Per-shape autotuning of the forward / data-gradient GEMM configuration (g_tune[kAutotune] = 1, set
 // from DCP_AUTOTUNE=1 by the Python layer; the cudnn.benchmark of this library).  The first call
 // of every distinct problem (geometry, channels, taps, epilogue) outside a stream capture times
 // the candidate configurations -- the heuristic's choice, 64- vs 32-deep k-tiles, a 3-stage
@@ -2627,7 +1668,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 // order (fp32 rounding).  Off by default (the default path is bit-reproducible run to run).
 // ---------------------------------------------------------------------------
 struct TgCfg {
-  int bn, ns, bk, big;  // g_tune[0], [1], [8], [24] overrides (0 = the heuristic's)
+  int bn, ns, bk, big;  // g_tune[kTgTileN], [1], [8], [24] overrides (0 = the heuristic's)
 };
 static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 0},   // heuristic
@@ -2641,7 +1682,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
     {256, 2, 32, 2},  // 256-channel tiles, 32-deep k-tiles (2-3 % on two R50 shapes: profiles/r4/bn256_tile_ab_b1024.txt)
-    // (the 4-wave 256 x 256 tile, g_tune[24] = 4, is not a candidate: slower on every R50 shape,
+    // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };
 static std::mutex g_tg_mu;
@@ -2650,10 +1691,10 @@ static std::unordered_map<std::string, int> g_tg_choice;
 struct TuneOverride {
   int saved[4];
   explicit TuneOverride(const TgCfg& c) {
-    saved[0] = g_tune[0]; saved[1] = g_tune[1]; saved[2] = g_tune[8]; saved[3] = g_tune[24];
-    g_tune[0] = c.bn; g_tune[1] = c.ns; g_tune[8] = c.bk; g_tune[24] = c.big;
+    saved[0] = g_tune[kTgTileN]; saved[1] = g_tune[kTgStages]; saved[2] = g_tune[kTgKDepth]; saved[3] = g_tune[kTgBig];
+    g_tune[kTgTileN] = c.bn; g_tune[kTgStages] = c.ns; g_tune[kTgKDepth] = c.bk; g_tune[kTgBig] = c.big;
   }
-  ~TuneOverride() { g_tune[0] = saved[0]; g_tune[1] = saved[1]; g_tune[8] = saved[2]; g_tune[24] = saved[3]; }
+  ~TuneOverride() { g_tune[kTgTileN] = saved[0]; g_tune[kTgStages] = saved[1]; g_tune[kTgKDepth] = saved[2]; g_tune[kTgBig] = saved[3]; }
 };
 
 int tap_gemm_tuned_count() {
@@ -2674,7 +1715,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
   // (an add source aliasing the output would accumulate over the timing runs: never tuned)
-  if (g_tune[25] != 1 || !fast || pscale != nullptr || g_tune[0] || g_tune[1] || g_tune[8] || g_tune[24] ||
+  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] ||
       (long)N * Hy * Wy == 0 || (addsrc != nullptr && addsrc == dst)) {
     run();
     return;
@@ -2707,7 +1748,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     for (int c = 0; c < (int)(sizeof(kTgCfgs) / sizeof(kTgCfgs[0])); ++c) {
       const TgCfg& cfg = kTgCfgs[c];
       if (cfg.big == 3 && !big_ok) continue;
-      if ((cfg.big == 1 || cfg.big == 4) && !(big_ok && Co >= 256)) continue;
+      if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;
       if (cfg.bn == 256 && !(Co > 128 && bnb == nullptr && bias == nullptr && relu == 0)) continue;
       if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
       TuneOverride ov(cfg);
@@ -2771,58 +1812,6 @@ __global__ void __launch_bounds__(256) split_reduce1_kernel(const float4* __rest
   }
 }
 
-// split_reduce1 whose second level runs in the last-arriving workgroup of each 64-column group:
-// chunk sums -> tmp[chunk], then that workgroup adds the column group's chunk rows in chunk
-// order (4 waves over the rows, fixed LDS combine: deterministic whichever workgroup is last)
-__global__ void __launch_bounds__(256) split_reduce2_kernel(const float4* __restrict__ part, int splits, int n4,
-                                                            float4* __restrict__ tmp, float4* __restrict__ out,
-                                                            unsigned* __restrict__ ctr) {
-  __shared__ float4 red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
-  const int k0 = blockIdx.y * 64;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col < n4) {
-#pragma unroll 4
-    for (int k = k0 + sub; k < min(splits, k0 + 64); k += 4) {
-      const float4 v = part[(size_t)k * n4 + col];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-  }
-  red[sub][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (sub == 0 && col < n4) {
-    float4 t = red[0][threadIdx.x];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) {
-      const float4 v = red[q][threadIdx.x];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-    tmp[(size_t)blockIdx.y * n4 + col] = t;
-  }
-  if (!last_arrival(ctr + blockIdx.x, gridDim.y)) return;
-  const int chunks = gridDim.y;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (col < n4) {
-#pragma unroll 4
-    for (int k = sub; k < chunks; k += 4) {
-      const float4 v = tmp[(size_t)k * n4 + col];
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-  }
-  __syncthreads();  // red reused
-  red[sub][threadIdx.x & 63] = a;
-  __syncthreads();
-  if (sub == 0 && col < n4) {
-    float4 t = red[0][threadIdx.x];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) {
-      const float4 v = red[q][threadIdx.x];
-      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-    }
-    out[col] = t;
-  }
-}
-
 // One launch for a narrow reduction (few columns, up to a few thousand splits: the BN-backward sums
 // of a small batch's dgrad epilogue, 2C columns over one partial row per 128-pixel tile): a
 // 1024-thread workgroup per 64 float4 columns, its 16 waves striding over the split rows with 8
@@ -2862,23 +1851,6 @@ __global__ void __launch_bounds__(1024) split_reduce_rows_kernel(const float4* _
   }
 }
 
-unsigned* ticket_counters(int n) {
-  static std::mutex mu;
-  static unsigned* pool[64] = {nullptr};
-  if (n > kTicketCounters) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  if (!pool[dev]) {
-    void* p = nullptr;
-    if (hipMalloc(&p, sizeof(unsigned) * kTicketCounters) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(unsigned) * kTicketCounters) != hipSuccess) return nullptr;
-    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-    pool[dev] = (unsigned*)p;
-  }
-  return pool[dev];
-}
-
 // out[i] = sum_k part[k][i]; n % 4 == 0.  part must hold splits*n + ceil(splits/64)*n floats
 // when splits > 64 (the chunk sums are written behind the partials).
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream) {
@@ -2890,25 +1862,15 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
     return;
   }
   // narrow and not too deep (a small batch's BN-backward sums: 2C <= 4096 columns, <= 2048 tiles):
-  // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[29] = 2 off,
+  // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[kRowReduce] = 2 off,
   // > 2: the depth limit (A/B)
-  const int row_max = g_tune[29] > 2 ? g_tune[29] : 2048;
-  if (n4 <= 1024 && splits <= row_max && g_tune[29] != 2) {
+  const int row_max = g_tune[kRowReduce] > 2 ? g_tune[kRowReduce] : 2048;
+  if (n4 <= 1024 && splits <= row_max && g_tune[kRowReduce] != 2) {
     hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 63) / 64), dim3(1024), 0, stream, (const float4*)part,
                        splits, n4, (float4*)out);
     return;
   }
   float* tmp = const_cast<float*>(part) + (size_t)splits * n;
-  // one launch with the second level in each column group's last workgroup: g_tune[23] = 1 only.
-  // Measured much slower (R50 b1024 14,181 -> 13,538, b32 graph 4,618 -> 3,693 img/s,
-  // profiles/r3/ticket_reduce_ab.txt): the device-scope release fence every workgroup needs before
-  // its ticket writes back its XCD's whole L2, which costs far more than the launch it saves.
-  unsigned* ctr = g_tune[23] == 1 ? ticket_counters((n4 + 63) / 64) : nullptr;
-  if (ctr) {
-    hipLaunchKernelGGL(split_reduce2_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
-                       splits, n4, (float4*)tmp, (float4*)out, ctr);
-    return;
-  }
   hipLaunchKernelGGL(split_reduce1_kernel, dim3((n4 + 63) / 64, chunks), dim3(256), 0, stream, (const float4*)part,
                      splits, n4, (float4*)tmp);
   // second level: 4 waves per 64 columns split the chunk rows (a thread-per-column loop over
@@ -2919,13 +1881,13 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
 // split-K plan of the weight-gradient GEMM, >= 256 rows per split: ~2 blocks per CU for
 // 1x1 convs / linears (fewer, longer splits: less partial-slab traffic), ~4 for k x k
 // (measured per shape with tools/conv_bench.py --cfgs "5=2,5=4")
-static bool wgrad_big(int Co, int ldw) { return g_tune[7] != 2 && Co >= 256 && ldw >= 256; }
+static bool wgrad_big(int Co, int ldw) { return g_tune[kWgTileMode] != 2 && Co >= 256 && ldw >= 256; }
 // 64-row tiles: Co <= 64 with enough columns to fill 256-wide tiles at least half
-static bool wgrad_narrow(int Co, int ldw) { return g_tune[7] != 3 && Co <= 64 && ldw >= 128; }
+static bool wgrad_narrow(int Co, int ldw) { return g_tune[kWgTileMode] != 3 && Co <= 64 && ldw >= 128; }
 
 // 16-column subtiles per wave of the narrow kernel: 192-column tiles where they pad less
 static int wgrad_nj(int ldw) {
-  if (g_tune[14] == 4 || g_tune[14] == 3) return g_tune[14];
+  if (g_tune[kWgCols] == 4 || g_tune[kWgCols] == 3) return g_tune[kWgCols];
   return ((ldw + 191) / 192) * 3 < ((ldw + 255) / 256) * 4 ? 3 : 4;
 }
 
@@ -2939,14 +1901,14 @@ int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_spl
   const bool big = wgrad_big(Co, ldw);
   const int tiles = wgrad_tiles(Co, ldw);
   const int per_cu = (big || wgrad_narrow(Co, ldw)) ? (big ? 1 : 2) : (taps == 1 ? 2 : 4);
-  const int target = (g_tune[5] > 0 ? g_tune[5] : per_cu) * num_cu;
+  const int target = (g_tune[kWgSplitsPerCu] > 0 ? g_tune[kWgSplitsPerCu] : per_cu) * num_cu;
   // floor: a grid just past a whole number of resident rounds leaves a tail round of one block
   int splits = target / tiles;
   int max_splits = (M + 255) / 256;
   if (splits > max_splits) splits = max_splits;
-  // g_tune[27] > 0: at most that many splits (64: the one-level reduction, no second launch --
+  // g_tune[kWgSplitCap] > 0: at most that many splits (64: the one-level reduction, no second launch --
   // small batches, where every launch counts; an autotuner candidate)
-  if (g_tune[27] > 0 && splits > g_tune[27]) splits = g_tune[27];
+  if (g_tune[kWgSplitCap] > 0 && splits > g_tune[kWgSplitCap]) splits = g_tune[kWgSplitCap];
   if (splits < 1) splits = 1;
   int rps = (M + splits - 1) / splits;
   rps = (rps + 63) / 64 * 64;
@@ -3005,8 +1967,8 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     abort();
   }
   const int tiles = wgrad_tiles(Co, p.ldw);
-  p.ablate = g_tune[2];
-  if (g_tune[6] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
+  p.ablate = g_tune[kAblate];
+  if (g_tune[kWgFlushAblate] == 1) part = nullptr;  // A/B timing of the atomic flush only (dw not zeroed)
   int rps = 0;
   const int splits = wgrad_splits(p.M, Co, p.ldw, taps.n, num_cu, &rps);
   p.rows_per_split = rps;
@@ -3016,8 +1978,8 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
   if (splits == 1) {
     p.part = dw;  // split 0 stores straight into dw
   }
-  // 32 pixel rows per k-tile (g_tune[12] = 32): half the LDS of the 64-row tiles
-  const bool wbk32 = g_tune[12] == 32;
+  // 32 pixel rows per k-tile (g_tune[kWgRows] = 32): half the LDS of the 64-row tiles
+  const bool wbk32 = g_tune[kWgRows] == 32;
   if (narrow) {
     const int nj = wgrad_nj(p.ldw);
     if (wbk32 && nj == 4)

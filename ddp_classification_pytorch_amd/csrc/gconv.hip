@@ -551,11 +551,11 @@ int pick_sg(int C, int CG) {
   return 0;
 }
 
-// weight-gradient super-group: pick_sg's, or 32 channels with g_tune[16] = 32 (A/B only: the
+// weight-gradient super-group: pick_sg's, or 32 channels with g_tune[kGconvSG] = 32 (A/B only: the
 // 32-channel block-diagonal tiles measured 8% slower on ResNeXt-50, 8.6k vs 9.4k img/s at b512)
 int wgrad_sg(int C, int CG) {
   const int base = pick_sg(C, CG);
-  if (base != 0 && g_tune[16] == 32 && CG <= 32 && 32 % CG == 0 && C % 32 == 0) return 32;
+  if (base != 0 && g_tune[kGconvSG] == 32 && CG <= 32 && 32 % CG == 0 && C % 32 == 0) return 32;
   return base;
 }
 

@@ -8,15 +8,10 @@ typedef __bf16 bf16;
 
 namespace dcp {
 
-// tuning switches for in-process A/B experiments (tools/conv_bench.py --cfgs); all 0 = defaults
-// [0] BN override, [1] LDS stages, [2] ablation, [3] 8-wave kernel (0 auto, 1 on, 2 off), [4] compute variant,
-// [5] wgrad blocks per CU, [6] wgrad atomics, [7] wgrad tile (0 auto, 2 no 256-tile, 3 no 64-row tile),
-// [8] conv k-tile depth (32 with [1] = 3 or 4), [9]-[11] elementwise grids (bn.hip),
-// [12] wgrad 32-row k-tiles, [13] narrow-channel conv k-tile depth, [14] narrow wgrad
-// subtiles per wave (3 or 4; 0 auto), [15] = 1: no direct 3x3 weight gradient,
-// [16] = 32: grouped-conv weight gradient on 32-channel super-groups, [17] fused stem backward
-// ablation (timing only: 1 no MFMA phase, 2 no gather phase)
-extern int g_tune[32];
+// tuning switches (in-process A/B experiments, the autotuner's overrides): named slots, tune.h
+}  // namespace dcp
+#include "tune.h"
+namespace dcp {
 
 constexpr int kMaxTaps = 64;
 
@@ -53,7 +48,7 @@ struct AffineEpi {
   float slope;
 };
 
-// number of problems the tap-GEMM autotuner (g_tune[25] = 1) has measured in this process
+// number of problems the tap-GEMM autotuner (g_tune[kAutotune] = 1) has measured in this process
 int tap_gemm_tuned_count();
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,

@@ -297,7 +297,7 @@ struct StemBwdParams {
   const float* mean;
   float* part;         // [blocks][kSbPart]
   int N, H, Ho, Wo, act, rpb;  // rpb: output rows per workgroup
-  int ablate;                  // A/B timing only (g_tune[17]): 1 no MFMA phase, 2 no gather phase
+  int ablate;                  // A/B timing only (g_tune[kStemAblate]): 1 no MFMA phase, 2 no gather phase
 };
 
 __device__ __forceinline__ uint32_t sb_aoff(uint32_t r, uint32_t col) {
@@ -628,7 +628,7 @@ void launch_stem_bwd(const bf16* z, const bf16* x16, const bf16* dy, const uint8
                      hipStream_t s) {
   StemBwdParams p{z, x16, dy, idx, scale, shift, mean, part, N, H, H / 2, W / 2, act, 0};
   p.rpb = (N * H + nblocks - 1) / nblocks;
-  p.ablate = g_tune[17];
+  p.ablate = g_tune[kStemAblate];
   constexpr int lds = 65536 + 9 * kSbSlot + 768;
   switch (W) {
 #define DCP_STEMB(W_)                                                                                  \

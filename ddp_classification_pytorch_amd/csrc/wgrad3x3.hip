@@ -41,7 +41,7 @@ struct W3Params {
   int buf;           // bytes per strip buffer (window + output-gradient pixels)
   int nib;           // 64-channel input blocks
   int Wq;            // window row pitch in pixels: W + 2 rounded up to even (the swizzle's parity)
-  int ablate;        // tuning experiments only (g_tune[2]): 1 = no strip prefetch, 2 = no MFMA loop
+  int ablate;        // tuning experiments only (g_tune[kAblate]): 1 = no strip prefetch, 2 = no MFMA loop
   FastDiv div_wq, div_w, div_spi;
 };
 
@@ -186,14 +186,14 @@ static int w3_rows(int H, int W) {
 // blocks, at most 2 x 2 of them (wider layers keep the 256-tile implicit GEMM, which measured
 // faster there)
 int wgrad3x3_splits(int N, int H, int W, int C, int Co, int num_cu) {
-  if (g_tune[15] == 1 || C % 64 != 0 || Co % 64 != 0 || H < 1 || W < 1) return 0;
+  if (g_tune[kWg3x3] == 1 || C % 64 != 0 || Co % 64 != 0 || H < 1 || W < 1) return 0;
   const int pairs = (Co / 64) * (C / 64);
-  if (pairs > 4 && g_tune[15] != 2) return 0;
+  if (pairs > 4 && g_tune[kWg3x3] != 2) return 0;
   const int R = w3_rows(H, W);
   if (R == 0) return 0;
   const int strips = N * ((H + R - 1) / R);
   int splits = std::max(1, std::min(strips, num_cu / pairs));
-  if (g_tune[27] > 1) splits = std::max(1, std::min(splits, g_tune[27] / 2));  // cap on the slices (2 per split)
+  if (g_tune[kWgSplitCap] > 1) splits = std::max(1, std::min(splits, g_tune[kWgSplitCap] / 2));  // cap on the slices (2 per split)
   const int sps = (strips + splits - 1) / splits;
   return 2 * ((strips + sps - 1) / sps);
 }
@@ -214,7 +214,7 @@ void launch_wgrad3x3(const bf16* dy, const bf16* x, int N, int H, int W, int C, 
   p.buf = w3_buf(p.R, W);
   p.nib = C / 64;
   p.div_wq = make_fastdiv(p.Wq);
-  p.ablate = g_tune[2];
+  p.ablate = g_tune[kAblate];
   p.div_w = make_fastdiv(W);
   p.div_spi = make_fastdiv(p.spi);
   const int lds = 2 * p.buf;

@@ -14,7 +14,7 @@ import os
 
 import torch
 
-from .. import _ext
+from .. import _ext, tuning
 from ..data import (CappedImageFolder, DevicePrefetcher, ImageFolder, ListDataset, ShardSampler, SyntheticImages,
                     build_loader, build_transform, norm_stats)
 from ..parallel.ddp import graph_safe_nccl_env, init_distributed
@@ -44,7 +44,7 @@ def setup(args) -> Runtime:
         # DCP_AUTOTUNE environment variable (_ext.py) overrides the flag either way
         env = os.environ.get("DCP_AUTOTUNE")
         tune = getattr(args, "autotune", False) if env is None else env == "1"
-        kops.set_tuning(25, 1 if tune else 0)
+        kops.set_tuning(tuning.slot("autotune"), 1 if tune else 0)
     else:
         device = torch.device("cpu")
     set_seed(args.seed + rank)

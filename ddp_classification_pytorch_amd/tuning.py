@@ -1,0 +1,68 @@
+"""Named kernel-configuration slots (mirror of ``csrc/tune.h``).
+
+The HIP library selects kernel variants from a small table of integer switches (0 = the shipped
+heuristic): in-process A/B experiments (``tools/conv_bench.py --cfgs``), the per-shape conv
+autotuner, and ``DCP_TUNE="name=value,..."`` from the environment.  Python code addresses a slot
+only by name through this module; ``SLOTS`` must equal the library's own table (checked against
+``csrc/tune.h`` by tests/test_tuning_cpu.py and against the loaded library by :func:`verify`).
+"""
+from __future__ import annotations
+
+SLOTS = {
+    "tg_tile_n": 0, "tg_stages": 1, "ablate": 2, "tg_pingpong": 3, "tg_big_cvar": 4, "wg_splits_per_cu": 5,
+    "wg_flush_ablate": 6, "wg_tile_mode": 7, "tg_kdepth": 8, "ew_grid_cap": 9, "ew_rows": 10,
+    "bn_act_variant": 11, "wg_rows": 12, "narrow_kdepth": 13, "wg_cols": 14, "wg3x3": 15, "gconv_sg": 16,
+    "stem_ablate": 17, "c3_off": 18, "c3_variant": 19, "tg_big": 24, "autotune": 25, "wg_split_cap": 27,
+    "bn_bwd_cap": 28, "row_reduce": 29, "c3_epilogue": 30, "c3_window_kb": 31,
+}
+NUM_SLOTS = 32
+
+
+def slot(name) -> int:
+    """Slot index of ``name`` (a registered name, or a plain integer for old-style specs)."""
+    if isinstance(name, int):
+        return name
+    name = str(name).strip()
+    if name.lstrip("-").isdigit():
+        return int(name)
+    try:
+        return SLOTS[name]
+    except KeyError:
+        raise KeyError(f"unknown tuning slot {name!r}; known: {', '.join(sorted(SLOTS))}") from None
+
+
+def parse_spec(spec: str, sep: str = ","):
+    """``"tg_tile_n=64,tg_stages=3"`` (or ``;``-separated) -> [(slot, value), ...]."""
+    out = []
+    for kv in filter(None, (t.strip() for t in (spec or "").replace(";", sep).split(sep))):
+        k, v = kv.split("=")
+        out.append((slot(k), int(v)))
+    return out
+
+
+def apply(K, spec, reset: bool = False):
+    """Set the slots of ``spec`` on the kernel library ``K`` (optionally zeroing every slot first)."""
+    if reset:
+        for i in range(NUM_SLOTS):
+            K.set_tuning(i, 0)
+    for i, v in parse_spec(spec) if isinstance(spec, str) else spec:
+        K.set_tuning(slot(i), int(v))
+
+
+def verify(K) -> None:
+    """Fail loudly if the loaded library's slot table differs from this mirror."""
+    lib = {}
+    for kv in filter(None, K.tuning_slots().split(";")):
+        k, v = kv.split("=")
+        lib[k] = int(v)
+    if lib != SLOTS:
+        raise RuntimeError(f"tuning slot table mismatch: library {lib} vs tuning.py {SLOTS} (stale build?)")
+
+
+def parse_header(path: str):
+    """The name -> slot table of csrc/tune.h (tests)."""
+    import re
+
+    text = open(path).read()
+    enum = {k: int(v) for k, v in re.findall(r"\b(k\w+)\s*=\s*(\d+)", text)}
+    return {name: enum[ident] for name, ident in re.findall(r'\{"(\w+)",\s*(k\w+)\}', text)}

@@ -32,9 +32,10 @@ def _kernel_tuning_off_between_tests():
     (the baseline / arcface workloads default to it): every test starts and ends with it off, so
     tuning dispatches and their scratch never land inside another test's measurements."""
     from ddp_classification_pytorch_amd import _ext
+    from ddp_classification_pytorch_amd.tuning import slot as tslot
 
     if _ext.is_loaded():
-        _ext.hip_ops().set_tuning(25, 0)
+        _ext.hip_ops().set_tuning(tslot("autotune"), 0)
     yield
     if _ext.is_loaded():
-        _ext.hip_ops().set_tuning(25, 0)
+        _ext.hip_ops().set_tuning(tslot("autotune"), 0)

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from ddp_classification_pytorch_amd import _ext
+from ddp_classification_pytorch_amd.tuning import slot as tslot
 from ddp_classification_pytorch_amd.ops import _ref
 
 pytestmark = pytest.mark.gpu
@@ -431,11 +432,11 @@ def test_grouped_wgrad_supergroups(K, sg):
     torch.manual_seed(0)
     x, dy = rnd(2, 14, 14, 128), rnd(2, 14, 14, 128)
     try:
-        K.set_tuning(16, sg)
+        K.set_tuning(tslot("gconv_sg"), sg)
         dw = K.grouped_conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 32, 1, 1)
         torch.cuda.synchronize()
     finally:
-        K.set_tuning(16, 0)
+        K.set_tuning(tslot("gconv_sg"), 0)
     assert relerr(dw, _ref.grouped_conv_wgrad(dy.float(), x.float(), 3, 3, 32, 1, 1)) < 5e-3
 
 
@@ -727,7 +728,8 @@ def test_bn_stats_finalize_fused_matches(K, slab, N, H):
     assert torch.allclose(rm1, rm2, rtol=1e-5, atol=1e-8) and torch.allclose(rv1, rv2, rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("cfg", [((1, 3), (8, 32)), ((1, 4), (8, 32)), ((1, 3),)])
+@pytest.mark.parametrize("cfg", [(("tg_stages", 3), ("tg_kdepth", 32)), (("tg_stages", 4), ("tg_kdepth", 32)),
+                                 (("tg_stages", 3),)])
 @pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
                                    (3, 9, 11, 64, 72, 3, 1, 1), (2, 56, 56, 64, 256, 1, 1, 0)])
 def test_conv_pipeline_variants(K, cfg, shape):
@@ -741,13 +743,13 @@ def test_conv_pipeline_variants(K, cfg, shape):
     wb, wt = K.weight_prep(w.float().to(DEV), 0, True)
     try:
         for i, v in cfg:
-            K.set_tuning(i, v)
+            K.set_tuning(tslot(i), v)
         y, slabs = K.conv_fwd(x.to(DEV), wb, s, p, True)
         dx = K.conv_dgrad(dy.to(DEV), wt, H, W, s, p)
         torch.cuda.synchronize()
     finally:
         for i, _ in cfg:
-            K.set_tuning(i, 0)
+            K.set_tuning(tslot(i), 0)
     yr, _ = _ref.conv_fwd(x.float(), w.float(), s, p, False)
     assert relerr(y, yr) < 1e-2
     st = K.bn_stats(y, slabs)
@@ -757,7 +759,7 @@ def test_conv_pipeline_variants(K, cfg, shape):
     assert relerr(dx, dxr) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [((1, 3), (8, 32)), ((1, 4), (8, 32))])
+@pytest.mark.parametrize("cfg", [(("tg_stages", 3), ("tg_kdepth", 32)), (("tg_stages", 4), ("tg_kdepth", 32))])
 def test_conv_dgrad_bn_pipeline_variants(K, cfg):
     """The fused BN-backward dgrad epilogue behind the 32-deep ring variants equals the
     default pipeline's result (same fp32 reference tolerance)."""
@@ -771,12 +773,12 @@ def test_conv_dgrad_bn_pipeline_variants(K, cfg):
     g0, s0 = K.conv_dgrad_bn(*args)
     try:
         for i, v in cfg:
-            K.set_tuning(i, v)
+            K.set_tuning(tslot(i), v)
         g1, s1 = K.conv_dgrad_bn(*args)
         torch.cuda.synchronize()
     finally:
         for i, _ in cfg:
-            K.set_tuning(i, 0)
+            K.set_tuning(tslot(i), 0)
     assert relerr(g1, g0) < 1e-2
     assert relerr(s1[0], s0[0]) < 2e-2 and relerr(s1[1], s0[1]) < 2e-2
 
@@ -806,8 +808,9 @@ def test_bn_act_mask_and_masked_dgrad_bn(K):
     assert relerr(s1, s0) < 1e-5
 
 
-@pytest.mark.parametrize("cfg", [((12, 32),), ((12, 32), (5, 4)), ((14, 4),), ((14, 3),), ((12, 32), (14, 3)),
-                                 ((27, 8),), ((27, 8), (15, 1))])
+@pytest.mark.parametrize("cfg", [(("wg_rows", 32),), (("wg_rows", 32), ("wg_splits_per_cu", 4)), (("wg_cols", 4),),
+                                 (("wg_cols", 3),), (("wg_rows", 32), ("wg_cols", 3)), (("wg_split_cap", 8),),
+                                 (("wg_split_cap", 8), ("wg3x3", 1))])
 @pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64, 3, 1, 1), (2, 28, 28, 128, 512, 1, 1, 0),
                                    (2, 14, 14, 256, 128, 3, 2, 1), (3, 9, 11, 64, 72, 3, 1, 1),
                                    (8, 56, 56, 64, 64, 1, 1, 0)])  # > 64 splits: one-launch row reduction
@@ -820,12 +823,12 @@ def test_conv_wgrad_variants(K, cfg, shape):
     dy, x = rnd(N, Ho, Wo, Co), rnd(N, H, W, Ci)
     try:
         for i, v in cfg:
-            K.set_tuning(i, v)
+            K.set_tuning(tslot(i), v)
         dw = K.conv_wgrad(dy.to(DEV), x.to(DEV), k, k, s, p)
         torch.cuda.synchronize()
     finally:
         for i, _ in cfg:
-            K.set_tuning(i, 0)
+            K.set_tuning(tslot(i), 0)
     assert relerr(dw, _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)) < 5e-3
 
 
@@ -839,11 +842,11 @@ def test_wgrad3x3_direct(K, N, H, W, Ci, Co):
     dw = K.conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 1, 1)
     assert relerr(dw, _ref.conv_wgrad(dy.float(), x.float(), 3, 3, 1, 1)) < 5e-3
     try:
-        K.set_tuning(15, 1)
+        K.set_tuning(tslot("wg3x3"), 1)
         dw_gemm = K.conv_wgrad(dy.to(DEV), x.to(DEV), 3, 3, 1, 1)
         torch.cuda.synchronize()
     finally:
-        K.set_tuning(15, 0)
+        K.set_tuning(tslot("wg3x3"), 0)
     assert relerr(dw, dw_gemm) < 2e-3
 
 
@@ -855,11 +858,11 @@ def test_narrow_channel_conv_bk32(K, N, H, Ci, Co, k, pad):
     w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
     wb, _ = K.weight_prep(w.float().to(DEV), 0, False)
     try:
-        K.set_tuning(13, 32)
+        K.set_tuning(tslot("narrow_kdepth"), 32)
         y, slabs = K.conv_fwd_geo(x.to(DEV), wb, 1, pad, H, H, True)
         torch.cuda.synchronize()
     finally:
-        K.set_tuning(13, 0)
+        K.set_tuning(tslot("narrow_kdepth"), 0)
     yr, _ = _ref.conv_fwd_geo(x.float(), w.float(), 1, pad, H, H, False)
     assert relerr(y, yr) < 1e-2
     st = K.bn_stats(y, slabs)
@@ -913,24 +916,24 @@ def test_conv3x3_direct_c64(K, N, H, W, variant, de):
     torch.manual_seed(7)
     x = rnd(N, H, W, 64, scale=2.0).abs()  # post-ReLU-like input: non-zero channel means
     w = rnd(64, 3, 3, 64, scale=1.0 / 24)
-    K.set_tuning(19, variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double;
+    K.set_tuning(tslot("c3_variant"), variant)  # 0: 8 waves, double-buffered; 1: 4 waves, single; 2: 4 waves, double;
     # 3 / 4: variant 0 with s_setprio for the upper wave half / the upper half's subtiles reversed
-    K.set_tuning(30, 0 if de else 2)
+    K.set_tuning(tslot("c3_epilogue"), 0 if de else 2)
     try:
         y, part = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
         y3, none = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, False)
     finally:
-        K.set_tuning(19, 0)
-        K.set_tuning(30, 0)
+        K.set_tuning(tslot("c3_variant"), 0)
+        K.set_tuning(tslot("c3_epilogue"), 0)
     if W <= 100 and variant != 2:  # wider rows / the smaller windows of variant 2: implicit GEMM (slabs)
         assert part.shape[1:] == (3, 64)  # (n, mean, M2) partials of the direct kernel
     yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1, False)
     assert relerr(y, yr) < 1e-2
-    K.set_tuning(18, 1)
+    K.set_tuning(tslot("c3_off"), 1)
     try:
         y2, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 1, True)
     finally:
-        K.set_tuning(18, 0)
+        K.set_tuning(tslot("c3_off"), 0)
     assert relerr(y, y2) < 5e-3
     st = K.bn_stats(y, part)
     sr = _ref.bn_stats(y.float().cpu(), None)
@@ -1106,52 +1109,16 @@ def test_adaptive_avg_pool_kernels(K):
     assert relerr(dx, dxr) < 5e-3
 
 
-@pytest.mark.parametrize("shape", [(4, 56, 56, 64, 256, 1, 1, 0), (3, 28, 28, 128, 512, 1, 1, 0),
-                                   (2, 14, 14, 256, 256, 3, 1, 1), (2, 28, 28, 256, 512, 1, 2, 0),
-                                   (3, 9, 11, 64, 128, 3, 1, 1), (2, 7, 7, 512, 2048, 1, 1, 0),
-                                   (1, 13, 13, 128, 64, 3, 1, 1)])
-@pytest.mark.parametrize("bk", [32, 64])
-def test_persistent_tap_gemm_matches(K, shape, bk):
-    """The persistent cross-tile-prefetch tap GEMM (g_tune[20] = 1) == the one-tile-per-workgroup
-    kernel: forward with BN statistics and the data gradient (stride 1 and the stride-2 parity
-    classes), ragged M included."""
-    N, H, W, Ci, Co, k, s, p = shape
-    x = rnd(N, H, W, Ci).to(DEV)
-    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
-    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dy = rnd(N, Ho, Wo, Co).to(DEV)
-    wb, wt = K.weight_prep(w.float(), 0, True)
-    outs = []
-    try:
-        for mode in (2, 1):
-            K.set_tuning(20, mode)
-            K.set_tuning(21, bk)
-            y, slabs = K.conv_fwd(x, wb, s, p, True)
-            st = K.bn_stats(y, slabs)
-            dx = K.conv_dgrad(dy, wt, H, W, s, p)
-            torch.cuda.synchronize()
-            outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
-    finally:
-        K.set_tuning(20, 0)
-        K.set_tuning(21, 0)
-    (y0, s0, d0), (y1, s1, d1) = outs
-    assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
-    assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
-    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
-    assert relerr(y1, yr) < 1e-2
-
-
 @pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 1, 1), (3, 28, 28, 128, 512, 1, 1, 0),
                                    (2, 7, 7, 512, 2048, 1, 1, 0), (2, 28, 28, 256, 512, 1, 2, 0),
                                    (3, 9, 11, 128, 128, 3, 1, 1), (1, 13, 13, 256, 384, 3, 2, 1),
                                    (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1)])
-@pytest.mark.parametrize("mode", [1, 3, 4])
-@pytest.mark.parametrize("cvar", [0, 2])
+@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("cvar", [0, 2, 3])
 def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
-    """The 8-wave 256 x 256 (g_tune[24] = 1; 256 x 128 below 256 channels), 4-wave 256 x 128
-    (g_tune[24] = 3) and 4-wave 256 x 256 (g_tune[24] = 4: 128 x 128 per wave, AGPR accumulators;
-    Co >= 256 only) big-tile tap GEMMs, fragments read across the barrier or (g_tune[4] = 2)
-    after it, == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
+    """The 8-wave 256 x 256 (tg_big = 1; 256 x 128 below 256 channels) and 4-wave 256 x 128
+    (tg_big = 3) big-tile tap GEMMs, fragments read across the barrier, after it (tg_big_cvar = 2)
+    or in the ping-pong schedule (tg_big_cvar = 3: 8-wave tiles only; the others ignore it), == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
     M: quadrants past M write no slab) and the data gradient (stride 1 and the stride-2 parity
     classes), channel counts that are not a multiple of the tile."""
     N, H, W, Ci, Co, k, s, p = shape
@@ -1164,58 +1131,16 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
     outs = []
     try:
         for m in (2, mode):
-            K.set_tuning(24, m)
-            K.set_tuning(4, cvar if m != 2 else 0)
+            K.set_tuning(tslot("tg_big"), m)
+            K.set_tuning(tslot("tg_big_cvar"), cvar if m != 2 else 0)
             y, slabs = K.conv_fwd(x, wb, s, p, True)
             st = K.bn_stats(y, slabs)
             dx = K.conv_dgrad(dy, wt, H, W, s, p)
             torch.cuda.synchronize()
             outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
     finally:
-        K.set_tuning(24, 0)
-        K.set_tuning(4, 0)
-    (y0, s0, d0), (y1, s1, d1) = outs
-    assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
-    assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
-    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
-    assert relerr(y1, yr) < 1e-2
-    sr = _ref.bn_stats(y1, None)
-    assert relerr(s1[0, 1], sr[0, 1]) < 1e-4 and relerr(s1[0, 2], sr[0, 2]) < 1e-4
-    dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().cpu().permute(3, 1, 2, 0), H, W, s, p)
-    assert relerr(d1, dxr) < 1e-2
-
-
-@pytest.mark.parametrize("shape", [(2, 14, 14, 256, 256, 3, 1, 1), (3, 28, 28, 128, 512, 1, 1, 0),
-                                   (2, 7, 7, 512, 2048, 1, 1, 0), (2, 28, 28, 256, 512, 1, 2, 0),
-                                   (3, 9, 11, 128, 128, 3, 1, 1), (1, 13, 13, 256, 384, 3, 2, 1),
-                                   (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1),
-                                   (4, 14, 14, 64, 128, 1, 1, 0), (2, 14, 14, 128, 192, 3, 1, 1)])
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
-def test_pipelined_p8_tap_gemm_matches(K, shape, variant):
-    """The pipelined 8-wave 256 x 128 tap GEMM (g_tune[26]: 1 = 16x16x32, 2 = 32x32x16, 3 / 4 with
-    the read/MFMA interleave) == the 128-row kernel and the fp32 reference: forward with BN
-    statistics and the data gradient (stride 1, the stride-2 parity classes, ragged M and Co,
-    1..36 k-tiles: the steady ring loop, its tail and the no-steady-state short-K path)."""
-    N, H, W, Ci, Co, k, s, p = shape
-    torch.manual_seed(0)
-    x = rnd(N, H, W, Ci).to(DEV)
-    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
-    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dy = rnd(N, Ho, Wo, Co).to(DEV)
-    wb, wt = K.weight_prep(w.float(), 0, True)
-    outs = []
-    try:
-        for v in (0, variant):
-            K.set_tuning(24, 2)  # the 128-row kernel as the comparison
-            K.set_tuning(26, v)
-            y, slabs = K.conv_fwd(x, wb, s, p, True)
-            st = K.bn_stats(y, slabs)
-            dx = K.conv_dgrad(dy, wt, H, W, s, p)
-            torch.cuda.synchronize()
-            outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
-    finally:
-        K.set_tuning(24, 0)
-        K.set_tuning(26, 0)
+        K.set_tuning(tslot("tg_big"), 0)
+        K.set_tuning(tslot("tg_big_cvar"), 0)
     (y0, s0, d0), (y1, s1, d1) = outs
     assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
@@ -1259,61 +1184,6 @@ def test_conv_bn_prologue(K, shape):
     assert relerr(dw, dwr) < 5e-3
 
 
-@pytest.mark.parametrize("shape", [
-    (2, 28, 28, 128, 128), (3, 14, 14, 256, 256), (4, 7, 7, 512, 512), (2, 9, 11, 64, 72),
-    (5, 13, 13, 128, 64), (8, 2, 2, 512, 512), (1, 56, 56, 64, 128)])
-def test_conv3x3_window_kernel(K, shape):
-    """tap_win_kernel (g_tune[22] = 1): 3x3 / pad-1 / stride-1 forward (+ BN statistics) and data
-    gradient from one staged pixel window per 64-channel chunk == the fp32 reference, and == the
-    gather kernel to bf16 rounding."""
-    N, H, W, Ci, Co = shape
-    torch.manual_seed(0)
-    x = rnd(N, H, W, Ci).to(DEV)
-    w = rnd(Co, 3, 3, Ci, scale=1.0 / math.sqrt(9 * Ci))
-    dy = rnd(N, H, W, Co).to(DEV)
-    _, wt = K.weight_prep(w.float().to(DEV), 0, True)
-    try:
-        K.set_tuning(22, 1)
-        y, slabs = K.conv_fwd(x, w.to(DEV), 1, 1, True)
-        dx = K.conv_dgrad(dy, wt, H, W, 1, 1) if Co % 64 == 0 else None
-        torch.cuda.synchronize()
-    finally:
-        K.set_tuning(22, 0)
-    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float(), 1, 1, False)
-    assert relerr(y, yr) < 1e-2
-    st, sr = K.bn_stats(y, slabs), _ref.bn_stats(y.float().cpu(), None)
-    assert torch.equal(st[0, 0].cpu(), sr[0, 0])
-    assert relerr(st[0, 1], sr[0, 1]) < 1e-4 and relerr(st[0, 2], sr[0, 2]) < 1e-4
-    y2, _ = K.conv_fwd(x, w.to(DEV), 1, 1, True)
-    assert relerr(y, y2) < 5e-3
-    if dx is not None:
-        dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().permute(3, 1, 2, 0), H, W, 1, 1)
-        assert relerr(dx, dxr) < 1e-2
-
-
-@pytest.mark.parametrize("mode", [0, 1])
-def test_split_reduce_single_launch_ticket(K, mode):
-    """Weight gradient with > 64 split-K partials: the second reduction level as its own launch
-    (default) or in the last workgroup of each column group (last-arrival ticket, g_tune[23] = 1,
-    measured slower); both equal the fp32 reference and are bitwise reproducible run to run."""
-    torch.manual_seed(0)
-    N, H, C, Co = 48, 56, 128, 128  # 150,528 rows: 512 splits -> 8 chunks of 64
-    x = rnd(N, H, H, C).to(DEV)
-    dy = rnd(N, H, H, Co).to(DEV)
-    try:
-        K.set_tuning(23, mode)
-        dw1 = K.conv_wgrad(dy, x, 1, 1, 1, 0)
-        dw2 = K.conv_wgrad(dy, x, 1, 1, 1, 0)
-        torch.cuda.synchronize()
-    finally:
-        K.set_tuning(23, 0)
-    assert torch.equal(dw1, dw2)
-    dwr = _ref.conv_wgrad(dy[:4].float().cpu(), x[:4].float().cpu(), 1, 1, 1, 0)  # scale check on a slice
-    full = (dy.float().reshape(-1, Co).t() @ x.float().reshape(-1, C)).cpu()
-    assert relerr(dw1.reshape(Co, C), full) < 1e-3
-    assert dwr.shape == dw1.shape
-
-
 def test_iabn_gamma_and_sign_mul(K):
     """InplaceABN effective weight |g| + eps with its reciprocal, and the gradient d * sign(g)."""
     g = torch.randn(1000)
@@ -1339,13 +1209,13 @@ def test_conv_autotune_same_results(K):
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         dy = rnd(N, Ho, Wo, Co).to(DEV)
         wb, wt = K.weight_prep(w.float(), 0, True)
-        K.set_tuning(25, 0)  # (a workload run earlier in this process may have left it on)
+        K.set_tuning(tslot("autotune"), 0)  # (a workload run earlier in this process may have left it on)
         y0, s0 = K.conv_fwd(x, wb, s, p, True)
         d0 = K.conv_dgrad(dy, wt, H, W, s, p)
         g0 = K.conv_wgrad(dy, x, k, k, s, p)
         n0 = K.autotune_entries()
         try:
-            K.set_tuning(25, 1)
+            K.set_tuning(tslot("autotune"), 1)
             y1, s1 = K.conv_fwd(x, wb, s, p, True)
             d1 = K.conv_dgrad(dy, wt, H, W, s, p)
             g1 = K.conv_wgrad(dy, x, k, k, s, p)
@@ -1353,7 +1223,7 @@ def test_conv_autotune_same_results(K):
             y2, _ = K.conv_fwd(x, wb, s, p, True)
             assert K.autotune_entries() == n1 > n0
         finally:
-            K.set_tuning(25, 0)
+            K.set_tuning(tslot("autotune"), 0)
         torch.cuda.synchronize()
         assert torch.equal(y1, y0) and torch.equal(y2, y0), (N, H, Ci, Co, k, s)
         assert torch.equal(d1, d0), (N, H, Ci, Co, k, s)
@@ -1377,13 +1247,13 @@ def test_conv_fwd_256_channel_tiles(K, shape):
     outs = []
     try:
         for bn in (0, 256):
-            K.set_tuning(0, bn)
+            K.set_tuning(tslot("tg_tile_n"), bn)
             y, slabs = K.conv_fwd(x, wb, s, p, True)
             st = K.bn_stats(y, slabs)
             torch.cuda.synchronize()
             outs.append((y.float().cpu(), st.cpu()))
     finally:
-        K.set_tuning(0, 0)
+        K.set_tuning(tslot("tg_tile_n"), 0)
     (y0, s0), (y1, s1) = outs
     assert torch.equal(y1, y0)  # same k order: bit-identical outputs
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-4

@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd.tuning import slot as tslot  # noqa: E402
 
 # (Ci, Co, k, stride, H_in, count) at 224px
 R50 = [
@@ -132,7 +133,7 @@ def _apply(K, cfg):
         K.set_tuning(i, 0)
     for kv in filter(None, cfg.split(";")):
         i, v = kv.split("=")
-        K.set_tuning(int(i), int(v))
+        K.set_tuning(tslot(i), int(v))
 
 
 def ab(a):

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd.tuning import slot as tslot  # noqa: E402
 from tools.ew_bench import timeit  # noqa: E402
 
 # (H, C = BN channels / dgrad output, Co = conv output channels / dgrad input, res+add)
@@ -36,7 +37,7 @@ def main():
                 K.set_tuning(i, 0)
             for kv in filter(None, cfg.split(";")):
                 i, val = kv.split("=")
-                K.set_tuning(int(i), int(val))
+                K.set_tuning(tslot(i), int(val))
             t_bn = min(timeit(lambda: K.conv_dgrad_bn(dy, wt, 0, add, y, None if full else r, *v, 1, mask))
                        for _ in range(3))
             t_pl = min(timeit(lambda: K.conv_dgrad(dy, wt, H, H, 1, 0, add)) for _ in range(3))

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd.tuning import slot as tslot  # noqa: E402
 
 
 def timeit(fn, iters=20):
@@ -43,7 +44,7 @@ def main():
                 K.set_tuning(i, 0)
             for kv in filter(None, cfg.split(";")):
                 i, v = kv.split("=")
-                K.set_tuning(int(i), int(v))
+                K.set_tuning(tslot(i), int(v))
             best = [1e9, 1e9, 1e9]
             for _ in range(3):
                 best[0] = min(best[0], timeit(lambda: K.bn_act(x, r, sc, sh, 1, 0.0)))

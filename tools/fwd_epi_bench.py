@@ -12,6 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddp_classification_pytorch_amd import _ext  # noqa: E402
+from ddp_classification_pytorch_amd.tuning import slot as tslot  # noqa: E402
 from tools.ew_bench import timeit  # noqa: E402
 
 # (H, Ci, Co, k, stride)
@@ -35,13 +36,13 @@ def main():
         row = []
         for stats in (False, True):
             for abl in (0, 1, 2, 3):
-                K.set_tuning(2, abl)
+                K.set_tuning(tslot("ablate"), abl)
                 us = timeit(lambda: K.conv_fwd(x, w, s, k // 2, stats), iters=10)
                 row.append(us)
-            K.set_tuning(2, 0)
-        K.set_tuning(8, 64)  # 64-deep k-tiles for every shape (disables the 1x1 BK32 heuristic)
+            K.set_tuning(tslot("ablate"), 0)
+        K.set_tuning(tslot("tg_kdepth"), 64)  # 64-deep k-tiles for every shape (disables the 1x1 BK32 heuristic)
         bk64 = timeit(lambda: K.conv_fwd(x, w, s, k // 2, True), iters=10)
-        K.set_tuning(8, 0)
+        K.set_tuning(tslot("tg_kdepth"), 0)
         print(f"H={H:3d} {Ci:4d}->{Co:4d} k{k}: plain {row[0]:7.1f}us ({gb / row[0] * 1e3:5.2f} TB/s "
               f"{flops / row[0] / 1e6:6.0f} TF/s) noload {row[1]:7.1f} nomfma {row[2]:7.1f} epi-only {row[3]:7.1f} | "
               f"stats {row[4]:7.1f}us ({gb / row[4] * 1e3:5.2f} TB/s) noload {row[5]:7.1f} nomfma {row[6]:7.1f} "

@@ -56,6 +56,12 @@ for step in "$@"; do
       tail -1 $O/ddp1_b1024.log
       timeout -k 10 300 python -u bench.py --force-ddp --batch 128 --grad-comm bf16 --steps 30 --warmup 5 > $O/ddp1_b128bf16.log 2>&1
       tail -1 $O/ddp1_b128bf16.log ;;
+    convabs=*)
+      # convabs=IDX,IDX:CFGS -- the same A/B on a subset of the R50 shapes (conv_bench.py R50 indices)
+      v=${step#convabs=}; only=${v%%:*}; c=${v#*:}
+      timeout -k 10 900 python -u tools/conv_bench.py --batch 1024 --iters 10 --only "$only" --cfgs "$c" \
+        > $O/convabs.log 2>&1
+      tail -3 $O/convabs.log ;;
     convab=*)
       c=${step#convab=}
       timeout -k 10 900 python -u tools/conv_bench.py --batch 1024 --iters 10 --only 1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19,20,21,22 --cfgs "$c" \
