@@ -66,6 +66,8 @@ def parse(argv=None):
                     help="headline phase with cross-replica BN (reference default); off = local BN")
     ap.add_argument("--no-syncbn-phase", dest="syncbn_phase", action="store_false",
                     help="N > 1: skip the second, SyncBN-timed phase")
+    ap.add_argument("--no-syncbn-peer", dest="syncbn_peer", action="store_false",
+                    help="N > 1: skip the third phase, SyncBN over the peer-memory mailboxes (parallel/peer.py)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce precision (bf16: half the xGMI bytes; bucket engine: bf16 buckets, "
@@ -342,6 +344,8 @@ def main(argv=None):
         "per_rank_ms": [round(v / a.steps * 1000.0, 3) for v in per_rank],
         "syncbn_value": None,
         "syncbn_ms_per_step": None,
+        "syncbn_peer_value": None,
+        "syncbn_peer_ms_per_step": None,
         "comm": None,
         "comm_probe": None,
         "config": {
@@ -449,6 +453,31 @@ def main(argv=None):
         out["syncbn_ms_per_step"] = round(sdt / a.steps * 1000.0, 3)
         out["syncbn_per_rank_ms"] = [round(v / a.steps * 1000.0, 3) for v in sper]
 
+    def syncbn_peer_phase():
+        nonlocal run, graphed
+        # third phase: the same SyncBN with its statistics exchanged through the IPC-mapped peer
+        # mailboxes (parallel/peer.py: one kernel per exchange instead of an RCCL collective)
+        from ddp_classification_pytorch_amd.parallel import peer
+
+        pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group, transport="peer")
+        ex = peer.exchange_for(bn_group)
+        if ex is None:
+            raise RuntimeError("peer mailboxes unavailable (no peer access): stayed on RCCL")
+        if a.graph:
+            from ddp_classification_pytorch_amd.engine.graph import GraphedStep
+
+            run = graphed = None
+            torch.cuda.empty_cache()
+            run = GraphedStep(step, warmup=2, distributed=True)
+        for _ in range(2):
+            run()
+        sdt, _ = timed(a.steps)
+        sdt, sper = gather_max(sdt)
+        ex.check()
+        out["syncbn_peer_value"] = round(B * world * a.steps / sdt, 2)
+        out["syncbn_peer_ms_per_step"] = round(sdt / a.steps * 1000.0, 3)
+        pddp.convert_sync_batchnorm(pddp.unwrap(model), bn_group, transport="rccl")
+
     def probe_phase():
         out["comm_probe"] = comm_probe(dev, world, bn_group)
 
@@ -459,6 +488,8 @@ def main(argv=None):
         out["comm"] = {"engine": a.ddp_engine, "bucket_mb": [round(v, 2) for v in pddp.bucket_layout_mb(model)]}
     if go and dist_on and not a.syncbn and a.syncbn_phase:
         go = guarded("syncbn", syncbn_phase)
+        if go and a.syncbn_peer:
+            go = guarded("syncbn_peer", syncbn_peer_phase)
     if go and dist_on and a.comm_probe and dist.get_backend() == "nccl":
         go = guarded("probe", probe_phase)
     if timer is not None:

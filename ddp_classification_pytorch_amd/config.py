@@ -44,6 +44,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--dist-backend", default=None, help="nccl (=RCCL) on GPU, gloo on CPU")
     a("--syncbn", dest="syncbn", action="store_true", default=None, help="cross-replica BN (reference default)")
     a("--no-syncbn", dest="syncbn", action="store_false")
+    a("--syncbn-transport", default=None, choices=["rccl", "peer"],
+      help="SyncBN statistics exchange: rccl collectives (default) or the peer-memory mailboxes (parallel/peer.py)")
     a("--force-ddp", action="store_true",
       help="one process: still create a (world-1) process group and train through the data-parallel engine "
            "(measures the engine's own cost; tests its HIP-graph capture)")

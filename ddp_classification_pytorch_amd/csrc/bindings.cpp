@@ -1268,18 +1268,73 @@ Tensor prefix_mask(const Tensor& x, const Tensor& keep) {
   return y;
 }
 
-Tensor nested_eval(const Tensor& feat, const Tensor& W, const Tensor& labels) {
+// peer access from the current device to `peer` (the IPC-mapped SyncBN mailboxes, parallel/peer.py)
+void enable_peer_access(int64_t peer) {
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "enable_peer_access: hipGetDevice");
+  if (peer == dev) return;
+  int can = 0;
+  TORCH_CHECK(hipDeviceCanAccessPeer(&can, dev, (int)peer) == hipSuccess && can, "no peer access from device ", dev,
+              " to ", peer);
+  const hipError_t e = hipDeviceEnablePeerAccess((int)peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return;
+  }
+  TORCH_CHECK(e == hipSuccess, "hipDeviceEnablePeerAccess: ", hipGetErrorString(e));
+}
+
+// SyncBN peer exchange (parallel/peer.py): src fp32 [n] -> dst fp32 [world * n] (mode 0) or [n] (mode 1)
+void peer_exchange(const Tensor& src, const Tensor& dst, const Tensor& boxes, const Tensor& epoch, int64_t rank,
+                   int64_t world, int64_t slot, int64_t mode, const Tensor& err) {
+  CHECK_DEV(src);
+  CHECK_F32(src);
+  CHECK_F32(dst);
+  CHECK_CONTIG(src);
+  CHECK_CONTIG(dst);
+  TORCH_CHECK(boxes.scalar_type() == at::kLong && boxes.is_cuda() && boxes.numel() == world, "peer_exchange boxes");
+  TORCH_CHECK(epoch.scalar_type() == at::kInt && err.scalar_type() == at::kInt && epoch.is_cuda() && err.is_cuda(),
+              "peer_exchange epoch / err: int32 on the device");
+  const int64_t n = src.numel();
+  TORCH_CHECK(dst.numel() == (mode == 0 ? world * n : n), "peer_exchange dst size");
+  TORCH_CHECK(dcp::launch_peer_exchange(src.data_ptr<float>(), (int)n, dst.data_ptr<float>(), boxes.data_ptr<int64_t>(),
+                                        epoch.data_ptr<int>(), (int)rank, (int)world, (int)slot, (int)mode,
+                                        err.data_ptr<int>(), cur_stream()),
+              "peer_exchange: world / rank / size out of range");
+}
+
+// per-prefix-length (top-1, top-3) correct counts of TestNested; scalar = the one-workgroup-per-sample
+// kernel (C <= 4096), else the rank-ballot fast path (any C)
+Tensor nested_eval_impl(const Tensor& feat, const Tensor& W, const Tensor& labels, bool scalar) {
   CHECK_DEV(feat);
   CHECK_F32(feat);
   CHECK_F32(W);
   CHECK_CONTIG(feat);
   CHECK_CONTIG(W);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.device() == feat.device(),
+              "nested_eval labels: int64 on the feature's device");
   const int B = feat.size(0), D = feat.size(1), C = W.size(1);
-  TORCH_CHECK(W.size(0) == D && C <= 4096, "nested_eval shapes (C <= 4096)");
+  TORCH_CHECK(W.size(0) == D && labels.numel() == B, "nested_eval shapes");
   auto counts = at::zeros({D, 2}, feat.options().dtype(at::kInt));
+  if (B == 0 || D == 0) return counts;
+  if (scalar) {
+    TORCH_CHECK(C <= 4096, "nested_eval_scalar: C <= 4096");
+    dcp::launch_nested_eval_scalar(feat.data_ptr<float>(), W.data_ptr<float>(), labels.data_ptr<int64_t>(), B, D, C,
+                                   counts.data_ptr<int>(), cur_stream());
+    return counts;
+  }
+  auto ws = at::empty({(int64_t)dcp::nested_eval_workspace(B, D, C)}, feat.options().dtype(at::kByte));
   dcp::launch_nested_eval(feat.data_ptr<float>(), W.data_ptr<float>(), labels.data_ptr<int64_t>(), B, D, C,
-                          counts.data_ptr<int>(), cur_stream());
+                          counts.data_ptr<int>(), ws.data_ptr(), cur_stream());
   return counts;
+}
+
+Tensor nested_eval(const Tensor& feat, const Tensor& W, const Tensor& labels) {
+  return nested_eval_impl(feat, W, labels, false);
+}
+
+Tensor nested_eval_scalar(const Tensor& feat, const Tensor& W, const Tensor& labels) {
+  return nested_eval_impl(feat, W, labels, true);
 }
 
 Tensor dwconv_fwd(const Tensor& x, const Tensor& filt, int64_t k, int64_t s, int64_t p, bool reflect) {
@@ -1647,6 +1702,10 @@ TORCH_LIBRARY(dcp, m) {
   m.def("act_bwd(Tensor dy, Tensor y, int act) -> Tensor", &act_bwd);
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);
   m.def("nested_eval(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval);
+  m.def("enable_peer_access(int peer) -> ()", &enable_peer_access);
+  m.def("peer_exchange(Tensor src, Tensor(a!) dst, Tensor boxes, Tensor(b!) epoch, int rank, int world, int slot, "
+        "int mode, Tensor(c!) err) -> ()", &peer_exchange);
+  m.def("nested_eval_scalar(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval_scalar);
   m.def("dwconv_fwd(Tensor x, Tensor filt, int k, int s, int p, bool reflect) -> Tensor", &dwconv_fwd);
   m.def("dwconv_bwd(Tensor dy, Tensor filt, int H, int W, int k, int s, int p, bool reflect) -> Tensor", &dwconv_bwd);
   m.def("chan_scale_fwd(Tensor x, Tensor g, Tensor? res, bool relu) -> Tensor", &chan_scale_fwd);

@@ -1483,7 +1483,12 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
 }
 
 template <int WM, int WN, int NS, int CFW = 4>
-static void launch_big(const TapGemmParams& p, int epi, hipStream_t stream) {
+static void launch_big(TapGemmParams p, int epi, hipStream_t stream) {
+  // the 8-wave tile runs the ping-pong schedule by default (tg_big_cvar: 1 = the lockstep
+  // schedule, 2 = fragments read after the barrier, 3 = ping-pong); 3-6 % faster on the R50
+  // shapes the 256 x 256 tile takes (profiles/r5/pingpong_ab_b1024.txt)
+  if (WM * WN == 8) p.cvar = p.cvar == 0 ? 3 : (p.cvar == 1 ? 0 : p.cvar);
+  else if (p.cvar == 1) p.cvar = 0;
   constexpr int BM = 128 * WM, BN = 16 * CFW * WN;
   constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 64, (size_t)WM * (BN / 128) * 32768);
   const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
@@ -1668,7 +1673,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 // order (fp32 rounding).  Off by default (the default path is bit-reproducible run to run).
 // ---------------------------------------------------------------------------
 struct TgCfg {
-  int bn, ns, bk, big;  // g_tune[kTgTileN], [1], [8], [24] overrides (0 = the heuristic's)
+  int bn, ns, bk, big, cvar;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar overrides (0 = the heuristic's)
 };
 static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 0},   // heuristic
@@ -1682,6 +1687,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 3},   // 256 x 128 big tile
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
     {256, 2, 32, 2},  // 256-channel tiles, 32-deep k-tiles (2-3 % on two R50 shapes: profiles/r4/bn256_tile_ab_b1024.txt)
+    {0, 0, 0, 1, 1},  // 256 x 256 big tile, lockstep schedule (the ping-pong one is the tile's default)
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };
@@ -1689,12 +1695,18 @@ static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
 
 struct TuneOverride {
-  int saved[4];
+  static constexpr int kSlots[5] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar};
+  int saved[5];
   explicit TuneOverride(const TgCfg& c) {
-    saved[0] = g_tune[kTgTileN]; saved[1] = g_tune[kTgStages]; saved[2] = g_tune[kTgKDepth]; saved[3] = g_tune[kTgBig];
-    g_tune[kTgTileN] = c.bn; g_tune[kTgStages] = c.ns; g_tune[kTgKDepth] = c.bk; g_tune[kTgBig] = c.big;
+    const int v[5] = {c.bn, c.ns, c.bk, c.big, c.cvar};
+    for (int i = 0; i < 5; ++i) {
+      saved[i] = g_tune[kSlots[i]];
+      g_tune[kSlots[i]] = v[i];
+    }
   }
-  ~TuneOverride() { g_tune[kTgTileN] = saved[0]; g_tune[kTgStages] = saved[1]; g_tune[kTgKDepth] = saved[2]; g_tune[kTgBig] = saved[3]; }
+  ~TuneOverride() {
+    for (int i = 0; i < 5; ++i) g_tune[kSlots[i]] = saved[i];
+  }
 };
 
 int tap_gemm_tuned_count() {
@@ -1748,7 +1760,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     for (int c = 0; c < (int)(sizeof(kTgCfgs) / sizeof(kTgCfgs[0])); ++c) {
       const TgCfg& cfg = kTgCfgs[c];
       if (cfg.big == 3 && !big_ok) continue;
-      if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;
+      if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;  // (the ping-pong candidate too)
       if (cfg.bn == 256 && !(Co > 128 && bnb == nullptr && bias == nullptr && relu == 0)) continue;
       if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
       TuneOverride ov(cfg);

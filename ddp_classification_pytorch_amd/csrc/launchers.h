@@ -257,8 +257,16 @@ void launch_dropout(const void* x, void* y, size_t n, int is_bf16, float p, uint
 // adaptive average pool NHWC [N,H,W,C] -> [N,OH,OW,C]; backward = true: dy [N,OH,OW,C] -> dx [N,H,W,C]
 void launch_adaptive_avg(const bf16* src, bf16* dst, int N, int H, int W, int C, int OH, int OW, bool backward,
                          hipStream_t s);
+void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t* labels, int B, int D, int C,
+                               int* counts, hipStream_t s);
+// workspace bytes of launch_nested_eval (label score chains + per-class-block rank counts)
+// SyncBN peer-memory exchange (peer.hip): gather (mode 0, dst [world][n]) or rank-ordered sum
+// (mode 1, dst [n]) of n floats through the IPC-mapped mailboxes `boxes` ([world] base addresses)
+bool launch_peer_exchange(const float* src, int n, float* dst, const int64_t* boxes, int* epoch, int rank, int world,
+                          int slot, int mode, int* err, hipStream_t s);
+size_t nested_eval_workspace(int B, int D, int C);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
-                        hipStream_t s);
+                        void* ws, hipStream_t s);
 
 void launch_dwconv_fwd(const bf16* x, const float* w, bf16* y, int N, int H, int W, int C, int Ho, int Wo, int k,
                        int s, int p, int reflect, hipStream_t st);

@@ -153,12 +153,19 @@ __global__ void __launch_bounds__(256) prefix_mask_kernel(const bf16* __restrict
   }
 }
 
-// One workgroup per sample: scores_k = sum_{d<=k} f[d] * W[d][:] for k = 0..D-1;
-// count[k][0] += (rank of label == 0), count[k][1] += (rank < 3)
+// TestNested (NESTED/train.py:103-166, K19): for every prefix length k + 1 (k = 0..D-1) the
+// scores s_k[b][c] = sum_{d<=k} f[b][d] W[d][c] of every validation sample, and whether the label
+// ranks first / in the top 3: count[k][0] += (no class scores above the label), count[k][1] +=
+// (fewer than three do).  Scores are sequential fp32 fma chains over d (s = fma(f_d, w_d, s)), in
+// every kernel below, so all of them count exactly the same ranks; ties go to the label.
+//
+// nested_eval_scalar_kernel: one workgroup per sample, a block reduction per feature dimension
+// (the round-4 kernel; kept as the reference the fast path is tested against).
 constexpr int kNestedMaxPerThread = 16;  // C <= 4096
-__global__ void __launch_bounds__(256) nested_eval_kernel(const float* __restrict__ feat, const float* __restrict__ W,
-                                                          const int64_t* __restrict__ labels, int D, int C,
-                                                          int* __restrict__ counts) {
+__global__ void __launch_bounds__(256) nested_eval_scalar_kernel(const float* __restrict__ feat,
+                                                                 const float* __restrict__ W,
+                                                                 const int64_t* __restrict__ labels, int D, int C,
+                                                                 int* __restrict__ counts) {
   __shared__ float red[16];
   __shared__ float slab;
   const int b = blockIdx.x;
@@ -173,7 +180,7 @@ __global__ void __launch_bounds__(256) nested_eval_kernel(const float* __restric
 #pragma unroll
     for (int q = 0; q < kNestedMaxPerThread; ++q) {
       const int j = threadIdx.x + q * 256;
-      if (j < C) s[q] += fd * wr[j];
+      if (j < C) s[q] = fmaf(fd, wr[j], s[q]);
     }
 #pragma unroll
     for (int q = 0; q < kNestedMaxPerThread; ++q)
@@ -192,6 +199,135 @@ __global__ void __launch_bounds__(256) nested_eval_kernel(const float* __restric
       if (rank < 2.5f) atomicAdd(&counts[2 * d + 1], 1);
     }
   }
+}
+
+// Fast path, three launches.
+// (1) the label's own score chain L[b][d] (one wave per sample: 64 dims loaded at once, the chain
+//     itself serial over d -- the same fma order as every class's score);
+__global__ void __launch_bounds__(64) nested_label_prefix_kernel(const float* __restrict__ feat,
+                                                                 const float* __restrict__ W,
+                                                                 const int64_t* __restrict__ labels, int D, int C,
+                                                                 float* __restrict__ L) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int lab = (int)labels[b];
+  const float* f = feat + (size_t)b * D;
+  float acc = 0.f;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    const float fv = d < D ? f[d] : 0.f;
+    const float wv = d < D ? W[(size_t)d * C + lab] : 0.f;
+    float out = 0.f;
+    const int n = min(64, D - d0);
+    for (int i = 0; i < n; ++i) {
+      const float fi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fv), i));
+      const float wi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), i));
+      acc = fmaf(fi, wi, acc);
+      out = lane == i ? acc : out;
+    }
+    if (d < D) L[(size_t)b * D + d] = out;
+  }
+}
+
+// (2) ranks: a lane owns one class for NB samples, a wave 64 classes, a workgroup 4 waves (256
+//     classes) x NB samples.  Per dimension d and sample: one fma per lane, then the wave's count
+//     of classes scoring above the label is a ballot + popcount (the label's lane and classes past
+//     C masked out), kept in lane d % 64 of a count register; per 64 dimensions the
+//     four waves' counts are summed through LDS and stored: gt[class block][b][d].  The 64 weight
+//     values of a chunk are loaded before its dimension loop (all in flight together).
+template <int NB>
+__global__ void __launch_bounds__(256) nested_rank_kernel(const float* __restrict__ feat, const float* __restrict__ W,
+                                                          const int64_t* __restrict__ labels,
+                                                          const float* __restrict__ L, int B, int D, int C,
+                                                          int* __restrict__ gt) {
+  __shared__ float fs[NB][64];
+  __shared__ float ls[NB][64];
+  __shared__ int red[4][NB][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = blockIdx.x * 256 + wave * 64 + lane;
+  const int b0 = blockIdx.y * NB;
+  const bool cok = c < C;
+  uint64_t valid[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int b = b0 + j;
+    const int lab = b < B ? (int)labels[b] : -1;
+    valid[j] = __ballot(cok && c != lab && b < B);
+  }
+  float s[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) s[j] = 0.f;
+  const int cc = cok ? c : 0;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int n = min(64, D - d0);
+    __syncthreads();  // the previous chunk's fs / ls / red reads are done
+    for (int i = tid; i < NB * 64; i += 256) {
+      const int j = i >> 6, dd = i & 63, b = b0 + j, d = d0 + dd;
+      const bool ok = b < B && d < D;
+      fs[j][dd] = ok ? feat[(size_t)b * D + d] : 0.f;
+      ls[j][dd] = ok ? L[(size_t)b * D + d] : 0.f;
+    }
+    __syncthreads();
+    int cnt[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) cnt[j] = 0;
+    // 8 dimensions per step; the next step's 8 weights are loaded behind this step's work
+    float w[8], wn[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = (e < n && cok) ? W[(size_t)(d0 + e) * C + cc] : 0.f;
+#pragma unroll 1
+    for (int e0 = 0; e0 < n; e0 += 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int dd = e0 + 8 + e;
+        wn[e] = (dd < n && cok) ? W[(size_t)(d0 + dd) * C + cc] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int dd = e0 + e;
+        if (dd < n) {
+          const bool mine = lane == dd;
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            s[j] = fmaf(fs[j][dd], w[e], s[j]);
+            const int k = __popcll(__ballot(s[j] > ls[j][dd]) & valid[j]);
+            cnt[j] = mine ? k : cnt[j];
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = wn[e];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) red[wave][j][lane] = cnt[j];
+    __syncthreads();
+    for (int i = tid; i < NB * 64; i += 256) {
+      const int j = i >> 6, dd = i & 63, b = b0 + j, d = d0 + dd;
+      if (b < B && d < D)
+        gt[((size_t)blockIdx.x * B + b) * D + d] = red[0][j][dd] + red[1][j][dd] + red[2][j][dd] + red[3][j][dd];
+    }
+  }
+}
+
+// (3) per dimension: a sample's rank is the sum of its class blocks' counts; count the samples
+//     whose label ranks first / in the top three (one thread per d and 4 samples, one atomic pair)
+__global__ void __launch_bounds__(256) nested_count_kernel(const int* __restrict__ gt, int X, int B, int D,
+                                                           int* __restrict__ counts) {
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= D) return;
+  const int b0 = blockIdx.y * 4;
+  int top1 = 0, top3 = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int b = b0 + q;
+    if (b < B) {
+      int r = 0;
+      for (int x = 0; x < X; ++x) r += gt[((size_t)x * B + b) * D + d];
+      top1 += r == 0;
+      top3 += r < 3;
+    }
+  }
+  if (top1) atomicAdd(&counts[2 * d], top1);
+  if (top3) atomicAdd(&counts[2 * d + 1], top3);
 }
 
 // y[c][r] = x[r][c], bf16, 64x64 LDS tiles
@@ -343,9 +479,28 @@ void launch_prefix_mask(const bf16* x, bf16* y, int B, int D, const int* keep, h
   hipLaunchKernelGGL(prefix_mask_kernel, dim3((int)g), dim3(256), 0, s, x, y, B, D, keep);
 }
 
+void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t* labels, int B, int D, int C,
+                               int* counts, hipStream_t s) {
+  hipLaunchKernelGGL(nested_eval_scalar_kernel, dim3(B), dim3(256), 0, s, feat, W, labels, D, C, counts);
+}
+
+size_t nested_eval_workspace(int B, int D, int C) {
+  return (size_t)B * D * sizeof(float) + (size_t)((C + 255) / 256) * B * D * sizeof(int);
+}
+
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
-                        hipStream_t s) {
-  hipLaunchKernelGGL(nested_eval_kernel, dim3(B), dim3(256), 0, s, feat, W, labels, D, C, counts);
+                        void* ws, hipStream_t s) {
+  // 2 samples per workgroup: ~2,300 waves at the reference's val batch of 128 (the per-dimension
+  // fma -> ballot -> popcount chain is latency-bound below a few waves per SIMD; the weight
+  // matrix is re-read per sample pair from L2 / the Infinity Cache)
+  constexpr int NB = 2;
+  float* L = (float*)ws;
+  int* gt = (int*)((char*)ws + (size_t)B * D * sizeof(float));
+  const int X = (C + 255) / 256;
+  hipLaunchKernelGGL(nested_label_prefix_kernel, dim3(B), dim3(64), 0, s, feat, W, labels, D, C, L);
+  hipLaunchKernelGGL(nested_rank_kernel<NB>, dim3(X, (B + NB - 1) / NB), dim3(256), 0, s, feat, W, labels, L, B, D, C,
+                     gt);
+  hipLaunchKernelGGL(nested_count_kernel, dim3((D + 255) / 256, (B + 3) / 4), dim3(256), 0, s, gt, X, B, D, counts);
 }
 
 

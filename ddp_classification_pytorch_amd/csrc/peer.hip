@@ -1,0 +1,101 @@
+// One-shot peer-memory exchange for the SyncBN statistics.
+//
+// SyncBN issues one small blocking collective per BN layer and direction (49 all-gathers of
+// (n, mean, M2) forward, 49 all-reduces of (sum g, sum g * xhat) backward per ResNet-50 step):
+// 0.5-16 KB each, on the critical path, latency-bound.  Through RCCL each costs a collective
+// launch plus its protocol round trips (17 us at world size 1 on MI355X).  Here every rank owns
+// one "mailbox" buffer in its own HBM, mapped into every other rank's address space (HIP IPC,
+// parallel/peer.py), and one single-workgroup kernel per exchange:
+//   1. bumps the rank's device-side epoch e (so HIP-graph replays advance it too);
+//   2. stores its n floats into slot [e & 1][rank] of EVERY rank's mailbox (remote stores over
+//      xGMI; system-scope write-through stores, so nothing stays in this XCD's L2);
+//   3. after every storing wave drained its stores and a system-scope release, sets flag[rank] = e
+//      in every mailbox;
+//   4. polls its own mailbox's flags until every rank's is >= e (system-scope loads, s_sleep
+//      between polls, bounded: after ~0.5 s it records an error and stops waiting);
+//   5. after a system-scope acquire, reads the world slots [e & 1][*] (system-scope loads) and
+//      writes them out gathered ([world][n]) or summed in rank order ([n]; identical on every rank).
+// Slots alternate by epoch parity: a rank can be at most one exchange ahead of the slowest (it
+// needs everyone's flag for e before it starts e + 1), so its e + 1 stores never land in the
+// parity a slower rank is still reading for e.
+#include "common.cuh"
+#include "launchers.h"
+
+namespace dcp {
+
+namespace {
+constexpr int kPeerMaxWorld = 64;
+constexpr int kPeerSpinLimit = 1 << 23;  // s_sleep polls before giving up (~0.5 s)
+}  // namespace
+
+// mailbox layout (floats): [2 parities][world][slot] data, then flags (int) [world]
+__global__ void __launch_bounds__(1024) peer_exchange_kernel(const float* __restrict__ src, int n,
+                                                             float* __restrict__ dst, const int64_t* __restrict__ boxes,
+                                                             int* __restrict__ epoch, int rank, int world, int slot,
+                                                             int mode, int* __restrict__ err) {
+  __shared__ int e_sh;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const int e = *epoch + 1;
+    *epoch = e;
+    e_sh = e;
+  }
+  __syncthreads();
+  const int e = e_sh, par = e & 1;
+  const size_t flags_off = (size_t)2 * world * slot;
+  // 2. push this rank's data into every mailbox
+  for (int r = 0; r < world; ++r) {
+    float* box = reinterpret_cast<float*>(boxes[r]);
+    float* dstslot = box + ((size_t)par * world + rank) * slot;
+    for (int i = tid; i < n; i += blockDim.x)
+      __hip_atomic_store(dstslot + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  // 3. publish: one lane per mailbox
+  if (tid < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* flags = reinterpret_cast<int*>(reinterpret_cast<float*>(boxes[tid]) + flags_off);
+    __hip_atomic_store(flags + rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 4. wait for every rank's flag in this rank's own mailbox
+  if (tid < world) {
+    int* flags = reinterpret_cast<int*>(reinterpret_cast<float*>(boxes[rank]) + flags_off);
+    int spins = 0;
+    while (__hip_atomic_load(flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      if (++spins > kPeerSpinLimit) {
+        atomicOr(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  // 5. gather / rank-ordered sum
+  const float* mine = reinterpret_cast<const float*>(boxes[rank]) + (size_t)par * world * slot;
+  if (mode == 0) {
+    for (int i = tid; i < world * n; i += blockDim.x) {
+      const int r = i / n, j = i - r * n;
+      dst[i] = __hip_atomic_load(mine + (size_t)r * slot + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  } else {
+    for (int j = tid; j < n; j += blockDim.x) {
+      float acc = 0.f;
+      for (int r = 0; r < world; ++r)
+        acc += __hip_atomic_load(mine + (size_t)r * slot + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      dst[j] = acc;
+    }
+  }
+}
+
+bool launch_peer_exchange(const float* src, int n, float* dst, const int64_t* boxes, int* epoch, int rank, int world,
+                          int slot, int mode, int* err, hipStream_t s) {
+  if (world < 1 || world > kPeerMaxWorld || n > slot || rank < 0 || rank >= world) return false;
+  hipLaunchKernelGGL(peer_exchange_kernel, dim3(1), dim3(1024), 0, s, src, n, dst, boxes, epoch, rank, world, slot,
+                     mode, err);
+  return true;
+}
+
+}  // namespace dcp

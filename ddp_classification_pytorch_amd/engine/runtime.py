@@ -35,6 +35,8 @@ def setup(args) -> Runtime:
     backend = args.dist_backend or ("nccl" if want_cuda else "gloo")
     if getattr(args, "graph", False):
         graph_safe_nccl_env()
+    if getattr(args, "syncbn_transport", None):
+        os.environ["DCP_SYNCBN_TRANSPORT"] = args.syncbn_transport  # read by convert_sync_batchnorm
     rank, local, world = init_distributed(backend, force=getattr(args, "force_ddp", False))
     if want_cuda:
         torch.cuda.set_device(local)

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 from torch.autograd import Function
 
 from .. import _ext
+from ..parallel import peer as _peer
 from . import _ref
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "leaky_relu": 2, None: 0}
@@ -540,7 +541,7 @@ def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
         return (*k.bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
     st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
     gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
-    dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+    _peer.all_gather_into_tensor(gathered, st, cfg.group)
     _check_equal_counts(gathered, count)
     # the forward merge is exact for any counts; the backward normaliser assumes equal per-rank
     # batches (the sharded sampler pads every rank to the same length; parallel/ddp.py)
@@ -615,7 +616,7 @@ class _BNAct(Function):
                 sums = local
                 if cfg.training_stats and cfg.group is not None:
                     sums = local.clone()
-                    dist.all_reduce(sums, group=cfg.group)
+                    _peer.all_reduce(sums, cfg.group)
             dx, _ = k.bn_bwd_elemt(dy, y, None, scale, shift, beta.detach().float(), rgamma,
                                    sums if cfg.training_stats else None, float(ctx.count), cfg.act, cfg.slope, False,
                                    True)
@@ -628,7 +629,7 @@ class _BNAct(Function):
             sums = local
             if cfg.group is not None:
                 sums = local.clone()
-                dist.all_reduce(sums, group=cfg.group)
+                _peer.all_reduce(sums, cfg.group)
             # ReLU / identity: g is already masked; leaky: g is raw and the elementwise pass applies act'
             post_act = cfg.act if cfg.act == 2 else 0
             dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), post_act,
@@ -643,7 +644,7 @@ class _BNAct(Function):
                 sums = local
                 if cfg.training_stats and cfg.group is not None:
                     sums = local.clone()
-                    dist.all_reduce(sums, group=cfg.group)
+                    _peer.all_reduce(sums, cfg.group)
             dx, dres = k.bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums if cfg.training_stats else None,
                                       float(ctx.count), cfg.act, cfg.slope, want_dres)
             if not want_dres:
@@ -728,7 +729,7 @@ class _BNReluConv1x1(Function):
                 sums = local
                 if cfg.training_stats and cfg.group is not None:
                     sums = local.clone()
-                    dist.all_reduce(sums, group=cfg.group)
+                    _peer.all_reduce(sums, cfg.group)
             dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums if cfg.training_stats else None,
                                    float(ctx.count), 1, 0.0, False)
             dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
@@ -765,7 +766,7 @@ def _bn_backward(k, g, x, scale, shift, mean, invstd, count, cfg: BNConfig, need
         sums = local
         if cfg.training_stats and cfg.group is not None:
             sums = local.clone()
-            dist.all_reduce(sums, group=cfg.group)
+            _peer.all_reduce(sums, cfg.group)
     dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums if cfg.training_stats else None,
                            float(count), 0, cfg.slope, False)
     return dx, local
@@ -787,7 +788,7 @@ class _BNAddBNAct(Function):
             C = x.shape[-1]
             st = torch.cat([k.bn_stats(x, slabs), k.bn_stats(r, rslabs)], dim=2)
             gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
-            dist.all_gather_into_tensor(gathered, st, group=cfg.group)
+            _peer.all_gather_into_tensor(gathered, st, cfg.group)
             _check_equal_counts(gathered, x.numel() // C)
             count = rcount = (x.numel() // C) * cfg.world
             mean, invstd, scale, shift = k.bn_finalize(gathered[..., :C].contiguous(), gamma, beta, run_mean, run_var,
@@ -827,7 +828,7 @@ class _BNAddBNAct(Function):
                 sums, rsums = local, rlocal
                 if cfg.group is not None:
                     both = torch.cat([local, rlocal], dim=1)
-                    dist.all_reduce(both, group=cfg.group)
+                    _peer.all_reduce(both, cfg.group)
                     C = local.shape[1]
                     sums, rsums = both[:, :C].contiguous(), both[:, C:].contiguous()
                 dx, dr = k.bn2_bwd_elemt(g, x, r, scale, mean, invstd, sums, rscale, rmean, rinvstd, rsums,
@@ -841,7 +842,7 @@ class _BNAddBNAct(Function):
             sums = local
             if cfg.group is not None:
                 sums = local.clone()
-                dist.all_reduce(sums, group=cfg.group)
+                _peer.all_reduce(sums, cfg.group)
             dx, _ = k.bn_bwd_elemt(g, x, None, scale, shift, mean, invstd, sums, float(ctx.count), 0, cfg.slope,
                                    False)
         else:
@@ -853,7 +854,7 @@ class _BNAddBNAct(Function):
                 sums = local
                 if cfg.training_stats and cfg.group is not None:
                     sums = local.clone()
-                    dist.all_reduce(sums, group=cfg.group)
+                    _peer.all_reduce(sums, cfg.group)
             dx, g = k.bn_bwd_elemt(dy, x, rv, scale, shift, mean, invstd, sums if cfg.training_stats else None,
                                    float(ctx.count), cfg.act, cfg.slope, True)
         dr, rlocal = None, None
@@ -1065,7 +1066,7 @@ class _BNActPool(Function):
         sums = local
         if cfg.group is not None:
             sums = local.clone()
-            dist.all_reduce(sums, group=cfg.group)
+            _peer.all_reduce(sums, cfg.group)
         dx = k.maxpool_bn_bwd_elemt(dy, idx, x, scale, shift, mean, invstd, cfg.act, sums, float(ctx.count),
                                     *ctx.pool)
         dgamma = local[1] if ctx.needs_input_grad[2] else None
@@ -1531,7 +1532,7 @@ class _StemBNPool(Function):
         sums = local
         if cfg.group is not None:
             sums = local.clone()
-            dist.all_reduce(sums, group=cfg.group)
+            _peer.all_reduce(sums, cfg.group)
         dw = None
         if ctx.needs_input_grad[1]:  # the 4x4 s2d weight gradient, onto the 7x7 master
             dw = k.s2d_weight_bwd(k.stem_bwd_dw(tot, sums, scale, invstd, float(ctx.count)), ctx.c7)

@@ -91,13 +91,26 @@ def bn_process_group():
     return g
 
 
-def convert_sync_batchnorm(model: nn.Module, process_group=None) -> nn.Module:
+def convert_sync_batchnorm(model: nn.Module, process_group=None, transport: str = None) -> nn.Module:
     """Attach a process group to every fused BatchNorm2d (in place); by default the dedicated
-    SyncBN group (:func:`bn_process_group`), not the group the DDP Reducer all-reduces on."""
+    SyncBN group (:func:`bn_process_group`), not the group the DDP Reducer all-reduces on.
+    ``transport``: "rccl" (default; ``DCP_SYNCBN_TRANSPORT``) or "peer" -- the statistics
+    collectives through the IPC-mapped mailboxes of :mod:`parallel.peer` (one kernel per exchange,
+    collective setup; falls back to RCCL where a peer cannot be mapped)."""
     group = process_group if process_group is not None else bn_process_group()
     for m in model.modules():
         if isinstance(m, BatchNorm2d):
             m.process_group = group
+    transport = transport or os.environ.get("DCP_SYNCBN_TRANSPORT", "rccl")
+    if transport not in ("rccl", "peer"):
+        raise ValueError(f"unknown SyncBN transport {transport!r} (rccl | peer)")
+    if group is not None and torch.cuda.is_available():
+        from . import peer
+
+        if transport == "peer":
+            peer.enable(group)
+        else:
+            peer.disable(group)
     return model
 
 

@@ -144,8 +144,9 @@ def test_rccl_world1_ddp_step(engine):
         assert err < 2e-2, (n, float(err))
 
 
-def _worker(rank, world, port, syncbn, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+def _worker(rank, world, port, syncbn, out_dir, transport="rccl"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      DCP_SYNCBN_TRANSPORT=transport)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sys.path.insert(0, ROOT)
     from ddp_classification_pytorch_amd.models import build_model
@@ -173,13 +174,15 @@ def _worker(rank, world, port, syncbn, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("syncbn", [False, True])
-def test_ddp_two_ranks_matches_full_batch(syncbn):
+@pytest.mark.parametrize("syncbn,transport", [(False, "rccl"), (True, "rccl"), (True, "peer")])
+def test_ddp_two_ranks_matches_full_batch(syncbn, transport):
+    """(transport "peer": the SyncBN statistics through the IPC-mapped mailboxes of
+    parallel/peer.py, the two ranks' processes sharing the one GPU)"""
     from ddp_classification_pytorch_amd.models import build_model
     from ddp_classification_pytorch_amd.ops import functional as Fn
 
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), syncbn, d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), syncbn, d, transport), nprocs=2, join=True)
         got = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(1)
@@ -395,3 +398,65 @@ def test_bench_diagnostic_phase_failure_keeps_headline(inject):
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["syncbn_value"] is None
     errs = rec["diagnostic_errors"]
     assert ("syncbn" in errs) if inject == "syncbn" else ("deadline" in errs or "syncbn" in errs), errs
+
+
+def _peer_worker(rank, world, port, out_dir):
+    """PeerExchange between processes sharing the GPU: gathers and rank-ordered sums of
+    integer-valued floats (exact) against gloo's collectives, sizes from 1 float to a full slot,
+    many back-to-back exchanges (the epoch-parity mailboxes), and a HIP graph of exchanges
+    replayed (the device-side epoch advances per replay)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    from ddp_classification_pytorch_amd.parallel import peer
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ex = peer.enable(dist.group.WORLD, dev)
+    assert ex is not None and ex.world == world and ex.rank == rank
+    errs = []
+    g = torch.Generator().manual_seed(100 + rank)
+    for it, n in enumerate([1, 7, 192, 6144, peer.MAX_FLOATS] * 4):
+        x = torch.randint(-50, 50, (n,), generator=g).float()
+        ref_g = [torch.empty_like(x) for _ in range(world)]
+        dist.all_gather(ref_g, x)
+        ref_r = x.clone()
+        dist.all_reduce(ref_r)
+        out = torch.empty(world * n, device=dev)
+        ex.all_gather_into_tensor(out, x.to(dev))
+        red = x.to(dev)
+        ex.all_reduce(red)
+        if not torch.equal(out.cpu(), torch.cat(ref_g)):
+            errs.append(("gather", it, n))
+        if not torch.equal(red.cpu(), ref_r):
+            errs.append(("reduce", it, n))
+    # captured exchanges: 3 per replay, 5 replays; the inputs change between replays
+    src = torch.zeros(64, device=dev)
+    outs = [torch.empty(world * 64, device=dev) for _ in range(3)]
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        for o in outs:
+            ex.all_gather_into_tensor(o, src)
+            src.add_(1.0)
+    for rep in range(5):
+        src.fill_(1000.0 * rank + 10.0 * rep)
+        graph.replay()
+        torch.cuda.synchronize()
+        for j, o in enumerate(outs):
+            want = torch.cat([torch.full((64,), 1000.0 * r + 10.0 * rep + j) for r in range(world)])
+            if not torch.equal(o.cpu(), want):
+                errs.append(("graph", rep, j))
+    ex.check()
+    torch.save({"errs": errs, "epoch": int(ex.epoch.item())}, os.path.join(out_dir, f"peer{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_syncbn_peer_exchange_matches_gloo():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_peer_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        res = [torch.load(os.path.join(d, f"peer{r}.pt"), weights_only=True) for r in range(2)]
+    for r in res:
+        assert r["errs"] == [], r["errs"]
+        assert r["epoch"] == 2 * 20 + 3 * 5  # every exchange (eager and replayed) advanced the epoch

@@ -348,6 +348,26 @@ def test_nested_eval_counts(K):
     cnt = K.nested_eval(f.to(DEV), W.to(DEV), lab.to(DEV))
     ref = _ref.nested_eval(f, W, lab)
     assert torch.equal(cnt.cpu(), ref)
+    assert torch.equal(K.nested_eval_scalar(f.to(DEV), W.to(DEV), lab.to(DEV)).cpu(), ref)
+
+
+@pytest.mark.parametrize("B,D,C", [(128, 2048, 2173), (37, 300, 70), (8, 65, 257), (130, 129, 4500)])
+def test_nested_eval_fast_matches_scalar(K, B, D, C):
+    """K19: the rank-ballot TestNested path counts exactly what the one-workgroup-per-sample kernel
+    counts (identical fp32 fma chains), on the reference's shape (val batch 128, 2048 features,
+    2173 classes), ragged sample / dimension / class counts, and C past the scalar kernel's 4096
+    limit against the fp32 CPU reference; ReLU-like features with exact zeros included."""
+    torch.manual_seed(1)
+    f = torch.relu(torch.randn(B, D)).to(DEV)
+    W = (torch.randn(D, C) * 0.05).to(DEV)
+    lab = torch.randint(0, C, (B,)).to(DEV)
+    fast = K.nested_eval(f, W, lab)
+    if C <= 4096:
+        assert torch.equal(fast, K.nested_eval_scalar(f, W, lab))
+    else:
+        ref = _ref.nested_eval(f.cpu()[:, :64], W.cpu()[:64], lab.cpu())
+        assert (fast.cpu()[:64] - ref).abs().max().item() <= 1  # fma vs mul+add rounding: near-ties only
+    assert fast[:, 0].le(fast[:, 1]).all() and fast.max().item() <= B
 
 
 @pytest.mark.parametrize("Ci,Co,k,s", [(256, 64, 1, 1), (64, 128, 3, 1), (128, 64, 3, 2)])
@@ -1114,11 +1134,12 @@ def test_adaptive_avg_pool_kernels(K):
                                    (3, 9, 11, 128, 128, 3, 1, 1), (1, 13, 13, 256, 384, 3, 2, 1),
                                    (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1)])
 @pytest.mark.parametrize("mode", [1, 3])
-@pytest.mark.parametrize("cvar", [0, 2, 3])
+@pytest.mark.parametrize("cvar", [0, 1, 2, 3])
 def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
     """The 8-wave 256 x 256 (tg_big = 1; 256 x 128 below 256 channels) and 4-wave 256 x 128
-    (tg_big = 3) big-tile tap GEMMs, fragments read across the barrier, after it (tg_big_cvar = 2)
-    or in the ping-pong schedule (tg_big_cvar = 3: 8-wave tiles only; the others ignore it), == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
+    (tg_big = 3) big-tile tap GEMMs under every schedule: the 8-wave tile's default ping-pong
+    (tg_big_cvar = 0 / 3), fragments read across the barrier in lockstep (1; the 4-wave tile's
+    default) or after it (2), == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
     M: quadrants past M write no slab) and the data gradient (stride 1 and the stride-2 parity
     classes), channel counts that are not a multiple of the tile."""
     N, H, W, Ci, Co, k, s, p = shape

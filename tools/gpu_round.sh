@@ -56,6 +56,28 @@ for step in "$@"; do
       tail -1 $O/ddp1_b1024.log
       timeout -k 10 300 python -u bench.py --force-ddp --batch 128 --grad-comm bf16 --steps 30 --warmup 5 > $O/ddp1_b128bf16.log 2>&1
       tail -1 $O/ddp1_b128bf16.log ;;
+    refcfg)
+      # the reference's own configurations (BASELINE/main.py:29-30,148; ARCFACE/arc_main.py:38,69-73,
+      # arc_train_hpc.sh:3): small per-GPU batches, HIP graph and eager, local BN and world-1 RCCL SyncBN
+      run_ref() {  # tag, bench args...
+        local t=$1; shift
+        timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 "$@" > $O/ref_$t.log 2>&1
+        echo "$t $(tail -1 $O/ref_$t.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r["ms_per_step"], r.get("syncbn_value"), r.get("syncbn_ms_per_step"))')"
+      }
+      run_ref tresnet_b16_graph --config tresnet --batch 16 --graph
+      run_ref tresnet_b16_eager --config tresnet --batch 16 --eager
+      run_ref tresnet_b16_ddp1_graph --config tresnet --batch 16 --force-ddp --graph
+      run_ref tresnet_b16_ddp1_eager --config tresnet --batch 16 --force-ddp --eager
+      for b in 16 32 64; do
+        run_ref r50_b${b}_graph --batch $b --graph
+        run_ref r50_b${b}_eager --batch $b --eager
+        run_ref r50_b${b}_ddp1_graph --batch $b --force-ddp --graph
+      done
+      for b in 32 64; do
+        run_ref arc256_b${b}_graph --config arcface --image-size 256 --batch $b --graph
+        run_ref arc256_b${b}_eager --config arcface --image-size 256 --batch $b --eager
+        run_ref arc256_b${b}_ddp1_graph --config arcface --image-size 256 --batch $b --force-ddp --graph
+      done ;;
     convabs=*)
       # convabs=IDX,IDX:CFGS -- the same A/B on a subset of the R50 shapes (conv_bench.py R50 indices)
       v=${step#convabs=}; only=${v%%:*}; c=${v#*:}
