@@ -471,9 +471,18 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
   }
   auto dx = at::empty({N, H, W, C}, bf16_like(dy));
   const bf16* addp = nullptr;
+  int add_s2 = 0, add_hc = 0, add_wc = 0;
   if (add.has_value()) {
     CHECK_ACT(*add);
-    TORCH_CHECK(add->sizes() == dx.sizes(), "conv_dgrad_bn add shape");
+    if (add->sizes() != dx.sizes()) {
+      // a compact stride-2 gradient: the even (y, x) pixels of dx only (StridedGrad)
+      add_hc = (H + 1) / 2;
+      add_wc = (W + 1) / 2;
+      TORCH_CHECK(add->dim() == 4 && add->size(0) == N && add->size(1) == add_hc && add->size(2) == add_wc &&
+                      add->size(3) == C,
+                  "conv_dgrad_bn add shape: [N,H,W,C] or the stride-2 subgrid [N,ceil(H/2),ceil(W/2),C]");
+      add_s2 = 1;
+    }
     addp = bp(*add);
   }
   const bf16* resp = nullptr;
@@ -506,7 +515,8 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(const Tensor& dy, const Tensor& wt, int
       t.widx[i] = i;
     }
   dcp::BnBwdEpi e{bp(y), resp, scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
-                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act, maskp, (float)slope};
+                  invstd.data_ptr<float>(), part.data_ptr<float>(), (int)act, maskp, (float)slope, add_s2, add_hc,
+                  add_wc};
   auto st = cur_stream();
   dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, H, W, 1, 1, 0, 0, t, nullptr, nullptr,
                        0, zero_page(dy.get_device()), st, addp, &e);

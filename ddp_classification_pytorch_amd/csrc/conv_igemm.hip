@@ -609,7 +609,21 @@ tap_gemm_kernel(const TapGemmParams p) {
         const size_t off = (size_t)(ok ? m : 0) * p.Co + (cok ? cg : 0);
         yv[q] = ok ? *(const bf16x8*)(p.bnb.y + off) : bf16x8{};
         if (has_res) rv[q] = ok ? *(const bf16x8*)(p.bnb.res + off) : bf16x8{};
-        if (has_add) av[q] = ok ? *(const bf16x8*)(p.addsrc + off) : bf16x8{};
+        if (has_add) {
+          if (p.bnb.add_s2 == 0) {
+            av[q] = ok ? *(const bf16x8*)(p.addsrc + off) : bf16x8{};
+          } else {
+            // compact stride-2 add source: only even (y, x) pixels carry a gradient
+            const uint32_t mm = ok ? (uint32_t)m : 0u;
+            const uint32_t qq = fdiv(mm, p.div_wy);
+            const uint32_t xx = mm - qq * p.Wy;
+            const uint32_t nn = fdiv(qq, p.div_hy);
+            const uint32_t yy = qq - nn * p.Hy;
+            const bool on = ok && !(yy & 1u) && !(xx & 1u);
+            const size_t co = ((size_t)(nn * p.bnb.add_hc + (yy >> 1)) * p.bnb.add_wc + (xx >> 1)) * p.Co + cg;
+            av[q] = on ? *(const bf16x8*)(p.addsrc + co) : bf16x8{};
+          }
+        }
         if (MASKED) mk[q] = ok ? p.bnb.mask[off >> 3] : 0u;
       }
       if (b == 0) __syncthreads();
@@ -1547,7 +1561,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
     fprintf(stderr, "launch_tap_gemm: the folded BN epilogue is a plain forward store\n");
     abort();
   }
-  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0.f};
+  p.bnb = bnb ? *bnb : BnBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0.f, 0, 0, 0};
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hy = Hy; p.Wy = Wy; p.ss = ss;
   p.Hd = Hd; p.Wd = Wd; p.ds = ds; p.oy = oy; p.ox = ox;

@@ -36,6 +36,11 @@ struct BnBwdEpi {
   int act;              // 0 none, 1 ReLU (gradient stored masked), 2 leaky ReLU (stored RAW, summed masked)
   const uint8_t* mask;  // act'(z) > 0 as bits [M][C/8] (bn_act's mask output), or nullptr: recompute z
   float slope;          // leaky slope (act 2)
+  // addsrc on the stride-2 subgrid only: [N][add_hc][add_wc][C] holds the gradient of the even
+  // (y, x) pixels, zero elsewhere -- a projection block's 1x1 / stride-2 downsample dgrad, deposited
+  // compact instead of as a mostly-zero full-size tensor (ops/functional.py StridedGrad)
+  int add_s2;
+  int add_hc, add_wc;
 };
 
 // Eval-mode BN folded into the forward conv's store epilogue (running statistics: model.eval(),

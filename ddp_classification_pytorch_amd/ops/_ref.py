@@ -72,6 +72,10 @@ def conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, act, mas
     return g' itself (masking is idempotent); leaky ReLU returns the RAW dgrad (its BN backward
     re-applies act', so any other consumer's gradient can still be added).  ``mask``: the
     activation mask bits from :func:`bn_act_mask` (then ``res`` is not read)."""
+    if add is not None and add.shape != y.shape:  # compact stride-2 add source (StridedGrad)
+        full = add.new_zeros(y.shape)
+        full[:, ::2, ::2] = add
+        add = full
     g = conv_dgrad(dy, wt, y.shape[1], y.shape[2], 1, pad, add)
     if mask is not None:
         d = unpack_mask(mask) if act == ACT_RELU else torch.ones_like(_f(y))

@@ -206,19 +206,56 @@ class GradJoin:
         self.grad, self.expected, self.arrived, self.closed = None, secondaries, 0, False
 
     def deposit(self, g):
-        if self.closed or g is None:
+        if g is None:
             return g
-        self.grad = g if self.grad is None else self.grad + g
+        if self.closed:
+            return g.full() if isinstance(g, StridedGrad) else g
+        if self.grad is None:
+            self.grad = g
+        else:
+            a = self.grad.full() if isinstance(self.grad, StridedGrad) else self.grad
+            self.grad = a + (g.full() if isinstance(g, StridedGrad) else g)
         self.arrived += 1
         return None
 
-    def claim(self):
+    def claim(self, strided_ok: bool = False):
+        """(summed deposits, all secondaries arrived).  A compact :class:`StridedGrad` is returned
+        as such only to a caller that adds it itself (``strided_ok``), expanded otherwise."""
         self.closed = True
         g, self.grad = self.grad, None
+        if isinstance(g, StridedGrad) and not strided_ok:
+            g = g.full()
         return g, self.arrived >= self.expected
 
 
+class StridedGrad:
+    """The input gradient of a 1x1 / stride-2 / pad-0 conv (a projection block's downsample), kept
+    compact: ``compact`` [N, ceil(H/2), ceil(W/2), C] holds the gradient of the even (y, x) pixels
+    of the [N, H, W, C] input; every other pixel's is zero.  Computing it is a stride-1 1x1 GEMM
+    over the output grid (no parity classes, no zero tiles), and the block's first conv adds it in
+    its dgrad epilogue reading a quarter of the bytes (``conv_dgrad_bn``'s stride-2 add source)
+    instead of a full-size, 3/4-zero tensor written and read back through HBM."""
+
+    __slots__ = ("compact", "H", "W")
+
+    def __init__(self, compact, H, W):
+        self.compact, self.H, self.W = compact, H, W
+
+    def full(self):
+        N, _, _, C = self.compact.shape
+        out = self.compact.new_zeros((N, self.H, self.W, C))
+        out[:, ::2, ::2, :] = self.compact
+        return out
+
+
 ResidualLink = GradJoin  # identity-block residual hand-off (one secondary: the last BN's residual)
+
+# DCP_STRIDED_DEPOSIT=0: the downsample conv's input gradient as a full-size tensor (A/B)
+_STRIDED_DEPOSIT = [os.environ.get("DCP_STRIDED_DEPOSIT", "1") != "0"]
+
+
+def set_strided_deposit(enabled: bool):
+    _STRIDED_DEPOSIT[0] = bool(enabled)
 
 
 class BNSource:
@@ -365,9 +402,14 @@ class _Conv2d(Function):
         dy = dy.contiguous()
         k = K(dy)
         add, complete = None, True
+        src = ctx.bnsrc
+        fuse = (ctx.needs_input_grad[0] and src is not None and stride == 1 and src.tensors is not None)
         if ctx.link is not None:
-            add, complete = ctx.link.claim()
-            if add is not None:
+            # a compact stride-2 deposit is added by the fused BN-backward epilogue itself
+            add, complete = ctx.link.claim(strided_ok=fuse)
+            if isinstance(add, StridedGrad) and not complete:
+                add = add.full()
+            if add is not None and not isinstance(add, StridedGrad):
                 add = add.contiguous()
         dx = dw = None
         side = _WgradOnSide(dy)
@@ -375,20 +417,30 @@ class _Conv2d(Function):
             with side:
                 dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
         if ctx.needs_input_grad[0]:
-            src = ctx.bnsrc
-            if src is not None and complete and stride == 1 and src.tensors is not None:
+            if fuse and complete:
                 y, res, scale, shift, mean, invstd, mask = src.tensors
                 if mask is not None:
                     res = None  # the activation mask bits replace the residual read
-                dx, sums = k.conv_dgrad_bn(dy, wt, pad, add, y, res, scale, shift, mean, invstd, src.act, mask,
+                a = add.compact.contiguous() if isinstance(add, StridedGrad) else add
+                dx, sums = k.conv_dgrad_bn(dy, wt, pad, a, y, res, scale, shift, mean, invstd, src.act, mask,
                                            src.slope)
                 src.fused = (dx, sums)
-            elif add is not None:
-                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add)
             else:
-                dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
+                if isinstance(add, StridedGrad):
+                    add = add.full()
+                if (ctx.deposit is not None and stride == 2 and KH == 1 and KW == 1 and pad == 0
+                        and _STRIDED_DEPOSIT[0]):
+                    # projection downsample: the compact subgrid gradient (a stride-1 1x1 GEMM over
+                    # dY's grid), added on the subgrid by the block's first conv (StridedGrad)
+                    dx = StridedGrad(k.conv_dgrad(dy, wt, dy.shape[1], dy.shape[2], 1, 0), x.shape[1], x.shape[2])
+                elif add is not None:
+                    dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad, add)
+                else:
+                    dx = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], stride, pad)
             if ctx.deposit is not None:
                 dx = ctx.deposit.deposit(dx)
+            if isinstance(dx, StridedGrad):  # handed back to autograd: materialise
+                dx = dx.full()
         if ctx.needs_input_grad[1] and not side.on:
             dw = k.conv_wgrad(dy, x, KH, KW, stride, pad)
         side.join()

@@ -1280,3 +1280,56 @@ def test_conv_fwd_256_channel_tiles(K, shape):
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-4
     yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
     assert relerr(y1, yr) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C,Co,mask", [(2, 14, 256, 64, True), (3, 7, 512, 128, False), (2, 9, 64, 64, True)])
+def test_conv_dgrad_bn_strided_add(K, N, H, C, Co, mask):
+    """conv_dgrad_bn with a compact stride-2 add source (a projection block's downsample gradient,
+    StridedGrad) == the same call with that source expanded to full size (zeros off the even
+    pixels), odd H included."""
+    torch.manual_seed(0)
+    dy = rnd(N, H, H, Co).to(DEV)
+    w = rnd(Co, 1, 1, C, scale=1.0 / math.sqrt(C)).to(DEV)
+    _, wt = K.weight_prep(w.float(), 0, True)
+    y = rnd(N, H, H, C).to(DEV)
+    res = rnd(N, H, H, C).to(DEV)
+    scale, shift = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    mean, invstd = torch.randn(C).to(DEV), (torch.rand(C) + 0.5).to(DEV)
+    hc = (H + 1) // 2
+    compact = rnd(N, hc, hc, C).to(DEV)
+    full = torch.zeros(N, H, H, C, dtype=compact.dtype, device=DEV)
+    full[:, ::2, ::2] = compact
+    m = None
+    if mask:
+        _, m = K.bn_act_mask(y, res, scale, shift, 1, 0.0)
+    r = None if mask else res
+    d0, s0 = K.conv_dgrad_bn(dy, wt, 0, full, y, r, scale, shift, mean, invstd, 1, m, 0.0)
+    d1, s1 = K.conv_dgrad_bn(dy, wt, 0, compact, y, r, scale, shift, mean, invstd, 1, m, 0.0)
+    assert torch.equal(d0, d1) and torch.equal(s0, s1)
+
+
+def test_resnet50_strided_deposit_same_gradients(K):
+    """ResNet-50 training step with the downsample convs' input gradients deposited compact
+    (StridedGrad, default) == with them as full-size tensors: loss and every parameter gradient."""
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    g = torch.Generator().manual_seed(3)
+    imgs = torch.randint(0, 256, (4, 3, 64, 64), dtype=torch.uint8, generator=g).to(DEV)
+    labels = torch.randint(0, 10, (4,), generator=g).to(DEV)
+    res = {}
+    try:
+        for on in (False, True):
+            Fn.set_strided_deposit(on)
+            torch.manual_seed(0)
+            m = build_model("resnet50", num_classes=10).to(DEV)
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), nchw=True, in_scale=1 / 255.0,
+                                  **input_layout(m))
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+            res[on] = (loss.item(), {n: p.grad.detach().float().cpu() for n, p in m.named_parameters()})
+    finally:
+        Fn.set_strided_deposit(True)
+    assert res[False][0] == res[True][0]
+    for n, g0 in res[False][1].items():
+        assert relerr(res[True][1][n], g0) < 1e-5, n
