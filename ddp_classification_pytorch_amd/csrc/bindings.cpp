@@ -32,6 +32,23 @@ namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
+// fork / join events of the parity-class streams (conv_dgrad stride 2), one set per device; reused
+// call after call (an event re-recorded after every wait on it was issued, stream-ordered)
+hipEvent_t parity_event(int i) {
+  static std::mutex mu;
+  static std::unordered_map<int, std::vector<hipEvent_t>> pool;
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  auto& v = pool[dev];
+  while ((int)v.size() <= i) {
+    hipEvent_t e;
+    hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    v.push_back(e);
+  }
+  return v[i];
+}
+
 const bf16* bp(const Tensor& t) { return reinterpret_cast<const bf16*>(t.data_ptr()); }
 bf16* bpm(Tensor& t) { return reinterpret_cast<bf16*>(t.data_ptr()); }
 const float* fp(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
@@ -202,6 +219,52 @@ Tensor conv_wgrad_pro(const Tensor& dy, const Tensor& x, const Tensor& scale, co
   dcp::launch_wgrad(bp(dy), N, H, W, Co, bp(x), H, W, C, 1, taps, dw.data_ptr<float>(), part.data_ptr<float>(),
                     zero_page(dy.get_device()), ncu, cur_stream(), scale.data_ptr<float>(), shift.data_ptr<float>());
   return dw;
+}
+
+// conv3x3(relu(x * scale + shift)) for the 64 -> 64 channel stride-1 3x3 (the direct kernel's BN
+// prologue, K5 on a 3x3 consumer): the BN + ReLU is applied once per staged window element
+std::tuple<Tensor, Tensor> conv3x3_fwd_pro(const Tensor& x, const Tensor& w, const Tensor& scale, const Tensor& shift,
+                                           bool stats) {
+  CHECK_ACT(x);
+  CHECK_ACT(w);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), Co = w.size(0);
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C, "conv3x3_fwd_pro: [Co,3,3,C]");
+  TORCH_CHECK(dcp::conv3x3_c64_supported(H, W, C, Co), "conv3x3_fwd_pro: the direct 64-channel 3x3 geometry only");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "conv3x3_fwd_pro: too many pixels");
+  check_pro_vec(scale, C, "conv3x3_fwd_pro scale");
+  check_pro_vec(shift, C, "conv3x3_fwd_pro shift");
+  auto y = at::empty({N, H, W, Co}, bf16_like(x));
+  const int blocks = dcp::conv3x3_c64_blocks(N, H, W, num_cus(x.get_device()));
+  Tensor part = stats ? at::empty({blocks, 3, Co}, f32_like(x)) : at::empty({0}, f32_like(x));
+  dcp::launch_conv3x3_c64(bp(x), bp(w), bpm(y), stats ? part.data_ptr<float>() : nullptr, zero_page(x.get_device()),
+                          N, H, W, blocks, cur_stream(), scale.data_ptr<float>(), shift.data_ptr<float>());
+  return {y, part};
+}
+
+// weight gradient of conv3x3_fwd_pro: the direct 3x3 weight gradient recomputing relu(x * scale +
+// shift) on its staged windows
+Tensor conv3x3_wgrad_pro(const Tensor& dy, const Tensor& x, const Tensor& scale, const Tensor& shift) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  const int N = dy.size(0), H = dy.size(1), W = dy.size(2), Co = dy.size(3), C = x.size(3);
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == H && x.size(2) == W, "conv3x3_wgrad_pro: geometry");
+  check_pro_vec(scale, C, "conv3x3_wgrad_pro scale");
+  check_pro_vec(shift, C, "conv3x3_wgrad_pro shift");
+  TORCH_CHECK((int64_t)N * H * W < (1ll << 31), "conv3x3_wgrad_pro: too many pixels");
+  const int ncu = num_cus(dy.get_device());
+  const int s3 = dcp::wgrad3x3_splits(N, H, W, C, Co, ncu);
+  TORCH_CHECK(s3 > 0, "conv3x3_wgrad_pro: the direct 3x3 weight-gradient geometry only");
+  auto dw = at::empty({Co, 3, 3, C}, f32_like(dy));
+  const auto taps = fwd_taps(3, 3, 1);
+  auto part = at::empty({(int64_t)(s3 + (s3 + 63) / 64) * dw.numel()}, f32_like(dy));
+  dcp::launch_wgrad(bp(dy), N, H, W, Co, bp(x), H, W, C, 1, taps, dw.data_ptr<float>(), part.data_ptr<float>(),
+                    zero_page(dy.get_device()), ncu, cur_stream(), scale.data_ptr<float>(), shift.data_ptr<float>());
+  return dw;
+}
+
+// the direct 3x3 kernels' BN prologue applies (a bottleneck's bn1 -> conv2 at 64 channels)
+bool conv3x3_pro_fits(int64_t N, int64_t H, int64_t W, int64_t C, int64_t Co) {
+  return dcp::conv3x3_c64_supported(H, W, C, Co) && dcp::wgrad3x3_splits(N, H, W, C, Co, 256) > 0;
 }
 
 // backward of act(c * scale + shift [+ r]) from its output y: (dc = g * scale, g = dy * act'(y) or empty)
@@ -419,7 +482,17 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
                          nullptr, 0, z, st, addp);
     return dx;
   }
-  // stride 2: four parity classes of the input grid
+  // stride 2: four parity classes of the input grid.  tg_parity_streams = 1: the classes run
+  // concurrently on four pooled streams (fork / join through events; captured as parallel graph
+  // branches), so one class's short-K tail overlaps the others (A/B)
+  const bool par = dcp::g_tune[dcp::kDgradParityStreams] == 1;
+  hipEvent_t fork_ev = nullptr;
+  std::vector<hipStream_t> side;
+  if (par) {
+    fork_ev = parity_event(0);
+    hipEventRecord(fork_ev, st);
+  }
+  int ncls = 0;
   for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
       const int Hy = (H - ph + 1) / 2, Wy = (W - pw + 1) / 2;
@@ -436,9 +509,21 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
           ++t.n;
         }
       }
+      hipStream_t cs = st;
+      if (par) {
+        cs = at::hip::getStreamFromPool(false, dy.get_device()).stream();
+        hipStreamWaitEvent(cs, fork_ev, 0);
+        side.push_back(cs);
+      }
       dcp::launch_tap_gemm(bp(dy), N, Ho, Wo, Co, bp(wt), C, KH * KW, bpm(dx), H, W, Hy, Wy, 1, 2, ph, pw, t,
-                           nullptr, nullptr, 0, z, st);
+                           nullptr, nullptr, 0, z, cs);
+      ++ncls;
     }
+  for (size_t i = 0; i < side.size(); ++i) {  // join
+    hipEvent_t e = parity_event(1 + (int)i);
+    hipEventRecord(e, side[i]);
+    hipStreamWaitEvent(st, e, 0);
+  }
   if (add.has_value()) dx.add_(*add);
   return dx;
 }
@@ -832,6 +917,17 @@ bool is_partials(const Tensor& t, int C) {
   return t.dim() == 3 && t.size(1) == 3 && t.size(2) == C && t.scalar_type() == at::kFloat;
 }
 
+// many (n, mean, M2) partials (e.g. one per stem workgroup): merged first in chunks of 128 rows
+// (bn_partial_chunk_kernel), so the final merge is short; few: returned as they are
+Tensor chunk_partials(const Tensor& part, int C) {
+  const int P = part.size(0);
+  const int chunks = dcp::bn_partial_chunks(P);
+  if (chunks == 0) return part;
+  auto tmp = at::empty({chunks, 3, C}, part.options());
+  dcp::launch_bn_partial_chunk(part.data_ptr<float>(), P, C, tmp.data_ptr<float>(), cur_stream());
+  return tmp;
+}
+
 // per-channel (n, mean, M2) [1,3,C] from conv slabs or partials (if given) or directly from x
 Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   CHECK_ACT(x);
@@ -841,7 +937,8 @@ Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
   const bool from_slabs = slabs.has_value() && slabs->numel() > 0;
   auto out = at::empty({1, 3, C}, f32_like(x));
   if (from_slabs && is_partials(*slabs, C)) {
-    dcp::launch_bn_merge(slabs->data_ptr<float>(), slabs->size(0), C, out.data_ptr<float>(), cur_stream());
+    const Tensor pr = chunk_partials(*slabs, C);
+    dcp::launch_bn_merge(pr.data_ptr<float>(), pr.size(0), C, out.data_ptr<float>(), cur_stream());
     return out;
   }
   if (from_slabs)
@@ -869,7 +966,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
   auto coef = at::empty({4, C}, f32_like(x));
   float* cp = coef.data_ptr<float>();
   if (from_slabs && is_partials(*slabs, C)) {
-    dcp::launch_bn_merge_finalize(slabs->data_ptr<float>(), slabs->size(0), C, (float)eps, fp(gamma), fp(beta), cp,
+    const Tensor pr = chunk_partials(*slabs, C);
+    dcp::launch_bn_merge_finalize(pr.data_ptr<float>(), pr.size(0), C, (float)eps, fp(gamma), fp(beta), cp,
                                   cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean), fpm(run_var), (float)momentum,
                                   cur_stream());
     return {coef[0], coef[1], coef[2], coef[3]};
@@ -1713,6 +1811,10 @@ TORCH_LIBRARY(dcp, m) {
   m.def("prefix_mask(Tensor x, Tensor keep) -> Tensor", &prefix_mask);
   m.def("nested_eval(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval);
   m.def("enable_peer_access(int peer) -> ()", &enable_peer_access);
+  m.def("conv3x3_fwd_pro(Tensor x, Tensor w, Tensor scale, Tensor shift, bool stats) -> (Tensor, Tensor)",
+        &conv3x3_fwd_pro);
+  m.def("conv3x3_wgrad_pro(Tensor dy, Tensor x, Tensor scale, Tensor shift) -> Tensor", &conv3x3_wgrad_pro);
+  m.def("conv3x3_pro_fits(int N, int H, int W, int C, int Co) -> bool", &conv3x3_pro_fits);
   m.def("peer_exchange(Tensor src, Tensor(a!) dst, Tensor boxes, Tensor(b!) epoch, int rank, int world, int slot, "
         "int mode, Tensor(c!) err) -> ()", &peer_exchange);
   m.def("nested_eval_scalar(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval_scalar);

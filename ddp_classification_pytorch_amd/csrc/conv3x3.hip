@@ -50,12 +50,25 @@ struct C3Params {
   int ablate;        // timing ablations (g_tune[kAblate], direct epilogue only): 1 no stores, 2 no window loads
   int sched;         // g_tune[kC3Variant] = 3: s_setprio 1 for the upper wave half; 4: upper half out of phase
   FastDiv div_wp, div_w, div_spi;
+  // BN prologue (K5 on the 3x3 consumer): the input is a training-mode BN's INPUT, used as
+  // relu(x * pscale[c] + pshift[c]) -- applied ONCE per staged window element (each feeds nine
+  // taps), so the BN + ReLU output of the producing layer is never written.  nullptr: off.
+  const float* pscale;
+  const float* pshift;
 };
 
 __device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
   return wpix * 128u + ((c ^ (wpix & 7u)) << 4);
 }
 }  // namespace
+
+// relu(v * sc + sh) of the 8 bf16 channels of one 16-byte LDS chunk, in place
+__device__ __forceinline__ void bn_relu_chunk_lds(char* at, const float (&sc)[8], const float (&sh)[8]) {
+  bf16x8 v = *LDS_PTR(bf16x8, at);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]) * sc[e] + sh[e], 0.f));  // as bn_act_fwd_kernel
+  *LDS_PTR(bf16x8, at) = v;
+}
 
 // NU (1 or 2) 16-pixel subtiles s0, s0 + 2 of the staged strip: 9 taps x 2 k-halves x NU
 // fragment reads, 36 NU MFMAs, then the bf16 epilogue (statistics, staged 32-byte row stores).
@@ -247,6 +260,18 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
         bw[t][h][n] = *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + t) * 64 + 32 * h + 8 * lg);
 
   if (p.sched == 3 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  // BN prologue: a thread's window chunks all hold the same 8 channels -- chunk qq = tid + k * 64 NW
+  // keeps qq & 7 and (qq >> 3) & 7, so its channel chunk (qq & 7) ^ (pixel & 7) is fixed
+  const bool pro = p.pscale != nullptr;
+  float psc[8], psh[8];
+  if (pro) {
+    const int pc = ((tid & 7) ^ ((tid >> 3) & 7)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      psc[e] = p.pscale[pc + e];
+      psh[e] = p.pshift[pc + e];
+    }
+  }
   float K[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, cnt = 0.f;
   float K4[DE ? 2 : 1][4] = {}, t1[DE ? 2 : 1][4] = {}, t2[DE ? 2 : 1][4] = {};
   bool have_k = false;
@@ -283,6 +308,20 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (p.nbuf == 2 && s + 1 < s_end) load_strip(s + 1, b ^ 1);
+    if (pro) {
+      // BN + ReLU once per staged in-image element (the zero halo / padding stays zero: the conv
+      // pads the BN OUTPUT), then a raw barrier: the next strip's DMA stays in flight
+      char* wb = smem + b * p.wbytes;
+      for (int qq = tid; qq < p.xq; qq += 64 * NW) {
+        const uint32_t P = qq >> 3;
+        const uint32_t rr = fdiv(P, p.div_wp), xx = P - rr * Wp;
+        const int yy = y0 - 1 + (int)rr, xi = (int)xx - 1;
+        if (yy >= 0 && yy < H && xi >= 0 && xi < W) bn_relu_chunk_lds(wb + qq * 16, psc, psh);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     const char* win = smem + b * p.wbytes;
 
     const int nsub = (npix + 15) >> 4;
@@ -422,10 +461,11 @@ int conv3x3_c64_blocks(int N, int H, int W, int num_cu) {
 }
 
 void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
-                        int blocks, hipStream_t stream) {
+                        int blocks, hipStream_t stream, const float* pscale, const float* pshift) {
   const C3Cfg cfg = c3_cfg();
   C3Params p;
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
+  p.pscale = pscale; p.pshift = pshift;
   p.H = H; p.W = W;
   p.ablate = g_tune[kAblate];
   p.sched = g_tune[kC3Variant];

@@ -868,16 +868,43 @@ tap_gemm_big_kernel(const TapGemmParams p) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
+    // The load segment issues its LDS-DMA first and its fragment reads behind it, so the DMA's
+    // address work overlaps the reads' latency.  The tap table sits in one VGPR (lane t = tap t,
+    // read with v_readlane) and the (tap, channel) of the next k-tile to stage advances with
+    // scalar selects: a scalar-memory tap lookup would make the compiler wait lgkmcnt(0) -- for the
+    // fragment reads too -- before every DMA.
+    const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
+    int st_t = (NS - 1) / tiles_per_tap, st_c = ((NS - 1) - st_t * tiles_per_tap) * BK;
+    auto stage_next = [&](int slot) {
+      char* As = smem + slot * STAGE;
+      char* Bs = As + A_BYTES;
+      const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
+      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
+      const long boff = (long)tap_w(tv) * p.Cs + st_c;
+      const uint32_t tbit = 1u << st_t;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+        dma16_tracked(g, As + (wave * AI + i) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
+      st_c += BK;
+      const bool wrap = st_c >= p.Cs;
+      st_t += wrap ? 1 : 0;
+      st_c = wrap ? 0 : st_c;
+    };
     wait_vmcnt(LPT * min(NS - 2, nkt - 1));  // k-tile 0 (this wave's share)
     pp_barrier();                            // ... every wave's
     if (grp == 1) pp_barrier();
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot = kt % NS;
+      if (kt + NS - 1 < nkt) stage_next((kt + NS - 1) % NS);
+      __builtin_amdgcn_sched_barrier(0);
       frag_w(slot);
       frag_a(slot, 0);
       frag_a(slot, 4);
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
       if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
@@ -1891,7 +1918,10 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
   // one launch of the row-parallel kernel instead of two latency-bound ones; g_tune[kRowReduce] = 2 off,
   // > 2: the depth limit (A/B)
   const int row_max = g_tune[kRowReduce] > 2 ? g_tune[kRowReduce] : 2048;
-  if (n4 <= 1024 && splits <= row_max && g_tune[kRowReduce] != 2) {
+  // (wide and deep -- 1,024-channel BN sums over 1,568 tile rows at batch 1024 -- is ~12 MB on
+  // n4 / 64 = 8 workgroups, 28 us; the two-level pair spreads it over the chip)
+  const bool rows_ok = n4 <= 256 || (size_t)splits * n4 <= (size_t)512 * 1024;
+  if (n4 <= 1024 && splits <= row_max && rows_ok && g_tune[kRowReduce] != 2) {
     hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 63) / 64), dim3(1024), 0, stream, (const float4*)part,
                        splits, n4, (float4*)out);
     return;
@@ -1976,11 +2006,12 @@ void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co,
     p.dy_t[i] = (int8_t)taps.dy[i];
     p.dx_t[i] = (int8_t)taps.dx[i];
   }
-  if (!pro && is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
+  if (is_3x3_same(Ho, Wo, Hs, Ws, ss, taps)) {
     const int s3 = wgrad3x3_splits(N, Ho, Wo, Cs, Co, num_cu);
     if (s3 > 0) {
-      // part holds wgrad_plan_splits(...) = s3 partial slices (the caller sized it by that plan)
-      launch_wgrad3x3(dy, src, N, Ho, Wo, Cs, Co, part, s3, zero, stream);
+      // part holds wgrad_plan_splits(...) = s3 partial slices (the caller sized it by that plan);
+      // a BN prologue is recomputed on the staged window (the 3x3 consumer's K5)
+      launch_wgrad3x3(dy, src, N, Ho, Wo, Cs, Co, part, s3, zero, stream, pscale, pshift);
       launch_split_reduce(part, s3, Co * 9 * Cs, dw, stream);
       return;
     }

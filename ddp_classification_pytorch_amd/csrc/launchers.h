@@ -76,7 +76,8 @@ int wgrad_plan_splits(int N, int Ho, int Wo, int Co, int Hs, int Ws, int Cs, int
 // wgrad3x3.hip: direct 3x3 / stride-1 / pad-1 weight gradient (0 = not applicable)
 int wgrad3x3_splits(int N, int H, int W, int C, int Co, int num_cu);
 void launch_wgrad3x3(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Co, float* part, int splits,
-                     const bf16* zero, hipStream_t stream);
+                     const bf16* zero, hipStream_t stream, const float* pscale = nullptr,
+                     const float* pshift = nullptr);
 void launch_split_reduce(const float* part, int splits, int n, float* out, hipStream_t stream);
 void launch_wgrad(const bf16* dy, int N, int Ho, int Wo, int Co, const bf16* src, int Hs, int Ws, int Cs, int ss,
                   const TapList& taps, float* dw, float* part, const bf16* zero, int num_cu, hipStream_t stream,
@@ -120,6 +121,9 @@ void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, f
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                               float* shift, float* rm, float* rv, float momentum, hipStream_t s);
 // BN statistics from ready first-level partials [P][3][C] (e.g. the stem kernel's)
+// two-level merge of many partials: chunks of 128 rows (0 = merge directly), and the first level
+int bn_partial_chunks(int P);
+void launch_bn_partial_chunk(const float* part, int P, int C, float* tmp, hipStream_t s);
 void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s);
 void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const float* gamma, const float* beta,
                               float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
@@ -235,7 +239,7 @@ void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const 
 bool conv3x3_c64_supported(int H, int W, int C, int Co);
 int conv3x3_c64_blocks(int N, int H, int W, int num_cu);
 void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
-                        int blocks, hipStream_t stream);
+                        int blocks, hipStream_t stream, const float* pscale = nullptr, const float* pshift = nullptr);
 
 // host int64 table -> device through kernel arguments (graph-capture safe, see misc.hip)
 void launch_table_fill(const int64_t* host, int64_t n, int64_t* out, hipStream_t s);

@@ -43,6 +43,10 @@ struct W3Params {
   int Wq;            // window row pitch in pixels: W + 2 rounded up to even (the swizzle's parity)
   int ablate;        // tuning experiments only (g_tune[kAblate]): 1 = no strip prefetch, 2 = no MFMA loop
   FastDiv div_wq, div_w, div_spi;
+  // BN prologue (the forward's conv3x3_c64 PRO): x is a BN's input, the GEMM operand
+  // relu(x * pscale[c] + pshift[c]), recomputed once per staged window element; nullptr: off
+  const float* pscale;
+  const float* pshift;
 };
 
 // pixel-row swizzle of the 128-byte-row images (as swz128tr in conv_igemm.hip)
@@ -113,6 +117,36 @@ __global__ void __launch_bounds__(512, 1) wgrad3x3_kernel(const W3Params p) {
     // buffer b^1 (strip s-1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (p.pscale != nullptr) {
+      // BN + ReLU once per staged in-image window element, before the next strip's DMA is issued
+      // (the per-channel coefficients are ordinary loads: a compiler-counted wait behind an
+      // untracked DMA would drain it); the zero halo stays zero
+      char* xw = smem + b * p.buf;
+      const int n = fdiv(s, p.div_spi);
+      const int y0 = (s - n * p.spi) * p.R;
+      const int rows = min(p.R, H - y0);
+      for (int qq = tid; qq < p.xq; qq += 512) {
+        const uint32_t P = qq >> 3;
+        const uint32_t rr = fdiv(P, p.div_wq), xx = P - rr * Wq;
+        const int yy = y0 - 1 + (int)rr, xi = (int)xx - 1;
+        if ((int)rr < rows + 2 && yy >= 0 && yy < H && xi >= 0 && xi < W) {
+          const int c0 = ci0 + (int)(((qq & 7) ^ w3_g(xx)) * 8);
+          float sc[8], sh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc[e] = p.pscale[c0 + e];
+            sh[e] = p.pshift[c0 + e];
+          }
+          bf16x8 v = *LDS_PTR(bf16x8, xw + qq * 16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = f2bf(fmaxf(bf2f(v[e]) * sc[e] + sh[e], 0.f));  // as bn_act_fwd_kernel
+          *LDS_PTR(bf16x8, xw + qq * 16) = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     if (s + 1 < s_end && !(p.ablate & 1)) load_strip(s + 1, b ^ 1);
     const char* ximg = smem + b * p.buf;
     const char* dimg = ximg + p.xbytes;
@@ -199,9 +233,10 @@ int wgrad3x3_splits(int N, int H, int W, int C, int Co, int num_cu) {
 }
 
 void launch_wgrad3x3(const bf16* dy, const bf16* x, int N, int H, int W, int C, int Co, float* part, int slices,
-                     const bf16* zero, hipStream_t stream) {
+                     const bf16* zero, hipStream_t stream, const float* pscale, const float* pshift) {
   W3Params p;
   p.dy = dy; p.x = x; p.part = part; p.zero = zero;
+  p.pscale = pscale; p.pshift = pshift;
   p.H = H; p.W = W; p.C = C; p.Co = Co;
   p.R = w3_rows(H, W);
   p.spi = (H + p.R - 1) / p.R;

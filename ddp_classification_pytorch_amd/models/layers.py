@@ -173,19 +173,29 @@ class Linear(nn.Module):
         return f"in={self.in_features}, out={self.out_features}, bias={self.bias is not None}"
 
 
-def bn_relu_conv(bn: BatchNorm2d, conv: Conv2d, x, slabs=None, stats=False):
-    """conv(relu(bn(x))) where the 1x1 stride-1 ``conv`` is the BN output's only consumer (a
-    bottleneck's bn2 -> conv3).  A training-mode BN is then applied inside the conv's GEMMs
-    (``Fn.bn_relu_conv1x1``): the normalised activation is never written.
+def bn_relu_conv(bn: BatchNorm2d, conv: Conv2d, x, slabs=None, stats=False, fuse_bwd=False):
+    """conv(relu(bn(x))) where ``conv`` is the BN output's only consumer.  A training-mode BN is
+    then applied inside the conv: the normalised activation is never written.
+      * a 1x1 stride-1 conv (a bottleneck's bn2 -> conv3): in the GEMMs' operand registers
+        (``Fn.bn_relu_conv1x1``; opt-in, ``DCP_BN_PROLOGUE=1``: VALU-bound at K = 64);
+      * a 64 -> 64 channel 3x3 stride-1 conv (ResNet-50 layer1's bn1 -> conv2): once per staged
+        window element of the direct kernels, each element feeding nine taps
+        (``Fn.bn_relu_conv3x3``; default on, ``DCP_BN_PROLOGUE3=0`` off).
     Any other case runs bn then conv.  Returns (y, statistics slabs of y or None)."""
     C, Co = x.shape[-1], conv.out_channels
-    if (Fn.bn_prologue_enabled() and bn.training and not bn.frozen and not bn.inplace_abn and conv.groups == 1
-            and conv.kernel_size == 1 and conv.stride == 1 and conv.padding == 0 and bn.weight is not None
-            and conv.weight.shape[3] == C and Fn.bn_prologue_fits(C, Co)):
+    train_bn = (bn.training and not bn.frozen and not bn.inplace_abn and conv.groups == 1 and bn.weight is not None
+                and conv.weight.shape[3] == C)
+    if (train_bn and Fn.bn_prologue_enabled() and conv.kernel_size == 1 and conv.stride == 1 and conv.padding == 0
+            and Fn.bn_prologue_fits(C, Co)):
         bn._nbt_pending += 1
         return Fn.bn_relu_conv1x1(x, slabs, bn.weight, bn.bias, bn.running_mean, bn.running_var, True, bn.momentum,
                                   bn.eps, conv.weight, stats, group=bn.process_group)
-    return conv(bn(x, slabs, act="relu"), stats=stats)
+    if (train_bn and Fn.bn_prologue3x3_enabled() and x.is_cuda and conv.kernel_size == 3 and conv.stride == 1
+            and conv.padding == 1 and Fn.bn_prologue3x3_fits(x, C, Co)):
+        bn._nbt_pending += 1
+        return Fn.bn_relu_conv3x3(x, slabs, bn.weight, bn.bias, bn.running_mean, bn.running_var, True, bn.momentum,
+                                  bn.eps, conv.weight, stats, group=bn.process_group)
+    return conv(bn(x, slabs, act="relu", fuse_bwd=fuse_bwd), stats=stats)
 
 
 def conv_bn(conv: Conv2d, bn: BatchNorm2d, x, act="relu", residual=None, slope=0.01):

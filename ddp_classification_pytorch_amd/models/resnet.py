@@ -98,9 +98,9 @@ class Bottleneck(nn.Module):
         # The downsample branch runs after conv3 so its backward precedes conv1's.
         join = Fn.GradJoin(1)
         y, s = self.conv1(x, stats=t, link=join)
-        # a grouped conv2 (ResNeXt) fuses bn1's backward reduction into its dgrad
-        y = self.bn1(y, s, act="relu", fuse_bwd=self.conv2.groups > 1)
-        y, s = self.conv2(y, stats=t)
+        # bn1 + ReLU inside conv2's staged windows where the direct 64-channel 3x3 kernels run
+        # (layers.bn_relu_conv); a grouped conv2 (ResNeXt) fuses bn1's backward reduction into its dgrad
+        y, s = bn_relu_conv(self.bn1, self.conv2, y, s, stats=t, fuse_bwd=self.conv2.groups > 1)
         # bn2 + ReLU run inside conv3's GEMMs (layers.bn_relu_conv): no activation pass
         y, s = bn_relu_conv(self.bn2, self.conv3, y, s, stats=t)
         if self.downsample is not None:

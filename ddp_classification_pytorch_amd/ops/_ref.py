@@ -283,6 +283,19 @@ def conv_wgrad_pro(dy, x, scale, shift):
     return conv_wgrad(dy, bn_act(x, None, scale, shift, 1, 0.0), 1, 1, 1, 0)
 
 
+def conv3x3_fwd_pro(x, w, scale, shift, stats):
+    """3x3 / stride-1 / pad-1 conv of bf16(relu(x * scale + shift)); the padding is of the BN output."""
+    return conv_fwd(bn_act(x, None, scale, shift, 1, 0.0), w, 1, 1, stats)
+
+
+def conv3x3_wgrad_pro(dy, x, scale, shift):
+    return conv_wgrad(dy, bn_act(x, None, scale, shift, 1, 0.0), 3, 3, 1, 1)
+
+
+def conv3x3_pro_fits(N, H, W, C, Co):
+    return C == 64 and Co == 64
+
+
 def act_scale_bwd(dy, y, scale, act, slope, want_g):
     g = _f(dy) * _act_d(_f(y), act, slope)
     gd = g.to(dy.dtype)

@@ -737,25 +737,32 @@ def bn_prologue_fits(C: int, Co: int) -> bool:
     return C % 64 == 0 and Co % 8 == 0 and C <= 2048 and not (Co <= 64 and C >= 128)
 
 
-class _BNReluConv1x1(Function):
-    """y = conv1x1(relu(BN(x))) with the BN + ReLU applied to the conv's operands in registers.
+class _BNReluConv(Function):
+    """y = conv(relu(BN(x))) with the BN + ReLU applied to the conv's operands on the fly: a 1x1
+    stride-1 conv (in registers between the LDS fragment read and the MFMA, K5) or the 64 -> 64
+    channel 3x3 stride-1 conv of the direct kernels (once per staged window element -- each feeds
+    nine taps -- in conv3x3_c64 and wgrad3x3).
 
     Forward: the BN coefficients from x's producer statistics (SyncBN: the all-gather), then
-    ``conv_fwd_pro`` (and the statistics of y for the next BN).  Backward: the conv's dgrad gives
-    the gradient of relu(BN(x)); ``conv_wgrad_pro`` recomputes relu(BN(x)) from x in the
-    weight-gradient GEMM; the BN + ReLU backward runs from x as in :class:`_BNAct`."""
+    ``conv_fwd_pro`` / ``conv3x3_fwd_pro`` (and the statistics of y for the next BN).  Backward: the
+    conv's dgrad gives the gradient of relu(BN(x)); the weight gradient recomputes relu(BN(x))
+    from x; the BN + ReLU backward runs from x as in :class:`_BNAct`.  The normalised activation
+    is never written."""
 
     @staticmethod
-    def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig, weight, wb, wt, stats):
+    def forward(ctx, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig, weight, wb, wt, stats, k3):
         k = K(x)
         if cfg.training_stats:
             mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
         else:
             mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
             count = x.numel() // x.shape[-1]
-        y, yslabs = k.conv_fwd_pro(x, wb, scale, shift, stats)
+        if k3:
+            y, yslabs = k.conv3x3_fwd_pro(x, wb, scale, shift, stats)
+        else:
+            y, yslabs = k.conv_fwd_pro(x, wb, scale, shift, stats)
         ctx.save_for_backward(x, scale, shift, mean, invstd, wt)
-        ctx.cfg, ctx.count = cfg, count
+        ctx.cfg, ctx.count, ctx.k3 = cfg, count, k3
         ctx.mark_non_differentiable(yslabs)
         ctx.set_materialize_grads(False)
         return y, yslabs
@@ -763,16 +770,17 @@ class _BNReluConv1x1(Function):
     @staticmethod
     def backward(ctx, dy, _dslabs):
         if dy is None:
-            return (None,) * 11
+            return (None,) * 12
         x, scale, shift, mean, invstd, wt = ctx.saved_tensors
         cfg = ctx.cfg
         dy = dy.contiguous()
         k = K(dy)
         dx = dgamma = dbeta = dw = None
         need_x = ctx.needs_input_grad[0] or ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        g = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], 1, 0) if need_x else None
+        pad = 1 if ctx.k3 else 0
+        g = k.conv_dgrad(dy, wt, x.shape[1], x.shape[2], 1, pad) if need_x else None
         if ctx.needs_input_grad[7]:
-            dw = k.conv_wgrad_pro(dy, x, scale, shift)
+            dw = k.conv3x3_wgrad_pro(dy, x, scale, shift) if ctx.k3 else k.conv_wgrad_pro(dy, x, scale, shift)
         if g is not None:
             need_affine = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
             local = sums = None
@@ -786,21 +794,54 @@ class _BNReluConv1x1(Function):
                                    float(ctx.count), 1, 0.0, False)
             dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
             dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
-        return dx, None, dgamma, dbeta, None, None, None, dw, None, None, None
+        return dx, None, dgamma, dbeta, None, None, None, dw, None, None, None, None
 
 
-def bn_relu_conv1x1(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats=False,
-                    group=None):
-    """conv1x1(relu(BN(x))) through :class:`_BNReluConv1x1` -> (y, statistics slabs of y or None).
-    weight: fp32 [Co, 1, 1, C]."""
+_BNReluConv1x1 = _BNReluConv
+
+
+def _bn_relu_conv(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats, group, k3):
     world = dist.get_world_size(group) if group is not None else 1
     cfg = BNConfig(training_stats, momentum, eps, 1, 0.0, group, world)
     if slabs is not None and slabs.numel() == 0:
         slabs = None
     wb, wt = prepared_weight(weight, 0, True)
     want = bool(stats and x.is_cuda)
-    y, yslabs = _BNReluConv1x1.apply(x, slabs, gamma, beta, run_mean, run_var, cfg, weight, wb, wt, want)
+    y, yslabs = _BNReluConv.apply(x, slabs, gamma, beta, run_mean, run_var, cfg, weight, wb, wt, want, k3)
     return y, (yslabs if want else None)
+
+
+def bn_relu_conv1x1(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats=False,
+                    group=None):
+    """conv1x1(relu(BN(x))) through :class:`_BNReluConv` -> (y, statistics slabs of y or None).
+    weight: fp32 [Co, 1, 1, C]."""
+    return _bn_relu_conv(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats,
+                         group, False)
+
+
+def bn_relu_conv3x3(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats=False,
+                    group=None):
+    """conv3x3 / stride 1 / pad 1 (relu(BN(x))) for 64 -> 64 channels through the direct kernels'
+    window prologue -> (y, statistics partials of y or None).  weight: fp32 [Co, 3, 3, C]."""
+    return _bn_relu_conv(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats,
+                         group, True)
+
+
+# BN + ReLU inside a 64 -> 64 channel 3x3 consumer's staged window (bn_relu_conv3x3): on by default
+# (DCP_BN_PROLOGUE3=0 / set_bn_prologue3x3(False) off, A/B)
+_BN_PROLOGUE3 = [os.environ.get("DCP_BN_PROLOGUE3", "1") != "0"]
+
+
+def set_bn_prologue3x3(enabled: bool):
+    _BN_PROLOGUE3[0] = bool(enabled)
+
+
+def bn_prologue3x3_enabled() -> bool:
+    return _BN_PROLOGUE3[0]
+
+
+def bn_prologue3x3_fits(x, C: int, Co: int) -> bool:
+    return bool(K(x).conv3x3_pro_fits(x.shape[0], x.shape[1], x.shape[2], C, Co))
 
 
 def _bn_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
