@@ -899,7 +899,7 @@ tap_gemm_big_kernel(const TapGemmParams p) {
     if (grp == 1) pp_barrier();
     for (int kt = 0; kt < nkt; ++kt) {
       const int slot = kt % NS;
-      if (kt + NS - 1 < nkt) stage_next((kt + NS - 1) % NS);
+      if (kt + NS - 1 < nkt && !(p.ablate & 1)) stage_next((kt + NS - 1) % NS);
       __builtin_amdgcn_sched_barrier(0);
       frag_w(slot);
       frag_a(slot, 0);
@@ -908,8 +908,10 @@ tap_gemm_big_kernel(const TapGemmParams p) {
       if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
-      mfma_half(0);
-      mfma_half(4);
+      if (!(p.ablate & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
+        mfma_half(0);
+        mfma_half(4);
+      }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
@@ -1643,7 +1645,8 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   const int big = big_ok ? big_tile_pick(g_tune[kTgBig], p.M, Co, taps.n, ds) : 0;
   if (big != 0) {
     p.nkt = taps.n * p.cpt / 4;  // 32-deep k-tiles (cpt % 8 == 0 on FAST shapes)
-    if (big == 1) launch_big<2, 4, 4>(p, epi, stream);
+    if (big == 1 && g_tune[kTgBigStages] == 5) launch_big<2, 4, 5>(p, epi, stream);
+    else if (big == 1) launch_big<2, 4, 4>(p, epi, stream);
     else launch_big<2, 2, 3>(p, epi, stream);
     return;
   }

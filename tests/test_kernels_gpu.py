@@ -1135,13 +1135,17 @@ def test_adaptive_avg_pool_kernels(K):
                                    (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1)])
 @pytest.mark.parametrize("mode", [1, 3])
 @pytest.mark.parametrize("cvar", [0, 1, 2, 3])
-def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
+@pytest.mark.parametrize("stages", [0, 5])
+def test_big_tile_tap_gemm_matches(K, shape, mode, cvar, stages):
     """The 8-wave 256 x 256 (tg_big = 1; 256 x 128 below 256 channels) and 4-wave 256 x 128
     (tg_big = 3) big-tile tap GEMMs under every schedule: the 8-wave tile's default ping-pong
     (tg_big_cvar = 0 / 3), fragments read across the barrier in lockstep (1; the 4-wave tile's
     default) or after it (2), == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
     M: quadrants past M write no slab) and the data gradient (stride 1 and the stride-2 parity
-    classes), channel counts that are not a multiple of the tile."""
+    classes), channel counts that are not a multiple of the tile; the 256 x 256 tile also with its
+    5-slot (160 KB) LDS-DMA ring (tg_big_stages = 5)."""
+    if stages and mode != 1:
+        pytest.skip("the 5-slot ring is the 256 x 256 tile's")
     N, H, W, Ci, Co, k, s, p = shape
     torch.manual_seed(0)
     x = rnd(N, H, W, Ci).to(DEV)
@@ -1154,6 +1158,7 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
         for m in (2, mode):
             K.set_tuning(tslot("tg_big"), m)
             K.set_tuning(tslot("tg_big_cvar"), cvar if m != 2 else 0)
+            K.set_tuning(tslot("tg_big_stages"), stages if m != 2 else 0)
             y, slabs = K.conv_fwd(x, wb, s, p, True)
             st = K.bn_stats(y, slabs)
             dx = K.conv_dgrad(dy, wt, H, W, s, p)
@@ -1162,6 +1167,7 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar):
     finally:
         K.set_tuning(tslot("tg_big"), 0)
         K.set_tuning(tslot("tg_big_cvar"), 0)
+        K.set_tuning(tslot("tg_big_stages"), 0)
     (y0, s0, d0), (y1, s1, d1) = outs
     assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3

@@ -7,6 +7,7 @@
 #   bench           headline bench.py (20 steps)              configs every BASELINE.json config
 #   prof            rocprofv3 --kernel-trace --stats of the headline (10 steps)
 #   profcfg=CFG     the same for another bench config (e.g. arcface)
+#   profenv=V=X[:T] the headline profile with environment V=X (output prof_T)
 #   profsmall       the same for the batch-32 HIP-graph step (200 replays)
 #   pmcconv=S:CFGS  PMC passes (SQ / TCC hit-miss / FETCH_SIZE) over forward convs of shapes S under configs CFGS
 #   graph1024       headline batch eager vs HIP graph, interleaved twice
@@ -117,6 +118,15 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 30 --warmup 3 \
         > $O/prof.log 2>&1
       echo prof done ;;
+    profenv=*)
+      # profenv=V=X[:tag] -- the headline profile with environment V=X (kernel-level view of an A/B)
+      a=${step#profenv=}; kv=${a%%:*}; tg=${a#*:}; [ "$tg" = "$a" ] && tg=env
+      prof_env
+      export "$kv"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$tg -o run -- python3 -u bench.py --steps 30 --warmup 3 \
+        > $O/prof_$tg.log 2>&1
+      unset "${kv%%=*}"
+      echo prof $tg done ;;
     profcfg=*)
       # rocprofv3 kernel stats of another BASELINE config, e.g. profcfg=arcface
       c=${step#profcfg=}
