@@ -66,7 +66,7 @@ struct TapGemmParams {
   // wave-uniform lookup is one s_load_dword (byte arrays compile to vector loads, whose
   // vmcnt wait would drain the LDS-DMA ring).
   int tap[kMaxTaps];
-  int ablate;  // tuning experiments only: 1 = no staging in the k-loop, 2 = no MFMA
+  int ablate;  // tuning experiments only: 1 = no staging in the k-loop, 2 = no MFMA, 4 = no epilogue (big tile)
   int cvar;    // tuning experiments only: compute-loop variant
   // EPI 3 (stride-1 dgrad): backward of the BN(+ReLU)(+residual) layer that produced this
   // conv's input, fused into the epilogue (see launchers.h BnBwdEpi)
@@ -958,6 +958,7 @@ tap_gemm_big_kernel(const TapGemmParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (p.ablate & 4) return;  // timing ablation: no epilogue
 
   // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
   {
