@@ -45,6 +45,8 @@
 namespace dcp {
 
 int g_tune[kTuneSlots] = {0};
+static long long* g_tg_stamps = nullptr;
+void set_tg_stamps(long long* p) { g_tg_stamps = p; }
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
@@ -81,7 +83,13 @@ struct TapGemmParams {
   // a = bf16(relu(x * pscale[c] + pshift[c])) -- the BN + ReLU output is never written (K5)
   const float* pscale;
   const float* pshift;
+  int persist;  // big tile: 1 = persistent workgroups (g_tune[kTgBigPersist])
+  // timing instrumentation only (g_tune[kAblate] & 16, tools/pp_stamps.py): per-wave s_memtime at
+  // every ping-pong barrier of workgroups 0..7, [wg][wave][kStampSlots] int64; slot kStampSlots-1
+  // holds the wave's HW_ID register (SIMD / CU placement)
+  long long* stamps;
 };
+constexpr int kStampSlots = 72;
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
 __device__ __forceinline__ int tap_dx(int v) { return (int)(int8_t)((v >> 8) & 0xff); }
@@ -741,7 +749,7 @@ tap_gemm_kernel(const TapGemmParams p) {
 // slower on every R50 shape, profiles/r4/big4_tile_ab_b1024.txt, and was removed)
 template <int WM, int WN, int NS, int EPI, int CFW = 4>
 __global__ void __launch_bounds__(64 * WM * WN, 2)
-tap_gemm_big_kernel(const TapGemmParams p) {
+tap_gemm_big_kernel(const TapGemmParams p0) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BM = 128 * WM, BN = 16 * CFW * WN, BK = 32;
   constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;  // 64-byte rows, 16 rows per LDS-DMA
@@ -752,239 +760,276 @@ tap_gemm_big_kernel(const TapGemmParams p) {
   static_assert(BN % 128 == 0 && NT % 256 == 0 && NQ % NG == 0 && NS >= 3, "tile geometry");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const uint32_t tn = bid % ntn, tm = bid / ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const uint32_t ntn = (p0.Co + BN - 1) / BN, ntm = (p0.M + BM - 1) / BM;
+  // tg_big_persist = 1: one workgroup per CU walks tiles blockIdx.x, + gridDim.x, ... (the same
+  // XCD-contiguous tile order as one launch per tile): the epilogue's global stores drain while
+  // the next tile's ring fills, and no workgroup is re-dispatched per tile
+  const uint32_t ntiles = ntm * ntn;
+  const uint32_t tstep = p0.persist ? gridDim.x : ntiles;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += tstep) {
+    // the parameters re-read per tile through an opaque pointer (scalar-cache hits): hoisted out
+    // of the tile loop they stay live in SGPRs across it and spill
+    const TapGemmParams* pcur = &p0;
+    asm volatile("" : "+s"(pcur));
+    const TapGemmParams& p = *pcur;
+    // the lane index likewise: every lane-derived LDS / global offset is recomputed per tile
+    // instead of being hoisted and held in VGPRs through the k-loop
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const uint32_t bid = xcd_remap(tile, ntiles);
+    const uint32_t tn = bid % ntn, tm = bid / ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
 
-  // per-slot source pointers + tap-validity masks (as tap_gemm_kernel's FAST path); rows past M
-  // and channels past Co read a clamped valid row and are never stored or counted
-  const bf16* fa_ptr[AI];
-  uint32_t fa_vm[AI];
-  const bf16* fb_ptr[BI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int r = (wave * AI + i) * RPI + lane / CH;
-    const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
-    const uint32_t q = fdiv(mm, p.div_wy);
-    const uint32_t x = mm - q * p.Wy;
-    const uint32_t n = fdiv(q, p.div_hy);
-    const uint32_t y = q - n * p.Hy;
-    const int ys = y * p.ss, xs = x * p.ss;
-    fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
-    uint32_t vm = 0;
-    for (int t = 0; t < p.ntaps; ++t) {
-      const int tv = p.tap[t];
-      const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
-      vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
-    }
-    fa_vm[i] = vm;
-  }
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int r = (wave * BI + i) * RPI + lane / CH;
-    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
-  }
-  const int tiles_per_tap = p.cpt / CH;
-  auto stage = [&](int kt, int slot) {
-    char* As = smem + slot * STAGE;
-    char* Bs = As + A_BYTES;
-    const int t = kt / tiles_per_tap;
-    const int cbase = (kt - t * tiles_per_tap) * BK;
-    const int tv = p.tap[t];
-    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
-    const long boff = (long)tap_w(tv) * p.Cs + cbase;
-    const uint32_t tbit = 1u << t;
-#pragma unroll
+    // per-slot source pointers + tap-validity masks (as tap_gemm_kernel's FAST path); rows past M
+    // and channels past Co read a clamped valid row and are never stored or counted
+    const bf16* fa_ptr[AI];
+    uint32_t fa_vm[AI];
+    const bf16* fb_ptr[BI];
+  #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
-      dma16_tracked(g, As + (wave * AI + i) * 1024);
+      const int r = (wave * AI + i) * RPI + lane / CH;
+      const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+      const uint32_t q = fdiv(mm, p.div_wy);
+      const uint32_t x = mm - q * p.Wy;
+      const uint32_t n = fdiv(q, p.div_hy);
+      const uint32_t y = q - n * p.Hy;
+      const int ys = y * p.ss, xs = x * p.ss;
+      fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+      uint32_t vm = 0;
+      for (int t = 0; t < p.ntaps; ++t) {
+        const int tv = p.tap[t];
+        const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+        vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+      }
+      fa_vm[i] = vm;
     }
-#pragma unroll
-    for (int i = 0; i < BI; ++i)
-      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
-  };
-
-  f32x4 acc[CFW][8];  // [16-channel fragment][16-pixel fragment]
-#pragma unroll
-  for (int j = 0; j < CFW; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nkt = p.nkt;
-  const uint32_t c = lane >> 4;
-  bf16x8 wf[CFW], af[8];
-  auto frag_w = [&](int slot) {
-    const char* Bs = smem + slot * STAGE + A_BYTES;
-#pragma unroll
-    for (int j = 0; j < CFW; ++j)
-      wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (16 * CFW) + j * 16 + (lane & 15), c));
-  };
-  auto frag_a = [&](int slot, int i0) {
-    const char* As = smem + slot * STAGE;
-#pragma unroll
-    for (int i = i0; i < i0 + 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 128 + i * 16 + (lane & 15), c));
-  };
-  auto mfma_half = [&](int i0) {
-#pragma unroll
-    for (int j = 0; j < CFW; ++j)
-#pragma unroll
-      for (int i = i0; i < i0 + 4; ++i)
-        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
-  };
-  // raw barrier: this wave's fragment reads retired first (WAR on the slot re-staged after it);
-  // the counted vmcnt before it is the RAW wait -- no vmcnt(0), the ring stays in flight
-  auto ring_barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (i < nkt) stage(i, i);
-  if (WM == 2 && p.cvar == 3 && nkt > 0) {
-    // Ping-pong (g_tune[kTgBigCvar] = 3): the two row halves of the tile are two wave groups
-    // (waves 0-3: pixel rows 0-127, waves 4-7: 128-255), and the waves of a workgroup sit on the
-    // four SIMDs one from each group.  Group 1 runs one segment behind group 0, so in every
-    // interval between two workgroup barriers one wave of each SIMD runs its MFMA segment
-    // (k-tile kt's 32 MFMAs from registers) while its partner runs a load segment (the next
-    // k-tile's 12 fragment reads and its share of a later k-tile's LDS-DMA): the matrix pipe
-    // alternates between the two instead of idling through a common read phase.
-    // Synchronisation, counting workgroup barriers b (group 0 loads k-tile kt in (2kt, 2kt+1),
-    // computes it in (2kt+1, 2kt+2); group 1 one interval later):
-    //   RAW -- every wave retires its own DMA of k-tile kt (counted vmcnt) before barrier 2kt:
-    //   group 0 at the end of its compute segment kt-1, group 1 at the end of its load segment kt-1;
-    //   WAR -- k-tile kt's slot is last read in (2kt+1, 2kt+2) (each reader waits lgkmcnt(0)
-    //   before its next barrier) and is restaged (k-tile kt+NS) in load segments after 2kt+2.
-    // Each group passes the same number of barriers: group 1 one extra at the start, group 0 one
-    // extra at the end.
-    const int grp = wm;
-    auto pp_barrier = [&]() {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    // The load segment issues its LDS-DMA first and its fragment reads behind it, so the DMA's
-    // address work overlaps the reads' latency.  The tap table sits in one VGPR (lane t = tap t,
-    // read with v_readlane) and the (tap, channel) of the next k-tile to stage advances with
-    // scalar selects: a scalar-memory tap lookup would make the compiler wait lgkmcnt(0) -- for the
-    // fragment reads too -- before every DMA.
-    const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
-    int st_t = (NS - 1) / tiles_per_tap, st_c = ((NS - 1) - st_t * tiles_per_tap) * BK;
-    auto stage_next = [&](int slot) {
+  #pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int r = (wave * BI + i) * RPI + lane / CH;
+      fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+    }
+    const int tiles_per_tap = p.cpt / CH;
+    auto stage = [&](int kt, int slot) {
       char* As = smem + slot * STAGE;
       char* Bs = As + A_BYTES;
-      const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
-      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
-      const long boff = (long)tap_w(tv) * p.Cs + st_c;
-      const uint32_t tbit = 1u << st_t;
-#pragma unroll
+      const int t = kt / tiles_per_tap;
+      const int cbase = (kt - t * tiles_per_tap) * BK;
+      const int tv = p.tap[t];
+      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
+      const long boff = (long)tap_w(tv) * p.Cs + cbase;
+      const uint32_t tbit = 1u << t;
+  #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
         dma16_tracked(g, As + (wave * AI + i) * 1024);
       }
-#pragma unroll
-      for (int i = 0; i < BI; ++i) dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
-      st_c += BK;
-      const bool wrap = st_c >= p.Cs;
-      st_t += wrap ? 1 : 0;
-      st_c = wrap ? 0 : st_c;
+  #pragma unroll
+      for (int i = 0; i < BI; ++i)
+        dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
     };
-    wait_vmcnt(LPT * min(NS - 2, nkt - 1));  // k-tile 0 (this wave's share)
-    pp_barrier();                            // ... every wave's
-    if (grp == 1) pp_barrier();
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int slot = kt % NS;
-      if (kt + NS - 1 < nkt && !(p.ablate & 1)) stage_next((kt + NS - 1) % NS);
-      __builtin_amdgcn_sched_barrier(0);
-      frag_w(slot);
-      frag_a(slot, 0);
-      frag_a(slot, 4);
-      __builtin_amdgcn_sched_barrier(0);
-      if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
-      pp_barrier();
-      __builtin_amdgcn_s_setprio(1);
-      if (!(p.ablate & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
+
+    f32x4 acc[CFW][8];  // [16-channel fragment][16-pixel fragment]
+  #pragma unroll
+    for (int j = 0; j < CFW; ++j)
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nkt = p.nkt;
+    const uint32_t c = lane >> 4;
+    bf16x8 wf[CFW], af[8];
+    auto frag_w = [&](int slot) {
+      const char* Bs = smem + slot * STAGE + A_BYTES;
+  #pragma unroll
+      for (int j = 0; j < CFW; ++j)
+        wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (16 * CFW) + j * 16 + (lane & 15), c));
+    };
+    auto frag_a = [&](int slot, int i0) {
+      const char* As = smem + slot * STAGE;
+  #pragma unroll
+      for (int i = i0; i < i0 + 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 128 + i * 16 + (lane & 15), c));
+    };
+    auto mfma_half = [&](int i0) {
+  #pragma unroll
+      for (int j = 0; j < CFW; ++j)
+  #pragma unroll
+        for (int i = i0; i < i0 + 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+    };
+    // raw barrier: this wave's fragment reads retired first (WAR on the slot re-staged after it);
+    // the counted vmcnt before it is the RAW wait -- no vmcnt(0), the ring stays in flight
+    auto ring_barrier = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+  #pragma unroll
+    for (int i = 0; i < NS - 1; ++i)
+      if (i < nkt) stage(i, i);
+    if (WM == 2 && p.cvar >= 3 && nkt > 0) {
+      // Ping-pong (g_tune[kTgBigCvar] = 3): the two row halves of the tile are two wave groups
+      // (waves 0-3: pixel rows 0-127, waves 4-7: 128-255), and the waves of a workgroup sit on the
+      // four SIMDs one from each group.  Group 1 runs one segment behind group 0, so in every
+      // interval between two workgroup barriers one wave of each SIMD runs its MFMA segment
+      // (k-tile kt's 32 MFMAs from registers) while its partner runs a load segment (the next
+      // k-tile's 12 fragment reads and its share of a later k-tile's LDS-DMA): the matrix pipe
+      // alternates between the two instead of idling through a common read phase.
+      // Synchronisation, counting workgroup barriers b (group 0 loads k-tile kt in (2kt, 2kt+1),
+      // computes it in (2kt+1, 2kt+2); group 1 one interval later):
+      //   RAW -- every wave retires its own DMA of k-tile kt (counted vmcnt) before barrier 2kt:
+      //   group 0 at the end of its compute segment kt-1, group 1 at the end of its load segment kt-1;
+      //   WAR -- k-tile kt's slot is last read in (2kt+1, 2kt+2) (each reader waits lgkmcnt(0)
+      //   before its next barrier) and is restaged (k-tile kt+NS) in load segments after 2kt+2.
+      // Each group passes the same number of barriers: group 1 one extra at the start, group 0 one
+      // extra at the end.
+      const int grp = wm;
+      // issue priority (tg_big_cvar): 3 = the MFMA segment at priority 1 (flipped per segment),
+      // 4 = no priorities, 5 = waves 4-7 (the arbitration losers) at priority 1 for the whole loop
+      const int prio = p.cvar;
+      if (prio == 5 && grp == 1) __builtin_amdgcn_s_setprio(1);
+      long long* stp = (p.stamps != nullptr && blockIdx.x < 8 && tile == blockIdx.x)
+                           ? p.stamps + ((size_t)blockIdx.x * NW + wave) * kStampSlots : nullptr;
+      int nst = 0;
+      if (stp != nullptr && lane == 0) stp[kStampSlots - 1] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      auto pp_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (stp != nullptr && nst < kStampSlots - 2) {  // arrival time, then release time
+          const long long t0 = __builtin_amdgcn_s_memtime();
+          __builtin_amdgcn_s_barrier();
+          const long long t1 = __builtin_amdgcn_s_memtime();
+          if (lane == 0) {
+            stp[nst] = t0;
+            stp[nst + 1] = t1;
+          }
+          nst += 2;
+        } else {
+          __builtin_amdgcn_s_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      // The load segment issues its LDS-DMA first and its fragment reads behind it, so the DMA's
+      // address work overlaps the reads' latency.  The tap table sits in one VGPR (lane t = tap t,
+      // read with v_readlane) and the (tap, channel) of the next k-tile to stage advances with
+      // scalar selects: a scalar-memory tap lookup would make the compiler wait lgkmcnt(0) -- for the
+      // fragment reads too -- before every DMA.
+      const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
+      int st_t = (NS - 1) / tiles_per_tap, st_c = ((NS - 1) - st_t * tiles_per_tap) * BK;
+      auto stage_next = [&](int slot) {
+        char* As = smem + slot * STAGE;
+        char* Bs = As + A_BYTES;
+        const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
+        const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
+        const long boff = (long)tap_w(tv) * p.Cs + st_c;
+        const uint32_t tbit = 1u << st_t;
+  #pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+          dma16_tracked(g, As + (wave * AI + i) * 1024);
+        }
+  #pragma unroll
+        for (int i = 0; i < BI; ++i) dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
+        st_c += BK;
+        const bool wrap = st_c >= p.Cs;
+        st_t += wrap ? 1 : 0;
+        st_c = wrap ? 0 : st_c;
+      };
+      wait_vmcnt(LPT * min(NS - 2, nkt - 1));  // k-tile 0 (this wave's share)
+      pp_barrier();                            // ... every wave's
+      if (grp == 1) pp_barrier();
+      for (int kt = 0; kt < nkt; ++kt) {
+        const int slot = kt % NS;
+        if (kt + NS - 1 < nkt && !(p.ablate & 1)) stage_next((kt + NS - 1) % NS);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_w(slot);
+        frag_a(slot, 0);
+        frag_a(slot, 4);
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+        pp_barrier();
+        if (prio == 3) __builtin_amdgcn_s_setprio(1);
+        if (!(p.ablate & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
+          mfma_half(0);
+          mfma_half(4);
+        }
+        if (prio == 3) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+        pp_barrier();
+      }
+      if (grp == 0) pp_barrier();
+      if (prio == 5) __builtin_amdgcn_s_setprio(0);
+    } else if (p.cvar == 2) {
+      // g_tune[kTgBigCvar] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
+      for (int kt = 0; kt < nkt; ++kt) {
+        wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
+        ring_barrier();  // ... for every wave; slot kt-1 is free
+        if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+        frag_w(kt % NS);
+        frag_a(kt % NS, 0);
+        frag_a(kt % NS, 4);
         mfma_half(0);
         mfma_half(4);
       }
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
-      pp_barrier();
-    }
-    if (grp == 0) pp_barrier();
-  } else if (p.cvar == 2) {
-    // g_tune[kTgBigCvar] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
-    for (int kt = 0; kt < nkt; ++kt) {
-      wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
-      ring_barrier();  // ... for every wave; slot kt-1 is free
-      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
-      frag_w(kt % NS);
-      frag_a(kt % NS, 0);
-      frag_a(kt % NS, 4);
-      mfma_half(0);
-      mfma_half(4);
-    }
-  } else if (nkt > 0) {
-    // default: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of k-tile
-    // kt -- pixel fragments 0..3 after its first half, the rest after its second half (measured
-    // 2-4 % faster than reading them after the barrier: profiles/r3/big_tile_ab_b1024_pipelined.txt)
-    wait_vmcnt(LPT * min(NS - 2, nkt - 1));
-    ring_barrier();
-    if (NS - 1 < nkt) stage(NS - 1, NS - 1);
-    frag_w(0);
-    frag_a(0, 0);
-    frag_a(0, 4);
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int nx = (kt + 1) % NS;
-      mfma_half(0);
-      if (kt + 1 < nkt) {
-        wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));  // k-tile kt+1 landed (this wave's share)
-        ring_barrier();  // ... for every wave; every read of slot kt retired: re-stage it
-        if (kt + NS < nkt) stage(kt + NS, kt % NS);
-        frag_a(nx, 0);
-      }
-      mfma_half(4);
-      if (kt + 1 < nkt) {
-        frag_w(nx);
-        frag_a(nx, 4);
+    } else if (nkt > 0) {
+      // default: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of k-tile
+      // kt -- pixel fragments 0..3 after its first half, the rest after its second half (measured
+      // 2-4 % faster than reading them after the barrier: profiles/r3/big_tile_ab_b1024_pipelined.txt)
+      wait_vmcnt(LPT * min(NS - 2, nkt - 1));
+      ring_barrier();
+      if (NS - 1 < nkt) stage(NS - 1, NS - 1);
+      frag_w(0);
+      frag_a(0, 0);
+      frag_a(0, 4);
+      for (int kt = 0; kt < nkt; ++kt) {
+        const int nx = (kt + 1) % NS;
+        mfma_half(0);
+        if (kt + 1 < nkt) {
+          wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));  // k-tile kt+1 landed (this wave's share)
+          ring_barrier();  // ... for every wave; every read of slot kt retired: re-stage it
+          if (kt + NS < nkt) stage(kt + NS, kt % NS);
+          frag_a(nx, 0);
+        }
+        mfma_half(4);
+        if (kt + 1 < nkt) {
+          frag_w(nx);
+          frag_a(nx, 4);
+        }
       }
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (p.ablate & 4) return;  // timing ablation: no epilogue
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (p.ablate & 4) continue;  // timing ablation: no epilogue
 
-  // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
-  {
-    char* Q = smem + (wm * QN + (wn * 16 * CFW) / 128) * 32768;
-    const uint32_t cb = (wn * 16 * CFW) % 128;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t pl = i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < CFW; ++j) {
-        const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
-        *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+    // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
+    {
+      char* Q = smem + (wm * QN + (wn * 16 * CFW) / 128) * 32768;
+      const uint32_t cb = (wn * 16 * CFW) % 128;
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t pl = i * 16 + (lane & 15);
+  #pragma unroll
+        for (int j = 0; j < CFW; ++j) {
+          const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
+          bf16x4 o;
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+          *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+        }
       }
     }
-  }
-  __syncthreads();
-  // group g (threads 256g ..) stores quadrants g*QPG ..; every group passes the same barriers
-  // (tile_stats128_vv's), so the quadrant loop stays uniform
-  const int g = tid >> 8, gtid = tid & 255;
-#pragma unroll
-  for (int k = 0; k < QPG; ++k) {
-    const int q = g * QPG + k;
-    tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
+    __syncthreads();
+    // group g (threads 256g ..) stores quadrants g*QPG ..; every group passes the same barriers
+    // (tile_stats128_vv's), so the quadrant loop stays uniform
+    const int g = tid >> 8, gtid = tid & 255;
+  #pragma unroll
+    for (int k = 0; k < QPG; ++k) {
+      const int q = g * QPG + k;
+      tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
+    }
+    if (p.persist) __syncthreads();  // every image read retired before the ring is refilled
   }
 }
 
@@ -1535,7 +1580,15 @@ static void launch_big(TapGemmParams p, int epi, hipStream_t stream) {
   else if (p.cvar == 1) p.cvar = 0;
   constexpr int BM = 128 * WM, BN = 16 * CFW * WN;
   constexpr size_t lds = std::max((size_t)NS * (BM + BN) * 64, (size_t)WM * (BN / 128) * 32768);
-  const int grid = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.Co + BN - 1) / BN);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int grid = p.persist ? std::min(tiles, ncu) : tiles;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 0, CFW>,
@@ -1617,7 +1670,9 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // heuristic (tuning experiments only)
   const int env_bn = g_tune[kTgTileN], env_ns = g_tune[kTgStages];
   p.ablate = g_tune[kAblate];
+  p.stamps = (p.ablate & 16) ? g_tg_stamps : nullptr;
   p.cvar = g_tune[kTgBigCvar];
+  p.persist = g_tune[kTgBigPersist];
   int bn = Co <= 64 ? 64 : 128, ns = 2;
   // a short grid (< 1.5 rounds of 256 CUs at 128-channel tiles: batch 32-128 from stage 2 on, the
   // stride-2 parity classes, the linear heads) takes 64-channel tiles, twice the workgroups: the

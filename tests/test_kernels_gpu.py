@@ -1135,15 +1135,16 @@ def test_adaptive_avg_pool_kernels(K):
                                    (2, 7, 7, 1024, 256, 1, 1, 0), (5, 3, 3, 64, 320, 3, 1, 1)])
 @pytest.mark.parametrize("mode", [1, 3])
 @pytest.mark.parametrize("cvar", [0, 1, 2, 3])
-@pytest.mark.parametrize("stages", [0, 5])
-def test_big_tile_tap_gemm_matches(K, shape, mode, cvar, stages):
+@pytest.mark.parametrize("stages,persist", [(0, 0), (5, 0), (0, 1)])
+def test_big_tile_tap_gemm_matches(K, shape, mode, cvar, stages, persist):
     """The 8-wave 256 x 256 (tg_big = 1; 256 x 128 below 256 channels) and 4-wave 256 x 128
     (tg_big = 3) big-tile tap GEMMs under every schedule: the 8-wave tile's default ping-pong
     (tg_big_cvar = 0 / 3), fragments read across the barrier in lockstep (1; the 4-wave tile's
     default) or after it (2), == the fp32 reference and the 128-row kernel: forward with BN statistics (ragged
     M: quadrants past M write no slab) and the data gradient (stride 1 and the stride-2 parity
     classes), channel counts that are not a multiple of the tile; the 256 x 256 tile also with its
-    5-slot (160 KB) LDS-DMA ring (tg_big_stages = 5)."""
+    5-slot (160 KB) LDS-DMA ring (tg_big_stages = 5), and both tiles as persistent workgroups
+    looping over tiles (tg_big_persist = 1)."""
     if stages and mode != 1:
         pytest.skip("the 5-slot ring is the 256 x 256 tile's")
     N, H, W, Ci, Co, k, s, p = shape
@@ -1159,6 +1160,7 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar, stages):
             K.set_tuning(tslot("tg_big"), m)
             K.set_tuning(tslot("tg_big_cvar"), cvar if m != 2 else 0)
             K.set_tuning(tslot("tg_big_stages"), stages if m != 2 else 0)
+            K.set_tuning(tslot("tg_big_persist"), persist if m != 2 else 0)
             y, slabs = K.conv_fwd(x, wb, s, p, True)
             st = K.bn_stats(y, slabs)
             dx = K.conv_dgrad(dy, wt, H, W, s, p)
@@ -1168,6 +1170,7 @@ def test_big_tile_tap_gemm_matches(K, shape, mode, cvar, stages):
         K.set_tuning(tslot("tg_big"), 0)
         K.set_tuning(tslot("tg_big_cvar"), 0)
         K.set_tuning(tslot("tg_big_stages"), 0)
+        K.set_tuning(tslot("tg_big_persist"), 0)
     (y0, s0, d0), (y1, s1, d1) = outs
     assert relerr(y1, y0) < 1e-2 and relerr(d1, d0) < 1e-2
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
@@ -1339,6 +1342,35 @@ def test_resnet50_strided_deposit_same_gradients(K):
     assert res[False][0] == res[True][0]
     for n, g0 in res[False][1].items():
         assert relerr(res[True][1][n], g0) < 1e-5, n
+
+
+@pytest.mark.parametrize("shape", [(24, 56, 56, 128, 256, 3, 1, 1), (40, 28, 28, 512, 256, 1, 1, 0),
+                                   (16, 30, 30, 256, 512, 3, 2, 1), (9, 20, 20, 64, 320, 3, 1, 1)])
+def test_big_tile_persistent_identical(K, shape):
+    """Persistent big-tile workgroups (tg_big_persist = 1: one per CU, several tiles each -- these
+    grids have 1.1-5 tiles per CU) == one workgroup per tile, bit for bit: forward + BN statistics
+    and the data gradient (stride-2 parity classes included)."""
+    N, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(0)
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co).to(DEV)
+    wb, wt = K.weight_prep(w.float(), 0, True)
+    outs = []
+    try:
+        K.set_tuning(tslot("tg_big"), 1)
+        for persist in (0, 1):
+            K.set_tuning(tslot("tg_big_persist"), persist)
+            y, slabs = K.conv_fwd(x, wb, s, p, True)
+            dx = K.conv_dgrad(dy, wt, H, W, s, p)
+            torch.cuda.synchronize()
+            outs.append((y, slabs.clone(), dx))
+    finally:
+        K.set_tuning(tslot("tg_big"), 0)
+        K.set_tuning(tslot("tg_big_persist"), 0)
+    (y0, s0, d0), (y1, s1, d1) = outs
+    assert torch.equal(y0, y1) and torch.equal(s0, s1) and torch.equal(d0, d1)
 
 
 @pytest.mark.parametrize("shape", [(2, 56, 56, 128, 128, 3), (3, 14, 14, 512, 256, 3), (2, 13, 13, 64, 256, 1)])
