@@ -7,6 +7,7 @@
 // serves every output.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <torch/library.h>
 
 #include <mutex>
@@ -31,6 +32,16 @@ namespace {
   CHECK_BF16(t)
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+// kernel scratch from PyTorch's caching allocator: stream-ordered reuse, and a HIP-graph capture
+// takes it from the graph's private pool (registered once at library load)
+struct WorkspaceRegistration {
+  WorkspaceRegistration() {
+    dcp::set_workspace_allocator(
+        [](size_t n, hipStream_t s) -> void* { return c10::hip::HIPCachingAllocator::raw_alloc_with_stream(n, s); },
+        [](void* p) { c10::hip::HIPCachingAllocator::raw_delete(p); });
+  }
+} g_workspace_registration;
 
 // fork / join events of the parity-class streams (conv_dgrad stride 2), one set per device; reused
 // call after call (an event re-recorded after every wait on it was issued, stream-ordered)

@@ -46,6 +46,14 @@ namespace dcp {
 
 int g_tune[kTuneSlots] = {0};
 static long long* g_tg_stamps = nullptr;
+// stream-ordered device workspace (the framework registers PyTorch's caching allocator: capture-safe,
+// freed blocks reused only by later work on the same stream)
+static WorkspaceAlloc g_ws_alloc = nullptr;
+static WorkspaceFree g_ws_free = nullptr;
+void set_workspace_allocator(WorkspaceAlloc a, WorkspaceFree f) {
+  g_ws_alloc = a;
+  g_ws_free = f;
+}
 void set_tg_stamps(long long* p) { g_tg_stamps = p; }
 
 struct TapGemmParams {
@@ -84,6 +92,12 @@ struct TapGemmParams {
   const float* pscale;
   const float* pshift;
   int persist;  // big tile: 1 = persistent workgroups (g_tune[kTgBigPersist])
+  // big tile, stream-K (sk_ws != nullptr): the grid's workgroups split the tiles' k-steps evenly;
+  // a tile cut between workgroups g and g+1 is finished by g, which adds g+1's fp32 partial
+  // (slot g+1 of sk_ws, published by sk_flags[g+1]) before the epilogue.  Flags zeroed per launch.
+  f32x4* sk_ws;
+  uint32_t* sk_flags;
+  int sk_on;  // host side: stream-K requested for this launch (launch_big allocates sk_ws / sk_flags)
   // timing instrumentation only (g_tune[kAblate] & 16, tools/pp_stamps.py): per-wave s_memtime at
   // every ping-pong barrier of workgroups 0..7, [wg][wave][kStampSlots] int64; slot kStampSlots-1
   // holds the wave's HW_ID register (SIMD / CU placement)
@@ -749,7 +763,261 @@ tap_gemm_kernel(const TapGemmParams p) {
 // slower on every R50 shape, profiles/r4/big4_tile_ab_b1024.txt, and was removed)
 template <int WM, int WN, int NS, int EPI, int CFW = 4>
 __global__ void __launch_bounds__(64 * WM * WN, 2)
-tap_gemm_big_kernel(const TapGemmParams p0) {
+tap_gemm_big_kernel(const TapGemmParams p) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int BM = 128 * WM, BN = 16 * CFW * WN, BK = 32;
+  constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;  // 64-byte rows, 16 rows per LDS-DMA
+  constexpr int AI = BM / (NW * RPI), BI = BN / (NW * RPI), LPT = AI + BI;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int QN = BN / 128, NQ = WM * QN, NG = NT / 256, QPG = NQ / NG;  // epilogue quadrants
+  static_assert(AI >= 1 && BI >= 1 && AI * NW * RPI == BM && BI * NW * RPI == BN, "LDS-DMA split");
+  static_assert(BN % 128 == 0 && NT % 256 == 0 && NQ % NG == 0 && NS >= 3, "tile geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const uint32_t ntn = (p.Co + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const uint32_t bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const uint32_t tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // per-slot source pointers + tap-validity masks (as tap_gemm_kernel's FAST path); rows past M
+  // and channels past Co read a clamped valid row and are never stored or counted
+  const bf16* fa_ptr[AI];
+  uint32_t fa_vm[AI];
+  const bf16* fb_ptr[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int r = (wave * AI + i) * RPI + lane / CH;
+    const uint32_t mm = (uint32_t)min(m0 + r, p.M - 1);
+    const uint32_t q = fdiv(mm, p.div_wy);
+    const uint32_t x = mm - q * p.Wy;
+    const uint32_t n = fdiv(q, p.div_hy);
+    const uint32_t y = q - n * p.Hy;
+    const int ys = y * p.ss, xs = x * p.ss;
+    fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+    uint32_t vm = 0;
+    for (int t = 0; t < p.ntaps; ++t) {
+      const int tv = p.tap[t];
+      const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
+      vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
+    }
+    fa_vm[i] = vm;
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int r = (wave * BI + i) * RPI + lane / CH;
+    fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
+  }
+  const int tiles_per_tap = p.cpt / CH;
+  auto stage = [&](int kt, int slot) {
+    char* As = smem + slot * STAGE;
+    char* Bs = As + A_BYTES;
+    const int t = kt / tiles_per_tap;
+    const int cbase = (kt - t * tiles_per_tap) * BK;
+    const int tv = p.tap[t];
+    const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
+    const long boff = (long)tap_w(tv) * p.Cs + cbase;
+    const uint32_t tbit = 1u << t;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+      dma16_tracked(g, As + (wave * AI + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
+  };
+
+  f32x4 acc[CFW][8];  // [16-channel fragment][16-pixel fragment]
+#pragma unroll
+  for (int j = 0; j < CFW; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = p.nkt;
+  const uint32_t c = lane >> 4;
+  bf16x8 wf[CFW], af[8];
+  auto frag_w = [&](int slot) {
+    const char* Bs = smem + slot * STAGE + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < CFW; ++j)
+      wf[j] = *(const bf16x8*)(Bs + swzk<BK>(wn * (16 * CFW) + j * 16 + (lane & 15), c));
+  };
+  auto frag_a = [&](int slot, int i0) {
+    const char* As = smem + slot * STAGE;
+#pragma unroll
+    for (int i = i0; i < i0 + 4; ++i) af[i] = *(const bf16x8*)(As + swzk<BK>(wm * 128 + i * 16 + (lane & 15), c));
+  };
+  auto mfma_half = [&](int i0) {
+#pragma unroll
+    for (int j = 0; j < CFW; ++j)
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[j][i], 0, 0, 0);
+  };
+  // raw barrier: this wave's fragment reads retired first (WAR on the slot re-staged after it);
+  // the counted vmcnt before it is the RAW wait -- no vmcnt(0), the ring stays in flight
+  auto ring_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nkt) stage(i, i);
+  if (WM == 2 && p.cvar == 3 && nkt > 0) {
+    // Ping-pong (g_tune[kTgBigCvar] = 3): the two row halves of the tile are two wave groups
+    // (waves 0-3: pixel rows 0-127, waves 4-7: 128-255), and the waves of a workgroup sit on the
+    // four SIMDs one from each group.  Group 1 runs one segment behind group 0, so in every
+    // interval between two workgroup barriers one wave of each SIMD runs its MFMA segment
+    // (k-tile kt's 32 MFMAs from registers) while its partner runs a load segment (the next
+    // k-tile's 12 fragment reads and its share of a later k-tile's LDS-DMA): the matrix pipe
+    // alternates between the two instead of idling through a common read phase.
+    // Synchronisation, counting workgroup barriers b (group 0 loads k-tile kt in (2kt, 2kt+1),
+    // computes it in (2kt+1, 2kt+2); group 1 one interval later):
+    //   RAW -- every wave retires its own DMA of k-tile kt (counted vmcnt) before barrier 2kt:
+    //   group 0 at the end of its compute segment kt-1, group 1 at the end of its load segment kt-1;
+    //   WAR -- k-tile kt's slot is last read in (2kt+1, 2kt+2) (each reader waits lgkmcnt(0)
+    //   before its next barrier) and is restaged (k-tile kt+NS) in load segments after 2kt+2.
+    // Each group passes the same number of barriers: group 1 one extra at the start, group 0 one
+    // extra at the end.
+    const int grp = wm;
+    auto pp_barrier = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // The load segment issues its LDS-DMA first and its fragment reads behind it, so the DMA's
+    // address work overlaps the reads' latency.  The tap table sits in one VGPR (lane t = tap t,
+    // read with v_readlane) and the (tap, channel) of the next k-tile to stage advances with
+    // scalar selects: a scalar-memory tap lookup would make the compiler wait lgkmcnt(0) -- for the
+    // fragment reads too -- before every DMA.
+    const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
+    int st_t = (NS - 1) / tiles_per_tap, st_c = ((NS - 1) - st_t * tiles_per_tap) * BK;
+    auto stage_next = [&](int slot) {
+      char* As = smem + slot * STAGE;
+      char* Bs = As + A_BYTES;
+      const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
+      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
+      const long boff = (long)tap_w(tv) * p.Cs + st_c;
+      const uint32_t tbit = 1u << st_t;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+        dma16_tracked(g, As + (wave * AI + i) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
+      st_c += BK;
+      const bool wrap = st_c >= p.Cs;
+      st_t += wrap ? 1 : 0;
+      st_c = wrap ? 0 : st_c;
+    };
+    wait_vmcnt(LPT * min(NS - 2, nkt - 1));  // k-tile 0 (this wave's share)
+    pp_barrier();                            // ... every wave's
+    if (grp == 1) pp_barrier();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int slot = kt % NS;
+      if (kt + NS - 1 < nkt && !(p.ablate & 1)) stage_next((kt + NS - 1) % NS);
+      __builtin_amdgcn_sched_barrier(0);
+      frag_w(slot);
+      frag_a(slot, 0);
+      frag_a(slot, 4);
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      if (!(p.ablate & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
+        mfma_half(0);
+        mfma_half(4);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
+      pp_barrier();
+    }
+    if (grp == 0) pp_barrier();
+  } else if (p.cvar == 2) {
+    // g_tune[kTgBigCvar] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
+    for (int kt = 0; kt < nkt; ++kt) {
+      wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));  // k-tile kt landed (this wave's share)
+      ring_barrier();  // ... for every wave; slot kt-1 is free
+      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      frag_w(kt % NS);
+      frag_a(kt % NS, 0);
+      frag_a(kt % NS, 4);
+      mfma_half(0);
+      mfma_half(4);
+    }
+  } else if (nkt > 0) {
+    // default: the fragments of k-tile kt+1 are read across the barrier, behind the MFMAs of k-tile
+    // kt -- pixel fragments 0..3 after its first half, the rest after its second half (measured
+    // 2-4 % faster than reading them after the barrier: profiles/r3/big_tile_ab_b1024_pipelined.txt)
+    wait_vmcnt(LPT * min(NS - 2, nkt - 1));
+    ring_barrier();
+    if (NS - 1 < nkt) stage(NS - 1, NS - 1);
+    frag_w(0);
+    frag_a(0, 0);
+    frag_a(0, 4);
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int nx = (kt + 1) % NS;
+      mfma_half(0);
+      if (kt + 1 < nkt) {
+        wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));  // k-tile kt+1 landed (this wave's share)
+        ring_barrier();  // ... for every wave; every read of slot kt retired: re-stage it
+        if (kt + NS < nkt) stage(kt + NS, kt % NS);
+        frag_a(nx, 0);
+      }
+      mfma_half(4);
+      if (kt + 1 < nkt) {
+        frag_w(nx);
+        frag_a(nx, 4);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (p.ablate & 4) return;  // timing ablation: no epilogue
+
+  // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
+  {
+    char* Q = smem + (wm * QN + (wn * 16 * CFW) / 128) * 32768;
+    const uint32_t cb = (wn * 16 * CFW) % 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t pl = i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < CFW; ++j) {
+        const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+        *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
+      }
+    }
+  }
+  __syncthreads();
+  // group g (threads 256g ..) stores quadrants g*QPG ..; every group passes the same barriers
+  // (tile_stats128_vv's), so the quadrant loop stays uniform
+  const int g = tid >> 8, gtid = tid & 255;
+#pragma unroll
+  for (int k = 0; k < QPG; ++k) {
+    const int q = g * QPG + k;
+    tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
+  }
+}
+
+// The same tile as a loop over work segments: persistent workgroups (tg_big_persist) or stream-K
+// (p.sk_ws).  A separate kernel because the loop's carried scalars cost ~50 SGPRs spilled to VGPR
+// lanes, and every attempt to fold the one-tile kernel above into it (opaque per-tile parameter
+// pointers, laundered lane index) either spilled or copied the parameters to scratch and ran the
+// big tile 2.5x slower (d4d972e: 512-channel 7x7 3x3 220 -> 645 us).
+template <int WM, int WN, int NS, int EPI, int CFW = 4>
+__global__ void __launch_bounds__(64 * WM * WN, 2)
+tap_gemm_big_loop_kernel(const TapGemmParams p0) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int BM = 128 * WM, BN = 16 * CFW * WN, BK = 32;
   constexpr int ROWB = BK * 2, CH = BK / 8, RPI = 64 / CH;  // 64-byte rows, 16 rows per LDS-DMA
@@ -766,12 +1034,61 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
   // the next tile's ring fills, and no workgroup is re-dispatched per tile
   const uint32_t ntiles = ntm * ntn;
   const uint32_t tstep = p0.persist ? gridDim.x : ntiles;
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += tstep) {
-    // the parameters re-read per tile through an opaque pointer (scalar-cache hits): hoisted out
-    // of the tile loop they stay live in SGPRs across it and spill
-    const TapGemmParams* pcur = &p0;
-    asm volatile("" : "+s"(pcur));
-    const TapGemmParams& p = *pcur;
+  // Stream-K (p.sk_ws set; one workgroup per CU slot, ntiles >= gridDim.x): the ntiles x nkt
+  // k-steps are cut into gridDim.x equal contiguous ranges, so every workgroup does the same
+  // MFMA work and no tail round of partly idle CUs remains (784 256 x 256 tiles on 256 CUs were
+  // 4 rounds for 3.06 rounds of work).  A range covers whole tiles plus at most a tail piece of the
+  // tile where it begins (k-steps kb..nkt: published as an fp32 partial, then the next segment) and
+  // a head piece of the tile where it ends (k-steps 0..ke: the partial of the next workgroup added,
+  // then the tile's normal epilogue).  The tail piece is this workgroup's FIRST segment and the head
+  // piece its LAST, so the partial is waited for only after a whole range of work.
+  const bool sk = p0.sk_ws != nullptr;
+  const int nkt_all = p0.nkt;
+  // (32-bit: the host checks ntiles x nkt < 2^31; a 64-bit division here costs ~20 SGPRs)
+  uint32_t sk_it = 0, sk_end = 0;
+  if (sk) {
+    const uint64_t T = (uint64_t)ntiles * (uint32_t)nkt_all;
+    sk_it = (uint32_t)(blockIdx.x * T / gridDim.x);
+    sk_end = (uint32_t)((blockIdx.x + 1) * T / gridDim.x);
+  }
+  uint32_t next_tile = blockIdx.x;
+  for (;;) {
+    uint32_t tile;
+    int kb, ke;
+    if (sk) {
+      if (sk_it >= sk_end) break;
+      tile = sk_it / (uint32_t)nkt_all;
+      kb = (int)(sk_it - tile * (uint32_t)nkt_all);
+      ke = min(nkt_all, kb + (int)(sk_end - sk_it));
+      sk_it += (uint32_t)(ke - kb);
+    } else {
+      if (next_tile >= ntiles) break;
+      tile = next_tile;
+      kb = 0;
+      ke = nkt_all;
+      next_tile += tstep;
+    }
+    // The parameters re-read per tile from the kernel-argument segment (scalar loads) through an
+    // opaque constant-address-space pointer, into a local copy the compiler splits into scalars:
+    // nothing derived from them is carried across the loop (held across it, they spilled ~60
+    // SGPRs to VGPR lanes: 190 v_readlane in the kernel).  Laundering the address of the by-value
+    // argument instead copies the whole struct into per-lane scratch.  The tap table, indexed
+    // dynamically, is read through the pointer (pk->tap[t]), never from the copy.
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) TapGemmParams* KArgPtr;
+    KArgPtr pk = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pk));
+    const TapGemmParams p = *pk;
+#else  // (the host pass only needs the kernel to type-check)
+    const TapGemmParams* pk = &p0;
+    const TapGemmParams& p = p0;
+#endif
+    // the k-loop's scalars, read once per tile and pinned in registers: an asm result cannot be
+    // re-loaded from the argument segment inside the k-loop, where each scalar load's lgkmcnt wait
+    // would also drain the LDS fragment reads
+    int kWs = p.Ws, kCs = p.Cs, kabl = p.ablate;
+    const bf16* kzero = p.zero;
+    asm volatile("" : "+s"(kWs), "+s"(kCs), "+s"(kabl), "+s"(kzero));
     // the lane index likewise: every lane-derived LDS / global offset is recomputed per tile
     // instead of being hoisted and held in VGPRs through the k-loop
     int tid = threadIdx.x;
@@ -779,7 +1096,8 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    const uint32_t bid = xcd_remap(tile, ntiles);
+    // (stream-K: a workgroup's consecutive tiles are neighbours already -- one XCD's L2 sees them)
+    const uint32_t bid = sk ? tile : xcd_remap(tile, ntiles);
     const uint32_t tn = bid % ntn, tm = bid / ntn;
     const int m0 = tm * BM, n0 = tn * BN;
 
@@ -800,7 +1118,7 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       fa_ptr[i] = p.src + ((size_t)n * p.Hs * p.Ws + (size_t)ys * p.Ws + xs) * p.Cs + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
       uint32_t vm = 0;
       for (int t = 0; t < p.ntaps; ++t) {
-        const int tv = p.tap[t];
+        const int tv = pk->tap[t];
         const int hi = ys + tap_dy(tv), wi = xs + tap_dx(tv);
         vm |= ((unsigned)hi < (unsigned)p.Hs && (unsigned)wi < (unsigned)p.Ws) ? (1u << t) : 0u;
       }
@@ -812,18 +1130,20 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       fb_ptr[i] = p.wt + (size_t)min(n0 + r, p.Co - 1) * p.ldw + ((lane % CH) ^ swz_chunk<BK>(r)) * 8;
     }
     const int tiles_per_tap = p.cpt / CH;
+    // k-steps kb .. ke-1 of the tile; the loops below count kt from 0 (= k-step kb)
     auto stage = [&](int kt, int slot) {
       char* As = smem + slot * STAGE;
       char* Bs = As + A_BYTES;
-      const int t = kt / tiles_per_tap;
-      const int cbase = (kt - t * tiles_per_tap) * BK;
-      const int tv = p.tap[t];
-      const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + cbase;  // wave-uniform
-      const long boff = (long)tap_w(tv) * p.Cs + cbase;
+      const int ka = kb + kt;
+      const int t = ka / tiles_per_tap;
+      const int cbase = (ka - t * tiles_per_tap) * BK;
+      const int tv = pk->tap[t];
+      const long aoff = (long)(tap_dy(tv) * kWs + tap_dx(tv)) * kCs + cbase;  // wave-uniform
+      const long boff = (long)tap_w(tv) * kCs + cbase;
       const uint32_t tbit = 1u << t;
   #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+        const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : kzero;
         dma16_tracked(g, As + (wave * AI + i) * 1024);
       }
   #pragma unroll
@@ -837,7 +1157,7 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
   #pragma unroll
       for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nkt = p.nkt;
+    const int nkt = ke - kb;
     const uint32_t c = lane >> 4;
     bf16x8 wf[CFW], af[8];
     auto frag_w = [&](int slot) {
@@ -885,29 +1205,10 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       // Each group passes the same number of barriers: group 1 one extra at the start, group 0 one
       // extra at the end.
       const int grp = wm;
-      // issue priority (tg_big_cvar): 3 = the MFMA segment at priority 1 (flipped per segment),
-      // 4 = no priorities, 5 = waves 4-7 (the arbitration losers) at priority 1 for the whole loop
-      const int prio = p.cvar;
-      if (prio == 5 && grp == 1) __builtin_amdgcn_s_setprio(1);
-      long long* stp = (p.stamps != nullptr && blockIdx.x < 8 && tile == blockIdx.x)
-                           ? p.stamps + ((size_t)blockIdx.x * NW + wave) * kStampSlots : nullptr;
-      int nst = 0;
-      if (stp != nullptr && lane == 0) stp[kStampSlots - 1] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
       auto pp_barrier = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
-        if (stp != nullptr && nst < kStampSlots - 2) {  // arrival time, then release time
-          const long long t0 = __builtin_amdgcn_s_memtime();
-          __builtin_amdgcn_s_barrier();
-          const long long t1 = __builtin_amdgcn_s_memtime();
-          if (lane == 0) {
-            stp[nst] = t0;
-            stp[nst + 1] = t1;
-          }
-          nst += 2;
-        } else {
-          __builtin_amdgcn_s_barrier();
-        }
+        __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       };
       // The load segment issues its LDS-DMA first and its fragment reads behind it, so the DMA's
@@ -915,24 +1216,24 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       // read with v_readlane) and the (tap, channel) of the next k-tile to stage advances with
       // scalar selects: a scalar-memory tap lookup would make the compiler wait lgkmcnt(0) -- for the
       // fragment reads too -- before every DMA.
-      const int tap_lane = lane < p.ntaps ? p.tap[lane] : 0;
-      int st_t = (NS - 1) / tiles_per_tap, st_c = ((NS - 1) - st_t * tiles_per_tap) * BK;
+      const int tap_lane = lane < p.ntaps ? pk->tap[lane] : 0;
+      int st_t = (kb + NS - 1) / tiles_per_tap, st_c = ((kb + NS - 1) - st_t * tiles_per_tap) * BK;
       auto stage_next = [&](int slot) {
         char* As = smem + slot * STAGE;
         char* Bs = As + A_BYTES;
         const int tv = __builtin_amdgcn_readlane(tap_lane, st_t);
-        const long aoff = (long)(tap_dy(tv) * p.Ws + tap_dx(tv)) * p.Cs + st_c;  // wave-uniform
-        const long boff = (long)tap_w(tv) * p.Cs + st_c;
+        const long aoff = (long)(tap_dy(tv) * kWs + tap_dx(tv)) * kCs + st_c;  // wave-uniform
+        const long boff = (long)tap_w(tv) * kCs + st_c;
         const uint32_t tbit = 1u << st_t;
   #pragma unroll
         for (int i = 0; i < AI; ++i) {
-          const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : p.zero;
+          const bf16* g = (fa_vm[i] & tbit) ? fa_ptr[i] + aoff : kzero;
           dma16_tracked(g, As + (wave * AI + i) * 1024);
         }
   #pragma unroll
         for (int i = 0; i < BI; ++i) dma16_tracked((fb_ptr[i] + boff), Bs + (wave * BI + i) * 1024);
         st_c += BK;
-        const bool wrap = st_c >= p.Cs;
+        const bool wrap = st_c >= kCs;
         st_t += wrap ? 1 : 0;
         st_c = wrap ? 0 : st_c;
       };
@@ -941,7 +1242,7 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       if (grp == 1) pp_barrier();
       for (int kt = 0; kt < nkt; ++kt) {
         const int slot = kt % NS;
-        if (kt + NS - 1 < nkt && !(p.ablate & 1)) stage_next((kt + NS - 1) % NS);
+        if (kt + NS - 1 < nkt && !(kabl & 1)) stage_next((kt + NS - 1) % NS);
         __builtin_amdgcn_sched_barrier(0);
         frag_w(slot);
         frag_a(slot, 0);
@@ -949,18 +1250,17 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 1 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
         pp_barrier();
-        if (prio == 3) __builtin_amdgcn_s_setprio(1);
-        if (!(p.ablate & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
+        __builtin_amdgcn_s_setprio(1);
+        if (!(kabl & 2)) {  // timing ablations (g_tune[kAblate]): 1 no LDS-DMA, 2 no MFMA
           mfma_half(0);
           mfma_half(4);
         }
-        if (prio == 3) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 0 && kt + 1 < nkt) wait_vmcnt(LPT * min(NS - 2, nkt - 2 - kt));
         pp_barrier();
       }
       if (grp == 0) pp_barrier();
-      if (prio == 5) __builtin_amdgcn_s_setprio(0);
     } else if (p.cvar == 2) {
       // g_tune[kTgBigCvar] = 2 (A/B only): fragments read after the barrier, all 32 MFMAs behind them
       for (int kt = 0; kt < nkt; ++kt) {
@@ -1001,6 +1301,43 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (sk && kb > 0) {
+      // the tail piece of a tile that workgroup blockIdx.x - 1 finishes: publish the fp32 partial
+      // in register order (slot blockIdx.x; lane-contiguous 16-byte stores, 1 KB per instruction)
+      // WRITE-THROUGH (sc1): no release fence, whose L2 write-back stalled every workgroup at the
+      // start of its range; every storing wave drained, a barrier, then one lane's flag
+      // (Guideline 16 R1)
+      __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(p.sk_ws + ((size_t)blockIdx.x * NW + wave) * (CFW * 8 * 64)), (short)0, 0x7fffffff, 0x00020000);
+  #pragma unroll
+      for (int j = 0; j < CFW; ++j)
+  #pragma unroll
+        for (int i = 0; i < 8; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[j][i]), rs,
+                                                 ((j * 8 + i) * 64 + lane) * 16, 0, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(p.sk_flags + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    const f32x4* skp = nullptr;  // the partial to add in the epilogue (head piece of a cut tile)
+    if (sk && ke < nkt_all) {
+      // the head piece: wait for workgroup blockIdx.x + 1's partial of the same tile (published at
+      // the start of its range, so normally long done), one agent-scope acquire, add it
+      if (tid == 0) {
+        // bounded spin (the grid is at most one workgroup per CU slot, and the publisher waits on
+        // nothing before publishing, so it only has to become resident)
+        for (uint32_t spins = 0;
+             __hip_atomic_load(p.sk_flags + blockIdx.x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             spins < (1u << 26);
+             ++spins)
+          __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      skp = p.sk_ws + ((size_t)(blockIdx.x + 1) * NW + wave) * (CFW * 8 * 64) + lane;
+    }
     if (p.ablate & 4) continue;  // timing ablation: no epilogue
 
     // ---- epilogue: quadrant (h, qc) = pixels h*128.., channels qc*128.. at smem + (h*QN + qc) * 32 KB ----
@@ -1013,9 +1350,11 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
   #pragma unroll
         for (int j = 0; j < CFW; ++j) {
           const uint32_t cl = cb + j * 16 + (lane >> 4) * 4;
+          f32x4 a = acc[j][i];
+          if (skp != nullptr) a += skp[(j * 8 + i) * 64];  // fp32 partial, before the one rounding
           bf16x4 o;
   #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[j][i][r]);
+          for (int r = 0; r < 4; ++r) o[r] = f2bf(a[r]);
           *LDS_PTR(bf16x4, Q + eimg_off8<16>(pl, cl)) = o;
         }
       }
@@ -1029,7 +1368,7 @@ tap_gemm_big_kernel(const TapGemmParams p0) {
       const int q = g * QPG + k;
       tg_image_store<128, EPI>(p, smem + q * 32768, m0 + (q / QN) * 128, n0 + (q % QN) * 128, gtid);
     }
-    if (p.persist) __syncthreads();  // every image read retired before the ring is refilled
+    __syncthreads();  // every image read retired before the ring is refilled
   }
 }
 
@@ -1588,19 +1927,47 @@ static void launch_big(TapGemmParams p, int epi, hipStream_t stream) {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
   }
-  const int grid = p.persist ? std::min(tiles, ncu) : tiles;
+  int grid = p.persist ? std::min(tiles, ncu) : tiles;
+  // stream-K: one workgroup per CU slot (LDS-limited: 1 per CU for 256 x 256, 2 for 256 x 128), at
+  // most one tile's worth of ranges per workgroup boundary -> needs tiles >= slots
+  p.sk_ws = nullptr;
+  p.sk_flags = nullptr;
+  void* ws = nullptr;
+  const int per_cu = std::max(1, (int)(160 * 1024 / lds));
+  const int slots = p.sk_on >= 3 ? std::min(p.sk_on, ncu * per_cu) : ncu * per_cu;
+  if (p.sk_on && tiles >= slots && (long)tiles * p.nkt < (1l << 31) && g_ws_alloc != nullptr) {
+    const size_t flag_bytes = ((size_t)slots * 4 + 255) / 256 * 256;
+    const size_t part_bytes = (size_t)slots * (64 * WM * WN) * CFW * 8 * 16;  // per lane: CFW x 8 f32x4
+    ws = g_ws_alloc(flag_bytes + part_bytes, stream);
+    if (ws != nullptr) {
+      p.sk_flags = (uint32_t*)ws;
+      p.sk_ws = (f32x4*)((char*)ws + flag_bytes);
+      (void)hipMemsetAsync(ws, 0, flag_bytes, stream);
+      grid = slots;
+    }
+  }
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 0, CFW>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void*)tap_gemm_big_kernel<WM, WN, NS, 1, CFW>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_big_loop_kernel<WM, WN, NS, 0, CFW>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)tap_gemm_big_loop_kernel<WM, WN, NS, 1, CFW>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  if (epi == 1)
-    hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 1, CFW>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
-  else
-    hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0, CFW>), dim3(grid), dim3(64 * WM * WN), lds, stream, p);
+  const bool loop = p.persist || p.sk_ws != nullptr;
+  const dim3 blk(64 * WM * WN);
+  if (epi == 1) {
+    if (loop) hipLaunchKernelGGL((tap_gemm_big_loop_kernel<WM, WN, NS, 1, CFW>), dim3(grid), blk, lds, stream, p);
+    else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 1, CFW>), dim3(grid), blk, lds, stream, p);
+  } else {
+    if (loop) hipLaunchKernelGGL((tap_gemm_big_loop_kernel<WM, WN, NS, 0, CFW>), dim3(grid), blk, lds, stream, p);
+    else hipLaunchKernelGGL((tap_gemm_big_kernel<WM, WN, NS, 0, CFW>), dim3(grid), blk, lds, stream, p);
+  }
+  if (ws != nullptr) g_ws_free(ws);  // stream-ordered: reused only by later work on this stream
 }
 
 // 0 = the 128-row kernels, 1 = 256 x 256 big tile, 2 = 256 x 128 big tile.  mode = g_tune[kTgBig]
@@ -1673,6 +2040,10 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   p.stamps = (p.ablate & 16) ? g_tg_stamps : nullptr;
   p.cvar = g_tune[kTgBigCvar];
   p.persist = g_tune[kTgBigPersist];
+  // (values >= 3: stream-K over exactly that many workgroups -- tests on small shapes)
+  p.sk_on = g_tune[kTgBigSK] == 1 ? 1 : (g_tune[kTgBigSK] >= 3 ? g_tune[kTgBigSK] : 0);
+  p.sk_ws = nullptr;
+  p.sk_flags = nullptr;
   int bn = Co <= 64 ? 64 : 128, ns = 2;
   // a short grid (< 1.5 rounds of 256 CUs at 128-channel tiles: batch 32-128 from stage 2 on, the
   // stride-2 parity classes, the linear heads) takes 64-channel tiles, twice the workgroups: the
@@ -1773,7 +2144,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 // order (fp32 rounding).  Off by default (the default path is bit-reproducible run to run).
 // ---------------------------------------------------------------------------
 struct TgCfg {
-  int bn, ns, bk, big, cvar;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar overrides (0 = the heuristic's)
+  int bn, ns, bk, big, cvar, sk;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar, tg_big_sk overrides (0 = the heuristic's)
 };
 static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 0},   // heuristic
@@ -1788,6 +2159,8 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 1},   // 256 x 256 big tile (Co >= 256)
     {256, 2, 32, 2},  // 256-channel tiles, 32-deep k-tiles (2-3 % on two R50 shapes: profiles/r4/bn256_tile_ab_b1024.txt)
     {0, 0, 0, 1, 1},  // 256 x 256 big tile, lockstep schedule (the ping-pong one is the tile's default)
+    {0, 0, 0, 1, 0, 1},  // 256 x 256 big tile, stream-K
+    {0, 0, 0, 3, 0, 1},  // 256 x 128 big tile, stream-K
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };
@@ -1795,17 +2168,17 @@ static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
 
 struct TuneOverride {
-  static constexpr int kSlots[5] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar};
-  int saved[5];
+  static constexpr int kSlots[6] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar, kTgBigSK};
+  int saved[6];
   explicit TuneOverride(const TgCfg& c) {
-    const int v[5] = {c.bn, c.ns, c.bk, c.big, c.cvar};
-    for (int i = 0; i < 5; ++i) {
+    const int v[6] = {c.bn, c.ns, c.bk, c.big, c.cvar, c.sk};
+    for (int i = 0; i < 6; ++i) {
       saved[i] = g_tune[kSlots[i]];
       g_tune[kSlots[i]] = v[i];
     }
   }
   ~TuneOverride() {
-    for (int i = 0; i < 5; ++i) g_tune[kSlots[i]] = saved[i];
+    for (int i = 0; i < 6; ++i) g_tune[kSlots[i]] = saved[i];
   }
 };
 
@@ -1827,7 +2200,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
   // (an add source aliasing the output would accumulate over the timing runs: never tuned)
-  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] ||
+  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] || g_tune[kTgBigSK] ||
       (long)N * Hy * Wy == 0 || (addsrc != nullptr && addsrc == dst)) {
     run();
     return;

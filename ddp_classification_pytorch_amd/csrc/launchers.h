@@ -56,6 +56,11 @@ struct AffineEpi {
 // timing instrumentation of the ping-pong big tile (g_tune[kAblate] & 16): device buffer of
 // 8 x 8 x 72 int64 (nullptr: off)
 void set_tg_stamps(long long* p);
+// stream-ordered device workspace for kernels that need scratch (stream-K partials): bindings.cpp
+// registers PyTorch's caching allocator (raw_alloc_with_stream / raw_delete)
+using WorkspaceAlloc = void* (*)(size_t bytes, hipStream_t stream);
+using WorkspaceFree = void (*)(void* ptr);
+void set_workspace_allocator(WorkspaceAlloc alloc, WorkspaceFree free_fn);
 // number of problems the tap-GEMM autotuner (g_tune[kAutotune] = 1) has measured in this process
 int tap_gemm_tuned_count();
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,

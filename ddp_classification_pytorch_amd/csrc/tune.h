@@ -30,6 +30,7 @@ enum TuneSlot : int {
   kC3Variant = 19,     // direct 64->64 3x3 workgroup variant (0 = 8 waves, 1 / 2 = 4-wave, 3 / 4 = priority / phase)
   kDgradParityStreams = 20,  // stride-2 data gradient: 1 = the four parity classes on concurrent streams
   kTgBigPersist = 22,  // 256-row big tiles: 1 = persistent workgroups (one per CU, looping over tiles)
+  kTgBigSK = 23,       // 256-row big tiles, stream-K (k-steps split evenly over one workgroup per CU slot): 1 on, 2 off
   kTgBigStages = 21,   // 256 x 256 big tile: LDS-DMA ring slots (0 = 4; 5 = all 160 KB, three k-tiles in flight)
   kTgBig = 24,         // big-tile tap GEMM: 1 on (256 x 256 / 256 x 128), 2 off, 3 = 256 x 128 only
   kAutotune = 25,      // per-shape autotuning of the conv configurations (DCP_AUTOTUNE)
@@ -55,7 +56,7 @@ constexpr TuneSlotName kTuneSlotNames[] = {
     {"wg3x3", kWg3x3},               {"gconv_sg", kGconvSG},         {"stem_ablate", kStemAblate},
     {"c3_off", kC3Off},              {"c3_variant", kC3Variant},     {"tg_big", kTgBig},
     {"dgrad_parity_streams", kDgradParityStreams}, {"tg_big_stages", kTgBigStages},
-    {"tg_big_persist", kTgBigPersist},
+    {"tg_big_persist", kTgBigPersist}, {"tg_big_sk", kTgBigSK},
     {"autotune", kAutotune},         {"wg_split_cap", kWgSplitCap},  {"bn_bwd_cap", kBnBwdCap},
     {"row_reduce", kRowReduce},      {"c3_epilogue", kC3Epilogue},   {"c3_window_kb", kC3WindowKB},
 };

@@ -84,7 +84,16 @@ def _check_capture_safe_pg():
     hipErrorCapturedEvent and the watchdog aborts the process (the intermittent abort of
     tests/test_ddp_gpu.py::test_bench_force_ddp_rccl_world1[True] in round 4).  With fresh events
     per work no event the watchdog polls is ever recorded inside a capture, and the captured works
-    themselves never reach the watchdog's list, so no timing condition remains to wait for."""
+    themselves never reach the watchdog's list.
+
+    That alone is not enough (round 5: the same abort in
+    test_main_graph_force_ddp_side_stream_matches_eager, at the recapture after an epoch's eager
+    validation collectives): a capture that issues a collective makes the group's RCCL stream join
+    the capture, and HIP refuses a query of ANY event last recorded on that stream -- including
+    the end event of an eager work the watchdog has not yet retired (it sweeps its list every
+    ~100 ms).  So before the capture every eager work must have left every group's watchdog list:
+    ``_wait_for_pending_works`` returns exactly when the list is empty, an observable condition
+    instead of a sleep."""
     if not torch.distributed.is_initialized() or torch.distributed.get_backend() != "nccl":
         return
     if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE", "1") not in ("0", "false", "False"):
@@ -92,6 +101,22 @@ def _check_capture_safe_pg():
                            "process-group creation: call parallel.ddp.graph_safe_nccl_env() before "
                            "init_process_group (bench.py --graph and main.py --graph do)")
     torch.cuda.synchronize()
+    drain_rccl_watchdogs()
+
+
+def drain_rccl_watchdogs():
+    """Block until the watchdog of every RCCL process group (the default group, the SyncBN group,
+    any subgroup) has retired all its eager works (call after a device synchronize, so they are
+    complete; the wait is then at most one watchdog sweep)."""
+    from torch.distributed import distributed_c10d as c10d
+
+    for pg in list(c10d._world.pg_map):
+        try:
+            if c10d.get_backend(pg) != "nccl":
+                continue
+        except (RuntimeError, ValueError):
+            continue
+        pg._wait_for_pending_works()
 
 
 class GraphedStep:

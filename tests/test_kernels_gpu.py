@@ -1480,3 +1480,45 @@ def test_resnet50_bn_prologue3x3_same_training_step(K):
     for n, g0 in ref[1].items():
         e_off, e_on = relerr(res[False][1][n], g0), relerr(res[True][1][n], g0)
         assert e_on <= 1.5 * e_off + 2e-2, (n, e_on, e_off)
+
+
+@pytest.mark.parametrize("shape", [(4, 28, 28, 256, 256, 3, 1, 1), (6, 27, 25, 128, 384, 3, 2, 1),
+                                   (6, 14, 14, 512, 512, 3, 1, 1), (5, 28, 28, 256, 512, 1, 2, 0)])
+@pytest.mark.parametrize("mode", [1, 3])
+@pytest.mark.parametrize("sk", [3, 5, 7])
+def test_big_tile_stream_k_matches(K, shape, mode, sk):
+    """Stream-K big tiles (tg_big_sk >= 3: the tiles' k-steps split evenly over exactly `sk`
+    workgroups, so tiles are cut between workgroups at arbitrary k-steps, the tail piece published
+    as an fp32 partial and added by the workgroup that finishes the tile) == the same tile without
+    stream-K and the fp32 reference: forward with BN statistics and the data gradient (stride-2
+    shapes: the parity classes, each with its own k-step count)."""
+    N, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(1)
+    x = rnd(N, H, W, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci)).to(DEV)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Wo, Co).to(DEV)
+    wb, wt = K.weight_prep(w.float(), 0, True)
+    outs = []
+    try:
+        K.set_tuning(tslot("tg_big"), mode)
+        for v in (2, sk):
+            K.set_tuning(tslot("tg_big_sk"), v)
+            y, slabs = K.conv_fwd(x, wb, s, p, True)
+            st = K.bn_stats(y, slabs)
+            dx = K.conv_dgrad(dy, wt, H, W, s, p)
+            torch.cuda.synchronize()
+            outs.append((y.float().cpu(), st.cpu(), dx.float().cpu()))
+    finally:
+        K.set_tuning(tslot("tg_big"), 0)
+        K.set_tuning(tslot("tg_big_sk"), 0)
+    (y0, s0, d0), (y1, s1, d1) = outs
+    # a split tile sums two fp32 partial chains: equal up to fp32 rounding before the bf16 store
+    assert relerr(y1, y0) < 4e-3 and relerr(d1, d0) < 4e-3
+    assert relerr(s1[0, 1:], s0[0, 1:]) < 1e-3
+    yr, _ = _ref.conv_fwd(x.float().cpu(), w.float().cpu(), s, p, False)
+    assert relerr(y1, yr) < 1e-2
+    sr = _ref.bn_stats(y1, None)
+    assert relerr(s1[0, 1], sr[0, 1]) < 1e-4 and relerr(s1[0, 2], sr[0, 2]) < 1e-4
+    dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().cpu().permute(3, 1, 2, 0), H, W, s, p)
+    assert relerr(d1, dxr) < 1e-2
