@@ -1725,18 +1725,6 @@ void set_tuning(int64_t idx, int64_t value) {
   dcp::g_tune[idx] = (int)value;
 }
 
-// timing instrumentation only: the ping-pong big tile stamps its barriers into `buf` (int64,
-// >= 8 * 8 * 72 entries) while g_tune[kAblate] & 16 is set (tools/pp_stamps.py)
-void set_tg_stamps(const optional<Tensor>& buf) {
-  if (!buf.has_value()) {
-    dcp::set_tg_stamps(nullptr);
-    return;
-  }
-  CHECK_DEV(*buf);
-  TORCH_CHECK(buf->scalar_type() == at::kLong && buf->numel() >= 8 * 8 * 72 && buf->is_contiguous(), "stamp buffer");
-  dcp::set_tg_stamps(reinterpret_cast<long long*>(buf->data_ptr<int64_t>()));
-}
-
 // "name=slot;..." of every named slot (tune.h): the Python mirror (tuning.py) is checked against it
 std::string tuning_slots() {
   std::string out;
@@ -1747,7 +1735,6 @@ std::string tuning_slots() {
 TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
   m.def("tuning_slots() -> str", &tuning_slots);
-  m.def("set_tg_stamps(Tensor? buf) -> ()", &set_tg_stamps);
   m.def("autotune_entries() -> int", &autotune_entries);
   m.def("table_fill(Tensor host, Tensor device_like) -> Tensor", &table_fill);
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);

@@ -45,7 +45,6 @@
 namespace dcp {
 
 int g_tune[kTuneSlots] = {0};
-static long long* g_tg_stamps = nullptr;
 // stream-ordered device workspace (the framework registers PyTorch's caching allocator: capture-safe,
 // freed blocks reused only by later work on the same stream)
 static WorkspaceAlloc g_ws_alloc = nullptr;
@@ -54,7 +53,6 @@ void set_workspace_allocator(WorkspaceAlloc a, WorkspaceFree f) {
   g_ws_alloc = a;
   g_ws_free = f;
 }
-void set_tg_stamps(long long* p) { g_tg_stamps = p; }
 
 struct TapGemmParams {
   const bf16* src;   // [N][Hs][Ws][Cs]
@@ -98,12 +96,7 @@ struct TapGemmParams {
   f32x4* sk_ws;
   uint32_t* sk_flags;
   int sk_on;  // host side: stream-K requested for this launch (launch_big allocates sk_ws / sk_flags)
-  // timing instrumentation only (g_tune[kAblate] & 16, tools/pp_stamps.py): per-wave s_memtime at
-  // every ping-pong barrier of workgroups 0..7, [wg][wave][kStampSlots] int64; slot kStampSlots-1
-  // holds the wave's HW_ID register (SIMD / CU placement)
-  long long* stamps;
 };
-constexpr int kStampSlots = 72;
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
 __device__ __forceinline__ int tap_dx(int v) { return (int)(int8_t)((v >> 8) & 0xff); }
@@ -2037,7 +2030,6 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // heuristic (tuning experiments only)
   const int env_bn = g_tune[kTgTileN], env_ns = g_tune[kTgStages];
   p.ablate = g_tune[kAblate];
-  p.stamps = (p.ablate & 16) ? g_tg_stamps : nullptr;
   p.cvar = g_tune[kTgBigCvar];
   p.persist = g_tune[kTgBigPersist];
   // (values >= 3: stream-K over exactly that many workgroups -- tests on small shapes)

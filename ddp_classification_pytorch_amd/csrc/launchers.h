@@ -53,9 +53,6 @@ struct AffineEpi {
   float slope;
 };
 
-// timing instrumentation of the ping-pong big tile (g_tune[kAblate] & 16): device buffer of
-// 8 x 8 x 72 int64 (nullptr: off)
-void set_tg_stamps(long long* p);
 // stream-ordered device workspace for kernels that need scratch (stream-K partials): bindings.cpp
 // registers PyTorch's caching allocator (raw_alloc_with_stream / raw_delete)
 using WorkspaceAlloc = void* (*)(size_t bytes, hipStream_t stream);

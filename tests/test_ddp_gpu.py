@@ -303,7 +303,11 @@ def test_main_graph_force_ddp_side_stream_matches_eager(tmp_path):
     common = ["--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
               "--batchsize", "16", "--synthetic-train-size", "96", "--synthetic-val-size", "32", "--epochs", "2",
               "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "SGD",
-              "--lr", "0.05", "--force-ddp", "--syncbn"]
+              "--lr", "0.05", "--force-ddp", "--syncbn",
+              # a fixed kernel choice in both runs: the autotuner picks by timing, and tiles that sum a
+              # BN slab's rows in another order are enough for two 12-step runs to drift apart
+              # (round 5: one of three runs differed by 50 % in conv1 with the autotuner on)
+              "--no-autotune"]
     outs = {}
     for tag, flag in (("eager", []), ("graph", ["--graph"])):
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
