@@ -96,6 +96,7 @@ struct TapGemmParams {
   f32x4* sk_ws;
   uint32_t* sk_flags;
   int sk_on;  // host side: stream-K requested for this launch (launch_big allocates sk_ws / sk_flags)
+  int sk_unit;  // stream-K range granularity in k-steps (divides nkt)
 };
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
@@ -1040,9 +1041,14 @@ tap_gemm_big_loop_kernel(const TapGemmParams p0) {
   // (32-bit: the host checks ntiles x nkt < 2^31; a 64-bit division here costs ~20 SGPRs)
   uint32_t sk_it = 0, sk_end = 0;
   if (sk) {
-    const uint64_t T = (uint64_t)ntiles * (uint32_t)nkt_all;
-    sk_it = (uint32_t)(blockIdx.x * T / gridDim.x);
-    sk_end = (uint32_t)((blockIdx.x + 1) * T / gridDim.x);
+    // range boundaries on multiples of sk_unit k-steps (a divisor of nkt): every workgroup starts
+    // at one of nkt / sk_unit k positions, so the workgroups of an XCD stream the same few weight
+    // slices at a time (unquantised ranges start at every k and the whole weight matrix competes
+    // for the XCD's L2: no gain at all on the 4.7 MB 512-channel 3x3)
+    const uint32_t u = (uint32_t)p0.sk_unit;
+    const uint64_t U = (uint64_t)ntiles * ((uint32_t)nkt_all / u);
+    sk_it = (uint32_t)(blockIdx.x * U / gridDim.x) * u;
+    sk_end = (uint32_t)((blockIdx.x + 1) * U / gridDim.x) * u;
   }
   uint32_t next_tile = blockIdx.x;
   for (;;) {
@@ -1377,7 +1383,7 @@ struct WgradParams {
   int Hs, Ws, Cs, Ho, Wo, ss;
   int Co, M, ldw;    // ldw = T*Cs
   int cpt, kc_total, rows_per_split;
-  int ablate;  // tuning experiments only: 8 = skip the atomic flush
+  int ablate;  // tuning experiments only: 8 = skip the atomic flush; wgrad256: 1 no k-loop staging, 2 no MFMA, 32 no partial stores
   int direct;  // 1x1 stride-1 (no padding): the input pixel of GEMM row m is m
   // PRO (direct only): the input is a BN's input x, used as relu(x * pscale[c] + pshift[c]) (K5)
   const float* pscale;
@@ -1655,7 +1661,7 @@ wgrad256_kernel(const WgradParams p) {
   }
   for (int kt = 0; kt < nkt; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
+    if (kt + 1 < nkt && !(p.ablate & 1)) stage(kt + 1, buf ^ 1);  // (ablation 1: no k-loop staging)
     const char* Ai = smem + buf * STAGE;
     const char* Bi = Ai + IMG;
 #pragma unroll
@@ -1687,17 +1693,31 @@ wgrad256_kernel(const WgradParams p) {
         bf16x8 bfr[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) bfr[j] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
+        if (p.ablate & 2) {  // (ablation 2: fragments read, no MFMA)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bfr[j]));
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   if (nkt == 0) return;
+  if (p.ablate & 32) {  // timing ablation (g_tune[kAblate] & 32): no partial stores
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1928,7 +1948,24 @@ static void launch_big(TapGemmParams p, int epi, hipStream_t stream) {
   void* ws = nullptr;
   const int per_cu = std::max(1, (int)(160 * 1024 / lds));
   const int slots = p.sk_on >= 3 ? std::min(p.sk_on, ncu * per_cu) : ncu * per_cu;
-  if (p.sk_on && tiles >= slots && (long)tiles * p.nkt < (1l << 31) && g_ws_alloc != nullptr) {
+  // range granularity: the divisor u >= 8 of nkt (or nkt itself) that minimises the longest range,
+  // ceil(tiles * nkt / u / slots) * u k-steps; every range must still cover a whole tile's k-steps
+  // (a tile is then cut between at most two workgroups)
+  p.sk_unit = 0;
+  if (p.sk_on && tiles >= slots && (long)tiles * p.nkt < (1l << 31)) {
+    long best = -1;
+    for (int u = 1; u <= p.nkt; ++u) {
+      if (p.nkt % u != 0 || (u < 8 && u != p.nkt)) continue;
+      const long U = (long)tiles * (p.nkt / u);
+      if ((U / slots) * u < p.nkt) continue;
+      const long longest = (U + slots - 1) / slots * u;
+      if (best < 0 || longest <= best) {
+        best = longest;
+        p.sk_unit = u;
+      }
+    }
+  }
+  if (p.sk_unit > 0 && g_ws_alloc != nullptr) {
     const size_t flag_bytes = ((size_t)slots * 4 + 255) / 256 * 256;
     const size_t part_bytes = (size_t)slots * (64 * WM * WN) * CFW * 8 * 16;  // per lane: CFW x 8 f32x4
     ws = g_ws_alloc(flag_bytes + part_bytes, stream);
