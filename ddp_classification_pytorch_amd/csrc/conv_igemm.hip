@@ -1383,7 +1383,7 @@ struct WgradParams {
   int Hs, Ws, Cs, Ho, Wo, ss;
   int Co, M, ldw;    // ldw = T*Cs
   int cpt, kc_total, rows_per_split;
-  int ablate;  // tuning experiments only: 8 = skip the atomic flush; wgrad256: 1 no k-loop staging, 2 no MFMA, 32 no partial stores
+  int ablate;  // tuning experiments only: 8 = skip the atomic flush
   int direct;  // 1x1 stride-1 (no padding): the input pixel of GEMM row m is m
   // PRO (direct only): the input is a BN's input x, used as relu(x * pscale[c] + pshift[c]) (K5)
   const float* pscale;
@@ -1661,7 +1661,7 @@ wgrad256_kernel(const WgradParams p) {
   }
   for (int kt = 0; kt < nkt; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nkt && !(p.ablate & 1)) stage(kt + 1, buf ^ 1);  // (ablation 1: no k-loop staging)
+    if (kt + 1 < nkt) stage(kt + 1, buf ^ 1);
     const char* Ai = smem + buf * STAGE;
     const char* Bi = Ai + IMG;
 #pragma unroll
@@ -1693,32 +1693,17 @@ wgrad256_kernel(const WgradParams p) {
         bf16x8 bfr[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) bfr[j] = tr_frag512(Bi, row0, wn * 128 + j * 16, lane);
-        if (p.ablate & 2) {  // (ablation 2: fragments read, no MFMA)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bfr[j]));
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]));
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < 8; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   if (nkt == 0) return;
-  if (p.ablate & 32) {  // timing ablation (g_tune[kAblate] & 32): no partial stores
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
