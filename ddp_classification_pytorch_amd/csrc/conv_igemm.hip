@@ -1073,15 +1073,11 @@ tap_gemm_big_loop_kernel(const TapGemmParams p0) {
     // SGPRs to VGPR lanes: 190 v_readlane in the kernel).  Laundering the address of the by-value
     // argument instead copies the whole struct into per-lane scratch.  The tap table, indexed
     // dynamically, is read through the pointer (pk->tap[t]), never from the copy.
-#if defined(__HIP_DEVICE_COMPILE__)
     typedef const __attribute__((address_space(4))) TapGemmParams* KArgPtr;
-    KArgPtr pk = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(pk));
+    KArgPtr pk4 = (KArgPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pk4));
+    const TapGemmParams* pk = (const TapGemmParams*)pk4;  // (address space inferred back: scalar loads)
     const TapGemmParams p = *pk;
-#else  // (the host pass only needs the kernel to type-check)
-    const TapGemmParams* pk = &p0;
-    const TapGemmParams& p = p0;
-#endif
     // the k-loop's scalars, read once per tile and pinned in registers: an asm result cannot be
     // re-loaded from the argument segment inside the k-loop, where each scalar load's lgkmcnt wait
     // would also drain the LDS fragment reads
