@@ -10,10 +10,12 @@
 // plain 16x16x32 bf16 fragment.
 //
 // One workgroup = 256 consecutive destination pixels (linear n,y,x order) of
-// one super-group.  The source rows those pixels touch (a contiguous range of
-// global rows n*Hs+h) are staged once in LDS with 16-byte loads, so every tap
-// re-reads LDS instead of L2.  Pixel index 0 of the LDS image is a zero pixel
-// that out-of-range taps point at ("pad, don't mask").
+// one super-group (gconv_gather_kernel) or of several (gconv_gather_multi_kernel:
+// per-pixel setup done once, super-groups streamed through an LDS ring).  The
+// source rows those pixels touch (a contiguous range of global rows n*Hs+h) are
+// staged once in LDS with 16-byte loads, so every tap re-reads LDS instead of
+// L2.  Pixel index 0 of the LDS image is a zero pixel that out-of-range taps
+// point at ("pad, don't mask").
 //
 //   fwd  : dst = y  [N,Ho,Wo,C], src = x  rows  y*s + (kh-p)
 //   dgrad: dst = dx [N,H,W,C],   src = dy rows (y + (p-kh)) / s when divisible
@@ -49,6 +51,8 @@ struct GconvParams {
   const bf16* wfrag;  // fwd/dgrad: fragment-ordered block-diagonal weight (gconv_frag_kernel)
   const bf16* zero;   // >= 16 bytes of zeros (global)
   int nbuf;           // wgrad: 2 = double-buffered chunks
+  int ablate;         // multi kernel timing ablations (g_tune ablate): 1 = loads only, 2 = no loads
+  int spw, nbuf_g, bufb_g;  // fwd/dgrad multi kernel: super-groups per workgroup, LDS ring buffers, bytes each
   int Hs, Ws, Hd, Wd, C, CG, T;
   int ss, sd;       // src row = (dst_row*ss + oh) / sd, sd in {1, 2}
   int M;            // N*Hd*Wd
@@ -149,47 +153,62 @@ __device__ __forceinline__ bf16x8 w_frag(const GconvParams& p, int sg, int row, 
 // ---------------------------------------------------------------------------
 // fwd / dgrad: D[row = channel][col = pixel] = W_bd[row][k] * B[k][pixel]
 // ---------------------------------------------------------------------------
-// BN statistics of the forward tile (256 pixels x SG channels) from the bf16-rounded outputs:
-// per-wave shifted sums (shift = the wave's first output of each channel), lanes of one channel
-// group combined by shuffles, the four waves merged with Chan's formula -> (n, mean, M2) of the
-// tile's channels in partial row pb (the [P][3][C] layout bn_stats / bn_stats_finalize merge).
+// DPP data movement inside a row of 16 lanes (VALU, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ float gdpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+// sum over the 16 lanes of a row, every lane of the row receiving the same total: row_ror 8 is
+// xor 8, row_ror 4 on the then period-8 pattern is xor 4, the quad permutations xor 2 and xor 1
+__device__ __forceinline__ float row16_sum(float v) {
+  v += gdpp<0x128>(v);
+  v += gdpp<0x124>(v);
+  v += gdpp<0x4E>(v);
+  v += gdpp<0xB1>(v);
+  return v;
+}
+
+__device__ __forceinline__ bf16x4 cvt_bf16x4(f32x4 v) { return __builtin_convertvector(v, bf16x4); }
+
+// BN statistics of the forward tile (256 pixels x SG channels) from the bf16-rounded outputs ob:
+// per-wave shifted sums (shift = the row's first lane's first output of each channel, broadcast
+// with row_newbcast), the 16 lanes of one channel group summed with DPP, the four waves merged
+// with Chan's formula -> (n, mean, M2) of the tile's channels in partial row pb (the [P][3][C]
+// layout bn_stats / bn_stats_finalize merge).
 template <int SG, int NRT, int CPT>
-__device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const f32x4 (&acc)[NRT][CPT], char* smem,
-                                                 int m0, int sg, int pb, int wave, int lane) {
-  float K[NRT][4], s1[NRT][4], s2[NRT][4], cnt = 0.f;
+__device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const bf16x4 (&ob)[NRT][CPT], float* sc,
+                                                 bool lead_sync, int m0, int sg, int pb, int wave, int lane) {
+  const int wbase = m0 + wave * 64;
+  float K[NRT][4], s1[NRT][4], s2[NRT][4];
 #pragma unroll
   for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      K[rt][r] = __shfl(bf2f(f2bf(acc[rt][0][r])), lane & 48, 64);
+      K[rt][r] = gdpp<0x150>(bf2f(ob[rt][0][r]));  // row_newbcast:0
       s1[rt][r] = s2[rt][r] = 0.f;
     }
 #pragma unroll
   for (int ct = 0; ct < CPT; ++ct) {
-    const bool valid = m0 + wave * 64 + ct * 16 + (lane & 15) < p.M;
-    cnt += valid ? 1.f : 0.f;
+    const bool valid = wbase + ct * 16 + (lane & 15) < p.M;
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float d = valid ? bf2f(f2bf(acc[rt][ct][r])) - K[rt][r] : 0.f;
+        const float d = valid ? bf2f(ob[rt][ct][r]) - K[rt][r] : 0.f;
         s1[rt][r] += d;
         s2[rt][r] = fmaf(d, d, s2[rt][r]);
       }
   }
 #pragma unroll
-  for (int off = 1; off < 16; off *= 2) {
-    cnt += __shfl_xor(cnt, off, 64);
+  for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
-    for (int rt = 0; rt < NRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s1[rt][r] += __shfl_xor(s1[rt][r], off, 64);
-        s2[rt][r] += __shfl_xor(s2[rt][r], off, 64);
-      }
-  }
-  __syncthreads();  // every wave is done with the staged halo image: reuse it as scratch
-  float* sc = (float*)smem;  // [4 waves][SG channels][4]: cnt, K, s1, s2
+    for (int r = 0; r < 4; ++r) {
+      s1[rt][r] = row16_sum(s1[rt][r]);
+      s2[rt][r] = row16_sum(s2[rt][r]);
+    }
+  const float cnt = (float)min(max(p.M - wbase, 0), 64);  // valid pixels of the wave
+  if (lead_sync) __syncthreads();  // scratch aliases the staged halo image: every wave must be done with it
+  // sc: [4 waves][SG channels][4]: cnt, K, s1, s2
   if ((lane & 15) == 0)
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt)
@@ -210,10 +229,11 @@ __device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const f32
       const float* e = sc + (w * SG + c) * 4;
       const float nb = e[0];
       if (nb <= 0.f) continue;
-      const float mb = e[1] + e[2] / nb, m2b = fmaxf(e[3] - e[2] * e[2] / nb, 0.f);
-      const float ntot = nt + nb, delta = mb - mean;
-      mean += delta * nb / ntot;
-      m2 += m2b + delta * delta * nt * nb / ntot;
+      const float rnb = __builtin_amdgcn_rcpf(nb);
+      const float mb = e[1] + e[2] * rnb, m2b = fmaxf(e[3] - e[2] * e[2] * rnb, 0.f);
+      const float ntot = nt + nb, delta = mb - mean, f = nb * __builtin_amdgcn_rcpf(ntot);
+      mean += delta * f;
+      m2 += m2b + delta * delta * nt * f;
       nt = ntot;
     }
     float* o = p.stats + (size_t)pb * 3 * p.C + sg * SG + c;
@@ -228,7 +248,8 @@ __device__ __forceinline__ void gconv_tile_stats(const GconvParams& p, const f32
 // its elementwise pass (no reduction pass re-reading g and z).
 template <int SG, int NRT, int CPT>
 __device__ __forceinline__ void gconv_dgrad_bn_epilogue(const GconvParams& p, const f32x4 (&acc)[NRT][CPT],
-                                                        char* smem, int m0, int sg, int pb, int wave, int lane) {
+                                                        float* xs, bool lead_sync, int m0, int sg, int pb,
+                                                        int wave, int lane) {
   float sc[NRT][4], sh[NRT][4], mu[NRT][4], is[NRT][4], sg1[NRT][4], sg2[NRT][4];
 #pragma unroll
   for (int rt = 0; rt < NRT; ++rt)
@@ -263,16 +284,14 @@ __device__ __forceinline__ void gconv_dgrad_bn_epilogue(const GconvParams& p, co
     }
   }
 #pragma unroll
-  for (int off = 1; off < 16; off *= 2)
+  for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
-    for (int rt = 0; rt < NRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        sg1[rt][r] += __shfl_xor(sg1[rt][r], off, 64);
-        sg2[rt][r] += __shfl_xor(sg2[rt][r], off, 64);
-      }
-  __syncthreads();  // every wave is done with the staged image: reuse it as scratch
-  float* xs = (float*)smem;  // [4 waves][2][SG]
+    for (int r = 0; r < 4; ++r) {
+      sg1[rt][r] = row16_sum(sg1[rt][r]);
+      sg2[rt][r] = row16_sum(sg2[rt][r]);
+    }
+  if (lead_sync) __syncthreads();  // scratch aliases the staged image: every wave must be done with it
+  // xs: [4 waves][2][SG]
   if ((lane & 15) == 0)
 #pragma unroll
     for (int rt = 0; rt < NRT; ++rt)
@@ -361,25 +380,273 @@ __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) 
 
   if constexpr (DGRAD) {
     if (p.bnz) {
-      gconv_dgrad_bn_epilogue<SG, NRT, CPT>(p, acc, smem, m0, sg, pb, wave, lane);
+      gconv_dgrad_bn_epilogue<SG, NRT, CPT>(p, acc, (float*)smem, true, m0, sg, pb, wave, lane);
       return;
     }
   }
   // lane holds pixel column lane&15, channels (lane>>4)*4 .. +3 of each row tile
+  bf16x4 ob[NRT][CPT];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CPT; ++ct) ob[rt][ct] = cvt_bf16x4(acc[rt][ct]);
 #pragma unroll
   for (int ct = 0; ct < CPT; ++ct) {
     const int m = m0 + wave * 64 + ct * 16 + (lane & 15);
     if (m >= p.M) continue;
 #pragma unroll
-    for (int rt = 0; rt < NRT; ++rt) {
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[rt][ct][r]);
-      *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = o;
-    }
+    for (int rt = 0; rt < NRT; ++rt)
+      *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = ob[rt][ct];
   }
   if constexpr (!DGRAD) {
-    if (p.stats) gconv_tile_stats<SG, NRT, CPT>(p, acc, smem, m0, sg, pb, wave, lane);
+    if (p.stats) gconv_tile_stats<SG, NRT, CPT>(p, ob, (float*)smem, true, m0, sg, pb, wave, lane);
+  }
+}
+
+// gconv_dgrad_bn_epilogue with z and the BN coefficients read from the LDS-staged copies
+// (zl: [GP][SG] bf16 of this super-group, cl: [scale | shift | mean | invstd][SG] fp32)
+template <int SG, int NRT, int CPT>
+__device__ __forceinline__ void gconv_dgrad_bn_epilogue_lds(const GconvParams& p, const f32x4 (&acc)[NRT][CPT],
+                                                            const char* zl, const float* cl, float* xs, int m0,
+                                                            int sg, int pb, int wave, int lane) {
+  float sc[NRT][4], sh[NRT][4], mu[NRT][4], is[NRT][4], sg1[NRT][4], sg2[NRT][4];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt) {
+    const int c = rt * 16 + (lane >> 4) * 4;
+    const f32x4 a = *LDS_PTR(f32x4, cl + c), b = *LDS_PTR(f32x4, cl + SG + c);
+    const f32x4 m = *LDS_PTR(f32x4, cl + 2 * SG + c), v = *LDS_PTR(f32x4, cl + 3 * SG + c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[rt][r] = a[r];
+      sh[rt][r] = b[r];
+      mu[rt][r] = m[r];
+      is[rt][r] = v[r];
+      sg1[rt][r] = sg2[rt][r] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < CPT; ++ct) {
+    const int pl = wave * 64 + ct * 16 + (lane & 15);
+    const int m = m0 + pl;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) {
+      const int cl4 = rt * 16 + (lane >> 4) * 4;
+      const bf16x4 z = *LDS_PTR(bf16x4, zl + (pl * SG + cl4) * 2);
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float zf = bf2f(z[r]);
+        const bf16 gb = f2bf(zf * sc[rt][r] + sh[rt][r] > 0.f ? acc[rt][ct][r] : 0.f);
+        o[r] = gb;
+        const float g = bf2f(gb);
+        sg1[rt][r] += g;
+        sg2[rt][r] = fmaf(g, (zf - mu[rt][r]) * is[rt][r], sg2[rt][r]);
+      }
+      *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + cl4) = o;
+    }
+  }
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sg1[rt][r] = row16_sum(sg1[rt][r]);
+      sg2[rt][r] = row16_sum(sg2[rt][r]);
+    }
+  // xs: [4 waves][2][SG] (the caller's loop barrier orders it against the previous reader)
+  if ((lane & 15) == 0)
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = rt * 16 + (lane >> 4) * 4 + r;
+        xs[(wave * 2 + 0) * SG + c] = sg1[rt][r];
+        xs[(wave * 2 + 1) * SG + c] = sg2[rt][r];
+      }
+  __syncthreads();
+  if (threadIdx.x < 2 * SG) {
+    const int k = threadIdx.x / SG, c = threadIdx.x % SG;
+    const float t = (xs[(0 * 2 + k) * SG + c] + xs[(1 * 2 + k) * SG + c]) +
+                    (xs[(2 * 2 + k) * SG + c] + xs[(3 * 2 + k) * SG + c]);
+    p.bnsum[((size_t)pb * 2 + k) * p.C + sg * SG + c] = t;
+  }
+}
+
+// s_waitcnt vmcnt(n') for the largest n' <= n from a short ladder (n is wave-uniform at run time;
+// waiting until at most n' <= n operations are outstanding is at least as strict as n)
+__device__ __forceinline__ void wait_vmcnt_atmost(int n) {
+  if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// fwd / dgrad, SPW super-groups per workgroup (p.spw; the pixel block's super-groups
+// sg0 .. sg0+spw-1).  The one-super-group kernel above spends most of its vector-ALU issue on
+// per-block setup -- pixel geometry, 20 tap indices per lane, halo bounds -- that does not depend
+// on the super-group: here it is done once and reused.  The super-groups' halo images and weight
+// fragments stream through a ring of p.nbuf_g LDS buffers (LDS-DMA): a buffer is refilled with
+// super-group i + nbuf as soon as every wave has finished computing on super-group i, so every
+// buffer but the one being computed on has loads in flight (the one-super-group kernel keeps its
+// whole LDS image in flight the same way, through occupancy).  Buffer layout:
+// [weight fragments: NST*NRT*64 x 16 B][zero pixel][halo].
+template <int SG, bool DGRAD>
+__global__ void __launch_bounds__(256) gconv_gather_multi_kernel(const GconvParams p) {
+  constexpr int NRT = SG / 16;
+  constexpr int TPS = SG == 16 ? 2 : 1;
+  constexpr int NST = (GT + TPS - 1) / TPS;
+  constexpr int CPT = 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = (int)xcd_remap(blockIdx.x, p.ntiles);
+  const int nsgb = (p.nsg + p.spw - 1) / p.spw;
+  const int sgb = tile % nsgb, pb = tile / nsgb;
+  const int sg0 = sgb * p.spw, nsp = min(p.spw, p.nsg - sg0);
+  const int m0 = pb * GP, m1 = min(p.M, m0 + GP) - 1;
+  const bool full = m0 + GP <= p.M;
+  int R_lo, NR;
+  halo_rows(p, m0, m1, R_lo, NR);
+  const int nfr = NST * NRT * 64;  // 16-byte weight fragments per super-group
+  const int fragb = nfr * 16;
+  // dgrad fused with the BN backward: the super-group's z tile [GP][SG] and its four coefficient
+  // vectors [4][SG] are staged with the halo (no global loads in the loop: the compiler cannot
+  // count the untracked LDS-DMA, so any wait it placed for a global load would drain the ring)
+  const bool bnst = DGRAD && p.bnz != nullptr;
+  const int zo = fragb, co = zo + GP * SG * 2;
+  const int imgo = bnst ? co + 4 * SG * 4 : fragb;
+  const int nb = p.nbuf_g;
+  float* const scratch = (float*)(smem + nb * p.bufb_g);
+  // vector-memory instructions this wave issues per staged super-group (the same for every
+  // super-group of the block): one per 256-element round it takes part in
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int nhalo = NR * p.Ws * (SG / 8);
+  const int per_stage = (nfr - wv * 64 + 255) / 256 + max(0, (nhalo - wv * 64 + 255) / 256) +
+                        (bnst ? (GP * SG / 8) / 256 + 1 : 0);
+
+  auto bufp = [&](int i) { return smem + (i % nb) * p.bufb_g; };
+  auto stage = [&](int i) {
+    if (p.ablate == 2) return;
+    char* buf = bufp(i);
+    const char* wsrc = (const char*)(p.wfrag + (size_t)(sg0 + i) * nfr * 8);
+    for (int e0 = wave * 64; e0 < nfr; e0 += 256) {
+      const int e = e0 + lane;
+      if (e < nfr) dma16(wsrc + (size_t)e * 16, buf + e0 * 16);
+    }
+    if (bnst) {
+      constexpr int CH = SG / 8;
+#pragma unroll
+      for (int e0 = wave * 64; e0 < GP * CH; e0 += 256) {
+        const int e = e0 + lane;
+        const int m = min(m0 + e / CH, m1);  // rows past the image: any valid row (not stored)
+        dma16(p.bnz + (size_t)m * p.C + (sg0 + i) * SG + (e % CH) * 8, buf + zo + e0 * 16);
+      }
+      // [scale | shift | mean | invstd] x SG floats: wave w stages vector w (a wave-uniform pointer
+      // choice stays in scalar registers; a per-lane one reads the kernel arguments from memory)
+      const float* src = wv == 0 ? p.bn_scale : wv == 1 ? p.bn_shift : wv == 2 ? p.bn_mean : p.bn_invstd;
+      if (lane < SG / 4) dma16(src + (sg0 + i) * SG + lane * 4, buf + co + wv * SG * 4);
+    }
+    stage_halo<SG>(p, buf + imgo, sg0 + i, R_lo, NR);
+  };
+  for (int i = 0; i < min(nb, nsp); ++i) {
+    stage(i);
+    zero_pixel<SG>(bufp(i) + imgo);
+  }
+
+  // per-lane LDS byte offsets of every (k-step, pixel column) operand, shared by all super-groups
+  const int kc = lane >> 4;
+  const int chunk = SG == 16 ? (kc & 1) : kc;
+  int off[NST][CPT];
+  {
+    PixGeo g[CPT];
+#pragma unroll
+    for (int ct = 0; ct < CPT; ++ct) g[ct] = pix_geo(p, m0 + wave * 64 + ct * 16 + (lane & 15), R_lo);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      const int t0 = st * TPS;
+      const int t = SG == 16 ? t0 + (kc >> 1) : t0;
+      // select between the two (scalar) taps rather than index the kernel arguments per lane: a
+      // per-lane index becomes a global load whose wait would also drain the prologue's DMA
+      const int oh0 = __builtin_amdgcn_readfirstlane(p.oh[t0]), ow0 = __builtin_amdgcn_readfirstlane(p.ow[t0]);
+      const int oh1 = __builtin_amdgcn_readfirstlane(p.oh[t0 + 1]), ow1 = __builtin_amdgcn_readfirstlane(p.ow[t0 + 1]);
+      const int oh = (SG == 16 && (kc >> 1)) ? oh1 : oh0;
+      const int ow = (SG == 16 && (kc >> 1)) ? ow1 : ow0;
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct) off[st][ct] = imgo + tap_idx(p, g[ct], oh, ow, t < p.T) * (SG * 2) + chunk * 16;
+    }
+  }
+
+  for (int i = 0; i < nsp; ++i) {
+    // super-group i's loads are complete once at most the younger operations are outstanding:
+    // the stages issued after it (up to nb - 1 of them) and, in a full block after the first
+    // iteration, the previous epilogue's CPT*NRT output stores (issued after every stage so far;
+    // a ragged block may skip stores, so it does not count them)
+    const int younger = p.ablate == 2 ? 0 : (min(nsp - 1, i + nb - 1) - i) * per_stage + ((i > 0 && full && p.ablate == 0) ? CPT * NRT : 0);
+    wait_vmcnt_atmost(younger);
+    __syncthreads();
+    const int sg = sg0 + i;
+    const char* cur = bufp(i);
+    if (p.ablate == 1) {
+      if (i + nb < nsp) {
+        __syncthreads();
+        stage(i + nb);
+      }
+      continue;
+    }
+
+    f32x4 acc[NRT][CPT];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {  // 3x3 only (host-checked): nst == NST, no partial k-step loop
+      bf16x8 a[NRT], b[CPT];
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) a[rt] = *LDS_PTR(bf16x8, cur + ((st * NRT + rt) * 64 + lane) * 16);
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct) b[ct] = *LDS_PTR(bf16x8, cur + off[st][ct]);
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CPT; ++ct)
+          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt], b[ct], acc[rt][ct], 0, 0, 0);
+    }
+    if constexpr (DGRAD) {
+      if (bnst) {
+        // the epilogue reads this buffer's z and coefficients; its internal barrier follows the
+        // last such read, so the refill goes after it
+        gconv_dgrad_bn_epilogue_lds<SG, NRT, CPT>(p, acc, cur + zo, (const float*)(cur + co), scratch, m0, sg, pb,
+                                                  wave, lane);
+        if (i + nb < nsp) stage(i + nb);
+        continue;
+      }
+    }
+    if (i + nb < nsp) {
+      __syncthreads();  // every wave is done reading buffer i % nb: refill it
+      stage(i + nb);
+    }
+    bf16x4 ob[NRT][CPT];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct) ob[rt][ct] = cvt_bf16x4(acc[rt][ct]);
+#pragma unroll
+    for (int ct = 0; ct < CPT; ++ct) {
+      const int m = m0 + wave * 64 + ct * 16 + (lane & 15);
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+        *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = ob[rt][ct];
+    }
+    if constexpr (!DGRAD) {
+      if (p.stats) gconv_tile_stats<SG, NRT, CPT>(p, ob, scratch, false, m0, sg, pb, wave, lane);
+    }
   }
 }
 
@@ -628,6 +895,36 @@ bool launch_gather(GconvParams p, int N, bf16* frag, hipStream_t s) {
   const int nfrag = p.nsg * ((p.T + TPS - 1) / TPS) * (SG / 16) * 64;
   hipLaunchKernelGGL((gconv_frag_kernel<SG, DGRAD>), dim3((nfrag + 255) / 256), dim3(256), 0, s, p, frag);
   p.wfrag = frag;
+  // super-groups per workgroup (g_tune gconv_spw = spw, or 10 * spw + LDS ring buffers).  Default
+  // (tools/conv_bench.py --grouped --cfgs, b1024, profiles/r5/gconv_spw_ab_b1024.txt): two 16-channel
+  // super-groups with a two-stage ring where the source is read at stride 1 (-21 % fwd, -16 % dgrad
+  // over ResNeXt-50's grouped convs); one per workgroup for the stride-2 forward (its doubled halo
+  // halves the occupancy of the ring) and for 32-channel super-groups (twice the fragments and
+  // accumulators; no gain measured)
+  int spw = g_tune[kGconvSpw], nbuf = 2;
+  if (spw >= 10) {
+    nbuf = std::max(2, spw % 10);
+    spw /= 10;
+  }
+  if (spw <= 0) spw = (SG == 16 && p.ss == 1 && (size_t)npb * ((p.nsg + 1) / 2) >= 512) ? 2 : 1;
+  spw = std::min(spw, p.nsg);
+  if (spw > 1 && p.T == GT) {
+    const size_t fragb = (size_t)(nfrag / p.nsg) * 16;
+    const size_t bnb = (DGRAD && p.bnz) ? (size_t)GP * SG * 2 + 4 * SG * 4 : 0;
+    const size_t bufb = (fragb + bnb + lds + 15) / 16 * 16;
+    nbuf = std::min(nbuf, spw);
+    const size_t total = nbuf * bufb + 4 * SG * 16;
+    if (total <= kMaxLds) {
+      p.spw = spw;
+      p.nbuf_g = nbuf;
+      p.ablate = g_tune[kAblate];
+      p.bufb_g = (int)bufb;
+      p.ntiles = npb * ((p.nsg + spw - 1) / spw);
+      allow_lds(gconv_gather_multi_kernel<SG, DGRAD>, total);
+      hipLaunchKernelGGL((gconv_gather_multi_kernel<SG, DGRAD>), dim3(p.ntiles), dim3(256), total, s, p);
+      return true;
+    }
+  }
   allow_lds(gconv_gather_kernel<SG, DGRAD>, lds);
   hipLaunchKernelGGL((gconv_gather_kernel<SG, DGRAD>), dim3(p.ntiles), dim3(256), lds, s, p);
   return true;

@@ -32,6 +32,7 @@ enum TuneSlot : int {
   kTgBigPersist = 22,  // 256-row big tiles: 1 = persistent workgroups (one per CU, looping over tiles)
   kTgBigSK = 23,       // 256-row big tiles, stream-K (k-steps split evenly over one workgroup per CU slot): 1 on, 2 off
   kTgBigStages = 21,   // 256 x 256 big tile: LDS-DMA ring slots (0 = 4; 5 = all 160 KB, three k-tiles in flight)
+  kGconvSpw = 26,     // grouped conv fwd / dgrad: super-groups per workgroup (1 = one per workgroup)
   kTgBig = 24,         // big-tile tap GEMM: 1 on (256 x 256 / 256 x 128), 2 off, 3 = 256 x 128 only
   kAutotune = 25,      // per-shape autotuning of the conv configurations (DCP_AUTOTUNE)
   kWgSplitCap = 27,    // weight gradient: at most this many split-K partials
@@ -57,6 +58,7 @@ constexpr TuneSlotName kTuneSlotNames[] = {
     {"c3_off", kC3Off},              {"c3_variant", kC3Variant},     {"tg_big", kTgBig},
     {"dgrad_parity_streams", kDgradParityStreams}, {"tg_big_stages", kTgBigStages},
     {"tg_big_persist", kTgBigPersist}, {"tg_big_sk", kTgBigSK},
+    {"gconv_spw", kGconvSpw},
     {"autotune", kAutotune},         {"wg_split_cap", kWgSplitCap},  {"bn_bwd_cap", kBnBwdCap},
     {"row_reduce", kRowReduce},      {"c3_epilogue", kC3Epilogue},   {"c3_window_kb", kC3WindowKB},
 };

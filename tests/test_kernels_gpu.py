@@ -1012,6 +1012,41 @@ def test_grouped_conv_dgrad_bn(K, N, H, C):
     assert (g.cpu() != ref).float().mean().item() < 1e-3  # masks may differ only where z*scale+shift ~ 0
 
 
+@pytest.mark.parametrize("N,H,C,s", [(2, 56, 128, 1), (3, 13, 256, 2), (2, 14, 512, 1), (3, 7, 1024, 1),
+                                     (2, 14, 1024, 2)])
+@pytest.mark.parametrize("spw", [2, 3, 8, 83, 34])  # 10 * spw + ring buffers: 8 x 3 ring, 3 x 3 ring
+def test_grouped_conv_multi_supergroup_matches(K, N, H, C, s, spw):
+    """Forward (+BN partials) and data gradient (plain and BN-fused) with several super-groups per
+    workgroup (g_tune gconv_spw; an LDS ring of halo + weight-fragment (+ z) stages) against one
+    super-group per workgroup: the same MFMA sums in the same order, so bitwise-equal outputs."""
+    torch.manual_seed(21)
+    G = 32
+    Ho = (H + 2 - 3) // s + 1
+    d = lambda t: t.to(DEV)
+    x = rnd(N, H, H, C, scale=2.0)
+    w = rnd(C, 3, 3, C // G, scale=1.0 / math.sqrt(9 * C // G))
+    dy = rnd(N, Ho, Ho, C)
+    co = [torch.rand(C) + 0.5, torch.randn(C) * 0.3, torch.randn(C) * 0.2, torch.rand(C) + 0.5]
+    out = {}
+    try:
+        for v in (1, spw):
+            K.set_tuning(tslot("gconv_spw"), v)
+            y, part = K.grouped_conv_fwd_stats(d(x), d(w), G, s, 1)
+            dx = K.grouped_conv_dgrad(d(dy), d(w), H, H, G, s, 1)
+            g, sums = K.grouped_conv_dgrad_bn(d(dy), d(w), H, H, G, s, 1, d(x), *[d(c) for c in co])
+            torch.cuda.synchronize()
+            out[v] = (y.cpu(), part.cpu(), dx.cpu(), g.cpu(), sums.cpu())
+    finally:
+        K.set_tuning(tslot("gconv_spw"), 0)
+    y1, p1, dx1, g1, s1 = out[1]
+    y2, p2, dx2, g2, s2 = out[spw]
+    assert torch.equal(y1, y2) and torch.equal(dx1, dx2) and torch.equal(g1, g2)
+    assert torch.allclose(p1, p2, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(s1, s2, rtol=1e-5, atol=1e-4)
+    assert relerr(y2, _ref.grouped_conv_fwd(x.float(), w.float(), G, s, 1)) < 1e-2
+    assert relerr(dx2, _ref.grouped_conv_dgrad(dy.float(), w.float(), H, H, G, s, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("M,C", [(1024, 1000), (7, 16), (3000, 2048), (1, 8), (513, 4096)])
 def test_colsum(K, M, C):
     x = rnd(M, C)

@@ -175,20 +175,33 @@ def ab(a):
 
 
 def grouped(a):
+    """ResNeXt-50 grouped 3x3 convs as the model runs them (forward with the fused BN statistics,
+    data gradient with the fused BN backward, weight gradient); with --cfgs every shape is timed
+    under each tuning config in turn (interleaved in one process)."""
     K = _ext.hip_ops()
     dev = torch.device("cuda", 0)
     N, G = a.batch, 32
-    tot = [0.0] * 6
-    print(f"{'shape':28s} {'fwd us':>8s} {'dgrad':>8s} {'wgrad':>8s} {'GB/s fwd':>9s} | "
-          f"{'mi fwd':>8s} {'mi dg':>8s} {'mi wg':>8s}")
+    cfgs = a.cfgs.split(",") if a.cfgs else [""]
+    tot = [[0.0] * 3 for _ in cfgs]
+    mtot = [0.0] * 3
+    print(f"{'shape':24s} " + " | ".join(f"{(c or 'default')[:22]:>22s}" for c in cfgs) +
+          ("" if a.no_miopen else f" | {'miopen fwd/dg/wg':>22s}"))
     for C, s, H, cnt in RX50_GROUPED:
         Ho = (H + 2 - 3) // s + 1
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
         w = (torch.randn(C, 3, 3, C // G, device=dev) / (9 * C // G) ** 0.5).bfloat16()
         dy = torch.randn(N, Ho, Ho, C, device=dev).bfloat16()
-        t = [timeit(lambda: K.grouped_conv_fwd(x, w, G, s, 1), a.iters),
-             timeit(lambda: K.grouped_conv_dgrad(dy, w, H, H, G, s, 1), a.iters),
-             timeit(lambda: K.grouped_conv_wgrad(dy, x, 3, 3, G, s, 1), a.iters)]
+        co = [torch.rand(C, device=dev) + 0.5 for _ in range(4)]
+        res = []
+        for ci, c in enumerate(cfgs):
+            _apply(K, c)
+            t = [timeit(lambda: K.grouped_conv_fwd_stats(x, w, G, s, 1), a.iters),
+                 timeit(lambda: K.grouped_conv_dgrad_bn(dy, w, H, H, G, s, 1, x, *co), a.iters),
+                 timeit(lambda: K.grouped_conv_wgrad(dy, x, 3, 3, G, s, 1), a.iters)]
+            res.append(t)
+            for i, v in enumerate(t):
+                tot[ci][i] += cnt * v
+        _apply(K, "")
         mi = [0.0, 0.0, 0.0]
         if not a.no_miopen:
             xc, dyc = x.permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2)
@@ -198,17 +211,16 @@ def grouped(a):
                 dyc, xc, wc, None, [s, s], [1, 1], [1, 1], False, [0, 0], G, [True, False, False]), a.iters)
             mi[2] = timeit(lambda: torch.ops.aten.convolution_backward(
                 dyc, xc, wc, None, [s, s], [1, 1], [1, 1], False, [0, 0], G, [False, True, False]), a.iters)
-        gbs = (x.numel() + dy.numel()) * 2 / t[0] / 1e3
+            for i, v in enumerate(mi):
+                mtot[i] += cnt * v
         name = f"C{C} s{s} {H}->{Ho} x{cnt}"
-        print(f"{name:28s} {t[0]:8.1f} {t[1]:8.1f} {t[2]:8.1f} {gbs:9.0f} | {mi[0]:8.1f} {mi[1]:8.1f} {mi[2]:8.1f}",
-              flush=True)
-        for i, v in enumerate(t + mi):
-            tot[i] += cnt * v
-    print("per-step totals (ms): ours fwd/dgrad/wgrad = " + "/".join(f"{v / 1e3:.2f}" for v in tot[:3]) +
-          f" sum {sum(tot[:3]) / 1e3:.2f}")
+        print(f"{name:24s} " + " | ".join(f"{t[0]:6.1f} {t[1]:7.1f} {t[2]:7.1f}" for t in res) +
+              ("" if a.no_miopen else f" | {mi[0]:6.1f} {mi[1]:7.1f} {mi[2]:7.1f}"), flush=True)
+    for c, t in zip(cfgs, tot):
+        print(f"per-step totals (ms) {c or 'default'}: fwd/dgrad/wgrad = " + "/".join(f"{v / 1e3:.2f}" for v in t) +
+              f" sum {sum(t) / 1e3:.2f}")
     if not a.no_miopen:
-        print("                      miopen            = " + "/".join(f"{v / 1e3:.2f}" for v in tot[3:]) +
-              f" sum {sum(tot[3:]) / 1e3:.2f}")
+        print("per-step totals (ms) miopen: " + "/".join(f"{v / 1e3:.2f}" for v in mtot) + f" sum {sum(mtot) / 1e3:.2f}")
 
 
 if __name__ == "__main__":

@@ -23,11 +23,13 @@
 #   convbench       per-shape conv fwd/dgrad/wgrad timings vs the roofline (R50 shapes, b1024)
 #   convbench32     the same at batch 32 (the reference's per-process batch)
 #   benchab=CFG     headline bench default vs DCP_TUNE=CFG, interleaved twice
+#   cfgab=CFG:A|B   bench.py --config CFG under DCP_TUNE=A vs DCP_TUNE=B (both disable the autotuner alike), twice
 #   benchenv=V=X    headline bench default vs with environment V=X, interleaved twice
 #   blas            torch.mm (hipBLASLt) on the R50 1x1 stride-1 GEMM shapes, b1024 (library yardstick)
 #   small           the reference's per-process batches: b32 / b128, eager and HIP-graph replay
 #   smallenv=V=X    b32 graph / b128 eager, default vs with environment V=X
 #   large           ResNet-101 at per-GPU batch 2048 / 3072 (288 GB sizing, >2^32-element tensors)
+#   gconvab=CFGS    ResNeXt-50 grouped convs under each g_tune config (",gconv_spw=1" = default vs one super-group)
 #   convab=CFGS     tools/conv_bench.py --cfgs CFGS at b1024 (in-process interleaved A/B of g_tune configs)
 #   loop            main.py's training loop vs bench.py at batch 32 (eager, HIP graph) and 128
 #   ddp1            world-1 RCCL through the bucket engine (--force-ddp): b32 graph / eager, b1024 (+ SyncBN phase,
@@ -79,6 +81,12 @@ for step in "$@"; do
         run_ref arc256_b${b}_eager --config arcface --image-size 256 --batch $b --eager
         run_ref arc256_b${b}_ddp1_graph --config arcface --image-size 256 --batch $b --force-ddp --graph
       done ;;
+    gconvab=*)
+      # gconvab=CFGS -- ResNeXt-50 grouped convs (fwd+stats / dgrad+BN / wgrad) under each g_tune config, b1024
+      c=${step#gconvab=}
+      timeout -k 10 400 python -u tools/conv_bench.py --grouped --batch 1024 --iters 10 --no-miopen --cfgs "$c" \
+        > $O/gconvab.log 2>&1
+      tail -4 $O/gconvab.log ;;
     convabs=*)
       # convabs=IDX,IDX:CFGS -- the same A/B on a subset of the R50 shapes (conv_bench.py R50 indices)
       v=${step#convabs=}; only=${v%%:*}; c=${v#*:}
@@ -253,6 +261,15 @@ for step in "$@"; do
         echo "default: $(grep -o '"value": [0-9.]*' $O/benchab_default_$r.log)"
         DCP_TUNE="$c" timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > $O/benchab_tuned_$r.log 2>&1
         echo "DCP_TUNE=$c: $(grep -o '"value": [0-9.]*' $O/benchab_tuned_$r.log)"
+      done ;;
+    cfgab=*)
+      # cfgab=CONFIG:A|B -- bench.py --config CONFIG under DCP_TUNE=A vs DCP_TUNE=B, interleaved twice
+      v=${step#cfgab=}; cfg=${v%%:*}; ab=${v#*:}; A=${ab%%|*}; B=${ab#*|}
+      for r in 1 2; do
+        DCP_TUNE="$A" timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 5 > $O/cfgab_a_$r.log 2>&1
+        echo "$cfg DCP_TUNE=$A: $(grep -o '"value": [0-9.]*' $O/cfgab_a_$r.log)"
+        DCP_TUNE="$B" timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 5 > $O/cfgab_b_$r.log 2>&1
+        echo "$cfg DCP_TUNE=$B: $(grep -o '"value": [0-9.]*' $O/cfgab_b_$r.log)"
       done ;;
     benchenv=*)
       # headline bench, default vs with an environment assignment (e.g. DCP_WGRAD_STREAM=1), twice
