@@ -677,7 +677,17 @@ __device__ __forceinline__ bf16x8 tr8(const char* img_a, const char* img_b, int 
 // ---------------------------------------------------------------------------
 // wgrad: D[j][t, c] = sum_m dy[m][j] * x[src(m,t)][c] per super-group
 // ---------------------------------------------------------------------------
-template <int SG>
+// bit t (t = kh*3 + kw) set where tap t of a 3x3 stride-1-gather (sd == 1) hits the image
+__device__ __forceinline__ uint32_t tap_mask33(const GconvParams& p, const PixGeo& g) {
+  uint32_t cm = 0, m = 0;
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw) cm |= ((unsigned)(g.xx + p.ow[kw]) < (unsigned)p.Ws ? 1u : 0u) << kw;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) m |= (unsigned)(g.yy + p.oh[kh * 3]) < (unsigned)p.Hs ? cm << (3 * kh) : 0u;
+  return g.ok ? m : 0u;
+}
+
+template <int SG, bool K33>
 __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const GconvParams p) {
   constexpr int NRT = SG / 16;
   constexpr int NTG = NRT * NRT;          // tile groups (row tile x column half), 9 taps each
@@ -699,11 +709,13 @@ __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const GconvParams p) {
 
   bool tok[GT];
   int8_t toh[GT], tow[GT];
+  int toff[GT];  // K33: LDS byte offset of tap t's source pixel from tap (0, 0)'s reference
 #pragma unroll
   for (int t = 0; t < GT; ++t) {
     tok[t] = t < p.T;
     toh[t] = p.oh[t];
     tow[t] = p.ow[t];
+    toff[t] = __builtin_amdgcn_readfirstlane((p.oh[t] * p.Ws + p.ow[t]) * (SG * 2));
   }
 
   // LDS-DMA of one chunk (dy rows + source halo) into buffer `buf`
@@ -748,13 +760,29 @@ __global__ void __launch_bounds__(256) gconv_wgrad_kernel(const GconvParams p) {
       const PixGeo gb = pix_geo(p, m0 + rb, R_cur);
       const bool oka = m0 + ra <= m1, okb = m0 + rb <= m1;
       const int bcol = (chh * 16 + 4 * pp) * 2;
+      if constexpr (K33) {
+        // 3x3: the source pixel of tap t is base + toff[t] (uniform offsets), valid where bit t
+        // of a per-pixel mask is set -- built once from three row and three column tests instead
+        // of nine full bounds checks and index products per pixel
+        const uint32_t ma = oka ? tap_mask33(p, ga) : 0u, mb = okb ? tap_mask33(p, gb) : 0u;
+        const int ba = (1 + (ga.rb + ga.yy) * p.Ws + ga.xx) * (SG * 2) + bcol;
+        const int bb = (1 + (gb.rb + gb.yy) * p.Ws + gb.xx) * (SG * 2) + bcol;
 #pragma unroll
-      for (int t = 0; t < GT; ++t) {
-        if (t >= p.T) continue;  // uniform
-        const int ia = oka ? tap_idx(p, ga, toh[t], tow[t], tok[t]) : 0;
-        const int ib = okb ? tap_idx(p, gb, toh[t], tow[t], tok[t]) : 0;
-        const bf16x8 bf = tr8(img + ia * (SG * 2) + bcol, img + ib * (SG * 2) + bcol, lane);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+        for (int t = 0; t < GT; ++t) {
+          const int ia = (ma >> t) & 1u ? ba + toff[t] : bcol;
+          const int ib = (mb >> t) & 1u ? bb + toff[t] : bcol;
+          const bf16x8 bf = tr8(img + ia, img + ib, lane);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < GT; ++t) {
+          if (t >= p.T) continue;  // uniform
+          const int ia = oka ? tap_idx(p, ga, toh[t], tow[t], tok[t]) : 0;
+          const int ib = okb ? tap_idx(p, gb, toh[t], tow[t], tok[t]) : 0;
+          const bf16x8 bf = tr8(img + ia * (SG * 2) + bcol, img + ib * (SG * 2) + bcol, lane);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+        }
       }
     }
     if (p.nbuf == 1 && ci + 1 < nchunks) {
@@ -1025,13 +1053,15 @@ bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* pa
   p.nbuf = (2 * bufb <= kMaxLds && cps > 1) ? 2 : 1;
   const size_t lds = std::max(p.nbuf * bufb, red);
   if (lds > kMaxLds) return false;
-  if (SG == 16) {
-    allow_lds(gconv_wgrad_kernel<16>, lds);
-    hipLaunchKernelGGL(gconv_wgrad_kernel<16>, dim3(p.ntiles), dim3(256), lds, s, p);
-  } else {
-    allow_lds(gconv_wgrad_kernel<32>, lds);
-    hipLaunchKernelGGL(gconv_wgrad_kernel<32>, dim3(p.ntiles), dim3(256), lds, s, p);
-  }
+  const bool k33 = KH == 3 && KW == 3 && g_tune[kGconvSG] != 1;  // gconv_sg=1: the general tap path (A/B)
+  auto launch = [&](auto kernel) {
+    allow_lds(kernel, lds);
+    hipLaunchKernelGGL(kernel, dim3(p.ntiles), dim3(256), lds, s, p);
+  };
+  if (SG == 16)
+    k33 ? launch(gconv_wgrad_kernel<16, true>) : launch(gconv_wgrad_kernel<16, false>);
+  else
+    k33 ? launch(gconv_wgrad_kernel<32, true>) : launch(gconv_wgrad_kernel<32, false>);
   const int n = C * KH * KW * CG;
   hipLaunchKernelGGL(partial_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, splits, n, dw);
   return true;

@@ -24,7 +24,7 @@ enum TuneSlot : int {
   kNarrowKDepth = 13,  // narrow-channel (per-lane tap) tap GEMM k-tile depth: 32 / 64
   kWgCols = 14,        // weight gradient column tile: 4 = 256, 3 = 192
   kWg3x3 = 15,         // direct 3x3 weight gradient: 1 off, 2 forced on every pair count
-  kGconvSG = 16,       // grouped conv weight-gradient super-group: 32
+  kGconvSG = 16,       // grouped conv weight gradient: 32 = 32-channel super-groups, 1 = general tap path
   kStemAblate = 17,    // stem timing ablations: 1 no MFMA phase, 2 no gather phase
   kC3Off = 18,         // direct 64->64 3x3: 1 = the implicit GEMM instead
   kC3Variant = 19,     // direct 64->64 3x3 workgroup variant (0 = 8 waves, 1 / 2 = 4-wave, 3 / 4 = priority / phase)
