@@ -51,7 +51,7 @@ struct GconvParams {
   const bf16* wfrag;  // fwd/dgrad: fragment-ordered block-diagonal weight (gconv_frag_kernel)
   const bf16* zero;   // >= 16 bytes of zeros (global)
   int nbuf;           // wgrad: 2 = double-buffered chunks
-  int ablate;         // multi kernel timing ablations (g_tune ablate): 1 = loads only, 2 = no loads
+  int ablate;         // multi kernel timing ablations (g_tune ablate): 1 = loads only, 2 = no loads, 4 = no stores
   int spw, nbuf_g, bufb_g;  // fwd/dgrad multi kernel: super-groups per workgroup, LDS ring buffers, bytes each
   int Hs, Ws, Hd, Wd, C, CG, T;
   int ss, sd;       // src row = (dst_row*ss + oh) / sd, sd in {1, 2}
@@ -443,7 +443,7 @@ __device__ __forceinline__ void gconv_dgrad_bn_epilogue_lds(const GconvParams& p
         sg1[rt][r] += g;
         sg2[rt][r] = fmaf(g, (zf - mu[rt][r]) * is[rt][r], sg2[rt][r]);
       }
-      *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + cl4) = o;
+      if (p.ablate != 4) *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + cl4) = o;
     }
   }
 #pragma unroll
@@ -642,7 +642,7 @@ __global__ void __launch_bounds__(256) gconv_gather_multi_kernel(const GconvPara
       if (m >= p.M) continue;
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt)
-        *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = ob[rt][ct];
+        if (p.ablate != 4) *(bf16x4*)(p.dst + (size_t)m * p.C + sg * SG + rt * 16 + (lane >> 4) * 4) = ob[rt][ct];
     }
     if constexpr (!DGRAD) {
       if (p.stats) gconv_tile_stats<SG, NRT, CPT>(p, ob, scratch, false, m0, sg, pb, wave, lane);
@@ -930,13 +930,14 @@ bool launch_gather(GconvParams p, int N, bf16* frag, hipStream_t s) {
   // halves the occupancy of the ring) and for 32-channel super-groups (twice the fragments and
   // accumulators; no gain measured)
   int spw = g_tune[kGconvSpw], nbuf = 2;
+  const bool multi1 = spw >= 10 && spw / 10 == 1;  // 11: the multi kernel with one super-group (A/B)
   if (spw >= 10) {
     nbuf = std::max(2, spw % 10);
     spw /= 10;
   }
   if (spw <= 0) spw = (SG == 16 && p.ss == 1 && (size_t)npb * ((p.nsg + 1) / 2) >= 512) ? 2 : 1;
   spw = std::min(spw, p.nsg);
-  if (spw > 1 && p.T == GT) {
+  if ((spw > 1 || multi1) && p.T == GT) {
     const size_t fragb = (size_t)(nfrag / p.nsg) * 16;
     const size_t bnb = (DGRAD && p.bnz) ? (size_t)GP * SG * 2 + 4 * SG * 4 : 0;
     const size_t bufb = (fragb + bnb + lds + 15) / 16 * 16;
