@@ -80,6 +80,23 @@ __device__ __forceinline__ void dma16_tracked(const void* g, const char* lds) {
   __builtin_amdgcn_global_load_lds(g, LDS_PTR(void, lds), 16, 0, 0);
 }
 
+// v summed over the lanes sharing lane % FROM (xor offsets FROM, 2 FROM, .., 32; FROM in {8, 16,
+// 32}), every lane of a group receiving the same total: the pairwise adds of a __shfl_xor
+// butterfly in the same order (bitwise the same sums), on the VALU instead of LDS permutes --
+// row_ror:8 is lane ^ 8 inside a 16-lane DPP row, and gfx950's permlane16 / permlane32 swaps hand
+// every lane its l ^ 16 / l ^ 32 partner in the second result
+template <int FROM>
+__device__ __forceinline__ float xor_sum_from(float v) {
+  static_assert(FROM == 8 || FROM == 16 || FROM == 32, "xor_sum_from: FROM in {8, 16, 32}");
+  if constexpr (FROM <= 8) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, true));
+  if constexpr (FROM <= 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -167,12 +167,10 @@ __device__ __forceinline__ void tile_stats128_vv(const TapGemmParams& p, char* E
         s2[e] = fmaf(d, d, s2[e]);
       }
 #pragma unroll
-  for (int off = NCH; off < 64; off *= 2)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += __shfl_xor(s1[e], off, 64);
-      s2[e] += __shfl_xor(s2[e], off, 64);
-    }
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = xor_sum_from<NCH>(s1[e]);
+    s2[e] = xor_sum_from<NCH>(s2[e]);
+  }
   __syncthreads();  // every image read (stores, rows above) is done: rows 8.. become scratch
   float* xch = (float*)(E + 8 * RB);  // [4 waves][2][BN]
   if (lane < NCH)
