@@ -18,8 +18,18 @@ import sys
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*\)$", "", name) if not name.startswith("void at::") else name.split("(")[0]
-    return name[:110]
+    """Kernel name without its parameter list (the LAST balanced parenthesis group, so names with
+    '(anonymous namespace)' keep their kernel part) and without the anonymous-namespace marker."""
+    if name.startswith("void at::"):
+        name = name.split("(")[0]
+    elif name.endswith(")"):
+        depth = 0
+        for i in range(len(name) - 1, -1, -1):
+            depth += {")": 1, "(": -1}.get(name[i], 0)
+            if depth == 0:
+                name = name[:i]
+                break
+    return name.replace("(anonymous namespace)::", "")[:110]
 
 
 def main(argv=None):
