@@ -361,21 +361,25 @@ __global__ void __launch_bounds__(256) gconv_gather_kernel(const GconvParams p) 
 #pragma unroll
     for (int ct = 0; ct < CPT; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // forward: every k-step runs -- past the kernel's taps (st >= nst) the fragments are zero and
+  // the taps point at the zero pixel, so the products vanish, and a uniform branch around them cut
+  // the accumulators' live ranges into pieces shuttled through AGPRs (fwd 163 -> 154 us on the
+  // 1024-channel stride-2 shape); the data gradient keeps the branch (without it its 32-channel
+  // variant measured 449 -> 568 us, gconv_oldkernel_ab.txt)
 #pragma unroll
   for (int st = 0; st < NST; ++st) {
-    if (st < nst) {  // uniform
-      bf16x8 b[CPT];
+    if (DGRAD && st >= nst) continue;  // uniform
+    bf16x8 b[CPT];
 #pragma unroll
-      for (int ct = 0; ct < CPT; ++ct) {
-        const int idx = tap_idx(p, g[ct], toh[st], tow[st], tok[st]);
-        b[ct] = *LDS_PTR(bf16x8, smem + idx * (SG * 2) + chunk * 16);
-      }
-#pragma unroll
-      for (int rt = 0; rt < NRT; ++rt)
-#pragma unroll
-        for (int ct = 0; ct < CPT; ++ct)
-          acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st][rt], b[ct], acc[rt][ct], 0, 0, 0);
+    for (int ct = 0; ct < CPT; ++ct) {
+      const int idx = tap_idx(p, g[ct], toh[st], tow[st], tok[st]);
+      b[ct] = *LDS_PTR(bf16x8, smem + idx * (SG * 2) + chunk * 16);
     }
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < CPT; ++ct)
+        acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st][rt], b[ct], acc[rt][ct], 0, 0, 0);
   }
 
   if constexpr (DGRAD) {
