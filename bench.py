@@ -68,6 +68,9 @@ def parse(argv=None):
                     help="N > 1: skip the second, SyncBN-timed phase")
     ap.add_argument("--no-syncbn-peer", dest="syncbn_peer", action="store_false",
                     help="N > 1: skip the third phase, SyncBN over the peer-memory mailboxes (parallel/peer.py)")
+    ap.add_argument("--syncbn-shared-group", action="store_true",
+                    help="SyncBN collectives on the gradient communicator instead of their own "
+                         "(DCP_SYNCBN_SHARED_GROUP=1; parallel/ddp.py bn_process_group)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce precision (bf16: half the xGMI bytes; bucket engine: bf16 buckets, "
@@ -210,6 +213,8 @@ def main(argv=None):
     backend = os.environ.get("DCP_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
     dist_on = world > 1 or a.force_ddp
+    if a.syncbn_shared_group:
+        os.environ["DCP_SYNCBN_SHARED_GROUP"] = "1"
     if a.graph is None:  # default: HIP-graph replay on one GPU without a process group, eager otherwise
         a.graph = not dist_on
     if dist_on:
@@ -453,6 +458,55 @@ def main(argv=None):
         out["syncbn_ms_per_step"] = round(sdt / a.steps * 1000.0, 3)
         out["syncbn_per_rank_ms"] = [round(v / a.steps * 1000.0, 3) for v in sper]
 
+    def bn_stats_forward(transport):
+        """One no-grad training-mode forward with the SyncBN statistics exchanged over ``transport``:
+        the statistics every BN layer merged (its running-stat update), BN state restored after."""
+        from ddp_classification_pytorch_amd.models.layers import BatchNorm2d
+
+        net = pddp.unwrap(model)
+        pddp.convert_sync_batchnorm(net, bn_group, transport=transport)
+        bns = [m for m in net.modules() if isinstance(m, BatchNorm2d)]
+        saved = [(m.running_mean.clone(), m.running_var.clone(), m._nbt_pending) for m in bns]
+        x = Fn.to_device_nhwc(images, mean, std, nchw=True, in_scale=1.0 / 255.0, **layout)
+        with torch.no_grad():
+            net(x, labels) if a.config == "arcface" else net(x)
+        got = [(m.running_mean.clone(), m.running_var.clone()) for m in bns]
+        for m, (rm, rv, nbt) in zip(bns, saved):
+            m.running_mean.copy_(rm)
+            m.running_var.copy_(rv)
+            m._nbt_pending = nbt
+        return got
+
+    def peer_crosscheck(ex):
+        """The peer transport against RCCL on the same inputs: the collectives themselves
+        (a SyncBN-sized gather must be bitwise equal; the sums agree to fp32 summation order) and the
+        BN statistics of one forward of the model.  Worst relative difference over all of them."""
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(77 + rank)
+        st = torch.randn(3 * 2048, device=dev, generator=gen)
+        ref = torch.empty(world * st.numel(), device=dev)
+        dist.all_gather_into_tensor(ref, st, group=bn_group)
+        got = torch.empty_like(ref)
+        ex.all_gather_into_tensor(got, st)
+        red_ref = st.clone()
+        dist.all_reduce(red_ref, group=bn_group)
+        red_got = st.clone()
+        ex.all_reduce(red_got)
+        ex.check()
+
+        def rel(u, v):
+            return float(((u - v).abs().max() / v.abs().max().clamp_min(1e-30)).item())
+
+        diffs = {"gather": rel(got, ref), "reduce": rel(red_got, red_ref)}
+        a_st, b_st = bn_stats_forward("rccl"), bn_stats_forward("peer")
+        ex.check()
+        diffs["bn_stats"] = max(max(rel(p[0], q[0]), rel(p[1], q[1])) for p, q in zip(b_st, a_st))
+        t = torch.tensor([max(diffs.values())], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out["syncbn_peer_max_rel_diff"] = float(t.item())
+        out["syncbn_peer_rel_diff_parts"] = {k: float(v) for k, v in diffs.items()}
+
     def syncbn_peer_phase():
         nonlocal run, graphed
         # third phase: the same SyncBN with its statistics exchanged through the IPC-mapped peer
@@ -463,6 +517,7 @@ def main(argv=None):
         ex = peer.exchange_for(bn_group)
         if ex is None:
             raise RuntimeError("peer mailboxes unavailable (no peer access): stayed on RCCL")
+        peer_crosscheck(ex)  # leaves the peer transport on
         if a.graph:
             from ddp_classification_pytorch_amd.engine.graph import GraphedStep
 

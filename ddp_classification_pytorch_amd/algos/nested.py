@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from ..engine.checkpoint import is_rank0, load_checkpoint
 from ..engine.logger import MetricsLogger
-from ..engine.loop import valid_count
+from ..engine.loop import _check_transports, valid_count
 from ..engine.runtime import build_data, setup
 from ..models.heads import NetClassifier
 from ..models.nested import NetFeat
@@ -200,6 +200,7 @@ def run(args):
                 losses.update(loss.item(), B)
                 top1.update(100.0 * (rank < 1).sum().item() / B, B)
                 top3.update(100.0 * (rank < 3).sum().item() / B, B)
+                _check_transports()  # a timed-out SyncBN peer exchange ends the run (parallel/peer.py)
                 if bar is not None:
                     bar(i, n_steps, f"Loss: {losses.avg:.3f} | Top1: {top1.avg:.3f}% | Top3: {top3.avg:.3f}%")
         a1, a3, k = evaluate(epoch + 1, best)

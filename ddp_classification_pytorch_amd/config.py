@@ -46,15 +46,20 @@ def build_parser() -> argparse.ArgumentParser:
     a("--no-syncbn", dest="syncbn", action="store_false")
     a("--syncbn-transport", default=None, choices=["rccl", "peer"],
       help="SyncBN statistics exchange: rccl collectives (default) or the peer-memory mailboxes (parallel/peer.py)")
+    a("--syncbn-shared-group", action="store_true",
+      help="SyncBN collectives on the gradient communicator (the default group) instead of their own; the "
+           "fallback if two RCCL communicators in flight on one GPU misbehave (DCP_SYNCBN_SHARED_GROUP=1)")
     a("--force-ddp", action="store_true",
       help="one process: still create a (world-1) process group and train through the data-parallel engine "
            "(measures the engine's own cost; tests its HIP-graph capture)")
     a("--bucket-cap-mb", type=float, default=25.0)
     a("--first-bucket-mb", type=float, default=4.0)
     a("--device", default=None, help="cuda (default when available) or cpu")
-    a("--graph", action="store_true",
+    a("--graph", dest="graph", action="store_true", default=None,
       help="replay the training step as a HIP graph (launch-bound small batches); with several ranks the "
-           "bucket engine's all-reduces and per-bucket optimizer are captured too")
+           "bucket engine's all-reduces and per-bucket optimizer are captured too.  Default ON for the "
+           "baseline / arcface / cdr loops on the GPU (DCP_GRAPH=0 or --no-graph: eager)")
+    a("--no-graph", "--eager", dest="graph", action="store_false")
     # data
     a("--data", default="folder", choices=["folder", "imagefolder", "list", "synthetic", "synthetic-device", "shards"],
       help="synthetic: random images through the host DataLoader path; synthetic-device: random uint8 batches "
@@ -172,9 +177,26 @@ def resolve(args: argparse.Namespace) -> argparse.Namespace:
             args.model = "cifar_" + args.model
     if args.workload == "cdr" and args.num_class_dirs is None and args.data == "folder":
         args.num_class_dirs = 100  # CDR/main.py:73
+    if args.graph is None:
+        # HIP-graph replay wherever the step grapher is eligible: the ClassificationLoop workloads on a
+        # GPU (fixed-shape batches; a short last batch runs eagerly; torch-DDP steps stay eager, see
+        # engine/loop.py).  At the reference's per-GPU batches of 16-64 replay is 1.3-1.5x the eager
+        # step; NESTED / PLC run their own loops.
+        env = os.environ.get("DCP_GRAPH")
+        on_gpu = (args.device or "cuda").startswith("cuda") and _cuda_available()
+        args.graph = (env == "1") if env in ("0", "1") else (on_gpu and args.workload in ("baseline", "arcface", "cdr"))
     if args.nested > 0 and args.dropout > 0:
         raise ValueError("nested dropout and standard dropout are mutually exclusive (NESTED/train.py:489-490)")
     return args
+
+
+def _cuda_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def parse_args(argv=None):

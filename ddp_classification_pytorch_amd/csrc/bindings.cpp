@@ -1405,7 +1405,7 @@ void enable_peer_access(int64_t peer) {
 
 // SyncBN peer exchange (parallel/peer.py): src fp32 [n] -> dst fp32 [world * n] (mode 0) or [n] (mode 1)
 void peer_exchange(const Tensor& src, const Tensor& dst, const Tensor& boxes, const Tensor& epoch, int64_t rank,
-                   int64_t world, int64_t slot, int64_t mode, const Tensor& err) {
+                   int64_t world, int64_t slot, int64_t mode, const Tensor& err, int64_t timeout_ms) {
   CHECK_DEV(src);
   CHECK_F32(src);
   CHECK_F32(dst);
@@ -1418,7 +1418,8 @@ void peer_exchange(const Tensor& src, const Tensor& dst, const Tensor& boxes, co
   TORCH_CHECK(dst.numel() == (mode == 0 ? world * n : n), "peer_exchange dst size");
   TORCH_CHECK(dcp::launch_peer_exchange(src.data_ptr<float>(), (int)n, dst.data_ptr<float>(), boxes.data_ptr<int64_t>(),
                                         epoch.data_ptr<int>(), (int)rank, (int)world, (int)slot, (int)mode,
-                                        err.data_ptr<int>(), cur_stream()),
+                                        err.data_ptr<int>(), (int)std::min<int64_t>(timeout_ms, INT32_MAX),
+                                        cur_stream()),
               "peer_exchange: world / rank / size out of range");
 }
 
@@ -1720,6 +1721,47 @@ Tensor table_fill(const Tensor& host, const Tensor& device_like) {
 
 int64_t autotune_entries() { return dcp::tap_gemm_tuned_count() + wgrad_autotune_entries(); }
 
+// the autotuner's decisions (tap GEMM "tg\t..." and weight-gradient "wg\t..." lines) for a tuning
+// cache file (DCP_TUNE_CACHE, _ext.py): a later process replays them without timing anything
+std::string autotune_export() {
+  std::string out;
+  const std::string tg = dcp::tap_gemm_tune_export();
+  size_t pos = 0;
+  while (pos < tg.size()) {
+    const size_t nl = tg.find('\n', pos);
+    out += "tg\t" + tg.substr(pos, (nl == std::string::npos ? tg.size() : nl) - pos) + "\n";
+    pos = nl == std::string::npos ? tg.size() : nl + 1;
+  }
+  std::lock_guard<std::mutex> lk(g_wg_mu);
+  for (const auto& kv : g_wg_choice) out += "wg\t" + kv.first + "\t" + std::to_string(kv.second) + "\n";
+  return out;
+}
+
+int64_t autotune_import(const std::string& text) {
+  std::string tg;
+  int64_t n = 0;
+  const int nwg = (int)(sizeof(kWgCfgs) / sizeof(kWgCfgs[0]));
+  size_t pos = 0;
+  while (pos < text.size()) {
+    size_t nl = text.find('\n', pos);
+    if (nl == std::string::npos) nl = text.size();
+    const std::string line = text.substr(pos, nl - pos);
+    pos = nl + 1;
+    if (line.compare(0, 3, "tg\t") == 0) {
+      tg += line.substr(3) + "\n";
+    } else if (line.compare(0, 3, "wg\t") == 0) {
+      const size_t tab = line.rfind('\t');
+      if (tab <= 3) continue;
+      const int c = atoi(line.c_str() + tab + 1);
+      if (c < 0 || c >= nwg) continue;
+      std::lock_guard<std::mutex> lk(g_wg_mu);
+      g_wg_choice[line.substr(3, tab - 3)] = c;
+      ++n;
+    }
+  }
+  return n + dcp::tap_gemm_tune_import(tg);
+}
+
 void set_tuning(int64_t idx, int64_t value) {
   TORCH_CHECK(idx >= 0 && idx < dcp::kTuneSlots, "tuning index");
   dcp::g_tune[idx] = (int)value;
@@ -1736,6 +1778,8 @@ TORCH_LIBRARY(dcp, m) {
   m.def("set_tuning(int idx, int value) -> ()", &set_tuning);
   m.def("tuning_slots() -> str", &tuning_slots);
   m.def("autotune_entries() -> int", &autotune_entries);
+  m.def("autotune_export() -> str", &autotune_export);
+  m.def("autotune_import(str text) -> int", &autotune_import);
   m.def("table_fill(Tensor host, Tensor device_like) -> Tensor", &table_fill);
   m.def("mt_weight_prep(Tensor entries, Tensor blocks) -> ()", &mt_weight_prep);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, bool stats) -> (Tensor, Tensor)", &conv_fwd);
@@ -1827,7 +1871,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("conv3x3_wgrad_pro(Tensor dy, Tensor x, Tensor scale, Tensor shift) -> Tensor", &conv3x3_wgrad_pro);
   m.def("conv3x3_pro_fits(int N, int H, int W, int C, int Co) -> bool", &conv3x3_pro_fits);
   m.def("peer_exchange(Tensor src, Tensor(a!) dst, Tensor boxes, Tensor(b!) epoch, int rank, int world, int slot, "
-        "int mode, Tensor(c!) err) -> ()", &peer_exchange);
+        "int mode, Tensor(c!) err, int timeout_ms) -> ()", &peer_exchange);
   m.def("nested_eval_scalar(Tensor feat, Tensor W, Tensor labels) -> Tensor", &nested_eval_scalar);
   m.def("dwconv_fwd(Tensor x, Tensor filt, int k, int s, int p, bool reflect) -> Tensor", &dwconv_fwd);
   m.def("dwconv_bwd(Tensor dy, Tensor filt, int H, int W, int k, int s, int p, bool reflect) -> Tensor", &dwconv_bwd);

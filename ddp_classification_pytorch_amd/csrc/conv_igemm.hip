@@ -2195,6 +2195,37 @@ int tap_gemm_tuned_count() {
   return (int)g_tg_choice.size();
 }
 
+// The tuner's decisions as text ("<key>\t<choice>\n" per problem) and back: a tuning cache that
+// makes a later process run exactly the kernels an earlier one measured (DCP_TUNE_CACHE, _ext.py) --
+// reproducible kernel choices run to run, and profiles without tuning dispatches.  Keys never
+// contain tabs or newlines; entries whose choice is out of this build's candidate range are skipped.
+std::string tap_gemm_tune_export() {
+  std::lock_guard<std::mutex> lk(g_tg_mu);
+  std::string out;
+  for (const auto& kv : g_tg_choice) out += kv.first + "\t" + std::to_string(kv.second) + "\n";
+  return out;
+}
+
+int tap_gemm_tune_import(const std::string& text) {
+  const int ncfg = (int)(sizeof(kTgCfgs) / sizeof(kTgCfgs[0]));
+  std::lock_guard<std::mutex> lk(g_tg_mu);
+  int n = 0;
+  size_t pos = 0;
+  while (pos < text.size()) {
+    size_t nl = text.find('\n', pos);
+    if (nl == std::string::npos) nl = text.size();
+    const std::string line = text.substr(pos, nl - pos);
+    pos = nl + 1;
+    const size_t tab = line.rfind('\t');
+    if (tab == std::string::npos || tab == 0) continue;
+    const int c = atoi(line.c_str() + tab + 1);
+    if (c < 0 || c >= ncfg) continue;
+    g_tg_choice[line.substr(0, tab)] = c;
+    ++n;
+  }
+  return n;
+}
+
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                      const bf16* wt, int Co, int T,
                      bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,

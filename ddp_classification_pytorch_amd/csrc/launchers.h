@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 typedef __bf16 bf16;
 
 namespace dcp {
@@ -60,6 +62,9 @@ using WorkspaceFree = void (*)(void* ptr);
 void set_workspace_allocator(WorkspaceAlloc alloc, WorkspaceFree free_fn);
 // number of problems the tap-GEMM autotuner (g_tune[kAutotune] = 1) has measured in this process
 int tap_gemm_tuned_count();
+// the tuner's per-problem choices as "key\tchoice" lines, and back (returns entries accepted)
+std::string tap_gemm_tune_export();
+int tap_gemm_tune_import(const std::string& text);
 void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16* wt, int Co, int T, bf16* dst, int Hd,
                      int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox, const TapList& taps, float* stats,
                      const float* bias, int relu, const bf16* zero, hipStream_t stream, const bf16* addsrc = nullptr,
@@ -275,9 +280,10 @@ void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t*
                                int* counts, hipStream_t s);
 // workspace bytes of launch_nested_eval (label score chains + per-class-block rank counts)
 // SyncBN peer-memory exchange (peer.hip): gather (mode 0, dst [world][n]) or rank-ordered sum
-// (mode 1, dst [n]) of n floats through the IPC-mapped mailboxes `boxes` ([world] base addresses)
+// (mode 1, dst [n]) of n floats through the IPC-mapped mailboxes `boxes` ([world] base addresses);
+// a rank missing for timeout_ms sets *err and poisons dst with NaN (this and every later exchange)
 bool launch_peer_exchange(const float* src, int n, float* dst, const int64_t* boxes, int* epoch, int rank, int world,
-                          int slot, int mode, int* err, hipStream_t s);
+                          int slot, int mode, int* err, int timeout_ms, hipStream_t s);
 size_t nested_eval_workspace(int B, int D, int C);
 void launch_nested_eval(const float* feat, const float* W, const int64_t* labels, int B, int D, int C, int* counts,
                         void* ws, hipStream_t s);

@@ -12,9 +12,16 @@
 //   3. after every storing wave drained its stores and a system-scope release, sets flag[rank] = e
 //      in every mailbox;
 //   4. polls its own mailbox's flags until every rank's is >= e (system-scope loads, s_sleep
-//      between polls, bounded: after ~0.5 s it records an error and stops waiting);
+//      between polls), bounded by a wall-clock deadline (timeout_ms on the 100 MHz constant clock);
 //   5. after a system-scope acquire, reads the world slots [e & 1][*] (system-scope loads) and
 //      writes them out gathered ([world][n]) or summed in rank order ([n]; identical on every rank).
+// A missed deadline FAILS LOUDLY instead of reading a stale slot: the kernel records err = 1, writes
+// NaN into dst (so the statistics, the loss and every later step are visibly poisoned, never
+// silently wrong), and every later exchange of this rank sees err != 0 and fails immediately the
+// same way (no further waiting, no stores into the peers' mailboxes: a rank that lost the
+// protocol must not overwrite slots a slower rank has yet to read).  The host raises on err at its
+// next sync point (PeerExchange.check / peer.check_all, called by the training loop at every log
+// interval and epoch end, and by bench.py's peer phase).
 // Slots alternate by epoch parity: a rank can be at most one exchange ahead of the slowest (it
 // needs everyone's flag for e before it starts e + 1), so its e + 1 stores never land in the
 // parity a slower rank is still reading for e.
@@ -25,22 +32,32 @@ namespace dcp {
 
 namespace {
 constexpr int kPeerMaxWorld = 64;
-constexpr int kPeerSpinLimit = 1 << 23;  // s_sleep polls before giving up (~0.5 s)
+constexpr uint64_t kWallHz = 100000000ull;  // s_memrealtime: 100 MHz constant clock on CDNA
+
+__device__ __forceinline__ void poison(float* dst, int cnt, int tid) {
+  for (int i = tid; i < cnt; i += blockDim.x) dst[i] = __builtin_nanf("");
+}
 }  // namespace
 
 // mailbox layout (floats): [2 parities][world][slot] data, then flags (int) [world]
 __global__ void __launch_bounds__(1024) peer_exchange_kernel(const float* __restrict__ src, int n,
                                                              float* __restrict__ dst, const int64_t* __restrict__ boxes,
                                                              int* __restrict__ epoch, int rank, int world, int slot,
-                                                             int mode, int* __restrict__ err) {
-  __shared__ int e_sh;
+                                                             int mode, int* __restrict__ err, int timeout_ms) {
+  __shared__ int e_sh, bad_sh;
   const int tid = threadIdx.x;
+  const int cnt = mode == 0 ? world * n : n;
   if (tid == 0) {
     const int e = *epoch + 1;
     *epoch = e;
     e_sh = e;
+    bad_sh = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  if (bad_sh != 0) {  // an earlier exchange of this rank timed out: the protocol is lost, fail fast
+    poison(dst, cnt, tid);
+    return;
+  }
   const int e = e_sh, par = e & 1;
   const size_t flags_off = (size_t)2 * world * slot;
   // 2. push this rank's data into every mailbox
@@ -59,13 +76,17 @@ __global__ void __launch_bounds__(1024) peer_exchange_kernel(const float* __rest
     int* flags = reinterpret_cast<int*>(reinterpret_cast<float*>(boxes[tid]) + flags_off);
     __hip_atomic_store(flags + rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 4. wait for every rank's flag in this rank's own mailbox
+  // 4. wait for every rank's flag in this rank's own mailbox, up to the wall-clock deadline
+  if (tid == 0) bad_sh = 0;
+  __syncthreads();
   if (tid < world) {
     int* flags = reinterpret_cast<int*>(reinterpret_cast<float*>(boxes[rank]) + flags_off);
-    int spins = 0;
+    const uint64_t t0 = wall_clock64();
+    const uint64_t limit = (uint64_t)timeout_ms * (kWallHz / 1000ull);
     while (__hip_atomic_load(flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (++spins > kPeerSpinLimit) {
+      if (wall_clock64() - t0 > limit) {
         atomicOr(err, 1);
+        atomicOr(&bad_sh, 1);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -73,6 +94,10 @@ __global__ void __launch_bounds__(1024) peer_exchange_kernel(const float* __rest
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+  if (bad_sh != 0) {  // a rank never published: poison instead of reading a stale parity slot
+    poison(dst, cnt, tid);
+    return;
+  }
   // 5. gather / rank-ordered sum
   const float* mine = reinterpret_cast<const float*>(boxes[rank]) + (size_t)par * world * slot;
   if (mode == 0) {
@@ -91,10 +116,10 @@ __global__ void __launch_bounds__(1024) peer_exchange_kernel(const float* __rest
 }
 
 bool launch_peer_exchange(const float* src, int n, float* dst, const int64_t* boxes, int* epoch, int rank, int world,
-                          int slot, int mode, int* err, hipStream_t s) {
-  if (world < 1 || world > kPeerMaxWorld || n > slot || rank < 0 || rank >= world) return false;
+                          int slot, int mode, int* err, int timeout_ms, hipStream_t s) {
+  if (world < 1 || world > kPeerMaxWorld || n > slot || rank < 0 || rank >= world || timeout_ms < 1) return false;
   hipLaunchKernelGGL(peer_exchange_kernel, dim3(1), dim3(1024), 0, s, src, n, dst, boxes, epoch, rank, world, slot,
-                     mode, err);
+                     mode, err, timeout_ms);
   return true;
 }
 

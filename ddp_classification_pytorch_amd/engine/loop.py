@@ -47,6 +47,15 @@ def _allreduce(t):
     return t
 
 
+def _check_transports():
+    """Fail loudly if a SyncBN peer exchange timed out (parallel/peer.py: its results are NaN);
+    a no-op unless the peer transport is on.  Called where the loop synchronises anyway."""
+    if torch.cuda.is_available():
+        from ..parallel import peer
+
+        peer.check_all()
+
+
 def valid_count(sampler, n_total):
     """Samples of this rank that are not DistributedSampler padding."""
     if sampler is None or not hasattr(sampler, "world"):
@@ -220,6 +229,7 @@ class ClassificationLoop:
                 if timing:
                     ev1.synchronize()
                     gpu_ms = ev0.elapsed_time(ev1) / max(win_steps, 1)
+                _check_transports()
                 now = time.time()
                 win_ips = win_steps * B * self.rt.world / max(now - t_win, 1e-9)  # window wall rate (synced above)
                 t_win = now
@@ -245,6 +255,7 @@ class ClassificationLoop:
                                                   row_limit=60))
             prof.export_chrome_trace(os.path.join(pdir, "trace.json"))
         tot = _allreduce(acc).tolist()
+        _check_transports()
         self.logger.progress("", end="\n")
         n = max(tot[3], 1)
         return {"loss": tot[0] / n, "top1": tot[1] / n, "top3": tot[2] / n, "count": tot[3],

@@ -37,8 +37,12 @@ def setup(args) -> Runtime:
         graph_safe_nccl_env()
     if getattr(args, "syncbn_transport", None):
         os.environ["DCP_SYNCBN_TRANSPORT"] = args.syncbn_transport  # read by convert_sync_batchnorm
+    if getattr(args, "syncbn_shared_group", False):
+        os.environ["DCP_SYNCBN_SHARED_GROUP"] = "1"  # read by parallel.ddp.bn_process_group
     rank, local, world = init_distributed(backend, force=getattr(args, "force_ddp", False))
     if want_cuda:
+        # (one GPU per rank; tests run several gloo ranks on one device: wrap like bench.py)
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         kops = _ext.hip_ops()  # GPU path requires the gfx950 library: fail loudly here, not mid-epoch

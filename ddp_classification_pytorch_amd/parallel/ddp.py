@@ -81,9 +81,18 @@ _BN_GROUPS = {}
 
 def bn_process_group():
     """The SyncBN communicator: one extra group over all ranks, created once per default group
-    (collectively: every rank calls this in the same order, from convert_sync_batchnorm)."""
+    (collectively: every rank calls this in the same order, from convert_sync_batchnorm).
+
+    ``DCP_SYNCBN_SHARED_GROUP=1`` (``--syncbn-shared-group``): the default group instead -- the BN
+    statistics collectives then share the gradient communicator and its stream, serialised with the
+    bucket all-reduces in issue order (a statistics exchange can wait behind a 25 MiB bucket).  That
+    is the fallback for stacks where two RCCL communicators in flight at once on one GPU (the BN
+    group on the compute stream, the buckets on the side stream) could deadlock when kernel
+    residency differs across ranks."""
     if not dist.is_initialized():
         return None
+    if os.environ.get("DCP_SYNCBN_SHARED_GROUP", "0") == "1":
+        return dist.group.WORLD
     key = id(dist.group.WORLD)
     g = _BN_GROUPS.get(key)
     if g is None:

@@ -60,7 +60,7 @@ def _comm_stream(device, world=2):
 
 class _Bucket:
     __slots__ = ("index", "params", "offsets", "numels", "grad_buf", "comm_buf", "views", "pending", "launched",
-                 "pack_key", "pack_tab", "unpack_tab", "nbytes")
+                 "pack_key", "pack_tab", "unpack_tab", "nbytes", "used_off", "ones")
 
     def __init__(self, index, params, device, comm_dtype, align=16):
         self.index = index
@@ -71,11 +71,17 @@ class _Bucket:
             self.offsets.append(n)
             self.numels.append(p.numel())
             n += (p.numel() + align - 1) // align * align
+        # "used" tail: one slot per parameter, packed as 1/world by every rank that produced its
+        # gradient (0 otherwise), so after the all-reduce a slot is > 0 iff SOME rank used the
+        # parameter -- torch DDP's find_unused bitmap, riding in the same collective
+        self.used_off = n
+        n += (len(params) + align - 1) // align * align
         self.grad_buf = torch.zeros(n, dtype=torch.float32, device=device)
         self.comm_buf = (self.grad_buf if comm_dtype == torch.float32
                          else torch.zeros(n, dtype=comm_dtype, device=device))
         self.views = [self.grad_buf[o:o + k].view_as(p) for p, o, k in zip(params, self.offsets, self.numels)]
-        self.nbytes = n * self.comm_buf.element_size()
+        self.ones = torch.ones(len(params), dtype=torch.float32, device=device)
+        self.nbytes = self.used_off * self.comm_buf.element_size()  # the gradients (the used tail aside)
         self.pending = len(params)
         self.launched = False
         self.pack_key = None
@@ -214,22 +220,27 @@ class BucketReducer:
         # the first backward only records the ready order; its buckets launch together at the end
         return self._rebuilt
 
-    def _pack_tables(self, b, grads):
+    def _pack_tables(self, b, grads, used):
+        """Device tables of the bucket's pack launch: every gradient into its slice, and ``used``
+        (ones, or a 0/1 vector when this rank lacks some gradient) into the used tail."""
         from ..ops import functional as Fn
 
-        key = tuple(g.data_ptr() for g in grads)
+        key = tuple(g.data_ptr() for g in grads) + (used.data_ptr(),)
         if key != b.pack_key:
-            rows = [(b.comm_buf.data_ptr() + o * b.comm_buf.element_size(), g.data_ptr(), 0, 0, 0, n)
+            esz = b.comm_buf.element_size()
+            rows = [(b.comm_buf.data_ptr() + o * esz, g.data_ptr(), 0, 0, 0, n)
                     for g, o, n in zip(grads, b.offsets, b.numels)]
+            rows.append((b.comm_buf.data_ptr() + b.used_off * esz, used.data_ptr(), 0, 0, 0, len(b.params)))
             if b.pack_tab is None:
-                counts = torch.tensor([(n + CHUNK - 1) // CHUNK for n in b.numels], dtype=torch.int64)
+                counts = torch.tensor([(n + CHUNK - 1) // CHUNK for n in b.numels + [len(b.params)]],
+                                      dtype=torch.int64)
                 ent = torch.repeat_interleave(torch.arange(len(b.numels), dtype=torch.int64), counts)
                 first = torch.repeat_interleave(torch.cumsum(counts, 0) - counts, counts)
                 ch = torch.stack([ent, torch.arange(ent.numel(), dtype=torch.int64) - first], 1)
                 b.unpack_tab = [None, Fn.table_to_device(ch.to(torch.int32), torch.int32, self.device).view(-1, 2)]
                 if self.comm_dtype != torch.float32:
                     urows = [(b.grad_buf.data_ptr() + o * 4, b.comm_buf.data_ptr() + o * b.comm_buf.element_size(),
-                              0, 0, 0, n) for o, n in zip(b.offsets, b.numels)]
+                              0, 0, 0, n) for o, n in zip(b.offsets + [b.used_off], b.numels + [len(b.params)])]
                     b.unpack_tab[0] = Fn.table_to_device(urows, torch.int64, self.device).view(-1, 6)
             b.pack_tab = Fn.table_to_device(rows, torch.int64, self.device).view(-1, 6)
             b.pack_key = key
@@ -248,30 +259,45 @@ class BucketReducer:
                 self._reduce_cuda(b, grads, comm)
         else:
             self._reduce_cpu(b, grads)
-        # a parameter without a gradient on THIS rank (unused in this forward) contributed zeros
-        # to the all-reduce; it still gets the reduced view as its gradient, on every rank, so
-        # the replicas apply the same update whether or not another rank used it (torch DDP
-        # gives every rank the reduced bucket view too).  Unlike DDP with find_unused_parameters,
-        # a parameter no rank used gets a zero gradient rather than None: weight decay and
-        # momentum still move it -- identically on every rank, so nothing drifts.
-        if not all(present) and not self._warned_unused:
-            self._warned_unused = True
-            import warnings
+        # A parameter without a gradient on THIS rank (unused in this forward) contributed zeros to
+        # the all-reduce.  If ANOTHER rank used it, it gets the reduced view as its gradient, so the
+        # replicas apply the same update (torch DDP gives every rank the reduced bucket view too).
+        # If NO rank used it (its used slot summed to 0), it keeps grad None on every rank, as torch
+        # DDP with find_unused_parameters leaves it: the optimizer then skips it (no weight decay or
+        # momentum on a parameter that took no part).  Deciding that reads the used slots on the host
+        # -- a sync paid only by a rank that lacks a gradient, never on the all-used fast path.
+        unused = set()
+        if not all(present):
+            if self.cuda and torch.cuda.is_current_stream_capturing():
+                # no host read inside a HIP-graph capture: the zero-gradient view stays (every rank
+                # alike); a graphed step with unused parameters is not expected
+                pass
+            else:
+                slots = b.comm_buf[b.used_off:b.used_off + len(b.params)].float().cpu()
+                unused = {k for k, ok in enumerate(present) if not ok and float(slots[k]) <= 0.0}
+            if not self._warned_unused:
+                self._warned_unused = True
+                import warnings
 
-            warnings.warn("BucketReducer: some parameters received no gradient on this rank; they are updated "
-                          "with the all-reduced bucket view (zero where no rank used them)", stacklevel=2)
-        for p, v in zip(b.params, b.views):
-            p.grad = v
+                warnings.warn("BucketReducer: some parameters received no gradient on this rank; those another "
+                              "rank used get the all-reduced bucket view, those no rank used keep grad None",
+                              stacklevel=2)
+        for k, (p, v) in enumerate(zip(b.params, b.views)):
+            p.grad = None if k in unused else v
         self._step_optimizers(b)
 
     def _reduce_cuda(self, b, grads, comm):
         K = _ext.hip_ops()
         missing = [k for k, g in enumerate(grads) if g is None]
-        if missing:  # an unused parameter this step: its bucket slice carries zeros
+        used = b.ones
+        if missing:  # an unused parameter this step: its bucket slice carries zeros, its used slot 0
+            used = b.ones.clone()
             for k in missing:
                 b.views[k].zero_()
                 grads[k] = b.views[k]
-        pack, chunks, unpack = self._pack_tables(b, grads)
+                used[k] = 0.0
+            self._hold.append([used])  # read by the pack launch (side stream): alive to the join
+        pack, chunks, unpack = self._pack_tables(b, grads, used)
         mode = 2 if self.comm_dtype == torch.bfloat16 else 0
         K.mt_copy(pack, chunks, 1.0 / self.world, mode)
         if comm != self._compute:
@@ -291,6 +317,7 @@ class BucketReducer:
                     dst.zero_()
                 else:
                     dst.copy_(g.reshape(-1).to(torch.float32) / self.world)
+                b.comm_buf[b.used_off + k] = 0.0 if g is None else 1.0 / self.world
             if self.reduce:
                 dist.all_reduce(b.comm_buf, group=self.group)
             if b.comm_buf is not b.grad_buf:

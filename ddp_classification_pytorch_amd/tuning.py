@@ -16,6 +16,9 @@ SLOTS = {
     "bn_bwd_cap": 28, "row_reduce": 29, "c3_epilogue": 30, "c3_window_kb": 31,
 }
 NUM_SLOTS = 32
+# the loaded library's own table (set by verify); apply() skips names it does not have at the same
+# index -- a DCP_LIB build from another tree may number its slots differently
+LIB_SLOTS = None
 
 
 def slot(name) -> int:
@@ -45,16 +48,32 @@ def apply(K, spec, reset: bool = False):
     if reset:
         for i in range(NUM_SLOTS):
             K.set_tuning(i, 0)
-    for i, v in parse_spec(spec) if isinstance(spec, str) else spec:
-        K.set_tuning(slot(i), int(v))
+    items = []
+    if isinstance(spec, str):
+        for kv in filter(None, (t.strip() for t in (spec or "").replace(";", ",").split(","))):
+            k, v = kv.split("=")
+            items.append((k.strip(), int(v)))
+    else:
+        items = list(spec)
+    for name, v in items:
+        i = slot(name)
+        if LIB_SLOTS is not None and not isinstance(name, int) and not str(name).strip().lstrip("-").isdigit():
+            if LIB_SLOTS.get(str(name).strip()) != i:
+                import warnings
+
+                warnings.warn(f"tuning slot {name!r} (index {i}) is not in the loaded library's table; skipped")
+                continue
+        K.set_tuning(i, int(v))
 
 
 def verify(K) -> None:
     """Fail loudly if the loaded library's slot table differs from this mirror."""
+    global LIB_SLOTS
     lib = {}
     for kv in filter(None, K.tuning_slots().split(";")):
         k, v = kv.split("=")
         lib[k] = int(v)
+    LIB_SLOTS = lib
     if lib != SLOTS:
         raise RuntimeError(f"tuning slot table mismatch: library {lib} vs tuning.py {SLOTS} (stale build?)")
 
@@ -66,3 +85,35 @@ def parse_header(path: str):
     text = open(path).read()
     enum = {k: int(v) for k, v in re.findall(r"\b(k\w+)\s*=\s*(\d+)", text)}
     return {name: enum[ident] for name, ident in re.findall(r'\{"(\w+)",\s*(k\w+)\}', text)}
+
+
+def load_cache(K, path: str) -> int:
+    """Replay an autotuning cache written by :func:`save_cache`: every listed problem runs the
+    recorded kernel configuration without being timed again (returns the entries accepted)."""
+    import os
+
+    if not path or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        return int(K.autotune_import(f.read()))
+
+
+def save_cache(K, path: str) -> int:
+    """Write the autotuner's decisions of this process (merged with what ``path`` already holds)
+    atomically: the per-shape choices of ``cudnn.benchmark``-style tuning, kept across processes so
+    a later run uses exactly the same kernels (reproducible numerics, profiles without tuning)."""
+    import os
+    import tempfile
+
+    if not path:
+        return 0
+    if os.path.exists(path):
+        load_cache(K, path)  # merge: entries of this process win (imported first, then re-exported)
+    text = K.autotune_export()
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(dir=d, prefix=".tune_cache.")
+    with os.fdopen(fd, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+    return text.count("\n")

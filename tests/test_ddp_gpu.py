@@ -45,6 +45,10 @@ def test_bench_two_ranks_one_gpu():
     assert rec["n_gpus"] == 2 and rec["world_size"] == 2 and rec["config"]["global_batch"] == 16
     assert rec["value"] > 0 and rec["syncbn_value"] > 0 and rec["dist_backend"] == "gloo"
     assert len(rec["per_rank_ms"]) == 2
+    # the peer-memory SyncBN phase ran and agrees with the RCCL/gloo transport on the same inputs
+    assert "diagnostic_errors" not in rec, rec.get("diagnostic_errors")
+    assert rec["syncbn_peer_value"] > 0
+    assert rec["syncbn_peer_max_rel_diff"] <= 1e-6, rec["syncbn_peer_rel_diff_parts"]
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -299,25 +303,26 @@ def test_main_graph_force_ddp_side_stream_matches_eager(tmp_path):
     """main.py --graph through the bucket engine on a world-1 RCCL group with the side
     communication stream forced (DCP_COMM_STREAM=1, the N-rank configuration): 2 epochs, the step
     recaptured at the epoch boundary, SyncBN collectives and per-bucket SGD inside the graph --
-    the weights equal the eager run's."""
+    the weights equal the eager run's.  The autotuner is on in both runs; they share one tuning
+    cache (DCP_TUNE_CACHE: the eager run records its per-shape choices at exit, the graph run
+    replays them), so both run the same kernels -- round 5 had to switch the tuner off here because
+    two independently tuned runs could pick kernels that sum BN slabs in another order."""
     common = ["--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
               "--batchsize", "16", "--synthetic-train-size", "96", "--synthetic-val-size", "32", "--epochs", "2",
               "--workers", "0", "--log-interval", "100", "--num-classes", "10", "--optimizer", "SGD",
-              "--lr", "0.05", "--force-ddp", "--syncbn",
-              # a fixed kernel choice in both runs: the autotuner picks by timing, and tiles that sum a
-              # BN slab's rows in another order are enough for two 12-step runs to drift apart
-              # (round 5: one of three runs differed by 50 % in conv1 with the autotuner on)
-              "--no-autotune"]
+              "--lr", "0.05", "--force-ddp", "--syncbn", "--autotune"]
+    cache = str(tmp_path / "tune_cache.txt")
     outs = {}
-    for tag, flag in (("eager", []), ("graph", ["--graph"])):
+    for tag, flag in (("eager", ["--no-graph"]), ("graph", ["--graph"])):
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(_free_port()), DCP_COMM_STREAM="1")
+                   MASTER_PORT=str(_free_port()), DCP_COMM_STREAM="1", DCP_TUNE_CACHE=cache)
         for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
             env.pop(k, None)
         cmd = [sys.executable, os.path.join(ROOT, "main.py")] + common + ["--out-dir", str(tmp_path / tag)] + flag
         r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         outs[tag] = torch.load(tmp_path / tag / "last.pth", weights_only=True)
+        assert os.path.exists(cache)  # written by the first run, replayed by the second
     for name, me in outs["eager"]["models"].items():
         mg = outs["graph"]["models"][name]
         for k, v in me.items():
@@ -464,3 +469,24 @@ def test_syncbn_peer_exchange_matches_gloo():
     for r in res:
         assert r["errs"] == [], r["errs"]
         assert r["epoch"] == 2 * 20 + 3 * 5  # every exchange (eager and replayed) advanced the epoch
+
+
+def test_syncbn_peer_timeout_fails_loudly(tmp_path):
+    """a rank late past the peer exchange's deadline must end the run with a
+    message, never continue on a stale mailbox slot.  Two main.py ranks (gloo, one GPU) train with
+    SyncBN over the peer transport; rank 1's host sleeps 6 s before its 40th exchange while the
+    deadline is 1 s: rank 0's exchange kernel times out (err set, NaN written), the training loop's
+    check raises, and the job exits non-zero naming the peer exchange."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DCP_PEER_TIMEOUT_S="1", DCP_PEER_DELAY="1:6:40")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "main.py"),
+           "--workload", "baseline", "--model", "resnet18", "--data", "synthetic", "--dataset", "CIFAR10",
+           "--batchsize", "8", "--synthetic-train-size", "96", "--synthetic-val-size", "16", "--epochs", "1",
+           "--workers", "0", "--log-interval", "2", "--num-classes", "10", "--optimizer", "SGD", "--lr", "0.05",
+           "--syncbn", "--syncbn-transport", "peer", "--dist-backend", "gloo", "--no-graph", "--no-autotune",
+           "--out-dir", str(tmp_path / "out")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "SyncBN peer exchange" in r.stderr and "did not publish" in r.stderr, r.stderr[-3000:]

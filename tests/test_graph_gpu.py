@@ -130,7 +130,7 @@ def test_training_loop_graph_matches_eager(tmp_path, workload, extra):
               "--batchsize", "16", "--synthetic-train-size", "120", "--synthetic-val-size", "32", "--epochs", "2",
               "--workers", "0", "--log-interval", "100", "--num-classes", "10"] + extra
     outs = {}
-    for tag, flag in (("eager", []), ("graph", ["--graph"])):
+    for tag, flag in (("eager", ["--no-graph"]), ("graph", ["--graph"])):
         torch.manual_seed(0)
         entry.main(common + ["--out-dir", str(tmp_path / tag)] + flag)
         outs[tag] = torch.load(tmp_path / tag / "last.pth", weights_only=True)

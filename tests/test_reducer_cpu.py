@@ -169,3 +169,64 @@ def test_buckets_launch_in_index_order():
     assert launched == list(range(nb))
     r._finalize()
     assert launched == list(range(nb))
+
+
+class _Partial(torch.nn.Module):
+    """``a`` used by every rank, ``b`` only by rank 0, ``c`` by no rank."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(8, 8)
+        self.b = torch.nn.Linear(8, 8)
+        self.c = torch.nn.Linear(8, 8)
+
+    def forward(self, x, rank):
+        y = self.a(x)
+        return self.b(y) if rank == 0 else y
+
+
+def _unused_worker(rank, world, port, out_dir, comm):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import warnings
+
+    from ddp_classification_pytorch_amd.optim import FusedSGD
+    from ddp_classification_pytorch_amd.parallel.reducer import GradSyncDDP
+
+    torch.manual_seed(0)
+    m = _Partial()
+    net = GradSyncDDP(m, bucket_cap_mb=1, first_bucket_mb=0.001,
+                      comm_dtype=torch.bfloat16 if comm == "bf16" else torch.float32)
+    opt = net.attach_optimizer(FusedSGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=0.1))
+    c0 = m.c.weight.detach().clone()
+    grads = []
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for s in range(3):
+            x = torch.randn(4, 8, generator=torch.Generator().manual_seed(10 * s + rank))
+            loss = net(x, rank).square().mean()
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            grads.append({n: (None if p.grad is None else p.grad.clone()) for n, p in m.named_parameters()})
+    torch.save({"params": {n: p.detach().clone() for n, p in m.named_parameters()}, "c0": c0,
+                "c_grad_none": all(g["c.weight"] is None and g["c.bias"] is None for g in grads),
+                "b_grad_set": all(g["b.weight"] is not None for g in grads)},
+               os.path.join(out_dir, f"u{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_bucket_engine_unused_parameters(comm):
+    """a parameter NO rank used keeps grad None on every rank (the optimizer
+    skips it: no weight decay or momentum, as torch DDP with find_unused_parameters), while a
+    parameter only SOME ranks used gets the all-reduced gradient on every rank; replicas stay equal."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_unused_worker, args=(2, _free_port(), d, comm), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"u{k}.pt"), weights_only=True) for k in range(2)]
+    for k in range(2):
+        assert r[k]["c_grad_none"] and r[k]["b_grad_set"]
+        assert torch.equal(r[k]["params"]["c.weight"], r[k]["c0"])  # untouched by weight decay
+    for n in r[0]["params"]:
+        assert torch.equal(r[0]["params"][n], r[1]["params"][n]), n

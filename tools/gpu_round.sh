@@ -179,6 +179,46 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc2 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc2.log 2>&1
       timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $O/pmcc3 -o run -- python3 -u tools/pmc_conv.py --only "$shp" --cfgs "$cf" > $O/pmcc3.log 2>&1
       echo pmcconv done ;;
+    pmc6=*)
+      # pmc6=SHAPES -- counter passes over the kernels the step runs for those R50 shapes (autotuned
+      # choice; tools/pmc_r6.py, tools/pmc_r6_report.py): fwd / dgrad / wgrad, tuning dispatches excluded
+      shp=${step#pmc6=}
+      prof_env
+      timeout -s KILL 60 rocprofv3 -L > $O/pmc_counters_avail.txt 2>&1 || true
+      have() { local out=""; for c in "$@"; do grep -qw "$c" $O/pmc_counters_avail.txt && out="$out $c"; done; echo $out; }
+      P1=$(have SQ_WAVES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY)
+      P2=$(have TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_HIT_sum TCC_MISS_sum)
+      P3=$(have SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_BUSY_CYCLES)
+      echo "P1=$P1 | P2=$P2 | P3=$P3"
+      # one tuning run first: every counter pass then replays the same per-shape choices (a tuning
+      # cache), so the passes count the same kernels (round-6 s1: independent tuning picked different
+      # kernels in different passes for 5 of 36 blocks)
+      export DCP_TUNE_CACHE=$PWD/$O/pmc6_tune.txt
+      rm -f $DCP_TUNE_CACHE
+      timeout -k 10 300 python3 -u tools/pmc_r6.py --only "$shp" --iters 1 > $O/pmc6_tune.log 2>&1
+      i=0
+      for P in "$P1 GRBM_GUI_ACTIVE" "$P2 GRBM_GUI_ACTIVE" "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE GRBM_GUI_ACTIVE" "$P3 GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $O/pmc6/p$i -o run -- python3 -u tools/pmc_r6.py --only "$shp" > $O/pmc6_p$i.log 2>&1
+        echo "pass $i done"
+      done
+      unset DCP_TUNE_CACHE
+      python3 tools/pmc_r6_report.py $O/pmc6 --log $O/pmc6_p1.log > $O/pmc6_report.txt 2>&1 || true
+      echo pmc6 done ;;
+    profclean)
+      # kernel statistics of the headline step AFTER autotuning: only the last 20 graph-replayed steps
+      prof_env
+      # tune in a first process (cache), profile a second that replays the choices: no tuning dispatches
+      export DCP_TUNE_CACHE=$PWD/$O/profc_tune.txt
+      rm -f $DCP_TUNE_CACHE
+      timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 3 > $O/profc_tune.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/profc -o run -- python3 -u bench.py --steps 20 --warmup 5 \
+        > $O/profc.log 2>&1
+      unset DCP_TUNE_CACHE
+      db=$O/profc/run_results.db
+      python3 tools/rocpd_summary.py "$db" --last-steps 20 --top 60 > $O/profc_summary.txt 2>&1 || true
+      python3 tools/step_timeline.py "$db" > $O/profc_step.txt 2>&1 || true
+      tail -1 $O/profc.log; head -2 $O/profc_summary.txt; tail -1 $O/profc_step.txt ;;
     graph1024)
       # headline batch: eager vs HIP-graph replay, interleaved twice
       for r in 1 2; do

@@ -38,9 +38,20 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--csv", default=None)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--last-steps", type=int, default=0,
+                    help="count only the dispatches of the last K complete steps (each ending with a --marker "
+                         "dispatch): warm-up and autotuning dispatches excluded, per step = total / K")
+    ap.add_argument("--marker", default="mt_sgd_kernel")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, start, end from kernels").fetchall()
+    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    if a.last_steps > 0:
+        marks = [i for i, r in enumerate(rows) if a.marker in r[0]]
+        if len(marks) < a.last_steps + 1:
+            print(f"need {a.last_steps + 1} marker dispatches, found {len(marks)}", file=sys.stderr)
+            return 1
+        rows = rows[marks[-a.last_steps - 1] + 1: marks[-1] + 1]
+        a.steps = a.last_steps
     if not rows:
         print("no kernel dispatches", file=sys.stderr)
         return 1
