@@ -1633,6 +1633,66 @@ Tensor arcface_bwd(const Tensor& cosv, const Tensor& labels, int64_t C, double s
   return dcos;
 }
 
+// Fused ArcFace head (arcface.hip): xn [Bp][Dp], wn [Cp][Dp] from l2norm_rows (zero padding rows).
+// -> loss [B], rank [B], lse [Bp] and the per-row (target logit, d phi / d cos) [Bp][2] for backward
+std::tuple<Tensor, Tensor, Tensor, Tensor> arcface_fused_fwd(const Tensor& xn, const Tensor& wn, const Tensor& labels,
+                                                             int64_t B, int64_t C, double s, double m, bool easy) {
+  CHECK_ACT(xn);
+  CHECK_ACT(wn);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_cuda() && labels.numel() == B, "arcface_fused labels");
+  const int Bp = xn.size(0), Dp = xn.size(1), Cp = wn.size(0);
+  TORCH_CHECK(wn.size(1) == Dp && Bp >= B && Cp >= C, "arcface_fused_fwd shapes");
+  const int S = dcp::arcface_fused_fwd_splits(Bp, Cp);
+  auto loss = at::empty({B}, f32_like(xn));
+  auto rank = at::empty({B}, xn.options().dtype(at::kInt));
+  auto lse = at::empty({Bp}, f32_like(xn));
+  auto lab = at::empty({Bp, 2}, f32_like(xn));
+  auto part = at::empty({(int64_t)S * Bp * 4}, f32_like(xn));
+  TORCH_CHECK(dcp::launch_arcface_fused_fwd(bp(xn), bp(wn), labels.data_ptr<int64_t>(), B, Bp, C, Cp, Dp, (float)s,
+                                            (float)m, easy, lab.data_ptr<float>(), part.data_ptr<float>(),
+                                            loss.data_ptr<float>(), rank.data_ptr<int>(), lse.data_ptr<float>(),
+                                            cur_stream()),
+              "arcface_fused_fwd: unsupported shape (B, C padded to 64, D padded to 128 / 256 / 512)");
+  return {loss, rank, lse, lab};
+}
+
+Tensor arcface_fused_dx(const Tensor& xn, const Tensor& wn, const Tensor& wnT, const Tensor& labels, const Tensor& lse,
+                        const Tensor& lab, const Tensor& grad_out, double scale, const Tensor& inv_x, int64_t B,
+                        int64_t C, int64_t D, double s, bool out_bf16) {
+  CHECK_ACT(xn);
+  CHECK_ACT(wn);
+  CHECK_ACT(wnT);
+  const int Bp = xn.size(0), Dp = xn.size(1), Cp = wn.size(0);
+  TORCH_CHECK(wnT.size(0) == Dp && wnT.size(1) == Cp, "arcface_fused_dx: wnT [Dp][Cp]");
+  auto g = grad_out.to(at::kFloat).contiguous();
+  const int S = dcp::arcface_fused_dx_splits(Bp, Cp);
+  auto part = at::empty({(int64_t)S * Bp * Dp}, f32_like(xn));
+  auto dx = at::empty({B, D}, xn.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  TORCH_CHECK(dcp::launch_arcface_fused_dx(bp(xn), bp(wn), bp(wnT), labels.data_ptr<int64_t>(), B, Bp, C, Cp, Dp, D,
+                                           (float)s, lab.data_ptr<float>(), lse.data_ptr<float>(), g.data_ptr<float>(),
+                                           (float)scale, inv_x.data_ptr<float>(), part.data_ptr<float>(),
+                                           dx.data_ptr(), out_bf16, cur_stream()),
+              "arcface_fused_dx: unsupported shape");
+  return dx;
+}
+
+Tensor arcface_fused_dw(const Tensor& xn, const Tensor& xnT, const Tensor& wn, const Tensor& labels, const Tensor& lse,
+                        const Tensor& lab, const Tensor& grad_out, double scale, const Tensor& inv_w, int64_t B,
+                        int64_t C, int64_t D, double s) {
+  CHECK_ACT(xn);
+  CHECK_ACT(xnT);
+  CHECK_ACT(wn);
+  const int Bp = xn.size(0), Dp = xn.size(1), Cp = wn.size(0);
+  TORCH_CHECK(xnT.size(0) == Dp && xnT.size(1) == Bp, "arcface_fused_dw: xnT [Dp][Bp]");
+  auto g = grad_out.to(at::kFloat).contiguous();
+  auto dw = at::empty({C, D}, f32_like(xn));
+  TORCH_CHECK(dcp::launch_arcface_fused_dw(bp(xn), bp(xnT), bp(wn), labels.data_ptr<int64_t>(), B, Bp, C, Cp, Dp, D,
+                                           (float)s, lab.data_ptr<float>(), lse.data_ptr<float>(), g.data_ptr<float>(),
+                                           (float)scale, inv_w.data_ptr<float>(), dw.data_ptr<float>(), cur_stream()),
+              "arcface_fused_dw: unsupported shape");
+  return dw;
+}
+
 // ---------------------------------------------------------------------------
 // optimizers (multi-tensor). table: int64 [n,6] = (p, g, s1, s2, shadow, numel); chunks int32 [k,2]
 // ---------------------------------------------------------------------------
@@ -1892,6 +1952,12 @@ TORCH_LIBRARY(dcp, m) {
   m.def("l2norm_rows(Tensor x, int ldo, float eps, int rows_out=-1) -> (Tensor, Tensor)", &l2norm_rows);
   m.def("l2norm_bwd(Tensor dy, Tensor y, Tensor inv, int D, bool out_bf16) -> Tensor", &l2norm_bwd);
   m.def("transpose2d(Tensor x) -> Tensor", &transpose2d);
+  m.def("arcface_fused_fwd(Tensor xn, Tensor wn, Tensor labels, int B, int C, float s, float m, bool easy) -> "
+        "(Tensor, Tensor, Tensor, Tensor)", &arcface_fused_fwd);
+  m.def("arcface_fused_dx(Tensor xn, Tensor wn, Tensor wnT, Tensor labels, Tensor lse, Tensor lab, Tensor grad_out, "
+        "float scale, Tensor inv_x, int B, int C, int D, float s, bool out_bf16) -> Tensor", &arcface_fused_dx);
+  m.def("arcface_fused_dw(Tensor xn, Tensor xnT, Tensor wn, Tensor labels, Tensor lse, Tensor lab, Tensor grad_out, "
+        "float scale, Tensor inv_w, int B, int C, int D, float s) -> Tensor", &arcface_fused_dw);
   m.def(
       "arcface_fwd(Tensor cosv, Tensor labels, int C, float s, float m, bool easy, bool want_logits) -> (Tensor, "
       "Tensor, Tensor, Tensor)",

@@ -2075,6 +2075,14 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // big-tile kernel (tap_gemm_big_kernel): FAST, plain / statistics epilogue, >= 128 output
   // channels.  g_tune[kTgBig]: 1 = on wherever it applies (256 x 256 for Co >= 256, else 256 x 128),
   // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
+  // weight-stationary persistent kernel (conv_ws.hip) for plain 1x1 stride-1 GEMMs with K <= 256:
+  // g_tune[kTgWs] = 1 on wherever it applies (the autotuner's candidate), 2 off, 0 = heuristic (off)
+  if (g_tune[kTgWs] == 1 && fast && (epi == 0 || epi == 1) && taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 &&
+      taps.widx[0] == 0 && ss == 1 && ds == 1 && oy == 0 && ox == 0 && Hd == Hy && Wd == Wy && Hs == Hy && Ws == Wy &&
+      T == 1 && addsrc == nullptr && aff == nullptr && bnb == nullptr && pscale == nullptr && bias == nullptr &&
+      relu == 0 && conv1x1_ws_supported(Cs, Co, p.M)) {
+    if (p.ablate == 0 && launch_conv1x1_ws(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, stream)) return;
+  }
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
   const int big = big_ok ? big_tile_pick(g_tune[kTgBig], p.M, Co, taps.n, ds) : 0;
@@ -2152,7 +2160,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 // order (fp32 rounding).  Off by default (the default path is bit-reproducible run to run).
 // ---------------------------------------------------------------------------
 struct TgCfg {
-  int bn, ns, bk, big, cvar, sk;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar, tg_big_sk overrides (0 = the heuristic's)
+  int bn, ns, bk, big, cvar, sk, ws;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar, tg_big_sk, tg_ws overrides (0 = the heuristic's)
 };
 static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 0},   // heuristic
@@ -2169,6 +2177,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 1, 1},  // 256 x 256 big tile, lockstep schedule (the ping-pong one is the tile's default)
     {0, 0, 0, 1, 0, 1},  // 256 x 256 big tile, stream-K
     {0, 0, 0, 3, 0, 1},  // 256 x 128 big tile, stream-K
+    {0, 0, 0, 2, 0, 0, 1},  // weight-stationary persistent 1x1 kernel (conv_ws.hip; plain 1x1 stride-1, K <= 256)
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };
@@ -2176,17 +2185,17 @@ static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
 
 struct TuneOverride {
-  static constexpr int kSlots[6] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar, kTgBigSK};
-  int saved[6];
+  static constexpr int kSlots[7] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar, kTgBigSK, kTgWs};
+  int saved[7];
   explicit TuneOverride(const TgCfg& c) {
-    const int v[6] = {c.bn, c.ns, c.bk, c.big, c.cvar, c.sk};
-    for (int i = 0; i < 6; ++i) {
+    const int v[7] = {c.bn, c.ns, c.bk, c.big, c.cvar, c.sk, c.ws};
+    for (int i = 0; i < 7; ++i) {
       saved[i] = g_tune[kSlots[i]];
       g_tune[kSlots[i]] = v[i];
     }
   }
   ~TuneOverride() {
-    for (int i = 0; i < 6; ++i) g_tune[kSlots[i]] = saved[i];
+    for (int i = 0; i < 7; ++i) g_tune[kSlots[i]] = saved[i];
   }
 };
 
@@ -2239,7 +2248,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
   // (an add source aliasing the output would accumulate over the timing runs: never tuned)
-  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] || g_tune[kTgBigSK] ||
+  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] || g_tune[kTgBigSK] || g_tune[kTgWs] ||
       (long)N * Hy * Wy == 0 || (addsrc != nullptr && addsrc == dst)) {
     run();
     return;
@@ -2275,6 +2284,11 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
       if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;  // (the ping-pong candidate too)
       if (cfg.bn == 256 && !(Co > 128 && bnb == nullptr && bias == nullptr && relu == 0)) continue;
       if (cfg.bn == 64 && Co <= 64 && cfg.ns == 0) continue;  // the heuristic's tile already
+      if (cfg.ws == 1 && !(taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && ds == 1 && Hd == Hy &&
+                           Wd == Wy && Hs == Hy && Ws == Wy && T == 1 && addsrc == nullptr && aff == nullptr &&
+                           bnb == nullptr && bias == nullptr && relu == 0 &&
+                           conv1x1_ws_supported(Cs, Co, (long)N * Hy * Wy)))
+        continue;  // (the candidate would time the heuristic again)
       TuneOverride ov(cfg);
       run();  // warm
       float t = 1e30f;

@@ -279,6 +279,25 @@ void launch_adaptive_avg(const bf16* src, bf16* dst, int N, int H, int W, int C,
 void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t* labels, int B, int D, int C,
                                int* counts, hipStream_t s);
 // workspace bytes of launch_nested_eval (label score chains + per-class-block rank counts)
+// weight-stationary persistent 1x1 stride-1 forward GEMM (conv_ws.hip): src [M][K], wt [Co][ldw] -> dst [M][Co]
+// (+ per-128-row slab BN statistics); K in {64, 128, 256}, Co % 128 == 0; false = unsupported
+bool conv1x1_ws_supported(int K, int Co, long M);
+bool launch_conv1x1_ws(const bf16* src, const bf16* wt, int ldw, bf16* dst, float* stats, const bf16* zero, int M,
+                       int K, int Co, hipStream_t st);
+// Fused ArcFace head (arcface.hip): no [B, C] tensor.  xn [Bp][Dp] / wn [Cp][Dp] normalised bf16
+// (zero padding rows), Bp % 64 == Cp % 64 == 0, Dp in {128, 256, 512}; false = unsupported shape.
+int arcface_fused_fwd_splits(int Bp, int Cp);
+int arcface_fused_dx_splits(int Bp, int Cp);
+bool launch_arcface_fused_fwd(const bf16* xn, const bf16* wn, const int64_t* labels, int B, int Bp, int C, int Cp,
+                              int Dp, float s, float m, int easy, float* lab, float* part, float* loss, int* rank,
+                              float* lse, hipStream_t st);
+bool launch_arcface_fused_dx(const bf16* xn, const bf16* wn, const bf16* wnT, const int64_t* labels, int B, int Bp,
+                             int C, int Cp, int Dp, int D, float s, const float* lab, const float* lse,
+                             const float* gout, float scale, const float* inv_x, float* part, void* dx, bool dx_bf16,
+                             hipStream_t st);
+bool launch_arcface_fused_dw(const bf16* xn, const bf16* xnT, const bf16* wn, const int64_t* labels, int B, int Bp,
+                             int C, int Cp, int Dp, int D, float s, const float* lab, const float* lse,
+                             const float* gout, float scale, const float* inv_w, float* dw, hipStream_t st);
 // SyncBN peer-memory exchange (peer.hip): gather (mode 0, dst [world][n]) or rank-ordered sum
 // (mode 1, dst [n]) of n floats through the IPC-mapped mailboxes `boxes` ([world] base addresses);
 // a rank missing for timeout_ms sets *err and poisons dst with NaN (this and every later exchange)

@@ -40,7 +40,8 @@ enum TuneSlot : int {
   kRowReduce = 29,     // narrow split reduction in one launch: 2 off, > 2 depth limit
   kC3Epilogue = 30,    // direct 64->64 3x3 epilogue: 2 = LDS-staged (default: from the accumulators)
   kC3WindowKB = 31,    // direct 64->64 3x3 window buffer size (KB)
-  kTuneSlots = 32
+  kTgWs = 32,          // 1x1 stride-1 short-K forward: 1 = weight-stationary persistent kernel (conv_ws.hip), 2 = off
+  kTuneSlots = 40
 };
 
 struct TuneSlotName {
@@ -61,6 +62,7 @@ constexpr TuneSlotName kTuneSlotNames[] = {
     {"gconv_spw", kGconvSpw},
     {"autotune", kAutotune},         {"wg_split_cap", kWgSplitCap},  {"bn_bwd_cap", kBnBwdCap},
     {"row_reduce", kRowReduce},      {"c3_epilogue", kC3Epilogue},   {"c3_window_kb", kC3WindowKB},
+    {"tg_ws", kTgWs},
 };
 
 extern int g_tune[kTuneSlots];

@@ -1487,8 +1487,58 @@ class _ArcFace(Function):
         return dx, dw, None, None, None, None, None
 
 
+class _ArcFaceFused(Function):
+    """The ArcFace head without a [B, C] tensor (csrc/arcface.hip): the cosine tiles
+    live in MFMA registers only -- forward streams the normalised class weights through an online
+    log-sum-exp (loss, label rank, lse), backward recomputes each tile and feeds dcos straight into
+    the dX / dW MFMAs (the normalisation backward fused into their epilogues).  The per-step
+    memory is O((B + C) * D), so 100k+ classes fit where the unfused path needs 4 B*C bytes."""
+
+    @staticmethod
+    def forward(ctx, x, weight, labels, s, m, easy):
+        k = K(x)
+        B, D = x.shape
+        C = weight.shape[0]
+        Dp = 128 if D <= 128 else (256 if D <= 256 else 512)
+        Bp, Cp = round_up(B, 64), round_up(C, 64)
+        xn, inv_x = k.l2norm_rows(x.contiguous(), Dp, 1e-12, Bp)  # zero rows B..Bp
+        wn, inv_w = k.l2norm_rows(weight.detach().contiguous(), Dp, 1e-12, Cp)  # zero rows C..Cp
+        lab64 = labels.to(torch.int64).contiguous()
+        loss_rows, rank, lse, lab = k.arcface_fused_fwd(xn, wn, lab64, B, C, s, m, easy)
+        ctx.save_for_backward(xn, inv_x, wn, inv_w, lab64, lse, lab)
+        ctx.cfg = (B, C, D, s, x.dtype == torch.bfloat16)
+        ctx.mark_non_differentiable(rank)
+        ctx.set_materialize_grads(False)
+        return loss_rows.mean(), rank
+
+    @staticmethod
+    def backward(ctx, g, _grank):
+        if g is None:
+            return (None,) * 6
+        xn, inv_x, wn, inv_w, lab64, lse, lab = ctx.saved_tensors
+        B, C, D, s, x_bf16 = ctx.cfg
+        k = K(xn)
+        g = g.reshape(1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = k.arcface_fused_dx(xn, wn, k.transpose2d(wn), lab64, lse, lab, g, 1.0 / B, inv_x, B, C, D, s, x_bf16)
+        if ctx.needs_input_grad[1]:
+            dw = k.arcface_fused_dw(xn, k.transpose2d(xn), wn, lab64, lse, lab, g, 1.0 / B, inv_w, B, C, D, s)
+        return dx, dw, None, None, None, None
+
+
+def arcface_fused_enabled() -> bool:
+    """The fused head is the GPU default; DCP_ARCFACE_FUSED=0 selects the unfused path (A/B)."""
+    return os.environ.get("DCP_ARCFACE_FUSED", "1") != "0"
+
+
 def arcface_loss(x, weight, labels, s=30.0, m=0.5, easy_margin=True, return_logits=False):
-    """Returns (mean loss, rank of label, margin logits or empty)."""
+    """Returns (mean loss, rank of label, margin logits or empty).  On the GPU without
+    ``return_logits`` (training, the reference's loss) the fused head runs: no [B, C] tensor."""
+    if (x.is_cuda and not return_logits and x.dim() == 2 and x.shape[1] <= 512 and arcface_fused_enabled()
+            and x.dtype in (torch.float32, torch.bfloat16)):
+        loss, rank = _ArcFaceFused.apply(x, weight, labels, float(s), float(m), bool(easy_margin))
+        return loss, rank, torch.empty(0, device=x.device)
     return _ArcFace.apply(x, weight, labels, float(s), float(m), bool(easy_margin), bool(return_logits))
 
 

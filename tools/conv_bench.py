@@ -129,7 +129,7 @@ def main():
 
 
 def _apply(K, cfg):
-    for i in range(32):
+    for i in range(40):
         K.set_tuning(i, 0)
     for kv in filter(None, cfg.split(";")):
         i, v = kv.split("=")
