@@ -1633,6 +1633,20 @@ Tensor arcface_bwd(const Tensor& cosv, const Tensor& labels, int64_t C, double s
   return dcos;
 }
 
+// x [R][D] -> (y [Rp][Dp] bf16 normalised rows, yT [Dp][Rp], inverse norms [Rp]) in one pass
+std::tuple<Tensor, Tensor, Tensor> arcface_l2norm_t(const Tensor& x, int64_t Rp, int64_t Dp, double eps) {
+  CHECK_DEV(x);
+  CHECK_CONTIG(x);
+  const int R = x.size(0), D = x.size(1);
+  auto y = at::empty({Rp, Dp}, x.options().dtype(at::kBFloat16));
+  auto yT = at::empty({Dp, Rp}, x.options().dtype(at::kBFloat16));
+  auto inv = at::empty({Rp}, f32_like(x));
+  TORCH_CHECK(dcp::launch_arcface_l2norm_t(x.data_ptr(), x.scalar_type() == at::kBFloat16, R, D, (int)Rp, (int)Dp,
+                                           bpm(y), bpm(yT), inv.data_ptr<float>(), (float)eps, cur_stream()),
+              "arcface_l2norm_t: Rp % 64, D <= Dp in {128, 256}");
+  return {y, yT, inv};
+}
+
 // Fused ArcFace head (arcface.hip): xn [Bp][Dp], wn [Cp][Dp] from l2norm_rows (zero padding rows).
 // -> loss [B], rank [B], lse [Bp] and the per-row (target logit, d phi / d cos) [Bp][2] for backward
 std::tuple<Tensor, Tensor, Tensor, Tensor> arcface_fused_fwd(const Tensor& xn, const Tensor& wn, const Tensor& labels,
@@ -1652,7 +1666,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> arcface_fused_fwd(const Tensor& xn, c
                                             (float)m, easy, lab.data_ptr<float>(), part.data_ptr<float>(),
                                             loss.data_ptr<float>(), rank.data_ptr<int>(), lse.data_ptr<float>(),
                                             cur_stream()),
-              "arcface_fused_fwd: unsupported shape (B, C padded to 64, D padded to 128 / 256 / 512)");
+              "arcface_fused_fwd: unsupported shape (B, C padded to 64, D padded to 128 / 256)");
   return {loss, rank, lse, lab};
 }
 
@@ -1686,9 +1700,12 @@ Tensor arcface_fused_dw(const Tensor& xn, const Tensor& xnT, const Tensor& wn, c
   TORCH_CHECK(xnT.size(0) == Dp && xnT.size(1) == Bp, "arcface_fused_dw: xnT [Dp][Bp]");
   auto g = grad_out.to(at::kFloat).contiguous();
   auto dw = at::empty({C, D}, f32_like(xn));
+  const int S = dcp::arcface_fused_dw_splits(Bp, Cp);
+  auto part = at::empty({S > 1 ? (int64_t)S * Cp * Dp : 1}, f32_like(xn));
   TORCH_CHECK(dcp::launch_arcface_fused_dw(bp(xn), bp(xnT), bp(wn), labels.data_ptr<int64_t>(), B, Bp, C, Cp, Dp, D,
                                            (float)s, lab.data_ptr<float>(), lse.data_ptr<float>(), g.data_ptr<float>(),
-                                           (float)scale, inv_w.data_ptr<float>(), dw.data_ptr<float>(), cur_stream()),
+                                           (float)scale, inv_w.data_ptr<float>(), part.data_ptr<float>(),
+                                           dw.data_ptr<float>(), cur_stream()),
               "arcface_fused_dw: unsupported shape");
   return dw;
 }
@@ -1952,6 +1969,7 @@ TORCH_LIBRARY(dcp, m) {
   m.def("l2norm_rows(Tensor x, int ldo, float eps, int rows_out=-1) -> (Tensor, Tensor)", &l2norm_rows);
   m.def("l2norm_bwd(Tensor dy, Tensor y, Tensor inv, int D, bool out_bf16) -> Tensor", &l2norm_bwd);
   m.def("transpose2d(Tensor x) -> Tensor", &transpose2d);
+  m.def("arcface_l2norm_t(Tensor x, int Rp, int Dp, float eps) -> (Tensor, Tensor, Tensor)", &arcface_l2norm_t);
   m.def("arcface_fused_fwd(Tensor xn, Tensor wn, Tensor labels, int B, int C, float s, float m, bool easy) -> "
         "(Tensor, Tensor, Tensor, Tensor)", &arcface_fused_fwd);
   m.def("arcface_fused_dx(Tensor xn, Tensor wn, Tensor wnT, Tensor labels, Tensor lse, Tensor lab, Tensor grad_out, "

@@ -2177,7 +2177,8 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 1, 1},  // 256 x 256 big tile, lockstep schedule (the ping-pong one is the tile's default)
     {0, 0, 0, 1, 0, 1},  // 256 x 256 big tile, stream-K
     {0, 0, 0, 3, 0, 1},  // 256 x 128 big tile, stream-K
-    {0, 0, 0, 2, 0, 0, 1},  // weight-stationary persistent 1x1 kernel (conv_ws.hip; plain 1x1 stride-1, K <= 256)
+    // (the weight-stationary persistent 1x1 kernel, g_tune[kTgWs] = 1, is not a candidate: 26-53 %
+    // slower on every R50 short-K shape, profiles/r6/ws_1x1_ab_b1024.txt)
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
     // profiles/r4/big4_tile_ab_b1024.txt)
 };

@@ -285,7 +285,10 @@ bool conv1x1_ws_supported(int K, int Co, long M);
 bool launch_conv1x1_ws(const bf16* src, const bf16* wt, int ldw, bf16* dst, float* stats, const bf16* zero, int M,
                        int K, int Co, hipStream_t st);
 // Fused ArcFace head (arcface.hip): no [B, C] tensor.  xn [Bp][Dp] / wn [Cp][Dp] normalised bf16
-// (zero padding rows), Bp % 64 == Cp % 64 == 0, Dp in {128, 256, 512}; false = unsupported shape.
+// (zero padding rows), Bp % 64 == Cp % 64 == 0, Dp in {128, 256}, (128 + Bp / 64) KB of LDS for
+// the dW kernel at Dp = 256; false = unsupported shape.
+bool launch_arcface_l2norm_t(const void* x, bool is_bf16, int R, int D, int Rp, int Dp, bf16* y, bf16* yT, float* inv,
+                             float eps, hipStream_t st);
 int arcface_fused_fwd_splits(int Bp, int Cp);
 int arcface_fused_dx_splits(int Bp, int Cp);
 bool launch_arcface_fused_fwd(const bf16* xn, const bf16* wn, const int64_t* labels, int B, int Bp, int C, int Cp,
@@ -295,9 +298,11 @@ bool launch_arcface_fused_dx(const bf16* xn, const bf16* wn, const bf16* wnT, co
                              int C, int Cp, int Dp, int D, float s, const float* lab, const float* lse,
                              const float* gout, float scale, const float* inv_x, float* part, void* dx, bool dx_bf16,
                              hipStream_t st);
+int arcface_fused_dw_splits(int Bp, int Cp);
 bool launch_arcface_fused_dw(const bf16* xn, const bf16* xnT, const bf16* wn, const int64_t* labels, int B, int Bp,
                              int C, int Cp, int Dp, int D, float s, const float* lab, const float* lse,
-                             const float* gout, float scale, const float* inv_w, float* dw, hipStream_t st);
+                             const float* gout, float scale, const float* inv_w, float* part, float* dw,
+                             hipStream_t st);
 // SyncBN peer-memory exchange (peer.hip): gather (mode 0, dst [world][n]) or rank-ordered sum
 // (mode 1, dst [n]) of n floats through the IPC-mapped mailboxes `boxes` ([world] base addresses);
 // a rank missing for timeout_ms sets *err and poisons dst with NaN (this and every later exchange)

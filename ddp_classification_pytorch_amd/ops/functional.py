@@ -1499,13 +1499,14 @@ class _ArcFaceFused(Function):
         k = K(x)
         B, D = x.shape
         C = weight.shape[0]
-        Dp = 128 if D <= 128 else (256 if D <= 256 else 512)
+        Dp = 128 if D <= 128 else 256
         Bp, Cp = round_up(B, 64), round_up(C, 64)
-        xn, inv_x = k.l2norm_rows(x.contiguous(), Dp, 1e-12, Bp)  # zero rows B..Bp
-        wn, inv_w = k.l2norm_rows(weight.detach().contiguous(), Dp, 1e-12, Cp)  # zero rows C..Cp
+        # normalised operands and their transposes (the backward's MFMA A operands), one pass each
+        xn, xnT, inv_x = k.arcface_l2norm_t(x.contiguous(), Bp, Dp, 1e-12)  # zero rows B..Bp
+        wn, wnT, inv_w = k.arcface_l2norm_t(weight.detach().contiguous(), Cp, Dp, 1e-12)  # zero rows C..Cp
         lab64 = labels.to(torch.int64).contiguous()
         loss_rows, rank, lse, lab = k.arcface_fused_fwd(xn, wn, lab64, B, C, s, m, easy)
-        ctx.save_for_backward(xn, inv_x, wn, inv_w, lab64, lse, lab)
+        ctx.save_for_backward(xn, xnT, inv_x, wn, wnT, inv_w, lab64, lse, lab)
         ctx.cfg = (B, C, D, s, x.dtype == torch.bfloat16)
         ctx.mark_non_differentiable(rank)
         ctx.set_materialize_grads(False)
@@ -1515,15 +1516,15 @@ class _ArcFaceFused(Function):
     def backward(ctx, g, _grank):
         if g is None:
             return (None,) * 6
-        xn, inv_x, wn, inv_w, lab64, lse, lab = ctx.saved_tensors
+        xn, xnT, inv_x, wn, wnT, inv_w, lab64, lse, lab = ctx.saved_tensors
         B, C, D, s, x_bf16 = ctx.cfg
         k = K(xn)
         g = g.reshape(1)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = k.arcface_fused_dx(xn, wn, k.transpose2d(wn), lab64, lse, lab, g, 1.0 / B, inv_x, B, C, D, s, x_bf16)
+            dx = k.arcface_fused_dx(xn, wn, wnT, lab64, lse, lab, g, 1.0 / B, inv_x, B, C, D, s, x_bf16)
         if ctx.needs_input_grad[1]:
-            dw = k.arcface_fused_dw(xn, k.transpose2d(xn), wn, lab64, lse, lab, g, 1.0 / B, inv_w, B, C, D, s)
+            dw = k.arcface_fused_dw(xn, xnT, wn, lab64, lse, lab, g, 1.0 / B, inv_w, B, C, D, s)
         return dx, dw, None, None, None, None
 
 
@@ -1532,11 +1533,20 @@ def arcface_fused_enabled() -> bool:
     return os.environ.get("DCP_ARCFACE_FUSED", "1") != "0"
 
 
+def arcface_fused_supported(B: int, D: int) -> bool:
+    """Shapes the fused kernels cover: D <= 256 (padded to 128 / 256), and the dW kernel's LDS
+    (two staged row tiles of 2 x 16 KB x Dp / 128 plus 16 B per padded row) within 160 KB."""
+    if D > 256:
+        return False
+    Dp = 128 if D <= 128 else 256
+    return 4 * 64 * Dp * 2 + round_up(B, 64) * 16 <= 160 * 1024
+
+
 def arcface_loss(x, weight, labels, s=30.0, m=0.5, easy_margin=True, return_logits=False):
     """Returns (mean loss, rank of label, margin logits or empty).  On the GPU without
     ``return_logits`` (training, the reference's loss) the fused head runs: no [B, C] tensor."""
-    if (x.is_cuda and not return_logits and x.dim() == 2 and x.shape[1] <= 512 and arcface_fused_enabled()
-            and x.dtype in (torch.float32, torch.bfloat16)):
+    if (x.is_cuda and not return_logits and x.dim() == 2 and arcface_fused_supported(x.shape[0], x.shape[1])
+            and arcface_fused_enabled() and x.dtype in (torch.float32, torch.bfloat16)):
         loss, rank = _ArcFaceFused.apply(x, weight, labels, float(s), float(m), bool(easy_margin))
         return loss, rank, torch.empty(0, device=x.device)
     return _ArcFace.apply(x, weight, labels, float(s), float(m), bool(easy_margin), bool(return_logits))

@@ -1557,3 +1557,42 @@ def test_big_tile_stream_k_matches(K, shape, mode, sk):
     assert relerr(s1[0, 1], sr[0, 1]) < 1e-4 and relerr(s1[0, 2], sr[0, 2]) < 1e-4
     dxr = _ref.conv_dgrad(dy.float().cpu(), w.float().cpu().permute(3, 1, 2, 0), H, W, s, p)
     assert relerr(d1, dxr) < 1e-2
+
+
+# weight-stationary persistent 1x1 kernel (conv_ws.hip): K in {64, 128, 256}, Co % 128 == 0; M with
+# partial 256-row tiles and partial 128-row slabs, several tiles per workgroup (the cross-tile ring
+# and the stores that drain under the next tile), both epilogues (plain / BN statistics)
+WS_SHAPES = [
+    # N, H, W, Ci, Co
+    (2, 56, 56, 64, 256),
+    (2, 28, 28, 128, 512),
+    (3, 14, 14, 256, 1024),
+    (5, 7, 7, 256, 2048),
+    (1, 9, 11, 64, 128),      # M = 99: one partial tile, the second slab empty
+    (7, 13, 17, 128, 256),    # M = 1547: ragged last tile
+    (64, 14, 14, 256, 1024),  # 49 tiles x 8 column blocks: several tiles per workgroup
+]
+
+
+@pytest.mark.parametrize("shape", WS_SHAPES)
+def test_conv1x1_weight_stationary(K, shape):
+    N, H, W, Ci, Co = shape
+    torch.manual_seed(Ci + Co + N)
+    x = rnd(N, H, W, Ci)
+    w = rnd(Co, 1, 1, Ci, scale=1.0 / math.sqrt(Ci))
+    try:
+        K.set_tuning(tslot("tg_ws"), 1)
+        y, slabs = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, True)
+        y0, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, False)
+        torch.cuda.synchronize()
+    finally:
+        K.set_tuning(tslot("tg_ws"), 0)
+    ytap, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, True)  # the tap GEMM: same k order, same bits
+    yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 0, False)
+    assert relerr(y, yr) < 1e-2
+    assert torch.equal(y, ytap) and torch.equal(y0, ytap)
+    st = K.bn_stats(y, slabs)
+    sr = _ref.bn_stats(y.float().cpu(), None)
+    assert torch.equal(st[0, 0].cpu(), sr[0, 0])
+    assert relerr(st[0, 1], sr[0, 1]) < 1e-4
+    assert relerr(st[0, 2], sr[0, 2]) < 1e-4

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--classes", default="10000,100000")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--mode", default="both", choices=["both", "fused", "unfused"])
+    ap.add_argument("--graph", action="store_true",
+                    help="time HIP-graph replays of the head step (as bench.py / main.py run it): no host launch cost")
     a = ap.parse_args()
     _ext.hip_ops()
     dev = torch.device("cuda", 0)
@@ -38,7 +41,8 @@ def main():
         W = (torch.randn(C, a.dim, device=dev) * 0.05).requires_grad_(True)
         lab = torch.randint(0, C, (a.batch,), device=dev)
         res = {}
-        for fused in ("1", "0"):
+        modes = {"both": ("1", "0"), "fused": ("1",), "unfused": ("0",)}[a.mode]
+        for fused in modes:
             os.environ["DCP_ARCFACE_FUSED"] = fused
             for _ in range(3):
                 step(x, W, lab)
@@ -48,15 +52,30 @@ def main():
             step(x, W, lab)
             torch.cuda.synchronize()
             peak = (torch.cuda.max_memory_allocated() - base) / 2**20
+            run = lambda: step(x, W, lab)  # noqa: E731
+            if a.graph:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    step(x, W, lab)
+                torch.cuda.current_stream().wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                x.grad = W.grad = None
+                with torch.cuda.graph(g):
+                    loss, _, _ = Fn.arcface_loss(x, W, lab, 30.0, 0.5, True)
+                    loss.backward()
+                run = g.replay
+                for _ in range(3):
+                    run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                step(x, W, lab)
+                run()
             e1.record()
             torch.cuda.synchronize()
             res[fused] = (e0.elapsed_time(e1) / a.iters * 1e3, peak)
         os.environ.pop("DCP_ARCFACE_FUSED", None)
-        f, u = res["1"], res["0"]
+        f, u = res.get("1", (float("nan"), 0.0)), res.get("0", (float("nan"), 0.0))
         print(f"{a.batch:6d} {C:7d} {a.dim:4d} | {f[0]:9.1f} {u[0]:10.1f} {u[0] / f[0]:7.2f} | {f[1]:8.1f} {u[1]:10.1f}",
               flush=True)
 

@@ -142,12 +142,22 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run -- python3 -u bench.py --config $c --steps 8 --warmup 2 \
         > $O/prof_$c.log 2>&1
       echo prof $c done ;;
-    profsmall)
-      # rocprofv3 kernel statistics of the batch-32 HIP-graph step, 200 replays (tuning diluted)
+    profsmall*)
+      # profsmall[=ARGS]: kernel statistics + one-step timeline of a small-batch HIP-graph step after
+      # autotuning (tuning cache replayed, last 100 replays counted): default R50 batch 32;
+      # e.g. profsmall="--config tresnet --batch 16 --force-ddp --syncbn"
+      args=${step#profsmall}; args=${args#=}; [ -z "$args" ] && args="--batch 32"
+      tg=$(echo "$args" | tr -c 'a-z0-9' '_' | sed 's/__*/_/g; s/^_//; s/_$//')
       prof_env
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_small -o run -- python3 -u bench.py --batch 32 --graph --steps 200 --warmup 5 \
-        > $O/prof_small.log 2>&1
-      echo prof small done ;;
+      export DCP_TUNE_CACHE=$PWD/$O/profsmall_${tg}_tune.txt
+      rm -f $DCP_TUNE_CACHE
+      timeout -k 10 300 python3 -u bench.py $args --graph --steps 5 --warmup 5 > $O/profsmall_${tg}_tune.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/profsmall_$tg -o run -- python3 -u bench.py $args --graph --steps 100 --warmup 5 \
+        > $O/profsmall_$tg.log 2>&1
+      unset DCP_TUNE_CACHE
+      python3 tools/rocpd_summary.py $O/profsmall_$tg/run_results.db --last-steps 100 --top 60 > $O/profsmall_${tg}_summary.txt 2>&1 || true
+      python3 tools/step_timeline.py $O/profsmall_$tg/run_results.db > $O/profsmall_${tg}_step.txt 2>&1 || true
+      tail -1 $O/profsmall_$tg.log; head -1 $O/profsmall_${tg}_summary.txt; tail -1 $O/profsmall_${tg}_step.txt ;;
     profddp)
       # rocprofv3 kernel statistics of the world-1 RCCL bucket-engine batch-32 HIP-graph step
       prof_env
