@@ -6,14 +6,21 @@ the weight-gradient plans (``kWgCfgs``, bindings.cpp) by timing.  Two runs can t
 different kernels, and round 5 saw two 12-step trainings end 50 % apart in one layer.  These tests
 separate "another summation order, amplified by training" from "a faulty variant":
 
+* per conv shape of that step, every candidate's forward output equals the heuristic's (bitwise:
+  the same k order; stream-K adds one fp32 partial) and its BN statistics and data gradient match
+  (tools/variant_check.py);
 * one ResNet-50 step (batch 16, 64 px) under EACH candidate forced for every layer: the gradients
   are within the bf16 floor of the fp64 mirror (no worse than stock PyTorch bf16 autocast on the
-  same net), and the BN running statistics agree with the heuristic's to fp32-rounding level;
+  same net), and the BN running statistics move from the heuristic's no more than they move when
+  the heuristic runs on weights perturbed by 2^-24 relative (fp32 rounding): at random init one
+  forward pass of this net turns such a perturbation into a ~14 % change of the logits
+  (profiles/r6/autotune_divergence.txt), so that -- not a fixed tolerance -- is the yardstick;
 * 12 SGD steps under the heuristic, under a different candidate, and under the heuristic from
   weights perturbed at fp32-rounding level: the candidate's divergence from the heuristic tracks
   the perturbed run's, step by step -- the same chaotic growth, not a jump.
 """
 import copy
+import os
 
 import pytest
 import torch
@@ -82,7 +89,19 @@ def setup():
         out = mirror_forward(bf, imgs, training=True)
     torch.nn.functional.cross_entropy(out.float(), labels).backward()
     g_ref, g_bf = _grads(ref), _grads(bf)
-    yield K, base, imgs, labels, g_ref, relerr(g_bf, g_ref)
+    # the fp32-rounding yardstick: the heuristic on weights perturbed by 2^-24 relative
+    _force(K, TG_SLOTS, TG[0])
+    m0 = copy.deepcopy(base)
+    _step(m0, imgs, labels)
+    mp = copy.deepcopy(base)
+    g = torch.Generator(device=dev).manual_seed(5)
+    with torch.no_grad():
+        for p in mp.parameters():
+            p.mul_(1.0 + 2.0 ** -24 * torch.randn(p.shape, device=dev, generator=g))
+    _step(mp, imgs, labels)
+    torch.cuda.synchronize()
+    yard = relerr(_bn_stats(mp), _bn_stats(m0))
+    yield K, base, imgs, labels, g_ref, relerr(g_bf, g_ref), yard
     tuning.apply(K, "", reset=True)
 
 
@@ -96,16 +115,30 @@ def _one(K, base, imgs, labels, slots, values):
 
 @pytest.mark.parametrize("kind,idx", [("tg", i) for i in range(len(TG))] + [("wg", i) for i in range(len(WG))])
 def test_candidate_first_step_within_bf16_floor(setup, kind, idx):
-    K, base, imgs, labels, g_ref, e_floor = setup
+    K, base, imgs, labels, g_ref, e_floor, yard = setup
     g0, s0 = _one(K, base, imgs, labels, TG_SLOTS, TG[0])
     slots, values = (TG_SLOTS, TG[idx]) if kind == "tg" else (WG_SLOTS, WG[idx])
     g, s = _one(K, base, imgs, labels, slots, values)
     e = relerr(g, g_ref)
     # no worse than stock PyTorch bf16 autocast on the same net and input (test_model_parity's bar)
     assert e <= 1.25 * e_floor + 1e-3, (kind, idx, e, e_floor)
-    # the BN running statistics: the same bf16 conv outputs (up to an fp32 partial-sum order for
-    # stream-K), summed in another fp32 order at most
-    assert relerr(s, s0) < 1e-4, (kind, idx, relerr(s, s0))
+    # the BN running statistics: another fp32 summation order at most, amplified by the net exactly
+    # as an fp32-rounding-level weight perturbation is
+    assert relerr(s, s0) <= 3.0 * yard + 1e-6, (kind, idx, relerr(s, s0), yard)
+
+
+def test_candidate_per_shape_exact():
+    """Every candidate on every conv shape of the step: the forward output equals the heuristic's
+    (same k order; stream-K within rounding), BN statistics match the fp32 statistics of that
+    output, the data gradient matches -- no variant-specific defect on any layer."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "variant_check.py")], cwd=root,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "variants with a mismatch: 0" in r.stdout, r.stdout[-3000:]
 
 
 def _train(K, base, imgs, labels, slots, values, steps, perturb=0.0):
@@ -134,7 +167,7 @@ def test_candidate_divergence_is_rounding_growth(setup):
     heuristic from weights perturbed by 2^-24 relative (C: pure fp32 rounding noise).  At every
     step |B - A| stays within 30x of |C - A| (the same amplification of a rounding-level change),
     and the final relative divergence is small."""
-    K, base, imgs, labels, _, _ = setup
+    K, base, imgs, labels, _, _, _ = setup
     steps = 12
     a = _train(K, base, imgs, labels, TG_SLOTS, TG[0], steps)
     b = _train(K, base, imgs, labels, TG_SLOTS + WG_SLOTS, (64, 0, 0, 0, 0, 0) + WG[1], steps)
