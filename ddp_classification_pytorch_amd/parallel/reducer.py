@@ -234,7 +234,7 @@ class BucketReducer:
             if b.pack_tab is None:
                 counts = torch.tensor([(n + CHUNK - 1) // CHUNK for n in b.numels + [len(b.params)]],
                                       dtype=torch.int64)
-                ent = torch.repeat_interleave(torch.arange(len(b.numels), dtype=torch.int64), counts)
+                ent = torch.repeat_interleave(torch.arange(len(b.numels) + 1, dtype=torch.int64), counts)
                 first = torch.repeat_interleave(torch.cumsum(counts, 0) - counts, counts)
                 ch = torch.stack([ent, torch.arange(ent.numel(), dtype=torch.int64) - first], 1)
                 b.unpack_tab = [None, Fn.table_to_device(ch.to(torch.int32), torch.int32, self.device).view(-1, 2)]

@@ -27,7 +27,9 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _ddp_syncbn_worker(rank, world, port, out_dir):
+def _ddp_syncbn_worker(rank, world, port, out_dir, shared=False):
+    if shared:
+        os.environ["DCP_SYNCBN_SHARED_GROUP"] = "1"
     _init(rank, world, port)
     from ddp_classification_pytorch_amd.models import build_model
     from ddp_classification_pytorch_amd.ops import functional as Fn
@@ -44,6 +46,9 @@ def _ddp_syncbn_worker(rank, world, port, out_dir):
     loss.backward()
     lt = loss.detach().clone()
     dist.all_reduce(lt)
+    from ddp_classification_pytorch_amd.parallel.ddp import bn_process_group
+
+    assert (bn_process_group() is dist.group.WORLD) == shared
     if rank == 0:
         torch.save({"loss": lt / world, "grads": {n: p.grad.clone() for n, p in model.named_parameters()},
                     "rm": model.bn1.running_mean.clone(), "rv": model.bn1.running_var.clone(),
@@ -53,12 +58,16 @@ def _ddp_syncbn_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_ddp_syncbn_equals_single_process_full_batch():
+@pytest.mark.parametrize("shared", [False, True])
+def test_ddp_syncbn_equals_single_process_full_batch(shared):
+    """2-rank DDP + SyncBN == one process on the full batch; ``shared``: the BN statistics on the
+    gradient communicator (--syncbn-shared-group, the fallback for stacks where two communicators
+    in flight on one GPU misbehave) gives the same result."""
     from ddp_classification_pytorch_amd.models import build_model
     from ddp_classification_pytorch_amd.ops import functional as Fn
 
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_ddp_syncbn_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_ddp_syncbn_worker, args=(2, _free_port(), d, shared), nprocs=2, join=True)
         got = torch.load(os.path.join(d, "ddp.pt"), weights_only=True)
     imgs = torch.randn(8, 3, 32, 32, generator=torch.Generator().manual_seed(1))
     labels = torch.randint(0, 10, (8,), generator=torch.Generator().manual_seed(2))
