@@ -2077,11 +2077,17 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   // 3 = 256 x 128 only, 2 = off, 0 = heuristic (big_tile_pick)
   // weight-stationary persistent kernel (conv_ws.hip) for plain 1x1 stride-1 GEMMs with K <= 256:
   // g_tune[kTgWs] = 1 on wherever it applies (the autotuner's candidate), 2 off, 0 = heuristic (off)
-  if (g_tune[kTgWs] == 1 && fast && (epi == 0 || epi == 1) && taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 &&
-      taps.widx[0] == 0 && ss == 1 && ds == 1 && oy == 0 && ox == 0 && Hd == Hy && Wd == Wy && Hs == Hy && Ws == Wy &&
-      T == 1 && addsrc == nullptr && aff == nullptr && bnb == nullptr && pscale == nullptr && bias == nullptr &&
-      relu == 0 && conv1x1_ws_supported(Cs, Co, p.M)) {
+  const bool plain1x1 = fast && (epi == 0 || epi == 1) && taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 &&
+                        taps.widx[0] == 0 && ss == 1 && ds == 1 && oy == 0 && ox == 0 && Hd == Hy && Wd == Wy &&
+                        Hs == Hy && Ws == Wy && T == 1 && addsrc == nullptr && aff == nullptr && bnb == nullptr &&
+                        pscale == nullptr && bias == nullptr && relu == 0;
+  if (g_tune[kTgWs] == 1 && plain1x1 && conv1x1_ws_supported(Cs, Co, p.M)) {
     if (p.ablate == 0 && launch_conv1x1_ws(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, stream)) return;
+  }
+  // store-decoupled loader / consumer 1x1 kernel (conv1x1_ps.hip): g_tune[kTgPs] = 1 on wherever it
+  // applies (the autotuner's candidate), 2 off, 0 = heuristic (off)
+  if (g_tune[kTgPs] == 1 && plain1x1 && conv1x1_ps_supported(Cs, Co, p.M)) {
+    if (launch_conv1x1_ps(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, p.ablate, stream)) return;
   }
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
@@ -2160,7 +2166,7 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
 // order (fp32 rounding).  Off by default (the default path is bit-reproducible run to run).
 // ---------------------------------------------------------------------------
 struct TgCfg {
-  int bn, ns, bk, big, cvar, sk, ws;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar, tg_big_sk, tg_ws overrides (0 = the heuristic's)
+  int bn, ns, bk, big, cvar, sk, ws, ps;  // tg_tile_n, tg_stages, tg_kdepth, tg_big, tg_big_cvar, tg_big_sk, tg_ws, tg_ps overrides (0 = the heuristic's)
 };
 static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 0},   // heuristic
@@ -2177,6 +2183,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 1, 1},  // 256 x 256 big tile, lockstep schedule (the ping-pong one is the tile's default)
     {0, 0, 0, 1, 0, 1},  // 256 x 256 big tile, stream-K
     {0, 0, 0, 3, 0, 1},  // 256 x 128 big tile, stream-K
+    {0, 0, 0, 2, 0, 0, 0, 1},  // store-decoupled loader / consumer 1x1 kernel (plain 1x1 stride-1, K <= 256)
     // (the weight-stationary persistent 1x1 kernel, g_tune[kTgWs] = 1, is not a candidate: 26-53 %
     // slower on every R50 short-K shape, profiles/r6/ws_1x1_ab_b1024.txt)
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
@@ -2186,17 +2193,17 @@ static std::mutex g_tg_mu;
 static std::unordered_map<std::string, int> g_tg_choice;
 
 struct TuneOverride {
-  static constexpr int kSlots[7] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar, kTgBigSK, kTgWs};
-  int saved[7];
+  static constexpr int kSlots[8] = {kTgTileN, kTgStages, kTgKDepth, kTgBig, kTgBigCvar, kTgBigSK, kTgWs, kTgPs};
+  int saved[8];
   explicit TuneOverride(const TgCfg& c) {
-    const int v[7] = {c.bn, c.ns, c.bk, c.big, c.cvar, c.sk, c.ws};
-    for (int i = 0; i < 7; ++i) {
+    const int v[8] = {c.bn, c.ns, c.bk, c.big, c.cvar, c.sk, c.ws, c.ps};
+    for (int i = 0; i < 8; ++i) {
       saved[i] = g_tune[kSlots[i]];
       g_tune[kSlots[i]] = v[i];
     }
   }
   ~TuneOverride() {
-    for (int i = 0; i < 7; ++i) g_tune[kSlots[i]] = saved[i];
+    for (int i = 0; i < 8; ++i) g_tune[kSlots[i]] = saved[i];
   }
 };
 
@@ -2249,7 +2256,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
   const bool fast = (Cs % 64) == 0 && taps.n <= 32;
   // only the FAST shapes have alternatives; A/B overrides set by hand win over the tuner
   // (an add source aliasing the output would accumulate over the timing runs: never tuned)
-  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] || g_tune[kTgBigSK] || g_tune[kTgWs] ||
+  if (g_tune[kAutotune] != 1 || !fast || pscale != nullptr || g_tune[kTgTileN] || g_tune[kTgStages] || g_tune[kTgKDepth] || g_tune[kTgBig] || g_tune[kTgBigSK] || g_tune[kTgWs] || g_tune[kTgPs] ||
       (long)N * Hy * Wy == 0 || (addsrc != nullptr && addsrc == dst)) {
     run();
     return;
@@ -2290,6 +2297,11 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                            bnb == nullptr && bias == nullptr && relu == 0 &&
                            conv1x1_ws_supported(Cs, Co, (long)N * Hy * Wy)))
         continue;  // (the candidate would time the heuristic again)
+      if (cfg.ps == 1 && !(taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && ds == 1 && Hd == Hy &&
+                           Wd == Wy && Hs == Hy && Ws == Wy && T == 1 && addsrc == nullptr && aff == nullptr &&
+                           bnb == nullptr && bias == nullptr && relu == 0 &&
+                           conv1x1_ps_supported(Cs, Co, (long)N * Hy * Wy)))
+        continue;
       TuneOverride ov(cfg);
       run();  // warm
       float t = 1e30f;

@@ -41,6 +41,7 @@ enum TuneSlot : int {
   kC3Epilogue = 30,    // direct 64->64 3x3 epilogue: 2 = LDS-staged (default: from the accumulators)
   kC3WindowKB = 31,    // direct 64->64 3x3 window buffer size (KB)
   kTgWs = 32,          // 1x1 stride-1 short-K forward: 1 = weight-stationary persistent kernel (conv_ws.hip), 2 = off
+  kTgPs = 33,          // 1x1 stride-1 short-K forward: 1 = store-decoupled loader/consumer kernel (conv1x1_ps.hip), 2 = off
   kTuneSlots = 40
 };
 
@@ -62,7 +63,7 @@ constexpr TuneSlotName kTuneSlotNames[] = {
     {"gconv_spw", kGconvSpw},
     {"autotune", kAutotune},         {"wg_split_cap", kWgSplitCap},  {"bn_bwd_cap", kBnBwdCap},
     {"row_reduce", kRowReduce},      {"c3_epilogue", kC3Epilogue},   {"c3_window_kb", kC3WindowKB},
-    {"tg_ws", kTgWs},
+    {"tg_ws", kTgWs},                {"tg_ps", kTgPs},
 };
 
 extern int g_tune[kTuneSlots];

@@ -601,6 +601,27 @@ def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
     return (*k.bn_finalize(gathered, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
 
 
+# torch's SyncBatchNorm synchronises only when the group has more than one rank
+# (torch/nn/modules/batchnorm.py: need_sync = world_size > 1) -- the reference's SyncBN
+# (BASELINE/main.py:148) at world 1 is plain batch norm.  DCP_SYNCBN_WORLD1=1 keeps the collectives
+# at world 1 anyway (tests and probes that exercise the SyncBN transport on one GPU).
+_SYNCBN_WORLD1 = [os.environ.get("DCP_SYNCBN_WORLD1", "0") == "1"]
+
+
+def set_syncbn_world1(enabled: bool):
+    _SYNCBN_WORLD1[0] = bool(enabled)
+
+
+def _sync_group(group):
+    """(group, world) for a BN's statistics: (None, 1) when there is nothing to synchronise."""
+    if group is None:
+        return None, 1
+    world = dist.get_world_size(group)
+    if world == 1 and not _SYNCBN_WORLD1[0]:
+        return None, 1
+    return group, world
+
+
 _SYNCBN_CHECK = [os.environ.get("DCP_SYNCBN_CHECK", "0") == "1"]
 
 
@@ -801,7 +822,7 @@ _BNReluConv1x1 = _BNReluConv
 
 
 def _bn_relu_conv(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, weight, stats, group, k3):
-    world = dist.get_world_size(group) if group is not None else 1
+    group, world = _sync_group(group)
     cfg = BNConfig(training_stats, momentum, eps, 1, 0.0, group, world)
     if slabs is not None and slabs.numel() == 0:
         slabs = None
@@ -964,7 +985,7 @@ class _BNAddBNAct(Function):
 def batch_norm_add_bn_act(x, slabs, gamma, beta, run_mean, run_var, r, rslabs, rgamma, rbeta, rrun_mean, rrun_var,
                           training_stats, momentum, eps, rmomentum, reps, act="relu", slope=0.01, group=None):
     """act(BN(x) + BN_r(r)) with both BNs in training or eval mode (see :class:`_BNAddBNAct`)."""
-    world = dist.get_world_size(group) if group is not None else 1
+    group, world = _sync_group(group)
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world)
     rcfg = BNConfig(training_stats, rmomentum, reps, 0, float(slope), group, world)
     slabs = None if slabs is None or slabs.numel() == 0 else slabs
@@ -1007,7 +1028,7 @@ def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, mom
     away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention).  ``fuse_bwd``:
     offer this plain BN + ReLU's backward reduction to its consumer even under the masked-only
     default (the consumer is a grouped conv, whose dgrad fusion measured a win: ResNeXt)."""
-    world = dist.get_world_size(group) if group is not None else 1
+    group, world = _sync_group(group)
     iabn = bool(iabn) and residual is None and ACT[act] in (0, 2) and gamma is not None and beta is not None
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn, rgamma if iabn else None)
     if slabs is None or (slabs.numel() == 0):
@@ -1170,7 +1191,7 @@ class _BNActPool(Function):
 def batch_norm_act_maxpool(x, slabs, gamma, beta, run_mean, run_var, momentum, eps, act="relu", k=3, s=2, p=1,
                            group=None):
     """Training-mode BN(+act) followed by a max pool, fused (returns the pooled activations)."""
-    world = dist.get_world_size(group) if group is not None else 1
+    group, world = _sync_group(group)
     cfg = BNConfig(True, momentum, eps, ACT[act], 0.0, group, world)
     if slabs is None or slabs.numel() == 0:
         slabs = None
@@ -1708,7 +1729,7 @@ def stem_bn_pool(x16, weight, buf, gamma, beta, run_mean, run_var, momentum, eps
     """s2d stem conv + training-mode BN + act + 3x3/2 max pool as one autograd op (see
     _StemBNPool); ``weight`` is the 7x7 master, ``buf`` the persistent [64,4,4,16] fp32 buffer
     of its s2d form (as stem_conv_s2d)."""
-    world = dist.get_world_size(group) if group is not None else 1
+    group, world = _sync_group(group)
     cfg = BNConfig(True, momentum, eps, ACT[act], 0.0, group, world)
     _s2d_weight_refresh(weight, buf)
     wb, _ = prepared_weight(buf, 0, False)

@@ -56,7 +56,9 @@ def test_bench_force_ddp_rccl_world1(graph):
     """bench.py --force-ddp: a world-1 RCCL group through the bucket engine, eager and HIP-graph
     replay, with the SyncBN phase, the bucket telemetry (eager) and the collective probe in the
     JSON line."""
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    # DCP_SYNCBN_WORLD1: keep the SyncBN collectives at world 1 (torch -- and so the default -- skips them)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               DCP_SYNCBN_WORLD1="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--force-ddp", "--steps", "3", "--warmup", "2",
@@ -85,7 +87,7 @@ def test_bench_rejects_world_mismatch():
 
 def _rccl_worker(rank, world, port, out_dir, engine="torch"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), DCP_SYNCBN_WORLD1="1")
     sys.path.insert(0, ROOT)
     from ddp_classification_pytorch_amd.models import build_model
     from ddp_classification_pytorch_amd.ops import functional as Fn
@@ -228,7 +230,7 @@ def _rccl_graph_worker(rank, world, port, out_dir, grad_comm, optim="sgd", comm_
     all-reduce and the per-bucket SGD / Adam on that stream, the autograd gradients held to the
     join."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), DCP_COMM_STREAM=comm_stream)
+                      LOCAL_RANK=str(rank), DCP_COMM_STREAM=comm_stream, DCP_SYNCBN_WORLD1="1")
     sys.path.insert(0, ROOT)
     import datetime
 
@@ -315,7 +317,7 @@ def test_main_graph_force_ddp_side_stream_matches_eager(tmp_path):
     outs = {}
     for tag, flag in (("eager", ["--no-graph"]), ("graph", ["--graph"])):
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(_free_port()), DCP_COMM_STREAM="1", DCP_TUNE_CACHE=cache)
+                   MASTER_PORT=str(_free_port()), DCP_COMM_STREAM="1", DCP_TUNE_CACHE=cache, DCP_SYNCBN_WORLD1="1")
         for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
             env.pop(k, None)
         cmd = [sys.executable, os.path.join(ROOT, "main.py")] + common + ["--out-dir", str(tmp_path / tag)] + flag
