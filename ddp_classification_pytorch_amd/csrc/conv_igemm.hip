@@ -2085,9 +2085,11 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
     if (p.ablate == 0 && launch_conv1x1_ws(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, stream)) return;
   }
   // store-decoupled loader / consumer 1x1 kernel (conv1x1_ps.hip): g_tune[kTgPs] = 1 on wherever it
-  // applies (the autotuner's candidate), 2 off, 0 = heuristic (off)
-  if (g_tune[kTgPs] == 1 && plain1x1 && conv1x1_ps_supported(Cs, Co, p.M)) {
-    if (launch_conv1x1_ps(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, p.ablate, stream)) return;
+  // applies with 4 consumer waves, 3 with 8 (autotuner candidates), 2 off, 0 = heuristic (off)
+  if ((g_tune[kTgPs] == 1 || g_tune[kTgPs] == 3) && plain1x1 && conv1x1_ps_supported(Cs, Co, p.M)) {
+    if (launch_conv1x1_ps(src, wt, T * Cs, dst, stats, zero, p.M, Cs, Co, p.ablate, g_tune[kTgPs] == 3 ? 8 : 4,
+                          stream))
+      return;
   }
   const bool big_ok = fast && taps.n > 0 && (epi == 0 || epi == 1) && bnb == nullptr && pscale == nullptr &&
                       Co >= 128;
@@ -2184,6 +2186,7 @@ static const TgCfg kTgCfgs[] = {
     {0, 0, 0, 1, 0, 1},  // 256 x 256 big tile, stream-K
     {0, 0, 0, 3, 0, 1},  // 256 x 128 big tile, stream-K
     {0, 0, 0, 2, 0, 0, 0, 1},  // store-decoupled loader / consumer 1x1 kernel (plain 1x1 stride-1, K <= 256)
+    {0, 0, 0, 2, 0, 0, 0, 3},  // the same with 8 consumer waves
     // (the weight-stationary persistent 1x1 kernel, g_tune[kTgWs] = 1, is not a candidate: 26-53 %
     // slower on every R50 short-K shape, profiles/r6/ws_1x1_ab_b1024.txt)
     // (the 4-wave 256 x 256 tile, g_tune[kTgBig] = 4, is not a candidate: slower on every R50 shape,
@@ -2297,7 +2300,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
                            bnb == nullptr && bias == nullptr && relu == 0 &&
                            conv1x1_ws_supported(Cs, Co, (long)N * Hy * Wy)))
         continue;  // (the candidate would time the heuristic again)
-      if (cfg.ps == 1 && !(taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && ds == 1 && Hd == Hy &&
+      if (cfg.ps != 0 && !(taps.n == 1 && taps.dy[0] == 0 && taps.dx[0] == 0 && ss == 1 && ds == 1 && Hd == Hy &&
                            Wd == Wy && Hs == Hy && Ws == Wy && T == 1 && addsrc == nullptr && aff == nullptr &&
                            bnb == nullptr && bias == nullptr && relu == 0 &&
                            conv1x1_ps_supported(Cs, Co, (long)N * Hy * Wy)))

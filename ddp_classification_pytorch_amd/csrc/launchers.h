@@ -286,10 +286,10 @@ bool launch_conv1x1_ws(const bf16* src, const bf16* wt, int ldw, bf16* dst, floa
                        int K, int Co, hipStream_t st);
 // store-decoupled persistent 1x1 stride-1 forward GEMM (conv1x1_ps.hip): loader waves fill an LDS-DMA
 // ring, consumer waves store straight from the accumulators; same contract as launch_conv1x1_ws
-// (ablate: 4 = no stores, 2 = no MFMA; timing experiments only)
+// (ablate: conv1x1_ps.hip PsParams; timing experiments only); cw: consumer waves, 4 or 8
 bool conv1x1_ps_supported(int K, int Co, long M);
 bool launch_conv1x1_ps(const bf16* src, const bf16* wt, int ldw, bf16* dst, float* stats, const bf16* zero, int M,
-                       int K, int Co, int ablate, hipStream_t st);
+                       int K, int Co, int ablate, int cw, hipStream_t st);
 // Fused ArcFace head (arcface.hip): no [B, C] tensor.  xn [Bp][Dp] / wn [Cp][Dp] normalised bf16
 // (zero padding rows), Bp % 64 == Cp % 64 == 0, Dp in {128, 256}, (128 + Bp / 64) KB of LDS for
 // the dW kernel at Dp = 256; false = unsupported shape.

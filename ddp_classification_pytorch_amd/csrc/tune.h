@@ -41,7 +41,7 @@ enum TuneSlot : int {
   kC3Epilogue = 30,    // direct 64->64 3x3 epilogue: 2 = LDS-staged (default: from the accumulators)
   kC3WindowKB = 31,    // direct 64->64 3x3 window buffer size (KB)
   kTgWs = 32,          // 1x1 stride-1 short-K forward: 1 = weight-stationary persistent kernel (conv_ws.hip), 2 = off
-  kTgPs = 33,          // 1x1 stride-1 short-K forward: 1 = store-decoupled loader/consumer kernel (conv1x1_ps.hip), 2 = off
+  kTgPs = 33,          // 1x1 stride-1 short-K forward: store-decoupled loader/consumer kernel (conv1x1_ps.hip), 1 = 4 / 3 = 8 consumer waves, 2 = off
   kTuneSlots = 40
 };
 

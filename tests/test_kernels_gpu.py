@@ -1575,20 +1575,21 @@ WS_SHAPES = [
 
 
 # ... and the store-decoupled loader / consumer kernel (conv1x1_ps.hip, tg_ps) on the same shapes
-@pytest.mark.parametrize("kernel", ["tg_ws", "tg_ps"])
+@pytest.mark.parametrize("kernel", ["tg_ws", "tg_ps", "tg_ps=3"])
 @pytest.mark.parametrize("shape", WS_SHAPES)
 def test_conv1x1_weight_stationary(K, shape, kernel):
     N, H, W, Ci, Co = shape
     torch.manual_seed(Ci + Co + N)
     x = rnd(N, H, W, Ci)
     w = rnd(Co, 1, 1, Ci, scale=1.0 / math.sqrt(Ci))
+    name, _, val = kernel.partition("=")
     try:
-        K.set_tuning(tslot(kernel), 1)
+        K.set_tuning(tslot(name), int(val or 1))
         y, slabs = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, True)
         y0, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, False)
         torch.cuda.synchronize()
     finally:
-        K.set_tuning(tslot(kernel), 0)
+        K.set_tuning(tslot(name), 0)
     ytap, _ = K.conv_fwd(x.to(DEV), w.to(DEV), 1, 0, True)  # the tap GEMM: same k order, same bits
     yr, _ = _ref.conv_fwd(x.float(), w.float(), 1, 0, False)
     assert relerr(y, yr) < 1e-2
