@@ -27,9 +27,11 @@ namespace {
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bf16")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be fp32")
 #define CHECK_ACT(t) \
-  CHECK_DEV(t);      \
-  CHECK_CONTIG(t);   \
-  CHECK_BF16(t)
+  do {               \
+    CHECK_DEV(t);    \
+    CHECK_CONTIG(t); \
+    CHECK_BF16(t);   \
+  } while (0)
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 
@@ -779,6 +781,32 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias
   return y;
 }
 
+// One-launch backward of y = act(x W^T + b) for N <= 64 rows (linear_small.hip): dy / y [N][>= out]
+// bf16 (the GEMM's padded output width), x [N][K], wt = W^T [K][ldw] bf16 -> (dx [N][K] bf16 or empty,
+// dw [out][K] fp32 or empty, db [out] fp32 or empty)
+std::tuple<Tensor, Tensor, Tensor> linear_bwd_small(const Tensor& dy, const optional<Tensor>& y, const Tensor& x,
+                                                    const Tensor& wt, int64_t act, int64_t out, bool need_dx,
+                                                    bool need_dw, bool need_db) {
+  CHECK_ACT(dy);
+  CHECK_ACT(x);
+  CHECK_ACT(wt);
+  const int N = dy.size(0), K = x.size(1);
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && x.size(0) == N && wt.dim() == 2 && wt.size(0) == K &&
+                  wt.size(1) >= out && dy.size(1) >= out && out >= 1,
+              "linear_bwd_small shapes");
+  TORCH_CHECK(act >= 0 && act <= 2 && (act == 0 || (y.has_value() && y->sizes() == dy.sizes())),
+              "linear_bwd_small: act 0 / 1 / 2 with y like dy");
+  if (y.has_value()) CHECK_ACT(*y);
+  TORCH_CHECK(dcp::linear_bwd_small_supported(N, K, (int)out), "linear_bwd_small: at most 64 rows");
+  auto dx = need_dx ? at::empty({N, K}, bf16_like(x)) : at::empty({0}, bf16_like(x));
+  auto dw = need_dw ? at::empty({out, K}, f32_like(x)) : at::empty({0}, f32_like(x));
+  auto db = need_db ? at::empty({out}, f32_like(x)) : at::empty({0}, f32_like(x));
+  dcp::launch_linear_bwd_small(bp(dy), y.has_value() ? bp(*y) : nullptr, bp(x), bp(wt), need_dx ? bpm(dx) : nullptr,
+                               need_dw ? dw.data_ptr<float>() : nullptr, need_db ? db.data_ptr<float>() : nullptr, N,
+                               K, (int)out, (int)dy.size(1), (int)wt.size(1), (int)act, cur_stream());
+  return {dx, dw, db};
+}
+
 // dy [B,N] bf16, x [B,K] bf16 -> dw fp32 [N,K]
 Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
   CHECK_ACT(dy);
@@ -963,12 +991,14 @@ Tensor bn_stats(const Tensor& x, const optional<Tensor>& slabs) {
 
 // local (single-rank) BN: statistics + finalize without the [1,3,C] round trip -> (mean, invstd,
 // scale, shift); running stats updated in place.  Same numbers as bn_finalize(bn_stats(x)).
+// iabn_eps >= 0: InplaceABN's effective weight |gamma| + iabn_eps, its reciprocal written to rgamma_out
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, const optional<Tensor>& slabs,
                                                              const optional<Tensor>& gamma,
                                                              const optional<Tensor>& beta,
                                                              const optional<Tensor>& run_mean,
                                                              const optional<Tensor>& run_var, double momentum,
-                                                             double eps) {
+                                                             double eps, double iabn_eps,
+                                                             const optional<Tensor>& rgamma_out) {
   CHECK_ACT(x);
   const int C = x.size(-1);
   const int M = x.numel() / C;
@@ -980,7 +1010,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
     const Tensor pr = chunk_partials(*slabs, C);
     dcp::launch_bn_merge_finalize(pr.data_ptr<float>(), pr.size(0), C, (float)eps, fp(gamma), fp(beta), cp,
                                   cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean), fpm(run_var), (float)momentum,
-                                  cur_stream());
+                                  cur_stream(), (float)iabn_eps, fpm(rgamma_out));
     return {coef[0], coef[1], coef[2], coef[3]};
   }
   if (from_slabs)
@@ -989,7 +1019,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
   auto part = at::empty({dcp::bn_stats_partials(M, C, from_slabs), 3, C}, f32_like(x));
   dcp::launch_bn_stats_finalize(bp(x), from_slabs ? slabs->data_ptr<float>() : nullptr, M, C, part.data_ptr<float>(),
                                 (float)eps, fp(gamma), fp(beta), cp, cp + C, cp + 2 * C, cp + 3 * C, fpm(run_mean),
-                                fpm(run_var), (float)momentum, cur_stream());
+                                fpm(run_var), (float)momentum, cur_stream(), (float)iabn_eps, fpm(rgamma_out));
   return {coef[0], coef[1], coef[2], coef[3]};
 }
 
@@ -1035,7 +1065,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(const Tensor& st, const o
                                                        const optional<Tensor>& beta,
                                                        const optional<Tensor>& run_mean,
                                                        const optional<Tensor>& run_var, double momentum,
-                                                       double eps) {
+                                                       double eps, double iabn_eps,
+                                                       const optional<Tensor>& rgamma_out) {
   CHECK_DEV(st);
   CHECK_F32(st);
   CHECK_CONTIG(st);
@@ -1045,7 +1076,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(const Tensor& st, const o
   auto scale = at::empty({C}, st.options()), shift = at::empty({C}, st.options());
   dcp::launch_bn_finalize(st.data_ptr<float>(), W, C, (float)eps, fp(gamma), fp(beta), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), fpm(run_mean),
-                          fpm(run_var), (float)momentum, cur_stream());
+                          fpm(run_var), (float)momentum, cur_stream(), (float)iabn_eps, fpm(rgamma_out));
   return {mean, invstd, scale, shift};
 }
 
@@ -1139,18 +1170,21 @@ Tensor bn_bwd_reduce(const Tensor& dy, const Tensor& x, const optional<Tensor>& 
 std::tuple<Tensor, Tensor> bn_bwd_elemt(const Tensor& dy, const Tensor& x, const optional<Tensor>& res,
                                         const Tensor& scale, const Tensor& shift, const Tensor& mean,
                                         const Tensor& invstd, const optional<Tensor>& sums, double count, int64_t act,
-                                        double slope, bool want_dres, bool inv) {
+                                        double slope, bool want_dres, bool inv, const optional<Tensor>& graw) {
   CHECK_ACT(dy);
   CHECK_ACT(x);
   const int C = x.size(-1);
   TORCH_CHECK(!inv || ((act == 0 || act == 2) && !res.has_value()), "bn_bwd_elemt: inv needs an invertible act");
   TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && C <= 2048, "bn_bwd_elemt shapes");
   auto dx = at::empty_like(x);
-  Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  // graw (InplaceABN, with sums): the second output is the raw weight's gradient sign(graw) * sums[1]
+  TORCH_CHECK(!graw.has_value() || (sums.has_value() && !want_dres && graw->numel() == C), "bn_bwd_elemt graw");
+  Tensor dres = want_dres ? at::empty_like(x) : (graw.has_value() ? at::empty({C}, f32_like(x)) : at::empty({0}, x.options()));
   dcp::launch_bn_bwd_elemt(bp(dy), bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
                            shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(), fp(sums),
                            (float)(1.0 / count), x.numel(), C, act, (float)slope, bpm(dx),
-                           want_dres ? bpm(dres) : nullptr, cur_stream(), inv ? 1 : 0);
+                           want_dres ? bpm(dres) : nullptr, cur_stream(), inv ? 1 : 0, fp(graw),
+                           graw.has_value() ? dres.data_ptr<float>() : nullptr);
   return {dx, dres};
 }
 
@@ -1883,11 +1917,11 @@ TORCH_LIBRARY(dcp, m) {
   m.def("colsum(Tensor x) -> Tensor", &colsum);
   m.def(
       "bn_stats_finalize(Tensor x, Tensor? slabs, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, "
-      "float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      "float momentum, float eps, float iabn_eps=-1., Tensor(a!)? rgamma_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &bn_stats_finalize);
   m.def(
       "bn_finalize(Tensor stats, Tensor? gamma, Tensor? beta, Tensor? run_mean, Tensor? run_var, float momentum, "
-      "float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      "float eps, float iabn_eps=-1., Tensor(a!)? rgamma_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &bn_finalize);
   m.def(
       "bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor run_mean, Tensor run_var, float eps) -> (Tensor, Tensor, "
@@ -1907,8 +1941,13 @@ TORCH_LIBRARY(dcp, m) {
       "act, float slope, bool inv=False) -> Tensor",
       &bn_bwd_reduce);
   m.def(
+      "linear_bwd_small(Tensor dy, Tensor? y, Tensor x, Tensor wt, int act, int out, bool need_dx, bool need_dw, "
+      "bool need_db) -> (Tensor, Tensor, Tensor)",
+      &linear_bwd_small);
+  m.def(
       "bn_bwd_elemt(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, "
-      "Tensor? sums, float count, int act, float slope, bool want_dres, bool inv=False) -> (Tensor, Tensor)",
+      "Tensor? sums, float count, int act, float slope, bool want_dres, bool inv=False, Tensor? graw=None) "
+      "-> (Tensor, Tensor)",
       &bn_bwd_elemt);
   m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)", &maxpool_fwd);
   m.def("conv_fwd_pro(Tensor x, Tensor w, Tensor scale, Tensor shift, bool stats) -> (Tensor, Tensor)", &conv_fwd_pro);

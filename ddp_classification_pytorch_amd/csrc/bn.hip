@@ -281,16 +281,23 @@ void launch_bn_partial_chunk(const float* part, int P, int C, float* tmp, hipStr
 }
 
 // merged (n, mean, M2) of channel c -> mean, invstd, scale, shift (+ running stats)
+// iabn_eps >= 0: InplaceABN's effective weight |gamma| + iabn_eps (and its reciprocal into rgamma) -- the
+// separate iabn_gamma launch of every layer folded in (its gradient's sign: bn_bwd_elemt's dg output)
 __device__ __forceinline__ void finalize_channel(const Welford& a, int c, float eps, const float* __restrict__ gamma,
                                                  const float* __restrict__ beta, float* __restrict__ mean,
                                                  float* __restrict__ invstd, float* __restrict__ scale,
                                                  float* __restrict__ shift, float* __restrict__ run_mean,
-                                                 float* __restrict__ run_var, float momentum) {
+                                                 float* __restrict__ run_var, float momentum, float iabn_eps,
+                                                 float* __restrict__ rgamma) {
   const float var = a.n > 0.f ? a.m2 / a.n : 0.f;
   const float is = rsqrtf(var + eps);
   mean[c] = a.mean;
   invstd[c] = is;
-  const float g = gamma ? gamma[c] : 1.f;
+  float g = gamma ? gamma[c] : 1.f;
+  if (iabn_eps >= 0.f) {
+    g = fabsf(g) + iabn_eps;
+    if (rgamma) rgamma[c] = 1.f / g;
+  }
   const float b = beta ? beta[c] : 0.f;
   scale[c] = g * is;
   shift[c] = b - a.mean * g * is;
@@ -306,13 +313,14 @@ __device__ __forceinline__ void finalize_channel(const Welford& a, int c, float 
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_finalize_kernel(
     const float* __restrict__ part, int P, int C, float eps, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
-    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float iabn_eps,
+    float* __restrict__ rgamma) {
   const Welford m = merge_partials(part, P, C);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) != 0 || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
   a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
-  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, iabn_eps, rgamma);
 }
 
 // local BN from the conv slabs in one launch (R <= kDirectSlabs): merge + finalize; the same
@@ -320,13 +328,14 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_finalize_kernel(
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
     const float* __restrict__ slabs, int R, int M, int C, float eps, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
-    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum) {
+    float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float iabn_eps,
+    float* __restrict__ rgamma) {
   const Welford m = merge_slabs(slabs, R, M, C);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) != 0 || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
   a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
-  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, iabn_eps, rgamma);
 }
 
 
@@ -372,13 +381,13 @@ __global__ void bn_finalize_kernel(const float* __restrict__ st, int W, int C, f
                                    float* __restrict__ mean, float* __restrict__ invstd,
                                    float* __restrict__ scale, float* __restrict__ shift,
                                    float* __restrict__ run_mean, float* __restrict__ run_var,
-                                   float momentum) {
+                                   float momentum, float iabn_eps, float* __restrict__ rgamma) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   Welford a{0.f, 0.f, 0.f};
   for (int w = 0; w < W; ++w)
     a.merge(st[((size_t)w * 3 + 0) * C + c], st[((size_t)w * 3 + 1) * C + c], st[((size_t)w * 3 + 2) * C + c]);
-  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum);
+  finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, iabn_eps, rgamma);
 }
 
 // eval / frozen BN: scale = gamma / sqrt(var + eps), shift = beta - mean*scale
@@ -620,11 +629,22 @@ __global__ void __launch_bounds__(256) bn_bwd_elemt_kernel(const bf16* __restric
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ sums, float inv_count, int M,
                                                            int C, float slope, bf16* __restrict__ dx,
-                                                           bf16* __restrict__ dres, int inv) {
+                                                           bf16* __restrict__ dres, int inv,
+                                                           const float* __restrict__ graw, float* __restrict__ dg) {
   // inv: InplaceABN backward from the output y (see bn_bwd_reduce_kernel); mean / invstd = beta /
   // 1/gamma, scale = the true gamma * invstd
   const RowTile t(C);
   if (t.slot >= t.rpi) return;
+  if (dg != nullptr && blockIdx.x == 0 && t.slot == 0) {
+    // InplaceABN's weight gradient: d(|g| + eps)/dg = sign(g) times the effective weight's gradient
+    // (sums row 1, this rank's) -- the separate sign_mul launch of every layer folded in.  A
+    // workgroup's row slot 0 covers every channel (C <= 2048: C / 8 <= 256 threads).
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float v = graw[t.c0 + k], d = sums[C + t.c0 + k];
+      dg[t.c0 + k] = v > 0.f ? d : (v < 0.f ? -d : 0.f);
+    }
+  }
   float sc[8], sh[8], ca[8], cb[8], cc[8];
   load8(scale + t.c0, sc);
   load8(shift + t.c0, sh);
@@ -795,16 +815,17 @@ void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* par
 
 void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
-                              float* shift, float* rm, float* rv, float momentum, hipStream_t s) {
+                              float* shift, float* rm, float* rv, float momentum, hipStream_t s, float iabn_eps,
+                              float* rgamma) {
   const int R = (M + 127) / 128;
   if (slabs && R <= kDirectSlabs) {
     hipLaunchKernelGGL(bn_slab_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C,
-                       eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
+                       eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum, iabn_eps, rgamma);
     return;
   }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
   hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps, gamma, beta,
-                     mean, invstd, scale, shift, rm, rv, momentum);
+                     mean, invstd, scale, shift, rm, rv, momentum, iabn_eps, rgamma);
 }
 
 void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s) {
@@ -813,9 +834,9 @@ void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s)
 
 void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const float* gamma, const float* beta,
                               float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
-                              float momentum, hipStream_t s) {
+                              float momentum, hipStream_t s, float iabn_eps, float* rgamma) {
   hipLaunchKernelGGL(bn_merge_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, part, P, C, eps,
-                     gamma, beta, mean, invstd, scale, shift, rm, rv, momentum);
+                     gamma, beta, mean, invstd, scale, shift, rm, rv, momentum, iabn_eps, rgamma);
 }
 
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s) {
@@ -837,9 +858,9 @@ void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStre
 
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
                         float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
-                        hipStream_t s) {
+                        hipStream_t s, float iabn_eps, float* rgamma) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, st, W, C, eps, gamma, beta, mean,
-                     invstd, scale, shift, rm, rv, momentum);
+                     invstd, scale, shift, rm, rv, momentum, iabn_eps, rgamma);
 }
 
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm,
@@ -916,11 +937,12 @@ void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const 
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
-                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv) {
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv, const float* graw,
+                         float* dg) {
   const int M = (int)(numel / C);
   const dim3 grid = ew_grid(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_elemt_kernel, grid, 0, s, res, act, dy, x, res, scale, shift, mean, invstd, sums,
-                       inv_count, M, C, slope, dx, dres, inv);
+                       inv_count, M, C, slope, dx, dres, inv, graw, dg);
 }
 
 

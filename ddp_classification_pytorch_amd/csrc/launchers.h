@@ -127,9 +127,11 @@ bool launch_gconv_mfma_wgrad(const bf16* dy, const bf16* x, float* dw, float* pa
 
 int bn_stats_partials(int M, int C, bool from_slabs);
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s);
+// iabn_eps >= 0 (the finalize launchers): InplaceABN's |gamma| + iabn_eps as the weight, 1 / it into rgamma
 void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, float* part, float eps,
                               const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
-                              float* shift, float* rm, float* rv, float momentum, hipStream_t s);
+                              float* shift, float* rm, float* rv, float momentum, hipStream_t s, float iabn_eps = -1.f,
+                              float* rgamma = nullptr);
 // BN statistics from ready first-level partials [P][3][C] (e.g. the stem kernel's)
 // two-level merge of many partials: chunks of 128 rows (0 = merge directly), and the first level
 int bn_partial_chunks(int P);
@@ -137,7 +139,7 @@ void launch_bn_partial_chunk(const float* part, int P, int C, float* tmp, hipStr
 void launch_bn_merge(const float* part, int P, int C, float* out, hipStream_t s);
 void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const float* gamma, const float* beta,
                               float* mean, float* invstd, float* scale, float* shift, float* rm, float* rv,
-                              float momentum, hipStream_t s);
+                              float momentum, hipStream_t s, float iabn_eps = -1.f, float* rgamma = nullptr);
 // stem.hip: the space-to-depth stem conv [N][H][W][16] x [64][4][4][16] -> [N][H][W][64]
 bool stem_fwd_supported(int H, int W, int C, int Co, int KH, int KW);
 int stem_fwd_blocks(int N, int H);
@@ -158,7 +160,7 @@ int colsum_partials(int M);
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s);
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
                         float* invstd, float* scale, float* shift, float* rm, float* rv, float momentum,
-                        hipStream_t s);
+                        hipStream_t s, float iabn_eps = -1.f, float* rgamma = nullptr);
 void launch_bn_eval_coeff(int C, float eps, const float* gamma, const float* beta, const float* rm, const float* rv,
                           float* mean, float* invstd, float* scale, float* shift, hipStream_t s);
 void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const float* shift, bf16* y, size_t numel,
@@ -174,9 +176,11 @@ void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const 
                           float* out, hipStream_t s, int inv = 0);
 // inv = 1: InplaceABN backward -- x is the layer OUTPUT y (act invertible: none / leaky), mean /
 // invstd are beta / 1/gamma, and the pre-activation is recovered in registers
+// dg != nullptr (with sums): also dg = sign(graw) * sums[1] -- InplaceABN's raw-weight gradient
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,
                          const float* mean, const float* invstd, const float* sums, float inv_count, size_t numel,
-                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv = 0);
+                         int C, int act, float slope, bf16* dx, bf16* dres, hipStream_t s, int inv = 0,
+                         const float* graw = nullptr, float* dg = nullptr);
 
 void launch_maxpool_fwd(const bf16* x, bf16* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
                         int s, int p, hipStream_t st, const float* scale = nullptr, const float* shift = nullptr,
@@ -284,6 +288,12 @@ void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t*
 bool conv1x1_ws_supported(int K, int Co, long M);
 bool launch_conv1x1_ws(const bf16* src, const bf16* wt, int ldw, bf16* dst, float* stats, const bf16* zero, int M,
                        int K, int Co, hipStream_t st);
+// small-batch linear backward in one launch (linear_small.hip): g = bf16(dy * act'(y)) (act 0 none,
+// 1 relu, 2 sigmoid on y), dx = g W [N][K] bf16, dW = g^T x [out][K] fp32, db = sum_n g [out] fp32;
+// wt = W^T bf16 [K][ldw]; any of dx / dw / db may be nullptr; false = unsupported (N > 64)
+bool linear_bwd_small_supported(int N, int K, int out);
+bool launch_linear_bwd_small(const bf16* dy, const bf16* y, const bf16* x, const bf16* wt, bf16* dx, float* dw,
+                             float* db, int N, int K, int out, int ldd, int ldw, int act, hipStream_t st);
 // store-decoupled persistent 1x1 stride-1 forward GEMM (conv1x1_ps.hip): loader waves fill an LDS-DMA
 // ring, consumer waves store straight from the accumulators; same contract as launch_conv1x1_ws
 // (ablate: conv1x1_ps.hip PsParams; timing experiments only); cw: consumer waves, 4 or 8

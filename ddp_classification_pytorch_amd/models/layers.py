@@ -112,13 +112,16 @@ class BatchNorm2d(nn.Module):
         if stats:
             self._nbt_pending += 1  # folded into num_batches_tracked lazily (no per-step device add)
         iabn = self.inplace_abn and residual is None and act in ("none", "leaky", "leaky_relu")
-        gamma, rgamma = self.weight, None
+        gamma, rgamma, iabn_eps = self.weight, None, None
         if iabn and self.weight is not None:
-            gamma, rgamma = Fn.iabn_gamma(self.weight, self.iabn_eps)
+            if stats and self.bias is not None and Fn.iabn_fold_enabled():
+                iabn_eps = self.iabn_eps  # |gamma| + eps and sign(gamma) inside the BN kernels
+            else:
+                gamma, rgamma = Fn.iabn_gamma(self.weight, self.iabn_eps)
         return Fn.batch_norm_act(x, slabs, gamma, self.bias, self.running_mean, self.running_var, stats, self.momentum,
                                  self.eps, act=act, slope=slope, residual=residual,
                                  group=self.process_group if stats else None, link=link, iabn=iabn,
-                                 fuse_bwd=fuse_bwd, rgamma=rgamma)
+                                 fuse_bwd=fuse_bwd, rgamma=rgamma, iabn_eps=iabn_eps)
 
     def forward_pool(self, x, slabs=None, act="relu", k=3, s=2, p=1):
         """BN + act + k x k / s max pool.  Training-mode statistics with a ReLU/identity

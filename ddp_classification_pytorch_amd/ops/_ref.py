@@ -212,8 +212,13 @@ def colsum(x):
     return _rows(x).sum(0)
 
 
-def bn_finalize(stats, gamma, beta, run_mean, run_var, momentum, eps):
-    """stats [W,3,C] (n, mean, M2 per rank) merged with Chan's formula."""
+def bn_finalize(stats, gamma, beta, run_mean, run_var, momentum, eps, iabn_eps=-1.0, rgamma_out=None):
+    """stats [W,3,C] (n, mean, M2 per rank) merged with Chan's formula.  iabn_eps >= 0: InplaceABN's
+    effective weight |gamma| + iabn_eps, its reciprocal written to rgamma_out."""
+    if iabn_eps >= 0 and gamma is not None:
+        gamma = gamma.abs() + iabn_eps
+        if rgamma_out is not None:
+            rgamma_out.copy_(1.0 / gamma)
     st = stats.double()
     n_t = st[:, 0].sum(0)
     mu = (st[:, 0] * st[:, 1]).sum(0) / n_t
@@ -231,8 +236,8 @@ def bn_finalize(stats, gamma, beta, run_mean, run_var, momentum, eps):
     return mu.float(), invstd.float(), scale.float(), shift.float()
 
 
-def bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, momentum, eps):
-    return bn_finalize(bn_stats(x, slabs), gamma, beta, run_mean, run_var, momentum, eps)
+def bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, momentum, eps, iabn_eps=-1.0, rgamma_out=None):
+    return bn_finalize(bn_stats(x, slabs), gamma, beta, run_mean, run_var, momentum, eps, iabn_eps, rgamma_out)
 
 
 def bn_eval_coeff(gamma, beta, run_mean, run_var, eps):
@@ -334,13 +339,15 @@ def bn_bwd_reduce(dy, x, res, scale, shift, mean, invstd, act, slope, inv=False)
     return torch.stack([dz.sum(0), (dz * xh).sum(0)])
 
 
-def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope, want_dres, inv=False):
+def bn_bwd_elemt(dy, x, res, scale, shift, mean, invstd, sums, count, act, slope, want_dres, inv=False, graw=None):
     if inv:  # InplaceABN: x is the output y; mean / invstd carry beta / 1/gamma
         x = _act_inv(x, act, slope)
         z = x
         dz = _f(dy) * _act_d(z, act, slope)
         xh = (x - mean) * invstd
         dx = scale * (dz - sums[0] / count - xh * sums[1] / count) if sums is not None else scale * dz
+        if graw is not None:  # the raw InplaceABN weight's gradient sign(g) * sums[1]
+            return dx.to(dy.dtype), (sums[1] * torch.sign(graw)).float()
         return dx.to(dy.dtype), (dz.to(dy.dtype) if want_dres else dy.new_empty(0))
     z = _f(x) * scale + shift
     if res is not None:

@@ -540,6 +540,13 @@ class _Linear(Function):
         x, wt, y = ctx.saved_tensors
         dy = dy.contiguous()
         k = K(dy)
+        if dy.is_cuda and dy.shape[0] <= 64 and _LINEAR_SMALL[0]:
+            # small batch (SE MLPs, heads at batch 16-64): act', dx, dW and db in ONE launch instead of
+            # up to seven (csrc/linear_small.hip)
+            need = ctx.needs_input_grad
+            want_db = ctx.has_bias and need[2]
+            gx, gw, gb = k.linear_bwd_small(dy, y, x, wt, ctx.act, ctx.out, need[0], need[1], want_db)
+            return (gx if need[0] else None), (gw if need[1] else None), (gb if want_db else None), None, None, None
         if ctx.act:
             dy = k.act_bwd(dy, y, ctx.act)
         dx = dw = db = None
@@ -550,6 +557,14 @@ class _Linear(Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = k.colsum(dy)[: ctx.out]  # the padded GEMM's column sums, the real outputs only
         return dx, dw, db, None, None, None
+
+
+# DCP_LINEAR_SMALL=0: the general linear backward at small batches too (A/B)
+_LINEAR_SMALL = [os.environ.get("DCP_LINEAR_SMALL", "1") != "0"]
+
+
+def set_linear_small(enabled: bool):
+    _LINEAR_SMALL[0] = bool(enabled)
 
 
 def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
@@ -570,9 +585,10 @@ def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):
 
 # ----------------------------------------------------------------------------- batch norm (+act, +residual)
 class BNConfig:
-    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world", "iabn", "rgamma")
+    __slots__ = ("training_stats", "momentum", "eps", "act", "slope", "group", "world", "iabn", "rgamma", "iabn_eps")
 
-    def __init__(self, training_stats, momentum, eps, act, slope, group, world, iabn=False, rgamma=None):
+    def __init__(self, training_stats, momentum, eps, act, slope, group, world, iabn=False, rgamma=None,
+                 iabn_eps=None):
         self.training_stats = training_stats
         self.momentum = momentum
         self.eps = eps
@@ -582,6 +598,10 @@ class BNConfig:
         self.world = world
         self.iabn = iabn  # InplaceABN: backward from the output (see _BNAct)
         self.rgamma = rgamma  # InplaceABN: 1 / gamma, when the caller has it (iabn_gamma)
+        # InplaceABN with the RAW weight (iabn_eps set): the BN finalize applies |g| + iabn_eps and writes
+        # 1 / it into rgamma, the backward's elementwise pass returns the raw weight's gradient -- no
+        # iabn_gamma / sign_mul launches per layer
+        self.iabn_eps = iabn_eps
 
 
 def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
@@ -589,8 +609,10 @@ def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
     statistics and the finalize as one launch pair; SyncBN all-gathers the per-rank
     (n, mean, M2) between them."""
     count = x.numel() // x.shape[-1]
+    ieps = -1.0 if cfg.iabn_eps is None else float(cfg.iabn_eps)
+    rg = cfg.rgamma if cfg.iabn_eps is not None else None
     if cfg.group is None:
-        return (*k.bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
+        return (*k.bn_stats_finalize(x, slabs, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps, ieps, rg), count)
     st = k.bn_stats(x, slabs)  # [1,3,C] (n, mean, M2)
     gathered = st.new_empty((cfg.world,) + tuple(st.shape[1:]))
     _peer.all_gather_into_tensor(gathered, st, cfg.group)
@@ -598,7 +620,7 @@ def _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg: BNConfig):
     # the forward merge is exact for any counts; the backward normaliser assumes equal per-rank
     # batches (the sharded sampler pads every rank to the same length; parallel/ddp.py)
     count = count * cfg.world
-    return (*k.bn_finalize(gathered, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps), count)
+    return (*k.bn_finalize(gathered, gamma, beta, run_mean, run_var, cfg.momentum, cfg.eps, ieps, rg), count)
 
 
 # torch's SyncBatchNorm synchronises only when the group has more than one rank
@@ -690,10 +712,19 @@ class _BNAct(Function):
                 if cfg.training_stats and cfg.group is not None:
                     sums = local.clone()
                     _peer.all_reduce(sums, cfg.group)
-            dx, _ = k.bn_bwd_elemt(dy, y, None, scale, shift, beta.detach().float(), rgamma,
-                                   sums if cfg.training_stats else None, float(ctx.count), cfg.act, cfg.slope, False,
-                                   True)
-            dgamma = local[1] if (local is not None and ctx.needs_input_grad[2]) else None
+            raw = cfg.iabn_eps is not None  # gamma is the RAW weight: its gradient carries sign(g)
+            fold = raw and cfg.training_stats and sums is local and ctx.needs_input_grad[2]
+            dx, dg = k.bn_bwd_elemt(dy, y, None, scale, shift, beta.detach().float(), rgamma,
+                                    sums if cfg.training_stats else None, float(ctx.count), cfg.act, cfg.slope, False,
+                                    True, gamma.detach().float() if fold else None)
+            dgamma = None
+            if local is not None and ctx.needs_input_grad[2]:
+                if fold:
+                    dgamma = dg
+                elif raw:
+                    dgamma = k.sign_mul(local[1].contiguous(), gamma.detach().float())
+                else:
+                    dgamma = local[1]
             dbeta = local[0] if (local is not None and ctx.needs_input_grad[3]) else None
             return dx, None, dgamma, dbeta, None, None, None, None, None, None
         if fused is not None and fused[0].data_ptr() == dy.data_ptr() and fused[0].shape == dy.shape:
@@ -1022,15 +1053,37 @@ def iabn_gamma(g, eps):
     return _IABNGamma.apply(g, float(eps))
 
 
+# Training-mode InplaceABN layers hand the RAW weight to batch_norm_act (iabn_eps): the BN finalize
+# and the backward's elementwise pass apply |g| + eps and sign(g) (TResNet-M: 36 + 36 launches per
+# step fewer).  DCP_IABN_FOLD=0: the separate iabn_gamma / sign_mul launches (A/B).
+_IABN_FOLD = [os.environ.get("DCP_IABN_FOLD", "1") != "0"]
+
+
+def set_iabn_fold(enabled: bool):
+    _IABN_FOLD[0] = bool(enabled)
+
+
+def iabn_fold_enabled() -> bool:
+    return _IABN_FOLD[0]
+
+
 def batch_norm_act(x, slabs, gamma, beta, run_mean, run_var, training_stats, momentum, eps, act="relu",
-                   slope=0.01, residual=None, group=None, link=None, iabn=False, fuse_bwd=False, rgamma=None):
+                   slope=0.01, residual=None, group=None, link=None, iabn=False, fuse_bwd=False, rgamma=None,
+                   iabn_eps=None):
     """``iabn``: InplaceABN storage (invertible act: identity / leaky, no residual, a gamma bounded
-    away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention).  ``fuse_bwd``:
-    offer this plain BN + ReLU's backward reduction to its consumer even under the masked-only
-    default (the consumer is a grouped conv, whose dgrad fusion measured a win: ResNeXt)."""
+    away from 0 -- BatchNorm2d passes |gamma| + eps, the inplace_abn convention; with ``iabn_eps``
+    (training statistics only) it passes the RAW weight and the kernels apply |gamma| + iabn_eps and
+    sign(gamma) themselves).  ``fuse_bwd``: offer this plain BN + ReLU's backward reduction to its
+    consumer even under the masked-only default (the consumer is a grouped conv, whose dgrad fusion
+    measured a win: ResNeXt)."""
     group, world = _sync_group(group)
     iabn = bool(iabn) and residual is None and ACT[act] in (0, 2) and gamma is not None and beta is not None
+    if iabn_eps is not None and not (iabn and training_stats):
+        raise ValueError("batch_norm_act: iabn_eps needs an InplaceABN layer with training statistics")
     cfg = BNConfig(training_stats, momentum, eps, ACT[act], float(slope), group, world, iabn, rgamma if iabn else None)
+    if iabn_eps is not None:
+        cfg.iabn_eps = float(iabn_eps)
+        cfg.rgamma = torch.empty(gamma.shape, dtype=torch.float32, device=gamma.device)  # written by the finalize
     if slabs is None or (slabs.numel() == 0):
         slabs = None
     # ReLU / identity only: their masks are idempotent, so a consumer that masked the

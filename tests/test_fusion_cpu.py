@@ -369,3 +369,36 @@ def test_eval_coefficient_cache_sees_untracked_bn_updates():
     c3 = Fn.bn_eval_coefficients(bn)
     Fn.bump_weight_generation()
     assert Fn.bn_eval_coefficients(bn)[2] is c3[2]
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_iabn_fold_matches_separate_gamma_launches(train):
+    """InplaceABN with the raw weight handed to the BN kernels (|gamma| + eps in the finalize,
+    sign(gamma) on the weight gradient in the backward's elementwise pass; DCP_IABN_FOLD default)
+    == the separate iabn_gamma / sign_mul ops: loss, every gradient and the running statistics, with
+    some gammas negative (the sign path).  Frozen statistics (train=False) keep the separate ops."""
+    out = []
+    for fold in (True, False):
+        Fn.set_iabn_fold(fold)
+        try:
+            torch.manual_seed(7)
+            m = build_model("tresnet_m", num_classes=10)
+            with torch.no_grad():
+                for mod in m.modules():
+                    if getattr(mod, "inplace_abn", False):
+                        mod.weight.mul_(torch.where(torch.rand_like(mod.weight) < 0.3, -1.0, 1.0))
+                        if not train:
+                            mod.frozen = True
+            g = torch.Generator().manual_seed(3)
+            imgs = torch.rand(2, 3, 64, 64, generator=g)
+            labels = torch.randint(0, 10, (2,), generator=g)
+            loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, cpad=3, nchw=True)), labels)
+            loss.backward()
+            rs = torch.cat([b.flatten() for n, b in m.named_buffers() if "running" in n])
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]), rs))
+        finally:
+            Fn.set_iabn_fold(True)
+    (l1, g1, r1), (l0, g0, r0) = out
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-6
+    assert torch.allclose(r1, r0, rtol=1e-6, atol=1e-7)

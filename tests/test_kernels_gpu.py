@@ -1260,6 +1260,70 @@ def test_iabn_gamma_and_sign_mul(K):
     assert torch.equal(K.sign_mul(d.to(DEV), g.to(DEV)).cpu(), _ref.sign_mul(d, g))
 
 
+@pytest.mark.parametrize("C", [64, 1024, 2048])
+def test_iabn_folded_finalize_and_weight_gradient(K, C):
+    """The InplaceABN effective weight folded into the BN kernels: the finalize with iabn_eps ==
+    the finalize of |g| + eps (and writes 1 / (|g| + eps)), and bn_bwd_elemt's graw output ==
+    sums[1] * sign(g) (zeros included), while its dx is unchanged."""
+    M = 3000
+    torch.manual_seed(C)
+    x = rnd(M, C).to(DEV)
+    g = torch.randn(C)
+    g[::5] = 0.0
+    b = torch.randn(C) * 0.1
+    eff = g.abs() + 1e-5
+    rg = torch.empty(C, device=DEV)
+    outs = []
+    for gamma, ie, out in ((g, 1e-5, rg), (eff, -1.0, None)):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        outs.append(K.bn_stats_finalize(x, None, gamma.to(DEV), b.to(DEV), rm, rv, 0.1, 1e-5, ie, out) + (rm, rv))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    assert torch.allclose(rg.cpu(), 1.0 / eff, rtol=1e-6)
+    mean, invstd, scale, shift = outs[1][:4]
+    y = K.bn_act(x, None, scale, shift, 2, 0.01)
+    dy = rnd(M, C).to(DEV)
+    sums = K.bn_bwd_reduce(dy, y, None, scale, shift, b.to(DEV), rg, 2, 0.01, True)
+    dx1, dg = K.bn_bwd_elemt(dy, y, None, scale, shift, b.to(DEV), rg, sums, float(M), 2, 0.01, False, True, g.to(DEV))
+    dx0, _ = K.bn_bwd_elemt(dy, y, None, scale, shift, b.to(DEV), rg, sums, float(M), 2, 0.01, False, True)
+    assert torch.equal(dx1, dx0)
+    assert torch.equal(dg.cpu(), _ref.sign_mul(sums[1].cpu(), g))
+
+
+def test_tresnet_iabn_fold_matches_separate_launches_gpu():
+    """TResNet-M on the GPU: the folded InplaceABN weight path (default) == the separate
+    iabn_gamma / sign_mul launches -- loss, gradients, running statistics (some gammas negative)."""
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    out = []
+    for fold in (True, False):
+        Fn.set_iabn_fold(fold)
+        try:
+            torch.manual_seed(7)
+            m = build_model("tresnet_m", num_classes=10).to(DEV)
+            with torch.no_grad():
+                for mod in m.modules():
+                    if getattr(mod, "inplace_abn", False):
+                        mod.weight.mul_(torch.where(torch.rand_like(mod.weight) < 0.3, -1.0, 1.0))
+            gen = torch.Generator().manual_seed(3)
+            imgs = torch.randint(0, 256, (4, 3, 64, 64), dtype=torch.uint8, generator=gen).to(DEV)
+            labels = torch.randint(0, 10, (4,), generator=gen).to(DEV)
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), in_scale=1 / 255.0, **input_layout(m))
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            rs = torch.cat([b.flatten() for n, b in m.named_buffers() if "running" in n]).cpu()
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]).cpu(),
+                        rs))
+        finally:
+            Fn.set_iabn_fold(True)
+    (l1, g1, r1), (l0, g0, r0) = out
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-6
+    assert torch.equal(r1, r0)
+
+
 def test_conv_autotune_same_results(K):
     """g_tune[25] = 1 (DCP_AUTOTUNE): the first call of each conv problem times the candidate
     configurations and keeps one; forward and data gradient are bitwise the untuned results (every
@@ -1599,3 +1663,44 @@ def test_conv1x1_weight_stationary(K, shape, kernel):
     assert torch.equal(st[0, 0].cpu(), sr[0, 0])
     assert relerr(st[0, 1], sr[0, 1]) < 1e-4
     assert relerr(st[0, 2], sr[0, 2]) < 1e-4
+
+
+@pytest.mark.parametrize("N", [1, 16, 64])
+@pytest.mark.parametrize("K_in,out", [(64, 64), (1024, 128), (128, 1000), (2048, 1000)])
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid"])
+def test_linear_backward_small_batch_one_launch(N, K_in, out, act):
+    """Fused small-batch linear backward (csrc/linear_small.hip, batches <= 64): dx, dW and db of
+    act(x W^T + b) == the fp32 reference on the same bf16 operands, and == the general multi-launch
+    backward up to fp32 summation order."""
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    torch.manual_seed(N + K_in + out)
+    w = (torch.randn(out, K_in) / math.sqrt(K_in)).to(DEV).requires_grad_()
+    b = (torch.randn(out) * 0.1).to(DEV).requires_grad_()
+    x = torch.randn(N, K_in).bfloat16().to(DEV).requires_grad_()
+    gy = torch.randn(N, out).to(DEV)
+    grads = []
+    for small in (True, False):
+        Fn.set_linear_small(small)
+        try:
+            for t in (w, b, x):
+                t.grad = None
+            y = Fn.linear(x, w, b, act=act)
+            (y.float() * gy).sum().backward()
+            torch.cuda.synchronize()
+            grads.append([t.grad.float().cpu().clone() for t in (x, w, b)])
+        finally:
+            Fn.set_linear_small(True)
+    # fp32 reference: the bf16 operands, the bf16 forward output for act' (as the kernels use it)
+    xr = x.detach().float().cpu().requires_grad_()
+    wr = w.detach().bfloat16().float().cpu().requires_grad_()
+    br = b.detach().cpu().requires_grad_()
+    z = xr @ wr.t() + br
+    yr = {"none": z, "relu": torch.relu(z), "sigmoid": torch.sigmoid(z)}[act]
+    (yr * gy.cpu()).sum().backward()
+    for got in grads:
+        assert relerr(got[0], xr.grad) < 2e-2
+        assert relerr(got[1], wr.grad) < 2e-2
+        assert relerr(got[2], br.grad) < 2e-2
+    for a, c in zip(*grads):
+        assert relerr(a, c) < 1e-2
