@@ -109,7 +109,12 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         for msg in ex.map(lambda so: _compile(so[0], so[1], torch_inc, force), zip(srcs, objs)):
             if verbose:
                 print("[dcp-build]", msg, flush=True)
-    if force or _stale(LIB_PATH, objs):
+    # the object list of the last link: a source added or REMOVED since then relinks too (a removed
+    # file leaves every remaining object older than the library)
+    manifest = os.path.join(BUILD, "link_manifest.txt")
+    listing = "\n".join(os.path.basename(o) for o in objs)
+    old_listing = open(manifest).read() if os.path.exists(manifest) else None
+    if force or _stale(LIB_PATH, objs) or old_listing != listing:
         tmp = LIB_PATH + f".tmp{os.getpid()}"
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs
         cmd += [f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
@@ -118,6 +123,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, LIB_PATH)
+        with open(manifest, "w") as f:
+            f.write(listing)
         if verbose:
             print("[dcp-build] linked", LIB_PATH, flush=True)
     return LIB_PATH

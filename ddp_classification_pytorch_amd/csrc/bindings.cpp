@@ -781,32 +781,6 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& bias
   return y;
 }
 
-// One-launch backward of y = act(x W^T + b) for N <= 64 rows (linear_small.hip): dy / y [N][>= out]
-// bf16 (the GEMM's padded output width), x [N][K], wt = W^T [K][ldw] bf16 -> (dx [N][K] bf16 or empty,
-// dw [out][K] fp32 or empty, db [out] fp32 or empty)
-std::tuple<Tensor, Tensor, Tensor> linear_bwd_small(const Tensor& dy, const optional<Tensor>& y, const Tensor& x,
-                                                    const Tensor& wt, int64_t act, int64_t out, bool need_dx,
-                                                    bool need_dw, bool need_db) {
-  CHECK_ACT(dy);
-  CHECK_ACT(x);
-  CHECK_ACT(wt);
-  const int N = dy.size(0), K = x.size(1);
-  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && x.size(0) == N && wt.dim() == 2 && wt.size(0) == K &&
-                  wt.size(1) >= out && dy.size(1) >= out && out >= 1,
-              "linear_bwd_small shapes");
-  TORCH_CHECK(act >= 0 && act <= 2 && (act == 0 || (y.has_value() && y->sizes() == dy.sizes())),
-              "linear_bwd_small: act 0 / 1 / 2 with y like dy");
-  if (y.has_value()) CHECK_ACT(*y);
-  TORCH_CHECK(dcp::linear_bwd_small_supported(N, K, (int)out), "linear_bwd_small: at most 64 rows");
-  auto dx = need_dx ? at::empty({N, K}, bf16_like(x)) : at::empty({0}, bf16_like(x));
-  auto dw = need_dw ? at::empty({out, K}, f32_like(x)) : at::empty({0}, f32_like(x));
-  auto db = need_db ? at::empty({out}, f32_like(x)) : at::empty({0}, f32_like(x));
-  dcp::launch_linear_bwd_small(bp(dy), y.has_value() ? bp(*y) : nullptr, bp(x), bp(wt), need_dx ? bpm(dx) : nullptr,
-                               need_dw ? dw.data_ptr<float>() : nullptr, need_db ? db.data_ptr<float>() : nullptr, N,
-                               K, (int)out, (int)dy.size(1), (int)wt.size(1), (int)act, cur_stream());
-  return {dx, dw, db};
-}
-
 // dy [B,N] bf16, x [B,K] bf16 -> dw fp32 [N,K]
 Tensor linear_wgrad(const Tensor& dy, const Tensor& x) {
   CHECK_ACT(dy);
@@ -1940,10 +1914,6 @@ TORCH_LIBRARY(dcp, m) {
       "bn_bwd_reduce(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, int "
       "act, float slope, bool inv=False) -> Tensor",
       &bn_bwd_reduce);
-  m.def(
-      "linear_bwd_small(Tensor dy, Tensor? y, Tensor x, Tensor wt, int act, int out, bool need_dx, bool need_dw, "
-      "bool need_db) -> (Tensor, Tensor, Tensor)",
-      &linear_bwd_small);
   m.def(
       "bn_bwd_elemt(Tensor dy, Tensor x, Tensor? res, Tensor scale, Tensor shift, Tensor mean, Tensor invstd, "
       "Tensor? sums, float count, int act, float slope, bool want_dres, bool inv=False, Tensor? graw=None) "

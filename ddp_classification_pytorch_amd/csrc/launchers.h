@@ -288,12 +288,6 @@ void launch_nested_eval_scalar(const float* feat, const float* W, const int64_t*
 bool conv1x1_ws_supported(int K, int Co, long M);
 bool launch_conv1x1_ws(const bf16* src, const bf16* wt, int ldw, bf16* dst, float* stats, const bf16* zero, int M,
                        int K, int Co, hipStream_t st);
-// small-batch linear backward in one launch (linear_small.hip): g = bf16(dy * act'(y)) (act 0 none,
-// 1 relu, 2 sigmoid on y), dx = g W [N][K] bf16, dW = g^T x [out][K] fp32, db = sum_n g [out] fp32;
-// wt = W^T bf16 [K][ldw]; any of dx / dw / db may be nullptr; false = unsupported (N > 64)
-bool linear_bwd_small_supported(int N, int K, int out);
-bool launch_linear_bwd_small(const bf16* dy, const bf16* y, const bf16* x, const bf16* wt, bf16* dx, float* dw,
-                             float* db, int N, int K, int out, int ldd, int ldw, int act, hipStream_t st);
 // store-decoupled persistent 1x1 stride-1 forward GEMM (conv1x1_ps.hip): loader waves fill an LDS-DMA
 // ring, consumer waves store straight from the accumulators; same contract as launch_conv1x1_ws
 // (ablate: conv1x1_ps.hip PsParams; timing experiments only); cw: consumer waves, 4 or 8

@@ -540,13 +540,6 @@ class _Linear(Function):
         x, wt, y = ctx.saved_tensors
         dy = dy.contiguous()
         k = K(dy)
-        if dy.is_cuda and dy.shape[0] <= 64 and _LINEAR_SMALL[0]:
-            # small batch (SE MLPs, heads at batch 16-64): act', dx, dW and db in ONE launch instead of
-            # up to seven (csrc/linear_small.hip)
-            need = ctx.needs_input_grad
-            want_db = ctx.has_bias and need[2]
-            gx, gw, gb = k.linear_bwd_small(dy, y, x, wt, ctx.act, ctx.out, need[0], need[1], want_db)
-            return (gx if need[0] else None), (gw if need[1] else None), (gb if want_db else None), None, None, None
         if ctx.act:
             dy = k.act_bwd(dy, y, ctx.act)
         dx = dw = db = None
@@ -557,14 +550,6 @@ class _Linear(Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = k.colsum(dy)[: ctx.out]  # the padded GEMM's column sums, the real outputs only
         return dx, dw, db, None, None, None
-
-
-# DCP_LINEAR_SMALL=0: the general linear backward at small batches too (A/B)
-_LINEAR_SMALL = [os.environ.get("DCP_LINEAR_SMALL", "1") != "0"]
-
-
-def set_linear_small(enabled: bool):
-    _LINEAR_SMALL[0] = bool(enabled)
 
 
 def linear(x, weight, bias=None, relu=False, keep_padded=False, act=None):

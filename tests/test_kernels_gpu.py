@@ -1663,44 +1663,3 @@ def test_conv1x1_weight_stationary(K, shape, kernel):
     assert torch.equal(st[0, 0].cpu(), sr[0, 0])
     assert relerr(st[0, 1], sr[0, 1]) < 1e-4
     assert relerr(st[0, 2], sr[0, 2]) < 1e-4
-
-
-@pytest.mark.parametrize("N", [1, 16, 64])
-@pytest.mark.parametrize("K_in,out", [(64, 64), (1024, 128), (128, 1000), (2048, 1000)])
-@pytest.mark.parametrize("act", ["none", "relu", "sigmoid"])
-def test_linear_backward_small_batch_one_launch(N, K_in, out, act):
-    """Fused small-batch linear backward (csrc/linear_small.hip, batches <= 64): dx, dW and db of
-    act(x W^T + b) == the fp32 reference on the same bf16 operands, and == the general multi-launch
-    backward up to fp32 summation order."""
-    from ddp_classification_pytorch_amd.ops import functional as Fn
-
-    torch.manual_seed(N + K_in + out)
-    w = (torch.randn(out, K_in) / math.sqrt(K_in)).to(DEV).requires_grad_()
-    b = (torch.randn(out) * 0.1).to(DEV).requires_grad_()
-    x = torch.randn(N, K_in).bfloat16().to(DEV).requires_grad_()
-    gy = torch.randn(N, out).to(DEV)
-    grads = []
-    for small in (True, False):
-        Fn.set_linear_small(small)
-        try:
-            for t in (w, b, x):
-                t.grad = None
-            y = Fn.linear(x, w, b, act=act)
-            (y.float() * gy).sum().backward()
-            torch.cuda.synchronize()
-            grads.append([t.grad.float().cpu().clone() for t in (x, w, b)])
-        finally:
-            Fn.set_linear_small(True)
-    # fp32 reference: the bf16 operands, the bf16 forward output for act' (as the kernels use it)
-    xr = x.detach().float().cpu().requires_grad_()
-    wr = w.detach().bfloat16().float().cpu().requires_grad_()
-    br = b.detach().cpu().requires_grad_()
-    z = xr @ wr.t() + br
-    yr = {"none": z, "relu": torch.relu(z), "sigmoid": torch.sigmoid(z)}[act]
-    (yr * gy.cpu()).sum().backward()
-    for got in grads:
-        assert relerr(got[0], xr.grad) < 2e-2
-        assert relerr(got[1], wr.grad) < 2e-2
-        assert relerr(got[2], br.grad) < 2e-2
-    for a, c in zip(*grads):
-        assert relerr(a, c) < 1e-2
