@@ -469,10 +469,10 @@ Tensor conv_dgrad(const Tensor& dy, const Tensor& wt, int64_t H, int64_t W, int6
   if (stride == 1 && pad == 1 && KH == 3 && KW == 3 && !add.has_value() && dcp::conv3x3_c64_supported(H, W, Co, C)) {
     // 64 -> 64 channel 3x3: the input gradient is the direct kernel's forward conv of dY with the
     // spatially flipped transposed weight, W'[c][kh][kw][co] = W[co][2-kh][2-kw][c] (conv3x3.hip:
-    // one staged window per strip instead of nine tap gathers; ResNet-50 layer1 conv2 dgrad)
-    auto wf = wt.flip({1, 2}).contiguous();
+    // one staged window per strip instead of nine tap gathers; ResNet-50 layer1 conv2 dgrad); the
+    // kernel reads the taps of wt in reverse order (no flipped copy)
     const int blocks = dcp::conv3x3_c64_blocks(N, H, W, num_cus(dy.get_device()));
-    dcp::launch_conv3x3_c64(bp(dy), bp(wf), bpm(dx), nullptr, z, N, H, W, blocks, st);
+    dcp::launch_conv3x3_c64(bp(dy), bp(wt), bpm(dx), nullptr, z, N, H, W, blocks, st, nullptr, nullptr, 1);
     return dx;
   }
   if (stride == 1) {

@@ -55,6 +55,9 @@ struct C3Params {
   // taps), so the BN + ReLU output of the producing layer is never written.  nullptr: off.
   const float* pscale;
   const float* pshift;
+  // 1: read tap 8 - t of w for tap t (the spatially flipped weight of the data gradient, read in
+  // place: no flipped copy per call)
+  int wflip;
 };
 
 __device__ __forceinline__ uint32_t c3_addr(uint32_t wpix, uint32_t c) {
@@ -257,7 +260,8 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW) conv3x3_c64_kernel(const C3Pa
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int n = 0; n < 2; ++n)
-        bw[t][h][n] = *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + t) * 64 + 32 * h + 8 * lg);
+        bw[t][h][n] =
+            *(const bf16x8*)(p.w + ((size_t)(32 * ch + 16 * n + lr) * 9 + (p.wflip ? 8 - t : t)) * 64 + 32 * h + 8 * lg);
 
   if (p.sched == 3 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   // BN prologue: a thread's window chunks all hold the same 8 channels -- chunk qq = tid + k * 64 NW
@@ -461,11 +465,12 @@ int conv3x3_c64_blocks(int N, int H, int W, int num_cu) {
 }
 
 void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
-                        int blocks, hipStream_t stream, const float* pscale, const float* pshift) {
+                        int blocks, hipStream_t stream, const float* pscale, const float* pshift, int wflip) {
   const C3Cfg cfg = c3_cfg();
   C3Params p;
   p.x = x; p.w = w; p.y = y; p.part = part; p.zero = zero;
   p.pscale = pscale; p.pshift = pshift;
+  p.wflip = wflip;
   p.H = H; p.W = W;
   p.ablate = g_tune[kAblate];
   p.sched = g_tune[kC3Variant];

@@ -253,7 +253,8 @@ void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const 
 bool conv3x3_c64_supported(int H, int W, int C, int Co);
 int conv3x3_c64_blocks(int N, int H, int W, int num_cu);
 void launch_conv3x3_c64(const bf16* x, const bf16* w, bf16* y, float* part, const bf16* zero, int N, int H, int W,
-                        int blocks, hipStream_t stream, const float* pscale = nullptr, const float* pshift = nullptr);
+                        int blocks, hipStream_t stream, const float* pscale = nullptr, const float* pshift = nullptr,
+                        int wflip = 0);
 
 // host int64 table -> device through kernel arguments (graph-capture safe, see misc.hip)
 void launch_table_fill(const int64_t* host, int64_t n, int64_t* out, hipStream_t s);
