@@ -997,6 +997,85 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_stats_finalize(const Tensor& x, co
   return {coef[0], coef[1], coef[2], coef[3]};
 }
 
+// per-device counters of bn_fin_act_kernel: zeroed once (outside any capture), re-armed by every
+// launch; all BN launches of a device run on one stream at a time, so one triple serves them all
+static uint32_t* fin_act_sync(int dev, hipStream_t st) {
+  static std::mutex mu;
+  static std::unordered_map<int, uint32_t*> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find(dev);
+  if (it != bufs.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  uint32_t* p = nullptr;
+  if (hipMalloc(&p, 64) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+  bufs[dev] = p;
+  return p;
+}
+
+// spin timeouts of bn_fin_act_kernel on this device so far (0 = every launch saw its finalize)
+int64_t bn_fin_act_timeouts(const Tensor& like) {
+  uint32_t* p = fin_act_sync(like.get_device(), cur_stream());
+  if (p == nullptr) return 0;
+  uint32_t v = 0;
+  TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess && hipMemcpy(&v, p + 2, 4, hipMemcpyDeviceToHost) == hipSuccess,
+              "bn_fin_act_timeouts: copy");
+  return v;
+}
+
+// local training BN from conv slabs / partials: finalize + BN + act (+ residual) (+ act' mask bits) in
+// ONE launch -> (y, mask or an empty tensor, mean, invstd, scale, shift); running stats updated in
+// place.  Bit-identical to bn_stats_finalize followed by bn_act / bn_act_mask (the two-launch path it
+// falls back to for deep slab stacks, during a first capture, or with g_tune bn_fin_act = 2).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn_fin_act(
+    const Tensor& x, const Tensor& slabs, const optional<Tensor>& res, const optional<Tensor>& gamma,
+    const optional<Tensor>& beta, const optional<Tensor>& run_mean, const optional<Tensor>& run_var, double momentum,
+    double eps, int64_t act, double slope, bool want_mask, double iabn_eps, const optional<Tensor>& rgamma_out) {
+  CHECK_ACT(x);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn channels must be a multiple of 8 and <= 2048");
+  if (res.has_value()) {
+    CHECK_ACT(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+  }
+  const bool have = slabs.numel() > 0;  // empty: statistics from x itself (two-launch path)
+  const bool part = have && is_partials(slabs, C);
+  if (have && !part)
+    TORCH_CHECK(slabs.dim() == 3 && slabs.size(0) == (M + 127) / 128 && slabs.size(1) == 2 && slabs.size(2) == C,
+                "slab shape");
+  auto y = at::empty_like(x);
+  Tensor mask;
+  if (want_mask) {
+    std::vector<int64_t> ms = x.sizes().vec();
+    ms.back() = C / 8;
+    mask = at::empty(ms, x.options().dtype(at::kByte));
+  } else {
+    mask = at::empty({0}, x.options().dtype(at::kByte));
+  }
+  auto st = cur_stream();
+  uint32_t* sync = dcp::g_tune[dcp::kBnFinAct] == 2 ? nullptr : fin_act_sync(x.get_device(), st);
+  const bool fused = sync != nullptr && have && (part || (int)slabs.size(0) <= dcp::bn_direct_slabs());
+  if (!fused) {
+    auto [mean, invstd, scale, shift] = bn_stats_finalize(x, have ? optional<Tensor>(slabs) : optional<Tensor>(),
+                                                          gamma, beta, run_mean, run_var, momentum, eps, iabn_eps,
+                                                          rgamma_out);
+    dcp::launch_bn_act_fwd(bp(x), res.has_value() ? bp(*res) : nullptr, scale.data_ptr<float>(),
+                           shift.data_ptr<float>(), bpm(y), x.numel(), C, (int)act, (float)slope, st,
+                           want_mask ? mask.data_ptr<uint8_t>() : nullptr);
+    return {y, mask, mean, invstd, scale, shift};
+  }
+  auto coef = at::empty({4, C}, f32_like(x));
+  float* cp = coef.data_ptr<float>();
+  const Tensor src = part ? chunk_partials(slabs, C) : slabs;
+  dcp::launch_bn_fin_act(bp(x), res.has_value() ? bp(*res) : nullptr, src.data_ptr<float>(), (int)src.size(0),
+                         part ? 1 : 0, M, C, (float)eps, fp(gamma), fp(beta), cp, cp + C, cp + 2 * C, cp + 3 * C,
+                         fpm(run_mean), fpm(run_var), (float)momentum, (float)iabn_eps, fpm(rgamma_out), bpm(y),
+                         want_mask ? mask.data_ptr<uint8_t>() : nullptr, (int)act, (float)slope, sync, st);
+  return {y, mask, coef[0], coef[1], coef[2], coef[3]};
+}
+
 // stem weight: 7x7 master [Co,7,7,C<=4] fp32 -> its s2d form written into w16 [Co,4,4,16] (in place)
 void s2d_weight(const Tensor& w7, const Tensor& w16) {
   CHECK_DEV(w7);
@@ -1908,6 +1987,11 @@ TORCH_LIBRARY(dcp, m) {
         "Tensor rscale, Tensor rmean, Tensor rinvstd, Tensor rsums, float count) -> (Tensor, Tensor)",
         &bn2_bwd_elemt);
   m.def("bn_act(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> Tensor", &bn_act);
+  m.def("bn_fin_act(Tensor x, Tensor slabs, Tensor? res, Tensor? gamma, Tensor? beta, Tensor? run_mean, "
+        "Tensor? run_var, float momentum, float eps, int act, float slope, bool want_mask, float iabn_eps=-1., "
+        "Tensor(a!)? rgamma_out=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+        &bn_fin_act);
+  m.def("bn_fin_act_timeouts(Tensor like) -> int", &bn_fin_act_timeouts);
   m.def("bn_act_mask(Tensor x, Tensor? res, Tensor scale, Tensor shift, int act, float slope) -> (Tensor, Tensor)",
         &bn_act_mask);
   m.def(

@@ -157,9 +157,9 @@ __global__ void __launch_bounds__(256) chan_welford_partial_kernel(const bf16* _
 constexpr int kMergeWaves = 16;
 constexpr int kPartialChunk = 128;
 template <int NW = kMergeWaves>
-__device__ __forceinline__ Welford merge_partials(const float* __restrict__ part, int P, int C) {
+__device__ __forceinline__ Welford merge_partials(const float* __restrict__ part, int P, int C, int cb) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = cb * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int p = w;
@@ -191,9 +191,9 @@ __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part
 // path for R <= kDirectSlabs (small activations: no bn_slab_partial launch, whose per-launch cost
 // dominated the statistics of every layer at batch 32-128)
 constexpr int kDirectSlabs = 1024;
-__device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, int R, int M, int C) {
+__device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, int R, int M, int C, int cb) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = cb * 64 + lane;
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
     int r = w;
@@ -237,7 +237,7 @@ __device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, 
 // slabs [R][2][C] -> out [3][C] (R <= kDirectSlabs)
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_merge_kernel(const float* __restrict__ slabs, int R, int M,
                                                                          int C, float* __restrict__ out) {
-  const Welford a = merge_slabs(slabs, R, M, C);
+  const Welford a = merge_slabs(slabs, R, M, C, blockIdx.x);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) == 0 && c < C) {
     out[c] = a.n;
@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_merge_kernel(const f
 // partials [P][3][C] -> out [3][C]
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_kernel(const float* __restrict__ part, int P, int C,
                                                        float* __restrict__ out) {
-  const Welford a = merge_partials(part, P, C);
+  const Welford a = merge_partials(part, P, C, blockIdx.x);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) == 0 && c < C) {
     out[c] = a.n;
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_kernel(const float*
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_partial_chunk_kernel(const float* __restrict__ part, int P,
                                                                             int C, float* __restrict__ out) {
   const int r0 = blockIdx.y * kPartialChunk;
-  const Welford a = merge_partials(part + (size_t)r0 * 3 * C, min(kPartialChunk, P - r0), C);
+  const Welford a = merge_partials(part + (size_t)r0 * 3 * C, min(kPartialChunk, P - r0), C, blockIdx.x);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) == 0 && c < C) {
     out[((size_t)blockIdx.y * 3 + 0) * C + c] = a.n;
@@ -283,6 +283,9 @@ void launch_bn_partial_chunk(const float* part, int P, int C, float* tmp, hipStr
 // merged (n, mean, M2) of channel c -> mean, invstd, scale, shift (+ running stats)
 // iabn_eps >= 0: InplaceABN's effective weight |gamma| + iabn_eps (and its reciprocal into rgamma) -- the
 // separate iabn_gamma launch of every layer folded in (its gradient's sign: bn_bwd_elemt's dg output)
+// WT: scale / shift stored write-through (agent-scope atomic stores) for readers in other workgroups
+// of the same launch (bn_fin_act_kernel)
+template <bool WT = false>
 __device__ __forceinline__ void finalize_channel(const Welford& a, int c, float eps, const float* __restrict__ gamma,
                                                  const float* __restrict__ beta, float* __restrict__ mean,
                                                  float* __restrict__ invstd, float* __restrict__ scale,
@@ -299,8 +302,13 @@ __device__ __forceinline__ void finalize_channel(const Welford& a, int c, float 
     if (rgamma) rgamma[c] = 1.f / g;
   }
   const float b = beta ? beta[c] : 0.f;
-  scale[c] = g * is;
-  shift[c] = b - a.mean * g * is;
+  if (WT) {
+    __hip_atomic_store(scale + c, g * is, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(shift + c, b - a.mean * g * is, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    scale[c] = g * is;
+    shift[c] = b - a.mean * g * is;
+  }
   if (run_mean) {
     const float unb = a.n > 1.f ? a.m2 / (a.n - 1.f) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * a.mean;
@@ -315,7 +323,7 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_merge_finalize_kernel(
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
     float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float iabn_eps,
     float* __restrict__ rgamma) {
-  const Welford m = merge_partials(part, P, C);
+  const Welford m = merge_partials(part, P, C, blockIdx.x);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) != 0 || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
@@ -330,7 +338,7 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
     const float* __restrict__ beta, float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ scale,
     float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float iabn_eps,
     float* __restrict__ rgamma) {
-  const Welford m = merge_slabs(slabs, R, M, C);
+  const Welford m = merge_slabs(slabs, R, M, C, blockIdx.x);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if ((threadIdx.x >> 6) != 0 || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
@@ -445,13 +453,14 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16* __restr
 // ---------------------------------------------------------------------------
 struct RowTile {
   int cpr, rpi, slot, ch, c0;
-  __device__ RowTile(int C) {
+  __device__ RowTile(int C, int tid) {
     cpr = C >> 3;
     rpi = 256 / cpr;
-    slot = threadIdx.x / cpr;
-    ch = threadIdx.x - slot * cpr;
+    slot = tid / cpr;
+    ch = tid - slot * cpr;
     c0 = ch * 8;
   }
+  __device__ explicit RowTile(int C) : RowTile(C, threadIdx.x) {}
 };
 
 __device__ __forceinline__ void load8(const float* __restrict__ p, float* v) {
@@ -460,32 +469,14 @@ __device__ __forceinline__ void load8(const float* __restrict__ p, float* v) {
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
 
+// the rows of one (virtual) 256-thread workgroup vb of VG: y = act(x*sc + sh [+ res*rsc + rsh])
 template <int ACT, bool RES>
-__global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
-                                                         const float* __restrict__ scale,
-                                                         const float* __restrict__ shift, bf16* __restrict__ y,
-                                                         int M, int C, float slope, int nt,
-                                                         uint8_t* __restrict__ mask,
-                                                         const float* __restrict__ rscale,
-                                                         const float* __restrict__ rshift) {
-  // mask != nullptr: also store act'(z) > 0 as one bit per element ([M][C/8] bytes), so the
-  // backward of a BN + residual + ReLU layer reads 1/16 of the residual's bytes for its mask.
-  // rscale != nullptr: the residual is itself a raw BN input (a projection shortcut's conv
-  // output) normalised on the fly, res * rscale + rshift -- its BN never writes an activation.
-  const RowTile t(C);
-  if (t.slot >= t.rpi) return;
-  float sc[8], sh[8], rsc[8], rsh[8];
-  load8(scale + t.c0, sc);
-  load8(shift + t.c0, sh);
-  if (RES && rscale) {
-    load8(rscale + t.c0, rsc);
-    load8(rshift + t.c0, rsh);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) rsc[k] = 1.f, rsh[k] = 0.f;
-  }
-  const int step = gridDim.x * t.rpi;
-  int m = blockIdx.x * t.rpi + t.slot;
+__device__ __forceinline__ void bn_act_rows(const RowTile& t, int vb, int VG, const bf16* __restrict__ x,
+                                            const bf16* __restrict__ res, const float* sc, const float* sh,
+                                            const float* rsc, const float* rsh, bf16* __restrict__ y, int M, int C,
+                                            float slope, int nt, uint8_t* __restrict__ mask) {
+  const int step = VG * t.rpi;
+  int m = vb * t.rpi + t.slot;
   constexpr int U = 4;
   for (; m + (U - 1) * step < M; m += U * step) {
     bf16x8 v[U], r[U];
@@ -528,6 +519,131 @@ __global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict_
     *(bf16x8*)(y + off) = o;
     if (mask) mask[(size_t)m * t.cpr + t.ch] = (uint8_t)bits;
   }
+}
+
+template <int ACT, bool RES>
+__global__ void __launch_bounds__(256) bn_act_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, bf16* __restrict__ y,
+                                                         int M, int C, float slope, int nt,
+                                                         uint8_t* __restrict__ mask,
+                                                         const float* __restrict__ rscale,
+                                                         const float* __restrict__ rshift) {
+  // mask != nullptr: also store act'(z) > 0 as one bit per element ([M][C/8] bytes), so the
+  // backward of a BN + residual + ReLU layer reads 1/16 of the residual's bytes for its mask.
+  // rscale != nullptr: the residual is itself a raw BN input (a projection shortcut's conv
+  // output) normalised on the fly, res * rscale + rshift -- its BN never writes an activation.
+  const RowTile t(C);
+  if (t.slot >= t.rpi) return;
+  float sc[8], sh[8], rsc[8], rsh[8];
+  load8(scale + t.c0, sc);
+  load8(shift + t.c0, sh);
+  if (RES && rscale) {
+    load8(rscale + t.c0, rsc);
+    load8(rshift + t.c0, rsh);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rsc[k] = 1.f, rsh[k] = 0.f;
+  }
+  bn_act_rows<ACT, RES>(t, blockIdx.x, gridDim.x, x, res, sc, sh, rsc, rsh, y, M, C, slope, nt, mask);
+}
+
+// ---------------------------------------------------------------------------
+// Local training-mode BN: statistics finalize + BN / act (+ residual) apply in ONE launch.  At small
+// batch every BN layer was two dependent launches of a few us each (bn_slab_finalize on one to 32
+// workgroups, then bn_act_fwd) -- pure launch latency.
+// Workgroups 0 .. nfin-1, dispatched first and waiting on nothing before they publish, merge the
+// statistics of 64 channels each with the code and order of bn_slab_finalize / bn_merge_finalize
+// (bit-identical coefficients), store scale / shift WRITE-THROUGH (agent-scope atomic stores: no
+// release fence, whose L2 write-back stalled the ticket reductions of round 3), drain their stores
+// and count themselves in sync[0].  Every workgroup waits for the nfin arrivals (bounded spin: a
+// timeout sets sync[2] and is reported by the host), reads its coefficients coherently and runs
+// bn_act_fwd's math as 4 virtual 256-thread workgroups; the last workgroup through resets sync[0..1]
+// for the next launch (stream-ordered: graph-replay safe).
+struct FinActParams {
+  const bf16* x;
+  const bf16* res;
+  const float* src;  // conv slabs [R][2][C] (partials == 0) or partials [P][3][C]
+  int nsrc, partials, M, C, nfin;
+  float eps, momentum, iabn_eps, slope;
+  const float* gamma;
+  const float* beta;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+  float* run_mean;
+  float* run_var;
+  float* rgamma;
+  bf16* y;
+  uint8_t* mask;
+  uint32_t* sync;  // [0] finalize arrivals, [1] workgroups through, [2] spin timeouts
+};
+
+template <int ACT, bool RES>
+__global__ void __launch_bounds__(1024) bn_fin_act_kernel(const FinActParams p) {
+  if ((int)blockIdx.x < p.nfin) {
+    const Welford m = p.partials ? merge_partials(p.src, p.nsrc, p.C, blockIdx.x)
+                                 : merge_slabs(p.src, p.nsrc, p.M, p.C, blockIdx.x);
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    if ((threadIdx.x >> 6) == 0 && c < p.C) {
+      Welford a{0.f, 0.f, 0.f};
+      a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
+      finalize_channel<true>(a, c, p.eps, p.gamma, p.beta, p.mean, p.invstd, p.scale, p.shift, p.run_mean,
+                             p.run_var, p.momentum, p.iabn_eps, p.rgamma);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(p.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    // one poller per workgroup, ~1 us apart: hundreds of workgroups hammering the counter's memory
+    // channel would slow the finalize workgroups' own slab loads
+    uint32_t spins = 0;
+    while (__hip_atomic_load(p.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)p.nfin) {
+      if (++spins > (1u << 22)) {
+        __hip_atomic_store(p.sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  __syncthreads();
+  // scale / shift staged once per workgroup: one coherent (sc1, past any stale L2 line of the reused
+  // allocation) 16-byte load per thread at most, then LDS reads -- per-thread coherent loads of
+  // 16 coefficients cost ~9 us per layer at batch 32
+  __shared__ f32x4 coef[2 * 2048 / 4];
+  {
+    const int n4 = p.C / 4;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.scale, (short)0, p.C * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(p.shift, (short)0, p.C * 4, 0x00020000);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+      coef[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, i * 16, 0, 16 /* sc1 */));
+      coef[n4 + i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, i * 16, 0, 16));
+    }
+  }
+  __syncthreads();
+  const RowTile t(p.C, threadIdx.x & 255);
+  float sc[8], sh[8], one[8], zero[8];
+  const float* cf = (const float*)coef;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = cf[t.c0 + k];
+    sh[k] = cf[p.C + t.c0 + k];
+    one[k] = 1.f;
+    zero[k] = 0.f;
+  }
+  if (threadIdx.x == 0) {
+    // every workgroup counted here has passed the wait: the last one re-arms the counters
+    const uint32_t done = __hip_atomic_fetch_add(p.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(p.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (t.slot >= t.rpi) return;
+  bn_act_rows<ACT, RES>(t, blockIdx.x * 4 + (threadIdx.x >> 8), gridDim.x * 4, p.x, p.res, sc, sh, one, zero, p.y,
+                        p.M, p.C, p.slope, 0, p.mask);
 }
 
 // sums over rows of dz = dy*act'(z) and dz*xhat -> per-workgroup partials out[blockIdx][2][C]
@@ -920,6 +1036,33 @@ void launch_bn_act_fwd(const bf16* x, const bf16* res, const float* scale, const
   DCP_ACT_RES_DISPATCH(bn_act_fwd_kernel, grid, 0, s, res, act, x, res, scale, shift, y, M, C, slope, g_tune[kBnActVariant],
                        mask, rscale, rshift);
 }
+
+void launch_bn_fin_act(const bf16* x, const bf16* res, const float* src, int nsrc, int partials, int M, int C,
+                       float eps, const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
+                       float* shift, float* rm, float* rv, float momentum, float iabn_eps, float* rgamma, bf16* y,
+                       uint8_t* mask, int act, float slope, uint32_t* sync, hipStream_t s) {
+  FinActParams p;
+  p.x = x; p.res = res; p.src = src; p.nsrc = nsrc; p.partials = partials; p.M = M; p.C = C;
+  p.nfin = (C + 63) / 64;
+  p.eps = eps; p.momentum = momentum; p.iabn_eps = iabn_eps; p.slope = slope;
+  p.gamma = gamma; p.beta = beta; p.mean = mean; p.invstd = invstd; p.scale = scale; p.shift = shift;
+  p.run_mean = rm; p.run_var = rv; p.rgamma = rgamma; p.y = y; p.mask = mask; p.sync = sync;
+  // the apply grid of bn_act_fwd in 1024-thread workgroups (4 virtual 256-thread ones each)
+  const int g = std::max(p.nfin, (int)((ew_grid(M, C).x + 3) / 4));
+  const dim3 grid(g);
+  if (act == ACT_RELU) {
+    if (res) hipLaunchKernelGGL((bn_fin_act_kernel<ACT_RELU, true>), grid, dim3(1024), 0, s, p);
+    else hipLaunchKernelGGL((bn_fin_act_kernel<ACT_RELU, false>), grid, dim3(1024), 0, s, p);
+  } else if (act == ACT_LEAKY) {
+    if (res) hipLaunchKernelGGL((bn_fin_act_kernel<ACT_LEAKY, true>), grid, dim3(1024), 0, s, p);
+    else hipLaunchKernelGGL((bn_fin_act_kernel<ACT_LEAKY, false>), grid, dim3(1024), 0, s, p);
+  } else {
+    if (res) hipLaunchKernelGGL((bn_fin_act_kernel<ACT_NONE, true>), grid, dim3(1024), 0, s, p);
+    else hipLaunchKernelGGL((bn_fin_act_kernel<ACT_NONE, false>), grid, dim3(1024), 0, s, p);
+  }
+}
+
+int bn_direct_slabs() { return kDirectSlabs; }
 
 // g_tune[kBnBwdCap] overrides the workgroup cap (A/B only: 256 and 1024 measured 0.5-1.2 % slower end to end
 // at b1024, profiles/r3/ew_rows_ab.txt)

@@ -249,6 +249,15 @@ void launch_cdr_threshold(const MTEntry* tab, const int2* chunks, int nchunks, u
 void launch_cdr_mask(const MTEntry* tab, const int2* chunks, int nchunks, const uint32_t* state, float clip,
                      hipStream_t s);
 
+// local training BN: statistics finalize (from conv slabs [R][2][C], R <= bn_direct_slabs(), or
+// partials [P][3][C]) + BN / act (+ residual, + mask bits) in one launch; sync: 3 zeroed uint32 counters
+// reserved for this stream (re-armed by every launch; sync[2] != 0 after a spin timeout)
+int bn_direct_slabs();
+void launch_bn_fin_act(const bf16* x, const bf16* res, const float* src, int nsrc, int partials, int M, int C,
+                       float eps, const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
+                       float* shift, float* rm, float* rv, float momentum, float iabn_eps, float* rgamma, bf16* y,
+                       uint8_t* mask, int act, float slope, uint32_t* sync, hipStream_t s);
+
 // direct 3x3 / s1 / p1 conv, 64 -> 64 channels (conv3x3.hip); part: [blocks][3][64] (n, mean, M2) or null
 bool conv3x3_c64_supported(int H, int W, int C, int Co);
 int conv3x3_c64_blocks(int N, int H, int W, int num_cu);

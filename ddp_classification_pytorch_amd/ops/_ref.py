@@ -317,6 +317,18 @@ def bn_act_mask(x, res, scale, shift, act, slope):
     return _act(z, act, slope).to(x.dtype), mask
 
 
+def bn_fin_act(x, slabs, res, gamma, beta, run_mean, run_var, momentum, eps, act, slope, want_mask, iabn_eps=-1.0,
+               rgamma_out=None):
+    """bn_stats_finalize + bn_act / bn_act_mask (the GPU op runs them as one launch)."""
+    mean, invstd, scale, shift = bn_stats_finalize(x, slabs if slabs.numel() else None, gamma, beta, run_mean, run_var,
+                                                   momentum, eps, iabn_eps, rgamma_out)
+    if want_mask:
+        y, mask = bn_act_mask(x, res, scale, shift, act, slope)
+    else:
+        y, mask = bn_act(x, res, scale, shift, act, slope), torch.empty(0, dtype=torch.uint8)
+    return y, mask, mean, invstd, scale, shift
+
+
 def bn2_act_mask(x, res, scale, shift, rscale, rshift, act, slope):
     return bn_act_mask(x, _f(res) * rscale + rshift, scale, shift, act, slope)
 

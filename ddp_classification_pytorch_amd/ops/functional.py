@@ -619,6 +619,16 @@ def set_syncbn_world1(enabled: bool):
     _SYNCBN_WORLD1[0] = bool(enabled)
 
 
+# local training BN: statistics finalize + apply in one launch (bn_fin_act, DCP_BN_FIN_ACT=1), bit-identical
+# to the two launches.  Opt-in: its in-kernel wait for the finalize workgroups measured slower than the
+# kernel boundary it replaces (R50 b32 graph 5,167 vs 5,273 img/s, profiles/r6/bn_fin_act_ab_s19_s20.txt)
+_FIN_ACT = [os.environ.get("DCP_BN_FIN_ACT", "0") == "1"]
+
+
+def set_bn_fin_act(enabled: bool):
+    _FIN_ACT[0] = bool(enabled)
+
+
 def _sync_group(group):
     """(group, world) for a BN's statistics: (None, 1) when there is nothing to synchronise."""
     if group is None:
@@ -647,17 +657,30 @@ class _BNAct(Function):
         k = K(x)
         C = x.shape[-1]
         count = x.numel() // C
-        if cfg.training_stats:
-            mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
-        else:
-            mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
+        # BN + residual + ReLU feeding a fused-backward conv: keep the ReLU mask as bits so that
+        # backward reads 1/16 of the residual's bytes for it
+        want_mask = src is not None and res is not None and cfg.act == 1
         mask = None
-        if src is not None and res is not None and cfg.act == 1:
-            # BN + residual + ReLU feeding a fused-backward conv: keep the ReLU mask as bits so
-            # that backward reads 1/16 of the residual's bytes for it
-            y, mask = k.bn_act_mask(x, res, scale, shift, cfg.act, cfg.slope)
+        if cfg.training_stats and cfg.group is None and _FIN_ACT[0]:
+            # local BN from the producing conv's statistics: finalize + apply as ONE launch (without
+            # slabs the op falls back to the statistics pass + apply)
+            ieps = -1.0 if cfg.iabn_eps is None else float(cfg.iabn_eps)
+            rg = cfg.rgamma if cfg.iabn_eps is not None else None
+            st = slabs if slabs is not None else x.new_empty(0, dtype=torch.float32)
+            y, mask, mean, invstd, scale, shift = k.bn_fin_act(x, st, res, gamma, beta, run_mean, run_var,
+                                                               cfg.momentum, cfg.eps, cfg.act, cfg.slope, want_mask,
+                                                               ieps, rg)
+            if not want_mask:
+                mask = None
         else:
-            y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
+            if cfg.training_stats:
+                mean, invstd, scale, shift, count = _bn_train_coeff(k, x, slabs, gamma, beta, run_mean, run_var, cfg)
+            else:
+                mean, invstd, scale, shift = k.bn_eval_coeff(gamma, beta, run_mean, run_var, cfg.eps)
+            if want_mask:
+                y, mask = k.bn_act_mask(x, res, scale, shift, cfg.act, cfg.slope)
+            else:
+                y = k.bn_act(x, res, scale, shift, cfg.act, cfg.slope)
         if cfg.iabn:
             # InplaceABN (mapillary inplace_abn, X3/K21): keep only the output.  The BN input x is
             # not saved (the consumer conv saves y anyway), so one activation per layer is freed;

@@ -402,3 +402,29 @@ def test_iabn_fold_matches_separate_gamma_launches(train):
     assert abs(l1 - l0) < 1e-6
     assert ((g1 - g0).norm() / g0.norm()).item() < 1e-6
     assert torch.allclose(r1, r0, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("model", ["resnet18", "tresnet_m"])
+def test_bn_fin_act_path_matches_two_launches(model):
+    """The one-launch BN finalize + apply wiring (DCP_BN_FIN_ACT=1, _BNAct.forward -> bn_fin_act) ==
+    the default two-op path on the CPU reference: loss, gradients, running statistics."""
+    out = []
+    for fused in (True, False):
+        Fn.set_bn_fin_act(fused)
+        try:
+            torch.manual_seed(5)
+            m = build_model(model, num_classes=10)
+            g = torch.Generator().manual_seed(2)
+            imgs = torch.rand(2, 3, 64, 64, generator=g)
+            labels = torch.randint(0, 10, (2,), generator=g)
+            from ddp_classification_pytorch_amd.models import input_layout
+            loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, nchw=True, **input_layout(m))), labels)
+            loss.backward()
+            rs = torch.cat([b.flatten() for n, b in m.named_buffers() if "running" in n])
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]), rs))
+        finally:
+            Fn.set_bn_fin_act(False)
+    (l1, g1, r1), (l0, g0, r0) = out
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    assert torch.equal(r1, r0)

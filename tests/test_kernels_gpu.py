@@ -1663,3 +1663,114 @@ def test_conv1x1_weight_stationary(K, shape, kernel):
     assert torch.equal(st[0, 0].cpu(), sr[0, 0])
     assert relerr(st[0, 1], sr[0, 1]) < 1e-4
     assert relerr(st[0, 2], sr[0, 2]) < 1e-4
+
+
+def _bn_two_launch(K, z, slabs, r, g, b, rm, rv, act, want_mask, ieps=-1.0, rgo=None):
+    mean, invstd, scale, shift = K.bn_stats_finalize(z, slabs, g, b, rm, rv, 0.1, 1e-5, ieps, rgo)
+    if want_mask:
+        y, mask = K.bn_act_mask(z, r, scale, shift, act, 0.01)
+    else:
+        y, mask = K.bn_act(z, r, scale, shift, act, 0.01), None
+    return y, mask, mean, invstd, scale, shift
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,act,res,want_mask,part", [
+    (2, 56, 64, 256, 1, True, True, False),      # 49 slabs, residual + mask bits
+    (32, 56, 64, 256, 1, False, False, False),   # 784 slabs (batch-32 layer1), 400+ workgroups
+    (4, 7, 256, 2048, 1, True, True, False),     # 2048 channels: 32 finalize workgroups
+    (2, 14, 64, 512, 2, False, False, False),    # leaky ReLU
+    (2, 14, 64, 128, 0, True, False, True),      # (n, mean, M2) partials instead of slabs
+    (1, 3, 64, 24, 1, False, False, False),      # 9 rows, 24 channels (3-chunk rows)
+])
+def test_bn_fin_act_matches_two_launches(K, N, H, Ci, Co, act, res, want_mask, part):
+    """bn_fin_act (finalize + BN/act in ONE launch, workgroups synchronised through write-through
+    coefficients and counters) == bn_stats_finalize followed by bn_act / bn_act_mask, bit for bit,
+    running statistics included; no spin timeout."""
+    torch.manual_seed(N * 1000 + Co)
+    x = rnd(N, H, H, Ci).to(DEV)
+    w = rnd(Co, 1, 1, Ci, scale=0.1).to(DEV)
+    z, slabs = K.conv_fwd(x, w, 1, 0, True)
+    if part:
+        slabs = K.bn_stats(z, slabs)
+    r = rnd(*z.shape).to(DEV) if res else None
+    g = torch.randn(Co, device=DEV)
+    b = torch.randn(Co, device=DEV) * 0.1
+    rm0, rv0 = torch.randn(Co, device=DEV), torch.rand(Co, device=DEV) + 0.5
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    got = K.bn_fin_act(z, slabs, r, g, b, rm0, rv0, 0.1, 1e-5, act, 0.01, want_mask)
+    ref = _bn_two_launch(K, z, slabs, r, g, b, rm1, rv1, act, want_mask)
+    for name, a, c in zip(("y", "mask", "mean", "invstd", "scale", "shift"), got, ref):
+        if c is None:
+            assert a.numel() == 0, name
+        else:
+            assert torch.equal(a, c), name
+    assert torch.equal(rm0, rm1) and torch.equal(rv0, rv1)
+    assert K.bn_fin_act_timeouts(z) == 0
+
+
+def test_bn_fin_act_iabn_and_graph_replay(K):
+    """The fused BN with InplaceABN's folded weight (|g| + eps, 1 / it written), and the same launch
+    captured in a HIP graph and replayed: every replay re-arms the counters and reproduces the
+    eager outputs (the running statistics advance once per replay, like the eager chain)."""
+    torch.manual_seed(5)
+    C = 512
+    x = rnd(8, 14, 14, 64).to(DEV)
+    w = rnd(C, 1, 1, 64, scale=0.1).to(DEV)
+    z, slabs = K.conv_fwd(x, w, 1, 0, True)
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV) * 0.1
+    rg0, rg1 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    rm0, rv0 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    got = K.bn_fin_act(z, slabs, None, g, b, rm0, rv0, 0.1, 1e-5, 2, 0.01, False, 1e-5, rg0)
+    ref = _bn_two_launch(K, z, slabs, None, g, b, rm1, rv1, 2, False, 1e-5, rg1)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[4]) and torch.equal(rg0, rg1)
+    assert torch.equal(rm0, rm1) and torch.equal(rv0, rv1)
+
+    rmg, rvg = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    K.bn_fin_act(z, slabs, None, g, b, rmg.clone(), rvg.clone(), 0.1, 1e-5, 1, 0.01, True)  # warm-up
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = K.bn_fin_act(z, slabs, None, g, b, rmg, rvg, 0.1, 1e-5, 1, 0.01, True)
+    rme, rve = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    for _ in range(5):
+        graph.replay()
+        eager = K.bn_fin_act(z, slabs, None, g, b, rme, rve, 0.1, 1e-5, 1, 0.01, True)
+        torch.cuda.synchronize()
+        for a, c in zip(out, eager):
+            assert torch.equal(a, c)
+        assert torch.equal(rmg, rme) and torch.equal(rvg, rve)
+    assert K.bn_fin_act_timeouts(z) == 0
+
+
+@pytest.mark.parametrize("model", ["resnet50", "tresnet_m"])
+def test_model_bn_fin_act_matches_two_launches_gpu(model):
+    """A training step with the one-launch BN finalize + apply (DCP_BN_FIN_ACT=1) == the two-launch
+    default, bit for bit: loss, every gradient, running statistics (ResNet-50: ReLU + residual masks;
+    TResNet-M: InplaceABN leaky BNs with the folded weight)."""
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    out = []
+    for fused in (True, False):
+        Fn.set_bn_fin_act(fused)
+        try:
+            torch.manual_seed(11)
+            m = build_model(model, num_classes=10).to(DEV)
+            gen = torch.Generator().manual_seed(4)
+            imgs = torch.randint(0, 256, (4, 3, 64, 64), dtype=torch.uint8, generator=gen).to(DEV)
+            labels = torch.randint(0, 10, (4,), generator=gen).to(DEV)
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), in_scale=1 / 255.0, **input_layout(m))
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            rs = torch.cat([b.flatten() for n, b in m.named_buffers() if "running" in n]).cpu()
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]).cpu(),
+                        rs))
+        finally:
+            Fn.set_bn_fin_act(False)
+    (l1, g1, r1), (l0, g0, r0) = out
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    assert torch.equal(r1, r0)
