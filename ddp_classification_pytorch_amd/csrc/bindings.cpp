@@ -1597,6 +1597,51 @@ std::tuple<Tensor, Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor
   return {dx, dg, dres};
 }
 
+// squeeze-excitation gate of a small batch (one workgroup): p [N,C] -> (h [N,R], g [N,C]);
+// w1 [>=R, C], w2 [>=C, R] bf16 (the prepared weights, rows past R / C unused)
+std::tuple<Tensor, Tensor> se_gate_fwd(const Tensor& p, const Tensor& w1, const optional<Tensor>& b1, const Tensor& w2,
+                                       const optional<Tensor>& b2, int64_t R) {
+  CHECK_ACT(p);
+  CHECK_ACT(w1);
+  CHECK_ACT(w2);
+  TORCH_CHECK(p.dim() == 2, "se_gate_fwd: p [N,C]");
+  const int N = p.size(0), C = p.size(1);
+  TORCH_CHECK(dcp::se_gate_supported(N, C, (int)R) && w1.dim() == 2 && w1.size(0) >= R && w1.size(1) == C &&
+                  w2.dim() == 2 && w2.size(0) >= C && w2.size(1) == R,
+              "se_gate_fwd shapes");
+  TORCH_CHECK((!b1.has_value() || b1->numel() >= R) && (!b2.has_value() || b2->numel() >= C), "se_gate_fwd bias");
+  auto h = at::empty({N, R}, p.options());
+  auto g = at::empty({N, C}, p.options());
+  dcp::launch_se_gate_fwd(bp(p), bp(w1), fp(b1), bp(w2), fp(b2), bpm(h), bpm(g), N, C, (int)R, cur_stream());
+  return {h, g};
+}
+
+// w1t = W1^T [C, >=R], w2t = W2^T [R, >=C] (the transposed prepared weights)
+// -> (dp [N,C] bf16, dW1 [R,C], db1 [R], dW2 [C,R], db2 [C] fp32)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> se_gate_bwd(const Tensor& dg, const Tensor& g, const Tensor& h,
+                                                               const Tensor& p, const Tensor& w1t, const Tensor& w2t) {
+  CHECK_ACT(dg);
+  CHECK_ACT(g);
+  CHECK_ACT(h);
+  CHECK_ACT(p);
+  CHECK_ACT(w1t);
+  CHECK_ACT(w2t);
+  const int N = p.size(0), C = p.size(1), R = h.size(1);
+  TORCH_CHECK(dcp::se_gate_supported(N, C, R) && dg.sizes() == p.sizes() && g.sizes() == p.sizes() && h.size(0) == N &&
+                  w1t.dim() == 2 && w1t.size(0) == C && w1t.size(1) >= R && w2t.dim() == 2 && w2t.size(0) == R &&
+                  w2t.size(1) >= C,
+              "se_gate_bwd shapes");
+  auto dp = at::empty_like(p);
+  auto dw1 = at::empty({R, C}, f32_like(p));
+  auto db1 = at::empty({R}, f32_like(p));
+  auto dw2 = at::empty({C, R}, f32_like(p));
+  auto db2 = at::empty({C}, f32_like(p));
+  dcp::launch_se_gate_bwd(bp(dg), bp(g), bp(h), bp(p), bp(w1t), (int)w1t.size(1), bp(w2t), (int)w2t.size(1),
+                          dw1.data_ptr<float>(), db1.data_ptr<float>(), dw2.data_ptr<float>(), db2.data_ptr<float>(),
+                          bpm(dp), N, C, R, cur_stream());
+  return {dp, dw1, db1, dw2, db2};
+}
+
 // ---------------------------------------------------------------------------
 // losses
 // ---------------------------------------------------------------------------
@@ -2046,6 +2091,10 @@ TORCH_LIBRARY(dcp, m) {
   m.def("dwconv_fwd(Tensor x, Tensor filt, int k, int s, int p, bool reflect) -> Tensor", &dwconv_fwd);
   m.def("dwconv_bwd(Tensor dy, Tensor filt, int H, int W, int k, int s, int p, bool reflect) -> Tensor", &dwconv_bwd);
   m.def("chan_scale_fwd(Tensor x, Tensor g, Tensor? res, bool relu) -> Tensor", &chan_scale_fwd);
+  m.def("se_gate_fwd(Tensor p, Tensor w1, Tensor? b1, Tensor w2, Tensor? b2, int R) -> (Tensor, Tensor)", &se_gate_fwd);
+  m.def("se_gate_bwd(Tensor dg, Tensor g, Tensor h, Tensor p, Tensor w1t, Tensor w2t) -> (Tensor, Tensor, Tensor, Tensor, "
+        "Tensor)",
+        &se_gate_bwd);
   m.def("chan_scale_bwd(Tensor dy, Tensor x, Tensor g, Tensor? res, bool relu, bool want_dres) -> (Tensor, Tensor, "
         "Tensor)",
         &chan_scale_bwd);

@@ -1066,7 +1066,14 @@ int bn_direct_slabs() { return kDirectSlabs; }
 
 // g_tune[kBnBwdCap] overrides the workgroup cap (A/B only: 256 and 1024 measured 0.5-1.2 % slower end to end
 // at b1024, profiles/r3/ew_rows_ab.txt)
-int bn_bwd_reduce_blocks(int M, int C) { return rows_grid(M, C, 32, g_tune[kBnBwdCap] > 0 ? g_tune[kBnBwdCap] : 512); }
+// 32 rows per thread where the cap binds (large activations); smaller ones spread over up to the cap's
+// workgroups at >= 4 rows per thread: at batch 16 a TResNet-M layer's reduction ran as ~49 workgroups of
+// 32 serial rows, 20 us of latency for a few MB (36 such layers per step)
+int bn_bwd_reduce_blocks(int M, int C) {
+  const int cap = g_tune[kBnBwdCap] > 0 ? g_tune[kBnBwdCap] : 512;
+  const int g = rows_grid(M, C, 32, cap);
+  return g < cap ? rows_grid(M, C, 4, cap) : g;
+}
 
 // partials must hold bn_bwd_reduce_blocks(M, C) x 2 x C floats; out [2][C]
 void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,

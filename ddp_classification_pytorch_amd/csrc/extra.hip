@@ -385,4 +385,184 @@ void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const b
   launch_partial_sum(part, S, N * C, dg, st);
 }
 
+// ---------------------------------------------------------------------------
+// Squeeze-excitation gate of a SMALL batch, one workgroup per direction, every product on MFMA
+// (TResNet-M at the reference's batch 16: 18 gates per step, each a [N, C] x [C, R] and a [N, R] x [R, C]
+// product with N = 16, C <= 256, R <= 128, that ran as two GEMM launches forward and ~10 small launches
+// backward: sigmoid' and ReLU' passes, two data-gradient GEMMs, two weight-gradient GEMMs + reductions,
+// two bias column sums).  The roundings follow that chain: h, g, d2 = dg g (1 - g), dh (then
+// d1 = dh [h > 0]) and dp are bf16; weight and bias gradients fp32.
+//   forward : h = relu(p W1^T + b1), g = sigmoid(h W2^T + b2)        (p [N,C], W1 [R,C], W2 [C,R])
+//   backward: dW2 = d2^T h, db2 = sum_n d2, dh = d2 W2, d1 = dh [h > 0],
+//             dW1 = d1^T p, db1 = sum_n d1, dp = d1 W1
+// Batch rows are padded to 32 in LDS (zero rows): the n-sums of the weight gradients are one 32-deep
+// MFMA k-step.  16 waves take the 16 x 16 output tiles round-robin.
+// v_mfma_f32_16x16x32_bf16 operands: A lane l = row (l & 15), k 8 (l >> 4) .. + 7; B the same with
+// column (l & 15); D lane l = column (l & 15), rows 4 (l >> 4) .. + 3.
+constexpr int kSeN = 32, kSeMaxC = 256, kSeMaxR = 128;
+
+bool se_gate_supported(int N, int C, int R) {
+  return N >= 1 && N <= kSeN && C % 32 == 0 && R % 32 == 0 && C <= kSeMaxC && R <= kSeMaxR;
+}
+
+namespace {
+// D (16 x 16) += A[m0 .. m0+15][0 .. K) x B[n0 .. n0+15][0 .. K)^T, both k-contiguous rows (LDS or global)
+__device__ __forceinline__ f32x4 se_mma(const bf16* A, int lda, const bf16* B, int ldb, int K, int lane) {
+  const int r = lane & 15, kq = 8 * (lane >> 4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < K; k += 32) {
+    const bf16x8 a = *(const bf16x8*)(A + r * lda + k + kq);
+    const bf16x8 b = *(const bf16x8*)(B + r * ldb + k + kq);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+}  // namespace
+
+__global__ void __launch_bounds__(1024) se_gate_fwd_kernel(const bf16* __restrict__ p, const bf16* __restrict__ w1,
+                                                          const float* __restrict__ b1, const bf16* __restrict__ w2,
+                                                          const float* __restrict__ b2, bf16* __restrict__ h,
+                                                          bf16* __restrict__ g, int N, int C, int R) {
+  constexpr int LP = kSeMaxC + 8, LH = kSeMaxR + 8;  // row pitches (16-byte skew)
+  __shared__ __attribute__((aligned(16))) bf16 sp[kSeN * LP];
+  __shared__ __attribute__((aligned(16))) bf16 sh[kSeN * LH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = (N + 15) / 16;
+  for (int i = tid; i < 16 * nb * (C / 8); i += blockDim.x) {
+    const int n = i / (C / 8), c = (i - n * (C / 8)) * 8;
+    *(bf16x8*)(sp + n * LP + c) = n < N ? *(const bf16x8*)(p + (size_t)n * C + c) : bf16x8{};
+  }
+  __syncthreads();
+  // h^T tiles: D[r][n] = W1[r][:] . p[n][:]
+  for (int t = wave; t < (R / 16) * nb; t += 16) {
+    const int rt = t % (R / 16), nt = t / (R / 16);
+    const f32x4 acc = se_mma(w1 + (size_t)rt * 16 * C, C, sp + nt * 16 * LP, LP, C, lane);
+    const int n = nt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rt * 16 + 4 * (lane >> 4) + q;
+      const bf16 hb = f2bf(fmaxf(acc[q] + (b1 ? b1[r] : 0.f), 0.f));
+      sh[n * LH + r] = hb;
+      if (n < N) h[(size_t)n * R + r] = hb;
+    }
+  }
+  __syncthreads();
+  // g^T tiles: D[c][n] = W2[c][:] . h[n][:]
+  for (int t = wave; t < (C / 16) * nb; t += 16) {
+    const int ct = t % (C / 16), nt = t / (C / 16);
+    const f32x4 acc = se_mma(w2 + (size_t)ct * 16 * R, R, sh + nt * 16 * LH, LH, R, lane);
+    const int n = nt * 16 + (lane & 15);
+    if (n < N)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = ct * 16 + 4 * (lane >> 4) + q;
+        g[(size_t)n * C + c] = f2bf(1.f / (1.f + __expf(-(acc[q] + (b2 ? b2[c] : 0.f)))));
+      }
+  }
+}
+
+// w1t = W1^T [C][ld1t], w2t = W2^T [R][ld2t] (the transposed prepared weights)
+__global__ void __launch_bounds__(1024) se_gate_bwd_kernel(const bf16* __restrict__ dg, const bf16* __restrict__ g,
+                                                          const bf16* __restrict__ h, const bf16* __restrict__ p,
+                                                          const bf16* __restrict__ w1t, int ld1t,
+                                                          const bf16* __restrict__ w2t, int ld2t,
+                                                          float* __restrict__ dw1, float* __restrict__ db1,
+                                                          float* __restrict__ dw2, float* __restrict__ db2,
+                                                          bf16* __restrict__ dp, int N, int C, int R) {
+  constexpr int LC = kSeMaxC + 8, LR = kSeMaxR + 8, LN = kSeN + 8;
+  __shared__ __attribute__((aligned(16))) bf16 sd2[kSeN * LC];    // d2 [n][c]
+  __shared__ __attribute__((aligned(16))) bf16 sd2t[kSeMaxC * LN];  // d2^T [c][n]
+  __shared__ __attribute__((aligned(16))) bf16 spt[kSeMaxC * LN];   // p^T [c][n]
+  __shared__ __attribute__((aligned(16))) bf16 sht[kSeMaxR * LN];   // h^T [r][n]
+  __shared__ __attribute__((aligned(16))) bf16 sd1[kSeN * LR];    // d1 [n][r]
+  __shared__ __attribute__((aligned(16))) bf16 sd1t[kSeMaxR * LN];  // d1^T [r][n]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = (N + 15) / 16;
+  for (int i = tid; i < kSeN * C; i += blockDim.x) {
+    const int n = i / C, c = i - n * C;
+    bf16 d = f2bf(0.f), pv = f2bf(0.f);
+    if (n < N) {
+      const float gv = bf2f(g[(size_t)n * C + c]);
+      d = f2bf(bf2f(dg[(size_t)n * C + c]) * gv * (1.f - gv));
+      pv = p[(size_t)n * C + c];
+    }
+    sd2[n * LC + c] = d;
+    sd2t[c * LN + n] = d;
+    spt[c * LN + n] = pv;
+  }
+  for (int i = tid; i < kSeN * R; i += blockDim.x) {
+    const int n = i / R, r = i - n * R;
+    sht[r * LN + n] = n < N ? h[(size_t)n * R + r] : f2bf(0.f);
+  }
+  __syncthreads();
+  // dW2 [c][r] = sum_n d2^T[c][n] h^T[r][n]: one 32-deep k-step per tile
+  for (int t = wave; t < (C / 16) * (R / 16); t += 16) {
+    const int ct = t / (R / 16), rt = t - ct * (R / 16);
+    const f32x4 acc = se_mma(sd2t + ct * 16 * LN, LN, sht + rt * 16 * LN, LN, kSeN, lane);
+    const int r = rt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dw2[(size_t)(ct * 16 + 4 * (lane >> 4) + q) * R + r] = acc[q];
+  }
+  for (int c = tid; c < C; c += blockDim.x) {
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a += bf2f(sd2t[c * LN + n]);
+    db2[c] = a;
+  }
+  // dh [n][r] = d2[n][:] . W2^T[r][:] -> d1 = bf16(dh) [h > 0]
+  for (int t = wave; t < nb * (R / 16); t += 16) {
+    const int nt = t / (R / 16), rt = t - nt * (R / 16);
+    const f32x4 acc = se_mma(sd2 + nt * 16 * LC, LC, w2t + (size_t)rt * 16 * ld2t, ld2t, C, lane);
+    const int r = rt * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = nt * 16 + 4 * (lane >> 4) + q;
+      const bf16 d = (n < N && bf2f(sht[r * LN + n]) > 0.f) ? f2bf(acc[q]) : f2bf(0.f);
+      sd1[n * LR + r] = d;
+      sd1t[r * LN + n] = d;
+    }
+  }
+  // rows n in [16 nb, 32) of d1^T: zero (the dW1 k-step reads all 32)
+  for (int i = tid; i < (kSeN - 16 * nb) * R; i += blockDim.x) {
+    const int n = 16 * nb + i / R, r = i % R;
+    sd1t[r * LN + n] = f2bf(0.f);
+  }
+  __syncthreads();
+  // dW1 [r][c] = sum_n d1^T[r][n] p^T[c][n]
+  for (int t = wave; t < (R / 16) * (C / 16); t += 16) {
+    const int rt = t / (C / 16), ct = t - rt * (C / 16);
+    const f32x4 acc = se_mma(sd1t + rt * 16 * LN, LN, spt + ct * 16 * LN, LN, kSeN, lane);
+    const int c = ct * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dw1[(size_t)(rt * 16 + 4 * (lane >> 4) + q) * C + c] = acc[q];
+  }
+  for (int r = tid; r < R; r += blockDim.x) {
+    float a = 0.f;
+    for (int n = 0; n < N; ++n) a += bf2f(sd1t[r * LN + n]);
+    db1[r] = a;
+  }
+  // dp [n][c] = d1[n][:] . W1^T[c][:]
+  for (int t = wave; t < nb * (C / 16); t += 16) {
+    const int nt = t / (C / 16), ct = t - nt * (C / 16);
+    const f32x4 acc = se_mma(sd1 + nt * 16 * LR, LR, w1t + (size_t)ct * 16 * ld1t, ld1t, R, lane);
+    const int c = ct * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = nt * 16 + 4 * (lane >> 4) + q;
+      if (n < N) dp[(size_t)n * C + c] = f2bf(acc[q]);
+    }
+  }
+}
+
+void launch_se_gate_fwd(const bf16* p, const bf16* w1, const float* b1, const bf16* w2, const float* b2, bf16* h,
+                        bf16* g, int N, int C, int R, hipStream_t st) {
+  hipLaunchKernelGGL(se_gate_fwd_kernel, dim3(1), dim3(1024), 0, st, p, w1, b1, w2, b2, h, g, N, C, R);
+}
+
+void launch_se_gate_bwd(const bf16* dg, const bf16* g, const bf16* h, const bf16* p, const bf16* w1t, int ld1t,
+                        const bf16* w2t, int ld2t, float* dw1, float* db1, float* dw2, float* db2, bf16* dp, int N,
+                        int C, int R, hipStream_t st) {
+  hipLaunchKernelGGL(se_gate_bwd_kernel, dim3(1), dim3(1024), 0, st, dg, g, h, p, w1t, ld1t, w2t, ld2t, dw1, db1, dw2,
+                     db2, dp, N, C, R);
+}
+
 }  // namespace dcp

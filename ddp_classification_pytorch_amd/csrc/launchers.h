@@ -338,6 +338,14 @@ void launch_dwconv_bwd(const bf16* dy, const float* w, bf16* dx, int N, int H, i
                        int s, int p, int reflect, hipStream_t st);
 void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* y, int N, int HW, int C, int relu,
                            hipStream_t st);
+// squeeze-excitation gate of a small batch, one MFMA workgroup per direction (extra.hip): p [N,C],
+// W1 [>=R rows, C], W2 [>=C rows, R] bf16 forward; their transposes W1^T [C][ld1t], W2^T [R][ld2t] backward
+bool se_gate_supported(int N, int C, int R);
+void launch_se_gate_fwd(const bf16* p, const bf16* w1, const float* b1, const bf16* w2, const float* b2, bf16* h,
+                        bf16* g, int N, int C, int R, hipStream_t st);
+void launch_se_gate_bwd(const bf16* dg, const bf16* g, const bf16* h, const bf16* p, const bf16* w1t, int ld1t,
+                        const bf16* w2t, int ld2t, float* dw1, float* db1, float* dw2, float* db2, bf16* dp, int N,
+                        int C, int R, hipStream_t st);
 void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg, float* part,
                            bf16* dres, int N, int HW, int C, int relu, hipStream_t st);
 

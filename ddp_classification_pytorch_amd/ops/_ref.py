@@ -719,3 +719,31 @@ def s2d_weight_bwd(g16, C):
     g8 = g16.float().reshape(Co, 4, 4, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Co, 8, 8, 4)
     return g8[:, 1:, 1:, :C].contiguous()
 
+
+
+def se_gate_fwd(p, w1, b1, w2, b2, R):
+    """Squeeze-excitation gate h = relu(p W1^T + b1), g = sigmoid(h W2^T + b2) with the unfused chain's
+    bf16 roundings (h and g)."""
+    C = p.shape[1]
+    a = _f(p) @ _f(w1[:R]).t()
+    if b1 is not None:
+        a = a + _f(b1)[:R]
+    h = torch.relu(a).to(p.dtype)
+    z = _f(h) @ _f(w2[:C]).t()
+    if b2 is not None:
+        z = z + _f(b2)[:C]
+    return h, torch.sigmoid(z).to(p.dtype)
+
+
+def se_gate_bwd(dg, g, h, p, w1t, w2t):
+    """w1t = W1^T [C, >=R], w2t = W2^T [R, >=C] (the transposed prepared weights)."""
+    C, R = p.shape[1], h.shape[1]
+    d2 = (_f(dg) * _f(g) * (1 - _f(g))).to(p.dtype)
+    dw2 = _f(d2).t() @ _f(h)
+    db2 = _f(d2).sum(0)
+    dh = (_f(d2) @ _f(w2t[:, :C]).t()).to(p.dtype)
+    d1 = torch.where(h > 0, dh, torch.zeros_like(dh))
+    dw1 = _f(d1).t() @ _f(p)
+    db1 = _f(d1).sum(0)
+    dp = (_f(d1) @ _f(w1t[:, :R]).t()).to(p.dtype)
+    return dp, dw1, db1, dw2, db2

@@ -1426,6 +1426,50 @@ class _ChanScale(Function):
         return dx, dg.to(g.dtype), dres, None, None, None
 
 
+# squeeze-excitation gate of a small batch as one kernel per direction (se_gate_fwd / se_gate_bwd);
+# DCP_SE_FUSED=0 keeps the GEMM chain (two GEMMs forward, ~10 small launches backward)
+_SE_FUSED = [os.environ.get("DCP_SE_FUSED", "1") != "0"]
+_SE_MAX_N, _SE_MAX_C, _SE_MAX_R = 32, 256, 128  # csrc/extra.hip kSeN / kSeMaxC / kSeMaxR
+
+
+def set_se_fused(enabled: bool):
+    _SE_FUSED[0] = bool(enabled)
+
+
+class _SEGate(Function):
+    @staticmethod
+    def forward(ctx, p, w1, b1, w2, b2, w1b, w1t, w2b, w2t):
+        h, g = K(p).se_gate_fwd(p, w1b, b1, w2b, b2, w1.shape[0])
+        ctx.save_for_backward(p, h, g, w1t, w2t)
+        ctx.has_b = (b1 is not None, b2 is not None)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        p, h, g, w1t, w2t = ctx.saved_tensors
+        dp, dw1, db1, dw2, db2 = K(dg).se_gate_bwd(dg.contiguous(), g, h, p, w1t, w2t)
+        return (dp, dw1, db1 if ctx.has_b[0] else None, dw2, db2 if ctx.has_b[1] else None, None, None, None, None)
+
+
+def se_gate_fusable(p, w1, w2) -> bool:
+    if not _SE_FUSED[0] or p.dim() != 2:
+        return False
+    N, C = p.shape
+    R = w1.shape[0]
+    return (tuple(w1.shape) == (R, C) and tuple(w2.shape) == (C, R) and C % 32 == 0 and R % 32 == 0
+            and N <= _SE_MAX_N and C <= _SE_MAX_C and R <= _SE_MAX_R)
+
+
+def se_gate(p, w1, b1, w2, b2):
+    """sigmoid(relu(p W1^T + b1) W2^T + b2) for pooled features p [N, C] (a squeeze-excitation gate,
+    TResNet-M's SE blocks, timm ``SEModule``): one kernel forward, one backward, the GEMM chain's bf16
+    roundings.  Callers check :func:`se_gate_fusable` (small N: one workgroup)."""
+    R, C = w1.shape
+    w1b, w1t = prepared_weight(w1, round_up(R, 64) if p.is_cuda else 0, True)
+    w2b, w2t = prepared_weight(w2, round_up(C, 64) if p.is_cuda else 0, True)
+    return _SEGate.apply(p.contiguous(), w1, b1, w2, b2, w1b, w1t, w2b, w2t)
+
+
 def channel_scale(x, g, residual=None, relu=False, link: "GradJoin | None" = None,
                   deposit: "GradJoin | None" = None):
     """act(x[n,h,w,c] * g[n,c] (+ residual)) — squeeze-and-excitation apply fused

@@ -428,3 +428,36 @@ def test_bn_fin_act_path_matches_two_launches(model):
     assert l1 == l0
     assert torch.equal(g1, g0)
     assert torch.equal(r1, r0)
+
+
+def test_se_gate_fused_matches_gemm_chain():
+    """TResNet-M's squeeze-excitation gates as one fused op per direction (Fn.se_gate) == the
+    Linear / GEMM chain on the CPU reference: loss and every gradient; the fused op really runs."""
+    from ddp_classification_pytorch_amd.models import input_layout
+    calls = [0]
+    orig = _ref.se_gate_fwd
+
+    def counting(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+
+    out = []
+    _ref.se_gate_fwd = counting
+    try:
+        for fused in (True, False):
+            Fn.set_se_fused(fused)
+            torch.manual_seed(5)
+            m = build_model("tresnet_m", num_classes=10)
+            g = torch.Generator().manual_seed(2)
+            imgs = torch.rand(2, 3, 64, 64, generator=g)
+            labels = torch.randint(0, 10, (2,), generator=g)
+            loss = Fn.cross_entropy(m(Fn.to_device_nhwc(imgs, nchw=True, **input_layout(m))), labels)
+            loss.backward()
+            out.append((loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None])))
+    finally:
+        _ref.se_gate_fwd = orig
+        Fn.set_se_fused(True)
+    assert calls[0] > 0
+    (l1, g1), (l0, g0) = out
+    assert abs(l1 - l0) < 1e-6
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-6

@@ -1774,3 +1774,65 @@ def test_model_bn_fin_act_matches_two_launches_gpu(model):
     assert l1 == l0
     assert torch.equal(g1, g0)
     assert torch.equal(r1, r0)
+
+
+@pytest.mark.parametrize("N,C,R,bias", [(16, 64, 64, True), (16, 128, 64, True), (16, 256, 128, True),
+                                        (32, 256, 128, False), (3, 96, 32, True), (20, 64, 128, True)])
+def test_se_gate_kernels_vs_fp32_reference(K, N, C, R, bias):
+    """The one-workgroup squeeze-excitation gate (forward: relu(p W1^T + b1) -> sigmoid(. W2^T + b2);
+    backward: every weight / bias gradient and dp) against the fp32 reference of the same op with the
+    same bf16 rounding points."""
+    torch.manual_seed(N + C + R)
+    p = rnd(N, C).to(DEV)
+    w1, w2 = rnd(R, C, scale=0.2).to(DEV), rnd(C, R, scale=0.2).to(DEV)
+    b1 = (torch.randn(R) * 0.1).to(DEV) if bias else None
+    b2 = (torch.randn(C) * 0.1).to(DEV) if bias else None
+    h, g = K.se_gate_fwd(p, w1, b1, w2, b2, R)
+    rh, rg = _ref.se_gate_fwd(p.cpu(), w1.cpu(), None if b1 is None else b1.cpu(), w2.cpu(),
+                              None if b2 is None else b2.cpu(), R)
+    assert relerr(h, rh) < 1e-2 and relerr(g, rg) < 1e-2
+    dg = rnd(N, C).to(DEV)
+    w1t, w2t = w1.t().contiguous(), w2.t().contiguous()
+    got = K.se_gate_bwd(dg, g, h, p, w1t, w2t)
+    ref = _ref.se_gate_bwd(dg.cpu(), g.cpu(), h.cpu(), p.cpu(), w1t.cpu(), w2t.cpu())
+    for name, a, b in zip(("dp", "dw1", "db1", "dw2", "db2"), got, ref):
+        assert a.shape == b.shape, name
+        assert relerr(a, b) < 2e-2, (name, relerr(a, b))
+
+
+def test_tresnet_se_gate_fused_matches_gemm_chain_gpu():
+    """TResNet-M training step on the GPU with the fused squeeze-excitation gates (default at small
+    batch) vs the GEMM chain: loss and gradients agree to bf16 summation-order rounding."""
+    from ddp_classification_pytorch_amd.models import build_model, input_layout
+    from ddp_classification_pytorch_amd.ops import functional as Fn
+
+    out = []
+    for fused in (True, False):
+        Fn.set_se_fused(fused)
+        try:
+            torch.manual_seed(7)
+            m = build_model("tresnet_m", num_classes=10).to(DEV)
+            with torch.no_grad():  # the zero-initialised last BN of each block would zero every SE gradient
+                for mod in m.modules():
+                    w = getattr(mod, "weight", None)
+                    if "BatchNorm" in type(mod).__name__ and w is not None and not bool(w.any()):
+                        w.fill_(0.5)
+            gen = torch.Generator().manual_seed(3)
+            imgs = torch.randint(0, 256, (4, 3, 64, 64), dtype=torch.uint8, generator=gen).to(DEV)
+            labels = torch.randint(0, 10, (4,), generator=gen).to(DEV)
+            x = Fn.to_device_nhwc(imgs, (0.5, 0.5, 0.5), (0.25, 0.25, 0.25), in_scale=1 / 255.0, **input_layout(m))
+            loss = Fn.cross_entropy(m(x), labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((loss.item(), {n: q.grad.float().cpu() for n, q in m.named_parameters() if q.grad is not None}))
+        finally:
+            Fn.set_se_fused(True)
+    (l1, g1), (l0, g0) = out
+    assert abs(l1 - l0) < 2e-2 * max(1.0, abs(l0))
+    tot1 = torch.cat([g1[k].flatten() for k in g0])
+    tot0 = torch.cat([g0[k].flatten() for k in g0])
+    assert ((tot1 - tot0).norm() / tot0.norm()).item() < 5e-2
+    se = [k for k in g0 if ".se." in k]
+    assert se and any(g0[k].abs().sum() > 0 for k in se)
+    for k in se:
+        assert relerr(g1[k], g0[k]) < 0.1, k
