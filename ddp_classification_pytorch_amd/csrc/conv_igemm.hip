@@ -97,6 +97,13 @@ struct TapGemmParams {
   uint32_t* sk_flags;
   int sk_on;  // host side: stream-K requested for this launch (launch_big allocates sk_ws / sk_flags)
   int sk_unit;  // stream-K range granularity in k-steps (divides nkt)
+  // 128-row kernel split-K (short grids with deep k-loops: small batches).  kmode 1: workgroup
+  // (x, y) runs k-tiles [nkt y / ksplit, nkt (y+1) / ksplit) of tile x and stores its raw fp32
+  // accumulators to kp; kmode 2: workgroup x sums tile x's ksplit slices in slice order and runs the
+  // epilogue (every EPI) on them.  0: off.
+  // slices are cut in 64-deep k units (k64 of them), so every tile width / k depth sums the same slices
+  f32x4* kp;
+  int ksplit, kmode, k64;
 };
 
 __device__ __forceinline__ int tap_dy(int v) { return (int)(int8_t)(v & 0xff); }
@@ -340,7 +347,7 @@ __device__ __forceinline__ void tg_image_store(const TapGemmParams& p, char* E, 
 // the raw s_barrier, drained by a counted vmcnt -- for deep-K shapes at one block per CU.
 // three waves per SIMD: the fused BN-backward epilogue otherwise lands one register past the
 // 168-register step and halves to two workgroups per CU
-template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64, bool PRO = false>
+template <int BN, int EPI, bool FAST, int NS = 2, int BK = 64, bool PRO = false, bool KS = false>
 __global__ void __launch_bounds__(256, 3)
 tap_gemm_kernel(const TapGemmParams p) {
   static_assert(NS == 2 || FAST, "the LDS ring needs the one-tap-per-k-tile path");
@@ -507,7 +514,17 @@ tap_gemm_kernel(const TapGemmParams p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nkt = p.nkt;
+  // this workgroup's k-tiles [kb, kb + nkt) (split-K slice; none in the reduce launch)
+  int kb = 0, nkt = p.nkt;
+  if constexpr (KS) {  // (a separate instantiation: the split paths cost the others registers)
+    if (p.kmode == 1) {
+      constexpr int U = 64 / BK;  // k-tiles per 64-deep unit
+      kb = (int)((long)p.k64 * blockIdx.y / p.ksplit) * U;
+      nkt = min(p.nkt, (int)((long)p.k64 * (blockIdx.y + 1) / p.ksplit) * U) - kb;
+    } else {
+      nkt = 0;
+    }
+  }
   auto compute = [&](const char* As, const char* Bs, int kt) {
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
@@ -544,15 +561,15 @@ tap_gemm_kernel(const TapGemmParams p) {
   };
   if constexpr (NS == 2) {
     if (nkt > 0) {
-      stage(0, 0);
+      stage(kb, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
     for (int kt = 0; kt < nkt; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nkt && !(p.ablate & 1)) stage(kt + 1, buf ^ 1);
+      if (kt + 1 < nkt && !(p.ablate & 1)) stage(kb + kt + 1, buf ^ 1);
       const char* As = smem + buf * STAGE;
-      if (!(p.ablate & 2)) compute(As, As + A_BYTES, kt);
+      if (!(p.ablate & 2)) compute(As, As + A_BYTES, kb + kt);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -560,17 +577,42 @@ tap_gemm_kernel(const TapGemmParams p) {
     constexpr int LPT = AI + BI;  // LDS-DMA instructions per thread per k-tile
 #pragma unroll
     for (int i = 0; i < NS - 1; ++i)
-      if (i < nkt) stage(i, i);
+      if (i < nkt) stage(kb + i, i);
     for (int kt = 0; kt < nkt; ++kt) {
       // tiles issued after kt: kt+1 .. min(kt+NS-2, nkt-1)
       wait_vmcnt(LPT * min(NS - 2, nkt - 1 - kt));
       __builtin_amdgcn_s_barrier();  // tile kt landed for every wave; tile kt-1's slot is free
       asm volatile("" ::: "memory");
-      if (kt + NS - 1 < nkt) stage(kt + NS - 1, (kt + NS - 1) % NS);
+      if (kt + NS - 1 < nkt) stage(kb + kt + NS - 1, (kt + NS - 1) % NS);
       const char* As = smem + (kt % NS) * STAGE;
-      compute(As, As + A_BYTES, kt);
+      compute(As, As + A_BYTES, kb + kt);
     }
     __syncthreads();
+  }
+  if constexpr (KS) {
+   if (p.kmode == 1) {
+    // split-K slice: raw accumulators, [slice][tile][j][i][thread] (16 bytes per lane, coalesced)
+    f32x4* o = p.kp + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (TN * 4 * 256) + tid;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[(j * 4 + i) * 256] = acc[j][i];
+    return;
+   }
+   // kmode 2: the slices of this tile in slice order (deterministic), one accumulator at a time (a
+   // slice-outer loop keeps every slice's loads live at once and spills), then the epilogue below
+    const f32x4* q = p.kp + (size_t)blockIdx.x * (TN * 4 * 256) + tid;
+    const size_t sstride = (size_t)gridDim.x * (TN * 4 * 256);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4* qq = q + (j * 4 + i) * 256;
+        f32x4 t = qq[0];
+#pragma unroll 1
+        for (int sl = 1; sl < p.ksplit; ++sl) t += qq[sl * sstride];
+        acc[j][i] = t;
+      }
   }
 
   if constexpr (EPI == 3 || EPI == 4) {
@@ -1894,9 +1936,32 @@ static void launch_tg(TapGemmParams p, int grid, hipStream_t stream) {
   if (full > 64 * 1024) {
     static bool attr = false;
     if (!attr) {
-      hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
+      (void)hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
+      if constexpr (BN == 64 && FAST && !PRO && NS <= 3)
+        (void)hipFuncSetAttribute((const void*)tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
       attr = true;
+    }
+  }
+  p.kmode = 0;
+  p.kp = nullptr;
+  // split-K (tg_split_slices): the 64-channel FAST tiles with <= 3 stages, the configurations the
+  // short grids it applies to run (the heuristic picks 64-channel tiles there)
+  if constexpr (BN == 64 && FAST && !PRO && NS <= 3) {
+    if (p.ksplit > 1 && g_ws_alloc != nullptr) {
+      const size_t bytes = (size_t)p.ksplit * grid * (BN / 32) * 4 * 256 * sizeof(f32x4);
+      void* ws = g_ws_alloc(bytes, stream);
+      if (ws != nullptr) {
+        p.kp = (f32x4*)ws;
+        p.kmode = 1;
+        hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO, true>), dim3(grid, p.ksplit), dim3(256), lds,
+                           stream, p);
+        p.kmode = 2;
+        hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO, true>), dim3(grid), dim3(256), lds, stream, p);
+        g_ws_free(ws);  // stream-ordered: reused only by later work on this stream
+        return;
+      }
     }
   }
   hipLaunchKernelGGL((tap_gemm_kernel<BN, EPI, FAST, NS, BK, PRO>), dim3(grid), dim3(256), lds, stream, p);
@@ -2002,6 +2067,25 @@ static int big_tile_pick(int mode, int M, int Co, int ntaps, int ds) {
   return pick != 0 && tiles >= 256 ? pick : 0;
 }
 
+// Split-K of the 128-row kernels: a grid under one round of 256 CUs with a deep k-loop -- at batch
+// 16-32 the 7x7 3x3 convs (104 workgroups x 72 k-tiles), the deep-K 1x1 convs of stage 4 and the
+// linear heads run one long latency-bound k-loop per workgroup.  ksplit slices of >= 8 64-deep units
+// (~3 rounds of workgroups), then one reduce launch sums the slices in order and runs the epilogue.
+// Decided on canonical 64-channel tiles and 64-deep units, so every 128-row configuration (tile
+// width, k depth, stages) sums the same slices: the autotuner's candidates stay bitwise equal (the
+// big tiles, which do not split, are not candidates where this applies).
+// g_tune[kTgSplitK]: 2 off, >= 3 exactly that many slices (A/B), 0 the heuristic.
+static int tg_split_slices(int M, int Co, int K) {
+  if (g_tune[kTgSplitK] == 2) return 0;
+  const int k64 = (K + 63) / 64;
+  const long grid_c = (long)((M + 127) / 128) * ((Co + 63) / 64);
+  int ks = 0;
+  if (g_tune[kTgSplitK] >= 3) ks = g_tune[kTgSplitK];
+  else if (grid_c < 256 && k64 >= 16) ks = (int)std::min<long>(k64 / 8, (768 + grid_c - 1) / grid_c);
+  if (ks > k64) ks = k64;
+  return ks >= 2 ? ks : 0;
+}
+
 static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
                           const bf16* wt, int Co, int T,
                           bf16* dst, int Hd, int Wd, int Hy, int Wy, int ss, int ds, int oy, int ox,
@@ -2052,6 +2136,10 @@ static void tap_gemm_impl(const bf16* src, int N, int Hs, int Ws, int Cs,
   p.sk_on = g_tune[kTgBigSK] == 1 ? 1 : (g_tune[kTgBigSK] >= 3 ? g_tune[kTgBigSK] : 0);
   p.sk_ws = nullptr;
   p.sk_flags = nullptr;
+  p.ksplit = tg_split_slices(p.M, Co, taps.n * Cs);  // (the 128-row kernels; tile widths 64 / 128 / 256)
+  p.k64 = (taps.n * Cs + 63) / 64;
+  p.kp = nullptr;
+  p.kmode = 0;
   int bn = Co <= 64 ? 64 : 128, ns = 2;
   // a short grid (< 1.5 rounds of 256 CUs at 128-channel tiles: batch 32-128 from stage 2 on, the
   // stride-2 parity classes, the linear heads) takes 64-channel tiles, twice the workgroups: the
@@ -2289,8 +2377,14 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs,
     float best = 1e30f, t_heur = 1e30f;
     choice = 0;
     const bool big_ok = bnb == nullptr && aff == nullptr && bias == nullptr && relu == 0 && Co >= 128;
+    // where the 128-row kernels split K, the (unsplit) big tiles would sum another way: not candidates
+    const bool ksplit = tg_split_slices(N * Hy * Wy, Co, taps.n * Cs) >= 2;
     for (int c = 0; c < (int)(sizeof(kTgCfgs) / sizeof(kTgCfgs[0])); ++c) {
       const TgCfg& cfg = kTgCfgs[c];
+      // (those that would not split: big tiles, 128 / 256-channel tiles, the 4-stage ring)
+      if (ksplit && (cfg.big == 1 || cfg.big == 3 || cfg.bn == 128 || cfg.bn == 256 || cfg.ns == 4 ||
+                     cfg.ws == 1 || cfg.ps != 0))
+        continue;
       if (cfg.big == 3 && !big_ok) continue;
       if (cfg.big == 1 && !(big_ok && Co >= 256)) continue;  // (the ping-pong candidate too)
       if (cfg.bn == 256 && !(Co > 128 && bnb == nullptr && bias == nullptr && relu == 0)) continue;

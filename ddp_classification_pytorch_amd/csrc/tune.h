@@ -43,6 +43,7 @@ enum TuneSlot : int {
   kTgWs = 32,          // 1x1 stride-1 short-K forward: 1 = weight-stationary persistent kernel (conv_ws.hip), 2 = off
   kTgPs = 33,          // 1x1 stride-1 short-K forward: store-decoupled loader/consumer kernel (conv1x1_ps.hip), 1 = 4 / 3 = 8 consumer waves, 2 = off
   kBnFinAct = 34,      // local training BN: 2 = finalize and apply as two launches (default: one, bn_fin_act_kernel)
+  kTgSplitK = 35,      // 128-row tap GEMM split-K for short grids with deep k-loops: 2 off, >= 3 slices (A/B), 0 heuristic
   kTuneSlots = 40
 };
 
@@ -65,6 +66,7 @@ constexpr TuneSlotName kTuneSlotNames[] = {
     {"autotune", kAutotune},         {"wg_split_cap", kWgSplitCap},  {"bn_bwd_cap", kBnBwdCap},
     {"row_reduce", kRowReduce},      {"c3_epilogue", kC3Epilogue},   {"c3_window_kb", kC3WindowKB},
     {"tg_ws", kTgWs},                {"tg_ps", kTgPs},               {"bn_fin_act", kBnFinAct},
+    {"tg_split_k", kTgSplitK},
 };
 
 extern int g_tune[kTuneSlots];

@@ -14,7 +14,7 @@ SLOTS = {
     "bn_act_variant": 11, "wg_rows": 12, "narrow_kdepth": 13, "wg_cols": 14, "wg3x3": 15, "gconv_sg": 16,
     "stem_ablate": 17, "c3_off": 18, "c3_variant": 19, "dgrad_parity_streams": 20, "tg_big_stages": 21, "tg_big_persist": 22, "tg_big_sk": 23, "tg_big": 24, "autotune": 25, "gconv_spw": 26, "wg_split_cap": 27,
     "bn_bwd_cap": 28, "row_reduce": 29, "c3_epilogue": 30, "c3_window_kb": 31, "tg_ws": 32, "tg_ps": 33,
-    "bn_fin_act": 34,
+    "bn_fin_act": 34, "tg_split_k": 35,
 }
 NUM_SLOTS = 40
 # the loaded library's own table (set by verify); apply() skips names it does not have at the same

@@ -113,11 +113,19 @@ def _one(K, base, imgs, labels, slots, values):
     return _grads(m), _bn_stats(m)
 
 
-@pytest.mark.parametrize("kind,idx", [("tg", i) for i in range(len(TG))] + [("wg", i) for i in range(len(WG))])
+# split-K of the 128-row tap GEMM (on by default where grids are short: at this batch the deep-K convs,
+# the fused BN-backward data gradients and the head): the heuristic (TG[0]) runs it; this arm turns it off
+SK = [(2,)]
+SK_SLOTS = ("tg_split_k",)
+
+
+@pytest.mark.parametrize("kind,idx", [("tg", i) for i in range(len(TG))] + [("wg", i) for i in range(len(WG))] +
+                         [("sk", 0)])
 def test_candidate_first_step_within_bf16_floor(setup, kind, idx):
     K, base, imgs, labels, g_ref, e_floor, yard = setup
     g0, s0 = _one(K, base, imgs, labels, TG_SLOTS, TG[0])
-    slots, values = (TG_SLOTS, TG[idx]) if kind == "tg" else (WG_SLOTS, WG[idx])
+    slots, values = {"tg": (TG_SLOTS, TG[idx] if kind == "tg" else None), "wg": (WG_SLOTS, WG[idx] if kind == "wg" else None),
+                     "sk": (SK_SLOTS, SK[idx] if kind == "sk" else None)}[kind]
     g, s = _one(K, base, imgs, labels, slots, values)
     e = relerr(g, g_ref)
     # no worse than stock PyTorch bf16 autocast on the same net and input (test_model_parity's bar)

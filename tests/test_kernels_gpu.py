@@ -1367,7 +1367,8 @@ def test_conv_autotune_same_results(K):
 def test_conv_fwd_256_channel_tiles(K, shape):
     """256-channel tap-GEMM tiles (g_tune[0] = 256: 64 x 128 outputs per wave, statistics
     epilogue) == the fp32 reference and the 128-channel tiles, ragged M and channel counts that are
-    not a multiple of 256 included; dgrad is unaffected (falls back to 128)."""
+    not a multiple of 256 included; dgrad is unaffected (falls back to 128).  Split-K off in both
+    arms: the 256-channel tile does not split (the autotuner drops it where the heuristic does)."""
     N, H, W, Ci, Co, k, s, p = shape
     torch.manual_seed(0)
     x = rnd(N, H, W, Ci).to(DEV)
@@ -1375,6 +1376,7 @@ def test_conv_fwd_256_channel_tiles(K, shape):
     wb, _ = K.weight_prep(w.float(), 0, True)
     outs = []
     try:
+        K.set_tuning(tslot("tg_split_k"), 2)
         for bn in (0, 256):
             K.set_tuning(tslot("tg_tile_n"), bn)
             y, slabs = K.conv_fwd(x, wb, s, p, True)
@@ -1383,6 +1385,7 @@ def test_conv_fwd_256_channel_tiles(K, shape):
             outs.append((y.float().cpu(), st.cpu()))
     finally:
         K.set_tuning(tslot("tg_tile_n"), 0)
+        K.set_tuning(tslot("tg_split_k"), 0)
     (y0, s0), (y1, s1) = outs
     assert torch.equal(y1, y0)  # same k order: bit-identical outputs
     assert torch.equal(s1[0, 0], s0[0, 0]) and relerr(s1[0, 1:], s0[0, 1:]) < 1e-4
@@ -1836,3 +1839,39 @@ def test_tresnet_se_gate_fused_matches_gemm_chain_gpu():
     assert se and any(g0[k].abs().sum() > 0 for k in se)
     for k in se:
         assert relerr(g1[k], g0[k]) < 0.1, k
+
+
+@pytest.mark.parametrize("N,H,Ci,Co,k,s,p", [(2, 7, 512, 512, 3, 1, 1), (4, 7, 2048, 512, 1, 1, 0),
+                                             (3, 14, 1024, 256, 1, 1, 0), (2, 14, 256, 256, 3, 2, 1)])
+def test_split_k_short_grids(K, N, H, Ci, Co, k, s, p):
+    """Split-K of the 128-row tap GEMM (short grids with deep k-loops: small batches): forward with BN
+    statistics and data gradient vs the fp32 reference, vs the unsplit kernels (tg_split_k = 2), and
+    bitwise equal whatever the slice count's k depth (32- vs 64-deep k-tiles cut at the same 64-deep
+    units)."""
+    from ddp_classification_pytorch_amd import tuning
+
+    torch.manual_seed(N * 100 + Ci)
+    x = rnd(N, H, H, Ci).to(DEV)
+    w = rnd(Co, k, k, Ci, scale=1.0 / math.sqrt(k * k * Ci))
+    Ho = (H + 2 * p - k) // s + 1
+    dy = rnd(N, Ho, Ho, Co).to(DEV)
+    wb, wt = K.weight_prep(w.float().to(DEV), 0, True)
+    outs = {}
+    for name, spec in (("split", ""), ("off", "tg_split_k=2"), ("split4", "tg_split_k=4"),
+                       ("split_bk32", "tg_kdepth=32,tg_stages=2")):
+        tuning.apply(K, spec, reset=True)
+        try:
+            y, sl = K.conv_fwd(x, wb, s, p, True)
+            d = K.conv_dgrad(dy, wt, H, H, s, p) if s == 1 else None
+            torch.cuda.synchronize()
+            outs[name] = (y, K.bn_stats(y, sl), d)
+        finally:
+            tuning.apply(K, "", reset=True)
+    ry, _ = _ref.conv_fwd(x.cpu(), w.bfloat16(), s, p, True)
+    for name, (y, st, d) in outs.items():
+        assert relerr(y, ry) < 1e-2, name
+        assert relerr(st[0, 1:], outs["off"][1][0, 1:]) < 1e-3, name
+        if d is not None:
+            assert relerr(d, outs["off"][2]) < 1e-2, name
+    assert torch.equal(outs["split"][0], outs["split_bk32"][0])
+
