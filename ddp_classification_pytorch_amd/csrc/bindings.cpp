@@ -1588,11 +1588,11 @@ std::tuple<Tensor, Tensor, Tensor> chan_scale_bwd(const Tensor& dy, const Tensor
   const int HW = x.numel() / (N * C);
   TORCH_CHECK(C % 8 == 0 && C <= 2048 && HW > 0 && g.numel() == (int64_t)N * C, "chan_scale_bwd shapes");
   auto dx = at::empty_like(x);
-  auto dg = at::empty({N, C}, f32_like(x));
+  auto dg = at::empty({N, C}, bf16_like(x));  // the gate's dtype (autograd needs it; no cast launch)
   auto part = at::empty({dcp::hw_splits(N, HW, C), N, C}, f32_like(x));
   Tensor dres = want_dres ? at::empty_like(x) : at::empty({0}, x.options());
   dcp::launch_chan_scale_bwd(bp(dy), bp(x), bp(g), res.has_value() ? bp(*res) : nullptr, bpm(dx),
-                             dg.data_ptr<float>(), part.data_ptr<float>(), want_dres ? bpm(dres) : nullptr, N, HW, C,
+                             bpm(dg), part.data_ptr<float>(), want_dres ? bpm(dres) : nullptr, N, HW, C,
                              relu ? 1 : 0, cur_stream());
   return {dx, dg, dres};
 }

@@ -22,6 +22,8 @@
 //   bn_bwd_elemt     -> dx (and d(residual) = dz)
 // The activation mask is recomputed from x (and the residual) instead of
 // saving the post-activation tensor.
+#include <type_traits>
+
 #include "common.cuh"
 #include "launchers.h"
 
@@ -348,8 +350,9 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
 
 
 // [P][K] -> [K] column sums; one workgroup per 64 columns, 4 waves x 4-deep unroll over P
+template <typename OUT = float>
 __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restrict__ part, int P, int K,
-                                                          float* __restrict__ out) {
+                                                          OUT* __restrict__ out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -380,7 +383,11 @@ __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restric
   __shared__ float red[4][64];
   red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (w == 0 && k < K) out[k] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && k < K) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if constexpr (std::is_same<OUT, float>::value) out[k] = t;
+    else out[k] = f2bf(t);  // (round to nearest even, as a torch .to(bfloat16) of the fp32 sum)
+  }
 }
 
 // stats [W][3][C] (one (n, mean, M2) per rank) -> mean, invstd, scale, shift (+ running stats)
@@ -956,7 +963,11 @@ void launch_bn_merge_finalize(const float* part, int P, int C, float eps, const 
 }
 
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
+  hipLaunchKernelGGL(partial_sum_kernel<float>, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
+}
+
+void launch_partial_sum_bf16(const float* part, int P, int K, bf16* out, hipStream_t s) {
+  hipLaunchKernelGGL(partial_sum_kernel<bf16>, dim3((K + 63) / 64), dim3(256), 0, s, part, P, K, out);
 }
 
 // ~16 rows per workgroup (at most 128 partials): a linear layer's bias gradient over a 1024-row
@@ -969,7 +980,7 @@ int colsum_partials(int M) {
 void launch_colsum(const bf16* x, int M, int C, float* part, float* out, hipStream_t s) {
   const int P = colsum_partials(M);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(P, (C + 2047) / 2048), dim3(256), 0, s, x, M, C, part);
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
+  hipLaunchKernelGGL(partial_sum_kernel<float>, dim3((C + 63) / 64), dim3(256), 0, s, part, P, C, out);
 }
 
 void launch_bn_finalize(const float* st, int W, int C, float eps, const float* gamma, const float* beta, float* mean,
@@ -1082,7 +1093,7 @@ void launch_bn_bwd_reduce(const bf16* dy, const bf16* x, const bf16* res, const 
   const int g = bn_bwd_reduce_blocks(M, C);
   DCP_ACT_RES_DISPATCH(bn_bwd_reduce_kernel, dim3(g), 2 * 2048 * 4, s, res, act, dy, x, res, scale, shift, mean,
                        invstd, M, C, slope, partials, inv);
-  hipLaunchKernelGGL(partial_sum_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, s, partials, g, 2 * C, out);
+  hipLaunchKernelGGL(partial_sum_kernel<float>, dim3((2 * C + 63) / 64), dim3(256), 0, s, partials, g, 2 * C, out);
 }
 
 void launch_bn_bwd_elemt(const bf16* dy, const bf16* x, const bf16* res, const float* scale, const float* shift,

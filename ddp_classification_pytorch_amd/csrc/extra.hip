@@ -377,12 +377,12 @@ void launch_chan_scale_fwd(const bf16* x, const bf16* g, const bf16* res, bf16* 
   const size_t total = (size_t)N * HW * (C / 8);
   hipLaunchKernelGGL(chan_scale_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, st, x, g, res, y, N, HW, C, relu);
 }
-void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg,
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, bf16* dg,
                            float* part, bf16* dres, int N, int HW, int C, int relu, hipStream_t st) {
   const int S = hw_splits(N, HW, C);
   hipLaunchKernelGGL(chan_scale_bwd_kernel, dim3(N, S), dim3(256), 0, st, dy, x, g, res, dx, part, dres, N, HW, C,
                      relu);
-  launch_partial_sum(part, S, N * C, dg, st);
+  launch_partial_sum_bf16(part, S, N * C, dg, st);  // the gate's gradient in its own dtype: no cast pass
 }
 
 // ---------------------------------------------------------------------------
@@ -406,15 +406,23 @@ bool se_gate_supported(int N, int C, int R) {
 }
 
 namespace {
-// D (16 x 16) += A[m0 .. m0+15][0 .. K) x B[n0 .. n0+15][0 .. K)^T, both k-contiguous rows (LDS or global)
+// D (16 x 16) += A[m0 .. m0+15][0 .. K) x B[n0 .. n0+15][0 .. K)^T, both k-contiguous rows (LDS or global),
+// K <= 256: every k-step's fragments are loaded before the MFMA chain (one load round trip per tile
+// instead of one per k-step -- the weight fragments come from L2)
 __device__ __forceinline__ f32x4 se_mma(const bf16* A, int lda, const bf16* B, int ldb, int K, int lane) {
   const int r = lane & 15, kq = 8 * (lane >> 4);
+  constexpr int KS = kSeMaxC / 32;
+  bf16x8 a[KS], b[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    if (s * 32 < K) {
+      a[s] = *(const bf16x8*)(A + r * lda + s * 32 + kq);
+      b[s] = *(const bf16x8*)(B + r * ldb + s * 32 + kq);
+    }
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < K; k += 32) {
-    const bf16x8 a = *(const bf16x8*)(A + r * lda + k + kq);
-    const bf16x8 b = *(const bf16x8*)(B + r * ldb + k + kq);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    if (s * 32 < K) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b[s], acc, 0, 0, 0);
   return acc;
 }
 }  // namespace

@@ -77,6 +77,7 @@ void launch_tap_gemm(const bf16* src, int N, int Hs, int Ws, int Cs, const bf16*
 void launch_act_scale_bwd(const bf16* dy, const bf16* y, const float* scale, int64_t M, int C, int act, float slope,
                           bf16* dc, bf16* g, hipStream_t s);
 void launch_partial_sum(const float* part, int P, int K, float* out, hipStream_t s);
+void launch_partial_sum_bf16(const float* part, int P, int K, bf16* out, hipStream_t s);
 // partial-slab split-K weight gradient: dw is fully written when part != nullptr
 // (part = wgrad_splits(...) x Co x T*Cs floats); part == nullptr -> fp32 atomics into a zeroed dw
 int wgrad_splits(int M, int Co, int ldw, int taps, int num_cu, int* rows_per_split);
@@ -346,7 +347,7 @@ void launch_se_gate_fwd(const bf16* p, const bf16* w1, const float* b1, const bf
 void launch_se_gate_bwd(const bf16* dg, const bf16* g, const bf16* h, const bf16* p, const bf16* w1t, int ld1t,
                         const bf16* w2t, int ld2t, float* dw1, float* db1, float* dw2, float* db2, bf16* dp, int N,
                         int C, int R, hipStream_t st);
-void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, float* dg, float* part,
+void launch_chan_scale_bwd(const bf16* dy, const bf16* x, const bf16* g, const bf16* res, bf16* dx, bf16* dg, float* part,
                            bf16* dres, int N, int HW, int C, int relu, hipStream_t st);
 
 // stem weight 7x7/2 [Co][7][7][C<=4] <-> space-to-depth 4x4 [Co][4][4][16] (misc.hip)

@@ -557,7 +557,7 @@ def chan_scale_bwd(dy, x, g, res, relu, want_dres):
         z = _f(x) * gg + (_f(res) if res is not None else 0)
         dz = torch.where(z > 0, dz, torch.zeros_like(dz))
     dx = (dz * gg).to(dy.dtype)
-    dg = (dz * _f(x)).reshape(N, -1, C).sum(1)
+    dg = (dz * _f(x)).reshape(N, -1, C).sum(1).to(g.dtype)  # the gate's dtype, like the GPU op
     return dx, dg, (dz.to(dy.dtype) if want_dres else dy.new_empty(0))
 
 

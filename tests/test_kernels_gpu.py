@@ -217,7 +217,9 @@ def test_hw_reductions_split(K, shape):
         rf = res.float() if res is not None else None
         got = K.chan_scale_bwd(dy.to(DEV), x.to(DEV), g.to(DEV), rd, relu, res is not None)
         want = _ref.chan_scale_bwd(dy.float(), x.float(), g.float(), rf, relu, res is not None)
-        assert relerr(got[0], want[0]) < 1e-2 and relerr(got[1], want[1]) < 1e-3
+        # (dg comes back in the gate's dtype, bf16: one rounding of the fp32 sum)
+        assert relerr(got[0], want[0]) < 1e-2 and relerr(got[1], want[1]) < 4e-3
+        assert got[1].dtype == torch.bfloat16
         if res is not None:
             assert relerr(got[2], want[2]) < 1e-2
 
