@@ -65,7 +65,8 @@ for step in "$@"; do
       run_ref() {  # tag, bench args...
         local t=$1; shift
         timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 "$@" > $O/ref_$t.log 2>&1
-        echo "$t $(tail -1 $O/ref_$t.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r["ms_per_step"], r.get("syncbn_value"), r.get("syncbn_ms_per_step"))')"
+        # (the JSON line is the last one starting with "{": a world-1 DDP run may print after it)
+        echo "$t $(grep '^{' $O/ref_$t.log | tail -1 | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r["ms_per_step"], r.get("syncbn_value"), r.get("syncbn_ms_per_step"))')"
       }
       run_ref tresnet_b16_graph --config tresnet --batch 16 --graph
       run_ref tresnet_b16_eager --config tresnet --batch 16 --eager
