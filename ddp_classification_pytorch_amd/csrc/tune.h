@@ -42,7 +42,7 @@ enum TuneSlot : int {
   kC3WindowKB = 31,    // direct 64->64 3x3 window buffer size (KB)
   kTgWs = 32,          // 1x1 stride-1 short-K forward: 1 = weight-stationary persistent kernel (conv_ws.hip), 2 = off
   kTgPs = 33,          // 1x1 stride-1 short-K forward: store-decoupled loader/consumer kernel (conv1x1_ps.hip), 1 = 4 / 3 = 8 consumer waves, 2 = off
-  kBnFinAct = 34,      // local training BN: 2 = finalize and apply as two launches (default: one, bn_fin_act_kernel)
+  kBnFinAct = 34,      // the bn_fin_act op (opt-in from Python, DCP_BN_FIN_ACT=1): 2 = run it as its two launches
   kTgSplitK = 35,      // 128-row tap GEMM split-K for short grids with deep k-loops: 2 off, >= 3 slices (A/B), 0 heuristic
   kTuneSlots = 40
 };
