@@ -2067,10 +2067,12 @@ static int big_tile_pick(int mode, int M, int Co, int ntaps, int ds) {
   return pick != 0 && tiles >= 256 ? pick : 0;
 }
 
-// Split-K of the 128-row kernels: a grid under one round of 256 CUs with a deep k-loop -- at batch
+// Split-K of the 128-row kernels: a grid under half a round of 256 CUs with a deep k-loop -- at batch
 // 16-32 the 7x7 3x3 convs (104 workgroups x 72 k-tiles), the deep-K 1x1 convs of stage 4 and the
 // linear heads run one long latency-bound k-loop per workgroup.  ksplit slices of >= 8 64-deep units
-// (~3 rounds of workgroups), then one reduce launch sums the slices in order and runs the epilogue.
+// (~2 rounds of workgroups), then one reduce launch sums the slices in order and runs the epilogue.
+// (Measured: grids < 256 tiles and ~3 rounds 1.5 % slower at R50 b32; < 512 and slices of 4 units 8 %
+// slower -- profiles/r6/split_k_width_ab_s37_s38.txt.)
 // Decided on canonical 64-channel tiles and 64-deep units, so every 128-row configuration (tile
 // width, k depth, stages) sums the same slices: the autotuner's candidates stay bitwise equal (the
 // big tiles, which do not split, are not candidates where this applies).
@@ -2081,7 +2083,9 @@ static int tg_split_slices(int M, int Co, int K) {
   const long grid_c = (long)((M + 127) / 128) * ((Co + 63) / 64);
   int ks = 0;
   if (g_tune[kTgSplitK] >= 3) ks = g_tune[kTgSplitK];
-  else if (grid_c < 256 && k64 >= 16) ks = (int)std::min<long>(k64 / 8, (768 + grid_c - 1) / grid_c);
+  else if (g_tune[kTgSplitK] == 1) {  // (A/B) one round of slices
+    if (grid_c < 128 && k64 >= 16) ks = (int)std::min<long>(k64 / 8, (256 + grid_c - 1) / grid_c);
+  } else if (grid_c < 128 && k64 >= 16) ks = (int)std::min<long>(k64 / 8, (512 + grid_c - 1) / grid_c);
   if (ks > k64) ks = k64;
   return ks >= 2 ? ks : 0;
 }
