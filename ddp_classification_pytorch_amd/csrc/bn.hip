@@ -189,50 +189,60 @@ __device__ __forceinline__ Welford merge_partials(const float* __restrict__ part
 }
 
 // conv slabs [R][2][C] (per-128-row (mean, M2), slab r holds min(128, M - 128 r) rows) merged
-// straight into (n, mean, M2) of channel blockIdx.x*64 + lane, complete in wave 0 -- the one-level
-// path for R <= kDirectSlabs (small activations: no bn_slab_partial launch, whose per-launch cost
-// dominated the statistics of every layer at batch 32-128)
+// straight into (n, mean, M2) of channel cb * kSlabCh + (lane & 15), complete in lanes 0-15 of wave 0 --
+// the one-level path for R <= kDirectSlabs (small activations: no bn_slab_partial launch, whose per-launch
+// cost dominated the statistics of every layer at batch 32-128).  16 channels per workgroup, so a
+// 64-channel layer's slabs spread over four CUs (one workgroup read all 400 KB of a batch-32 stage-1
+// layer's slabs at its CU's L2 -> LDS rate: 15 us): 64 row streams (4 per wave, 16 lanes = 16
+// consecutive channels = 64 contiguous bytes per slab row), 8 slabs' loads in flight per stream, then a
+// two-level fixed-order combine of the streams (deterministic).
 constexpr int kDirectSlabs = 1024;
+constexpr int kSlabCh = 16;
 __device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, int R, int M, int C, int cb) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = cb * 64 + lane;
+  const int c = cb * kSlabCh + (lane & 15);
+  const int rs = (lane >> 4) + 4 * w;  // row stream 0 .. 63
   Welford a{0.f, 0.f, 0.f};
   if (c < C) {
-    int r = w;
-    // 16 slabs' loads in flight per wave before the (in-order, so deterministic) merges: the merge
-    // of a small batch's <= 1024 slabs is bound by load round trips, not by the merge math.  (The
-    // large-batch two-level merges keep 4: 16 there measured 0.6 % slower end to end at batch
-    // 1024, profiles/r3/bn_reduce_pipelining_ab.txt.)
-    for (; r + 15 * kMergeWaves < R; r += 16 * kMergeWaves) {
-      float mb[16], m2b[16];
+    int r = rs;
+    for (; r + 7 * 64 < R; r += 8 * 64) {
+      float mb[8], m2b[8];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        mb[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 0) * C + c];
-        m2b[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 1) * C + c];
+      for (int u = 0; u < 8; ++u) {
+        mb[u] = slabs[((size_t)(r + u * 64) * 2 + 0) * C + c];
+        m2b[u] = slabs[((size_t)(r + u * 64) * 2 + 1) * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) a.merge((float)min(128, M - 128 * (r + u * kMergeWaves)), mb[u], m2b[u]);
+      for (int u = 0; u < 8; ++u) a.merge((float)min(128, M - 128 * (r + u * 64)), mb[u], m2b[u]);
     }
-    for (; r + 3 * kMergeWaves < R; r += 4 * kMergeWaves) {
-      float mb[4], m2b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        mb[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 0) * C + c];
-        m2b[u] = slabs[((size_t)(r + u * kMergeWaves) * 2 + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a.merge((float)min(128, M - 128 * (r + u * kMergeWaves)), mb[u], m2b[u]);
-    }
-    for (; r < R; r += kMergeWaves)
+    for (; r < R; r += 64)
       a.merge((float)min(128, M - 128 * r), slabs[((size_t)r * 2 + 0) * C + c], slabs[((size_t)r * 2 + 1) * C + c]);
   }
-  __shared__ float red[3][kMergeWaves][64];
-  red[0][w][lane] = a.n;
-  red[1][w][lane] = a.mean;
-  red[2][w][lane] = a.m2;
+  __shared__ float red[3][64][kSlabCh];
+  const int ch = lane & 15;
+  red[0][rs][ch] = a.n;
+  red[1][rs][ch] = a.mean;
+  red[2][rs][ch] = a.m2;
   __syncthreads();
-  if (w == 0)
-    for (int k = 1; k < kMergeWaves; ++k) a.merge(red[0][k][lane], red[1][k][lane], red[2][k][lane]);
+  if (rs < 8) {  // streams rs, rs + 8, .. rs + 56
+    Welford b{0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b.merge(red[0][rs + 8 * k][ch], red[1][rs + 8 * k][ch], red[2][rs + 8 * k][ch]);
+    a = b;
+  }
+  __syncthreads();
+  if (rs < 8) {
+    red[0][rs][ch] = a.n;
+    red[1][rs][ch] = a.mean;
+    red[2][rs][ch] = a.m2;
+  }
+  __syncthreads();
+  if (rs == 0) {
+    Welford b{0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b.merge(red[0][k][ch], red[1][k][ch], red[2][k][ch]);
+    a = b;
+  }
   return a;
 }
 
@@ -240,8 +250,8 @@ __device__ __forceinline__ Welford merge_slabs(const float* __restrict__ slabs, 
 __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_merge_kernel(const float* __restrict__ slabs, int R, int M,
                                                                          int C, float* __restrict__ out) {
   const Welford a = merge_slabs(slabs, R, M, C, blockIdx.x);
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  if ((threadIdx.x >> 6) == 0 && c < C) {
+  const int c = blockIdx.x * kSlabCh + (threadIdx.x & 63);
+  if (threadIdx.x < kSlabCh && c < C) {
     out[c] = a.n;
     out[C + c] = a.mean;
     out[2 * C + c] = a.m2;
@@ -341,8 +351,8 @@ __global__ void __launch_bounds__(64 * kMergeWaves) bn_slab_finalize_kernel(
     float* __restrict__ shift, float* __restrict__ run_mean, float* __restrict__ run_var, float momentum, float iabn_eps,
     float* __restrict__ rgamma) {
   const Welford m = merge_slabs(slabs, R, M, C, blockIdx.x);
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  if ((threadIdx.x >> 6) != 0 || c >= C) return;
+  const int c = blockIdx.x * kSlabCh + (threadIdx.x & 63);
+  if (threadIdx.x >= kSlabCh || c >= C) return;
   Welford a{0.f, 0.f, 0.f};
   a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
   finalize_channel(a, c, eps, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, iabn_eps, rgamma);
@@ -592,8 +602,9 @@ __global__ void __launch_bounds__(1024) bn_fin_act_kernel(const FinActParams p) 
   if ((int)blockIdx.x < p.nfin) {
     const Welford m = p.partials ? merge_partials(p.src, p.nsrc, p.C, blockIdx.x)
                                  : merge_slabs(p.src, p.nsrc, p.M, p.C, blockIdx.x);
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    if ((threadIdx.x >> 6) == 0 && c < p.C) {
+    const int cpb = p.partials ? 64 : kSlabCh;  // channels per finalize workgroup
+    const int c = blockIdx.x * cpb + (threadIdx.x & 63);
+    if ((int)threadIdx.x < cpb && c < p.C) {
       Welford a{0.f, 0.f, 0.f};
       a.merge(m.n, m.mean, m.m2);  // the W = 1 merge of bn_finalize_kernel
       finalize_channel<true>(a, c, p.eps, p.gamma, p.beta, p.mean, p.invstd, p.scale, p.shift, p.run_mean,
@@ -929,7 +940,8 @@ static int launch_stat_partials(const bf16* x, const float* slabs, int M, int C,
 void launch_bn_stats(const bf16* x, const float* slabs, int M, int C, float* part, float* out, hipStream_t s) {
   const int R = (M + 127) / 128;
   if (slabs && R <= kDirectSlabs) {
-    hipLaunchKernelGGL(bn_slab_merge_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C, out);
+    hipLaunchKernelGGL(bn_slab_merge_kernel, dim3((C + kSlabCh - 1) / kSlabCh), dim3(64 * kMergeWaves), 0, s, slabs,
+                       R, M, C, out);
     return;
   }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
@@ -942,8 +954,9 @@ void launch_bn_stats_finalize(const bf16* x, const float* slabs, int M, int C, f
                               float* rgamma) {
   const int R = (M + 127) / 128;
   if (slabs && R <= kDirectSlabs) {
-    hipLaunchKernelGGL(bn_slab_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kMergeWaves), 0, s, slabs, R, M, C,
-                       eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum, iabn_eps, rgamma);
+    hipLaunchKernelGGL(bn_slab_finalize_kernel, dim3((C + kSlabCh - 1) / kSlabCh), dim3(64 * kMergeWaves), 0, s,
+                       slabs, R, M, C, eps, gamma, beta, mean, invstd, scale, shift, rm, rv, momentum, iabn_eps,
+                       rgamma);
     return;
   }
   const int P = launch_stat_partials(x, slabs, M, C, part, s);
@@ -1054,7 +1067,7 @@ void launch_bn_fin_act(const bf16* x, const bf16* res, const float* src, int nsr
                        uint8_t* mask, int act, float slope, uint32_t* sync, hipStream_t s) {
   FinActParams p;
   p.x = x; p.res = res; p.src = src; p.nsrc = nsrc; p.partials = partials; p.M = M; p.C = C;
-  p.nfin = (C + 63) / 64;
+  p.nfin = partials ? (C + 63) / 64 : (C + kSlabCh - 1) / kSlabCh;
   p.eps = eps; p.momentum = momentum; p.iabn_eps = iabn_eps; p.slope = slope;
   p.gamma = gamma; p.beta = beta; p.mean = mean; p.invstd = invstd; p.scale = scale; p.shift = shift;
   p.run_mean = rm; p.run_var = rv; p.rgamma = rgamma; p.y = y; p.mask = mask; p.sync = sync;
