@@ -2466,37 +2466,51 @@ __global__ void __launch_bounds__(256) split_reduce1_kernel(const float4* __rest
 
 // One launch for a narrow reduction (few columns, up to a few thousand splits: the BN-backward sums
 // of a small batch's dgrad epilogue, 2C columns over one partial row per 128-pixel tile): a
-// 1024-thread workgroup per 64 float4 columns, its 16 waves striding over the split rows with 8
-// loads in flight each, then a fixed-order LDS combine -- deterministic, no second launch.
+// 1024-thread workgroup per 16 float4 columns -- 64 row streams (4 per wave), 8 loads in flight each,
+// then a fixed-order two-level combine of the streams in LDS: deterministic, no second launch.  (64
+// columns per workgroup left a 256-channel layer's sums on two CUs, each reading ~800 KB at batch 32.)
 __global__ void __launch_bounds__(1024) split_reduce_rows_kernel(const float4* __restrict__ part, int splits, int n4,
                                                                  float4* __restrict__ out) {
-  __shared__ float4 red[16][64];
+  __shared__ float4 red[64][16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  const int cl = lane & 15, rs = (lane >> 4) + 4 * w;  // column in the workgroup's 16, row stream 0 .. 63
+  const int col = blockIdx.x * 16 + cl;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < n4) {
-    int k = w;
-    for (; k + 7 * 16 < splits; k += 8 * 16) {
+    int k = rs;
+    for (; k + 7 * 64 < splits; k += 8 * 64) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 16 * u) * n4 + col];
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 64 * u) * n4 + col];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
       }
     }
-    for (; k < splits; k += 16) {
+    for (; k < splits; k += 64) {
       const float4 v = part[(size_t)k * n4 + col];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
   }
-  red[w][lane] = s;
+  red[rs][cl] = s;
   __syncthreads();
-  if (w == 0 && col < n4) {
-    float4 t = red[0][lane];
+  if (rs < 8) {  // streams rs, rs + 8, .. rs + 56
+    float4 t = red[rs][cl];
 #pragma unroll
-    for (int q = 1; q < 16; ++q) {
-      const float4 v = red[q][lane];
+    for (int q = 1; q < 8; ++q) {
+      const float4 v = red[rs + 8 * q][cl];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    s = t;
+  }
+  __syncthreads();
+  if (rs < 8) red[rs][cl] = s;
+  __syncthreads();
+  if (rs == 0 && col < n4) {
+    float4 t = red[0][cl];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      const float4 v = red[q][cl];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
     out[col] = t;
@@ -2521,7 +2535,7 @@ void launch_split_reduce(const float* part, int splits, int n, float* out, hipSt
   // n4 / 64 = 8 workgroups, 28 us; the two-level pair spreads it over the chip)
   const bool rows_ok = n4 <= 256 || (size_t)splits * n4 <= (size_t)512 * 1024;
   if (n4 <= 1024 && splits <= row_max && rows_ok && g_tune[kRowReduce] != 2) {
-    hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 63) / 64), dim3(1024), 0, stream, (const float4*)part,
+    hipLaunchKernelGGL(split_reduce_rows_kernel, dim3((n4 + 15) / 16), dim3(1024), 0, stream, (const float4*)part,
                        splits, n4, (float4*)out);
     return;
   }
