@@ -81,6 +81,36 @@ __global__ void __launch_bounds__(256) mt_weight_prep_kernel(const WPEntry* __re
   const int per_t = e.tci * e.tco;
   const int t = b.y / per_t, rr = b.y - t * per_t;
   const int co0 = (rr / e.tci) * 64, ci0 = (rr % e.tci) * 64;
+  // 4-wide path (uniform per block): 16-byte fp32 loads, 8-byte bf16 stores in both layouts (the
+  // 2-byte-per-lane stores of the scalar path ran the whole-model refresh at ~3.9 TB/s); every
+  // 4-group is then wholly inside or outside each bound.  The stem (Ci_src 3) takes the scalar path.
+  const bool vec = ((e.Ci_src | e.Ci | e.Cp) & 3) == 0 &&
+                   (((uintptr_t)e.w & 15u) | ((uintptr_t)e.wb & 7u) | ((uintptr_t)e.wt & 7u)) == 0;
+  if (vec) {
+    const int c4 = (threadIdx.x & 15) * 4, rw = threadIdx.x >> 4;  // 16 rows per pass
+#pragma unroll
+    for (int r = rw; r < 64; r += 16) {
+      const int co = co0 + r, ci = ci0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (co < e.Co && ci < e.Ci_src) v = *(const float4*)(e.w + ((size_t)co * e.T + t) * e.Ci_src + ci);
+      tile[r][c4] = v.x;
+      tile[r][c4 + 1] = v.y;
+      tile[r][c4 + 2] = v.z;
+      tile[r][c4 + 3] = v.w;
+      if (co < e.Cp && ci < e.Ci)
+        *(bf16x4*)(e.wb + ((size_t)co * e.T + t) * e.Ci + ci) = bf16x4{f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+    }
+    if (!e.wt) return;
+    __syncthreads();
+#pragma unroll
+    for (int r = rw; r < 64; r += 16) {
+      const int ci = ci0 + r, co = co0 + c4;
+      if (ci < e.Ci && co < e.Cp)
+        *(bf16x4*)(e.wt + ((size_t)ci * e.T + t) * e.Cp + co) =
+            bf16x4{f2bf(tile[c4][r]), f2bf(tile[c4 + 1][r]), f2bf(tile[c4 + 2][r]), f2bf(tile[c4 + 3][r])};
+    }
+    return;
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int co = co0 + r, ci = ci0 + tx;

@@ -29,6 +29,47 @@ __global__ void __launch_bounds__(256) mt_sgd_kernel(const MTEntry* __restrict__
   const MTEntry e = tab[ck.x];
   const int64_t base = (int64_t)ck.y * kChunk;
   const int64_t end = min(e.n, base + kChunk);
+  // 16-byte path (uniform per chunk): the 4-byte loop kept one 4-byte load per lane and tensor in
+  // flight per iteration (96 us for ResNet-50's 25.6M parameters, ~5.3 TB/s); the per-element math
+  // is the same, so both paths give identical results.  Bucket views at odd offsets take the scalar
+  // loop.
+  const uintptr_t mis = ((uintptr_t)(e.p + base) | (uintptr_t)(e.g + base) |
+                         (h.momentum != 0.f ? (uintptr_t)(e.s1 + base) : 0)) & 15u;
+  const uintptr_t smis = e.shadow ? ((uintptr_t)(e.shadow + base) & 7u) : 0;
+  if (mis == 0 && smis == 0 && ((end - base) & 3) == 0) {
+    const int64_t n4 = (end - base) >> 2;
+    float4* p4 = (float4*)(e.p + base);
+    const float4* g4 = (const float4*)(e.g + base);
+    float4* s4 = (float4*)(e.s1 + base);
+#pragma unroll 4
+    for (int64_t j = threadIdx.x; j < n4; j += blockDim.x) {
+      float gv[4], pv[4], bv[4];
+      *(float4*)gv = g4[j];
+      *(float4*)pv = p4[j];
+      const bool mom = h.momentum != 0.f;
+      if (mom && !h.first) *(float4*)bv = s4[j];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float g = gv[u] * h.grad_scale;
+        if (h.wd != 0.f) g += h.wd * pv[u];
+        if (mom) {
+          const float b = h.first ? g : h.momentum * bv[u] + (1.f - h.dampening) * g;
+          bv[u] = b;
+          g = h.nesterov ? g + h.momentum * b : b;
+        }
+        pv[u] -= h.lr * g;
+      }
+      if (mom) s4[j] = *(float4*)bv;
+      p4[j] = *(float4*)pv;
+      if (e.shadow) {
+        bf16x4 sv;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sv[u] = f2bf(pv[u]);
+        *(bf16x4*)(e.shadow + base + 4 * j) = sv;
+      }
+    }
+    return;
+  }
   for (int64_t i = base + threadIdx.x; i < end; i += blockDim.x) {
     float g = e.g[i] * h.grad_scale;
     float p = e.p[i];
