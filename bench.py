@@ -19,7 +19,7 @@ Rank 0 prints ONE JSON line; `value` = total images/s over all ranks, timed
 as the MAX over ranks of K steps bracketed by barrier + device sync.  With N > 1 a
 second timed phase of the same K steps runs the reference's cross-replica BN
 (SyncBN on its own RCCL communicator) and reports it as ``syncbn_value``; the
-headline ``value`` is local BN (per-GPU batch 1024).
+headline ``value`` is local BN (per-GPU batch 4096: 156 GB of the 288 GB HBM).
 """
 from __future__ import annotations
 
@@ -103,15 +103,19 @@ def parse(argv=None):
 
 
 CONFIGS = {
-    # per-GPU batch 1024 for every config (sized for 288 GB of HBM; the larger grids amortise
-    # per-kernel latency).  Measured on one MI355X (profiles/meas_r2/batch_sweep.txt):
+    # per-GPU batches sized for 288 GB of HBM (the larger grids amortise per-kernel latency and
+    # the per-step optimizer / weight refresh).  r50 (the headline), round 6, same box
+    # (profiles/r6/batch_sweep_s51_s52.txt): 1024 / 1536 / 2048 / 3072 / 4096: 14.63k / 14.91k /
+    # 15.05k / 15.34k / 15.41k img/s (39 / 59 / 78 / 117 / 156 GB); r101 (BASELINE config 5, "large
+    # per-GPU batch") 1024 / 3072: 9.05k / 9.66k (59 / 177 GB).  Round 2
+    # (profiles/meas_r2/batch_sweep.txt):
     # r50 512 / 1024 / 2048: 11.9k / 12.7k / 13.0k img/s (43 GB at 1024); arcface 256 / 512 / 1024:
     # 26.6k / 36.6k / 43.9k (11 GB); resnext 128 / 256 / 512 / 1024: 7.5k / 8.7k / 9.5k / 9.9k (56 GB);
     # r101 512 / 1024 / 1536: 7.7k / 8.4k / 8.6k (64 GB); tresnet 256 / 512 / 1024: 9.4k / 10.9k / 11.7k
-    "r50": dict(model="resnet50", batch=1024, image_size=224, num_classes=1000),
+    "r50": dict(model="resnet50", batch=4096, image_size=224, num_classes=1000),
     "arcface": dict(model="resnet50", batch=1024, image_size=112, num_classes=10000),
     "resnext": dict(model="resnext50_32x4d", batch=1024, image_size=224, num_classes=1000),
-    "r101": dict(model="resnet101", batch=1024, image_size=224, num_classes=1000),
+    "r101": dict(model="resnet101", batch=3072, image_size=224, num_classes=1000),
     "tresnet": dict(model="tresnet_m", batch=1024, image_size=224, num_classes=1000),
 }
 METRICS = {
