@@ -108,15 +108,15 @@ CONFIGS = {
     # (profiles/r6/batch_sweep_s51_s52.txt): 1024 / 1536 / 2048 / 3072 / 4096: 14.63k / 14.91k /
     # 15.05k / 15.34k / 15.41k img/s (39 / 59 / 78 / 117 / 156 GB); r101 (BASELINE config 5, "large
     # per-GPU batch") 1024 / 3072: 9.05k / 9.66k (59 / 177 GB); arcface 1024 / 2048 / 4096: 47.7k /
-    # 53.2k / 56.8k (10 / 20 / 40 GB); resnext 1024 / 2048 / 3072: 11.48k / 11.81k / 11.81k (53 / 106 /
-    # 158 GB); tresnet 1024 / 2048 / 4096: 13.59k / 14.17k / 14.49k (26 / 51 / 101 GB)
+    # 53.2k / 56.8k (10 / 20 / 40 GB), 8192 / 16384: 58.8k / 59.6k (80 / 159 GB, s61); resnext 1024 / 2048 / 3072: 11.48k / 11.81k / 11.81k (53 / 106 /
+    # 158 GB); tresnet 1024 / 2048 / 4096: 13.59k / 14.17k / 14.49k (26 / 51 / 101 GB), 8192: +0.8 %
     # (profiles/r6/config_batch_sweep_s57.txt).  Round 2
     # (profiles/meas_r2/batch_sweep.txt):
     # r50 512 / 1024 / 2048: 11.9k / 12.7k / 13.0k img/s (43 GB at 1024); arcface 256 / 512 / 1024:
     # 26.6k / 36.6k / 43.9k (11 GB); resnext 128 / 256 / 512 / 1024: 7.5k / 8.7k / 9.5k / 9.9k (56 GB);
     # r101 512 / 1024 / 1536: 7.7k / 8.4k / 8.6k (64 GB); tresnet 256 / 512 / 1024: 9.4k / 10.9k / 11.7k
     "r50": dict(model="resnet50", batch=4096, image_size=224, num_classes=1000),
-    "arcface": dict(model="resnet50", batch=4096, image_size=112, num_classes=10000),
+    "arcface": dict(model="resnet50", batch=8192, image_size=112, num_classes=10000),
     "resnext": dict(model="resnext50_32x4d", batch=2048, image_size=224, num_classes=1000),
     "r101": dict(model="resnet101", batch=3072, image_size=224, num_classes=1000),
     "tresnet": dict(model="tresnet_m", batch=4096, image_size=224, num_classes=1000),
