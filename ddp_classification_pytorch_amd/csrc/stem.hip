@@ -300,6 +300,8 @@ struct StemBwdParams {
   int ablate;                  // A/B timing only (g_tune[kStemAblate]): 1 no MFMA phase, 2 no gather phase
 };
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));  // the 16x16x16 bf16 MFMA operand type
+
 __device__ __forceinline__ uint32_t sb_aoff(uint32_t r, uint32_t col) {
   return r * 128u + (((col >> 3) ^ (((r >> 1) & 3u) << 1)) << 4) + (col & 7) * 2;
 }
@@ -330,6 +332,7 @@ template <int W>  // output columns (a multiple of 8)
 // (w < 4) or the z - mu image (w >= 4): 16 accumulator tiles
 __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
   constexpr int NKS = (W + 31) / 32;
+  constexpr bool kTail16 = W - (NKS - 1) * 32 <= 16;  // last k-step on 16-deep MFMAs
   static_assert(W + 4 <= kSbRing && NKS * 32 <= 128, "row does not fit");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // A images, double-buffered by row parity: set b at smem + b * 32 KB = {g' [128 px][64],
@@ -505,6 +508,35 @@ __global__ void __launch_bounds__(512, 1) stem_bwd_kernel(StemBwdParams p) {
     const char* aimg = smem + (gg & 1) * 32768 + half * 16384;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
+      if (kTail16 && ks == NKS - 1) {
+        // last k-step with <= 16 valid pixel rows (W = 112: rows 96..111): 16-deep MFMAs over those
+        // rows only, one transposed read per operand (lane group kq holds rows kq&1, kq>>1 of the
+        // 4-row quads 0..3, the same rows for A and B; the output layout is the 16x16x32 one)
+        const uint32_t rt = ks * 32 + (kq & 1) * 4 + (kq >> 1) * 8;
+        bf16x4 bt[4];
+#pragma unroll
+        for (int tx = 0; tx < 4; ++tx)
+          bt[tx] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, brow + (rt + q + tx) * 32 + pp * 8));
+        if (half == 0) {
+          bf16x4 one;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) one[j] = f2bf(rt + j < (uint32_t)W ? 1.f : 0.f);
+#pragma unroll
+          for (int tx = 0; tx < 4; ++tx)
+            g3[tx] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, one),
+                                                               __builtin_bit_cast(s16x4, bt[tx]), g3[tx], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x4 af =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16(LDS_PTR(bf16x4, aimg + sb_aoff(rt + q, i * 16 + pp * 4)));
+#pragma unroll
+          for (int tx = 0; tx < 4; ++tx)
+            acc[i][tx] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, af),
+                                                                   __builtin_bit_cast(s16x4, bt[tx]), acc[i][tx], 0, 0, 0);
+        }
+        continue;
+      }
       const uint32_t base = ks * 32 + (kq >> 1) * 16 + (kq & 1) * 4;
       const uint32_t ra = base + q, rb = base + 8 + q;  // this lane's pixel rows (k 0-3 / 4-7)
       bf16x8 bf[4];
