@@ -108,6 +108,26 @@ def test_weight_prep(K):
     assert relerr(wb, rb) < 5e-3 and relerr(wt, rt) < 5e-3
 
 
+@pytest.mark.parametrize("shape,co_pad,ci", [((70, 3, 3, 24), 128, 0), ((64, 1, 1, 256), 64, 0),
+                                             ((64, 4, 4, 6), 64, 8), ((1000, 2048), 1024, 0)])
+def test_mt_weight_prep_layouts(shape, co_pad, ci):
+    """The per-step whole-model weight refresh (misc.hip mt_weight_prep: 4-wide path when every row
+    is a multiple of 4 channels, scalar path otherwise -- the 6 -> 8 channel case) against the fp32
+    weight: the bf16 copy [Co_pad][T][Ci] and the transposed copy [Ci][T][Co_pad], zero padded."""
+    from ddp_classification_pytorch_amd.ops.functional import _MTWeightCache
+    torch.manual_seed(0)
+    w = torch.randn(*shape, device=DEV)
+    wb, wt = _MTWeightCache().get(w, co_pad, True, ci)
+    torch.cuda.synchronize()
+    Co, Ci_src = shape[0], shape[-1]
+    T = math.prod(shape[1:-1])
+    Ci = ci or Ci_src
+    ref = torch.zeros(co_pad, T, Ci)
+    ref[:Co, :, :Ci_src] = w.cpu().reshape(Co, T, Ci_src).bfloat16().float()
+    assert torch.equal(wb.float().cpu().reshape(co_pad, T, Ci), ref)
+    assert torch.equal(wt.float().cpu().reshape(Ci, T, co_pad), ref.permute(2, 1, 0))
+
+
 @pytest.mark.parametrize("B,K_,N,relu,bias", [(256, 2048, 512, True, True), (32, 512, 2176, False, True),
                                                (5, 256, 64, False, False)])
 def test_linear(K, B, K_, N, relu, bias):
